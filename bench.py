@@ -1,0 +1,222 @@
+"""Benchmark: TMRNet train step (ResNet50 + LSTM + NLBlock, seq_len=10, LFB=40) on MI355X.
+
+One step = crop+normalize of B clips x T synthetic 250x250x3 uint8 frames resident in HBM ->
+LFB row table (reference rule, on device) -> TMRNet forward (rows read from the resident bank)
+-> CE(sum) -> backward -> [RCCL all-reduce SUM of grads when N>1] -> fused SGD step.
+This is the per-step work of train_only_non-local_pretrained.py:698-725 (BASELINE.json configs[1],
+configs[2] at N=8).  Synthetic data/weights per SURVEY.md §8d (seeds 1-5, torch.manual_seed(0)).
+
+Prints ONE JSON line (rank 0).  Multi-GPU: launched by torch.distributed.run, one rank per GPU,
+each rank trains its own B clips (weak scaling), gradients summed across ranks.
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MFMA_F32_PEAK_TF = 157.3     # MI355X dense f32 MFMA (guides: 256 CU x 2.4 GHz x 256 FLOP/clk)
+MFMA_BF16_PEAK_TF = 2516.6
+HBM_PEAK_GBS = 8000.0
+GFLOP_PER_FRAME = {"c2": 24.33}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=64, help="clips per rank (reference batch)")
+    ap.add_argument("--seq", type=int, default=10)
+    ap.add_argument("--lfb", type=int, default=40)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-clips", type=int, default=4)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def synth_inputs(args, rank, dev, nvar=2):
+    B, T, L = args.clips, args.seq, args.lfb
+    # LFB geometry of SURVEY.md §8d: 40 videos x 2500 frames
+    lengths = [2500] * 40
+    from tmrnet_amd.lfb import valid_starts
+    vs = valid_starts(T, lengths)
+    g1 = torch.Generator().manual_seed(1)
+    frames = [torch.randint(0, 256, (B * T, 250, 250, 3), generator=g1, dtype=torch.uint8).to(dev)
+              for _ in range(nvar)]
+    g3 = torch.Generator().manual_seed(3)
+    bank = (torch.rand(len(vs), 512, generator=g3) * 2 - 1).to(dev)
+    vs_d = torch.tensor(vs, dtype=torch.int64, device=dev)
+    steps = args.warmup + args.steps + 2
+    g2 = torch.Generator().manual_seed(2 + 1000 * rank)
+    offs = torch.randint(0, 27, (steps, B, 2), generator=g2, dtype=torch.int32).to(dev)
+    rng = np.random.default_rng(4 + rank)
+    starts = torch.from_numpy(rng.choice(np.array(vs), size=(steps, B))).to(torch.int64).to(dev)
+    g5 = torch.Generator().manual_seed(5 + 1000 * rank)
+    labels = torch.randint(0, 7, (steps, B), generator=g5).to(dev)
+    return frames, bank, vs_d, offs, starts, labels
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import tmrnet_amd
+    from tmrnet_amd import ops, LFBRows
+    from tmrnet_amd.ddp import GradAllReduce
+    from oracle.tmrnet_ref import sgd_param_groups
+
+    torch.manual_seed(0)
+    model = tmrnet_amd.resnet_lstm(seq_len=args.seq).to(dev).train()
+    lr = 5e-7  # reference default (-l 5e-7), groups at lr/10 and lr (:646-655)
+    opt = tmrnet_amd.SGD(sgd_param_groups(model, lr), lr=lr / 10, momentum=0.9,
+                         weight_decay=5e-4)
+    crit = tmrnet_amd.CrossEntropyLoss(size_average=False)
+    reducer = GradAllReduce(model, dist) if dist is not None else None
+    frames, bank, vs_d, offs, starts, labels = synth_inputs(args, rank, dev)
+    B, T, L = args.clips, args.seq, args.lfb
+
+    def step(i):
+        opt.zero_grad(set_to_none=True)
+        x4 = ops.crop_normalize(frames[i % len(frames)], offs[i], T)
+        rows = ops.lfb_index(vs_d, starts[i], L)
+        out = model(x4, LFBRows(bank, rows))
+        loss = crit(out, labels[i])
+        loss.backward()
+        if reducer is not None:
+            reducer.all_reduce_sum()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    frames_total = B * T * world * args.steps
+    fps = frames_total / elapsed
+    ms = elapsed / args.steps * 1e3
+    loss_v = float(loss.item())
+
+    # ---- live roofline of the dominant kernel family (implicit-GEMM conv) ----
+    roof = None
+    if not args.no_roofline:
+        ops.PROF = []
+        torch.cuda.synchronize()
+        i = args.warmup + args.steps
+        step(i)
+        torch.cuda.synchronize()
+        recs, ops.PROF = ops.PROF, None
+        tot_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in recs)
+        tot_flops = sum(f for _, f, _, _ in recs)
+        achieved = tot_flops / (tot_ms * 1e-3) / 1e12
+        per_kind = {}
+        for kind, f, e0, e1 in recs:
+            a = per_kind.setdefault(kind, [0, 0.0, 0.0])
+            a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
+        roof = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, f32 MFMA)",
+                "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
+                "frac": round(achieved / MFMA_F32_PEAK_TF, 4), "traffic": None,
+                "launches": len(recs), "avg_launch_ms": round(tot_ms / max(1, len(recs)), 4),
+                "conv_ms_per_step": round(tot_ms, 2),
+                "per_kind": {k: {"launches": v[0], "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
+                                 "ms": round(v[2], 2)} for k, v in per_kind.items()},
+                "step_mfma_frac": round(fps / world * GFLOP_PER_FRAME["c2"] * 1e9 /
+                                        (MFMA_F32_PEAK_TF * 1e12), 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": "train frames/sec, TMRNet ResNet50 seq=10 LFB=40",
+            "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (uint8 250x250x3 frames, U(-1,1) LFB bank 99640x512, random-init weights)",
+            "config": {"workload": "C2/C3: TMRNet ResNet50+LSTM+NLBlock train step",
+                       "model": "resnet_lstm (train_only_non-local_pretrained)",
+                       "global_batch": B * world, "clips_per_gpu": B, "seq_len": T, "lfb_len": L,
+                       "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
+            "loss_last": loss_v,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args):
+    """The CPU oracle (pure-torch restatement of the reference step) on the host cores."""
+    from oracle import tmrnet_ref as ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B, T, L = args.cpu_clips, args.seq, args.lfb
+    torch.manual_seed(0)
+    m = ref.TMRNetRef(seq_len=T).train()
+    opt = torch.optim.SGD(ref.sgd_param_groups(m, 5e-7), lr=5e-8, momentum=0.9, weight_decay=5e-4)
+    g = torch.Generator().manual_seed(1)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32)
+    lt = torch.rand(B, L, 512, generator=g) * 2 - 1
+    labels = torch.randint(0, 7, (B,), generator=g)
+
+    def one():
+        x = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
+        ref.train_step_ref(m, opt, x, lt, labels)
+
+    one()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        one()
+    el = time.perf_counter() - t0
+    model_name = platform.processor() or "unknown"
+    try:
+        for l in subprocess.check_output(["lscpu"], text=True).splitlines():
+            if l.startswith("Model name"):
+                model_name = l.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return {"value": round(B * T * args.cpu_steps / el, 3), "unit": "frames/s", "cores": threads,
+            "kind": "port", "cpu": model_name,
+            "sample": "oracle TMRNetRef fp32 train step (crop+norm, fwd, CE-sum, bwd, SGD), "
+                      "%d clips x %d frames, L=%d, %d timed steps after 1 warm-up"
+                      % (B, T, L, args.cpu_steps)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * libtmr -- MI355X (gfx950) HIP kernels for TMRNet's per-clip train-step hot path.
+ *
+ * Plain C ABI: raw device pointers, sizes and a hipStream_t.  The caller (the
+ * Python layer in tmrnet_amd/, or any FFI) owns every buffer; the library never
+ * allocates.  Every entry point returns 0 on success and non-zero on error;
+ * tmr_last_error() returns a thread-local message for the last failure.
+ * Entry points keep no global mutable state and enqueue only on the passed
+ * stream, so they are re-entrant across threads/devices.
+ *
+ * Activations are NHWC fp32 ("rows x C" for per-channel ops, rows = N*H*W).
+ * Conv weights are consumed in KRSC ([Cout][R][S][Cin]); gradients are written
+ * in the reference's OIHW layout so they drop into torch parameters directly.
+ *
+ * Each entry point names the reference operation it replaces (paths relative to
+ * the reference checkout's code/ directory).  The reference itself has no
+ * native code: these replace the cuDNN/cuBLAS kernels that its PyTorch modules
+ * reach.
+ */
+#ifndef TMR_H_
+#define TMR_H_
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMR_ABI_VERSION 1
+
+int tmr_abi_version(void);
+const char* tmr_last_error(void);
+
+/* ---------------- convolution / GEMM (gemm_conv.hip) ----------------------
+ * Replaces torchvision resnet50's nn.Conv2d fwd/bwd (cuDNN), reached from
+ * `share.forward` at Training TMRNet/train_only_non-local_pretrained.py:228,
+ * and the nn.Linear / nn.LSTM GEMMs of :215-239 and NLBlock_MutiConv6_3.py:27-37.
+ */
+typedef struct tmr_conv_desc {
+  int n, h, w, c; /* input NHWC; c = stored channels (power of two >= 4) */
+  int k;          /* output channels */
+  int r, s, stride, pad;
+  int ho, wo; /* output spatial size */
+} tmr_conv_desc;
+
+/* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
+int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                   const float* bias, float* y, float beta, hipStream_t stream);
+/* dx[n,h,w,c] = beta*dx + conv_transpose(dy, w_krsc) */
+int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
+                     float beta, hipStream_t stream);
+size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d);
+/* dw_oihw[k, c_real, r, s] = beta*dw + sum_m dy[m,k] * im2col(x)[m,(r,s,c)] */
+int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float* dy, float* dw_oihw,
+                     int c_real, float beta, float* ws, size_t ws_bytes, hipStream_t stream);
+/* C[M][N] = beta*C + A[M][K] * B[N][K]^T (+bias) */
+int tmr_gemm_nt(int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+                const float* bias, float* C, int ldc, float beta, hipStream_t stream);
+/* C[M][N] = beta*C + A[M][K] * B[K][N] */
+int tmr_gemm_nn(int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
+                int ldc, float beta, hipStream_t stream);
+/* C[M][N] = beta*C + A[K][M]^T * B[K][N] */
+int tmr_gemm_tn(int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
+                int ldc, float beta, hipStream_t stream);
+
+/* ---------------- layout / input (pool_layout.hip) ------------------------------ */
+/* OIHW -> KRSC with input channels zero-padded to cpad (torch Conv2d weight layout in) */
+int tmr_weight_oihw_to_krsc(const float* w, float* wk, int k, int c, int r, int s, int cpad,
+                            hipStream_t stream);
+/* NCHW fp32 -> NHWC fp32 with channels zero-padded to cpad (module-boundary input, :227) */
+int tmr_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, int cpad,
+                     hipStream_t stream);
+/* NHWC (c channels of cstore stored) -> NCHW */
+int tmr_nhwc_to_nchw(const float* x, float* y, int n, int c, int cstore, int h, int w,
+                     hipStream_t stream);
+/* Per-clip RandomCrop + ToTensor + Normalize (train_only_non-local_pretrained.py:101-126,
+ * :335-341): frames uint8 [F][hin][win][3], offsets int32 [F/seq][2] = (x1,y1),
+ * out fp32 NHWC [F][crop][crop][4] (4th channel 0). */
+int tmr_crop_normalize(const uint8_t* frames, const int32_t* offsets, float* out, int f, int hin,
+                       int win, int seq_len, int crop, float m0, float m1, float m2, float s0,
+                       float s1, float s2, hipStream_t stream);
+
+/* ---------------- batch norm + ReLU + residual (bn.hip) ---------------------
+ * Replaces nn.BatchNorm2d (train mode, batch statistics, eps, momentum) + ReLU +
+ * the bottleneck residual add of torchvision resnet50.  ws: double workspace of
+ * tmr_bn_ws_bytes(rows, c) bytes. */
+size_t tmr_bn_ws_bytes(int rows, int c);
+/* batch stats of y -> save_mean, save_invstd, scale=gamma*invstd, shift=beta-mean*scale;
+ * running stats updated in place (unbiased var), PyTorch semantics */
+int tmr_bn_fwd_stats(const float* y, int rows, int c, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps,
+                     float* save_mean, float* save_invstd, float* scale, float* shift, void* ws,
+                     size_t ws_bytes, hipStream_t stream);
+/* eval mode: scale/shift from running stats */
+int tmr_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
+                       const float* running_var, float eps, int c, float* scale, float* shift,
+                       hipStream_t stream);
+/* z = act(y*scale + shift (+ residual)), act = ReLU if relu */
+int tmr_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
+                 float* z, int rows, int c, int relu, hipStream_t stream);
+/* backward of z = act(bn(y) (+res)): dy, optional dres (= grad at the pre-activation),
+ * dgamma, dbeta.  z is the saved output (ReLU mask z>0); NULL when relu==0. */
+int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* save_mean,
+               const float* save_invstd, const float* gamma, float* dy, float* dres,
+               float* dgamma, float* dbeta, int rows, int c, int relu, void* ws, size_t ws_bytes,
+               hipStream_t stream);
+
+/* ---------------- pooling (pool_layout.hip) --------------------------------------- */
+/* MaxPool2d(3,2,1) of share.maxpool (train_only_non-local_pretrained.py:207), NHWC */
+int tmr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int n, int h, int w, int c,
+                      int ho, int wo, hipStream_t stream);
+int tmr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int n, int h, int w,
+                      int c, int ho, int wo, hipStream_t stream);
+/* AdaptiveAvgPool2d(1) of share.avgpool (:214): x [n][hw][c] -> y [n][c] */
+int tmr_avgpool_fwd(const float* x, float* y, int n, int hw, int c, hipStream_t stream);
+int tmr_avgpool_bwd(const float* dy, float* dx, int n, int hw, int c, hipStream_t stream);
+
+/* ---------------- misc (head.hip) ------------------------------------------ */
+/* out[j] = beta*out[j] + sum_i x[i*ld + j]   (Linear bias grads) */
+int tmr_col_sum(const float* x, int rows, int cols, int ld, float* out, float beta,
+                hipStream_t stream);
+/* y = x * mask (mask already scaled by 1/(1-p)); mask from counter-based RNG */
+int tmr_dropout_mask(float* mask, long n, float p, uint64_t seed, uint64_t offset,
+                     hipStream_t stream);
+/* CrossEntropyLoss(reduction='sum', weight) fwd+bwd, train_only_non-local_pretrained.py:631,
+ * :720-721: loss[0] = sum_b w[y_b]*(lse_b - x_b[y_b]); dlogits = gscale*w[y_b]*(softmax-onehot);
+ * preds = argmax (torch.max tie rule: first). weight may be NULL. */
+int tmr_ce_sum(const float* logits, const int64_t* labels, const float* weight, int b, int k,
+               float gscale, float* loss, float* dlogits, int64_t* preds, hipStream_t stream);
+/* torch.optim.SGD step (momentum, dampening, weight_decay, nesterov), :725 */
+int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr, float momentum,
+                 float dampening, float weight_decay, int nesterov, int first_step,
+                 hipStream_t stream);
+/* LFB row table of get_long_feature (train_only_non-local_pretrained.py:293-311):
+ * rows[b][k] = index of the first valid start >= max(start_b - k - 1, 0) in the sorted
+ * valid-start list (== the reference's dict walk, incl. own-row fallback and
+ * cross-video reuse). */
+int tmr_lfb_index(const int64_t* valid_starts, int nstarts, const int64_t* clip_starts, int b,
+                  int l, int32_t* rows, hipStream_t stream);
+/* out[i][:] = bank[rows[i]][:]  (the (B,L,512) long_feature tensor of :713) */
+int tmr_lfb_gather(const float* bank, const int32_t* rows, float* out, long nrows, int d,
+                   hipStream_t stream);
+/* LayerNorm over the last dim (NLBlock layer_norm, NLBlock_MutiConv6_3.py:17,:35) + ReLU */
+int tmr_layernorm_relu_fwd(const float* x, const float* gamma, const float* beta, float* y,
+                           float* mean, float* rstd, int rows, int d, float eps,
+                           hipStream_t stream);
+int tmr_layernorm_relu_bwd(const float* dy, const float* x, const float* y, const float* gamma,
+                           const float* mean, const float* rstd, float* dx, float* dgamma,
+                           float* dbeta, int rows, int d, hipStream_t stream);
+
+/* elementwise glue of the clip head (train_only_non-local_pretrained.py:236-239,
+ * NLBlock_MutiConv6_3.py:38-40) */
+/* out = base + z*mask (mask NULL: base + z) -- NLBlock dropout + residual */
+int tmr_residual_mask(const float* base, const float* z, const float* mask, float* out, long n,
+                      hipStream_t stream);
+/* a = relu(h*mask) -- head dropout(0.5) then F.relu */
+int tmr_mask_relu_fwd(const float* h, const float* mask, float* a, long n, hipStream_t stream);
+int tmr_mask_relu_bwd(const float* da, const float* a, const float* mask, float* dh, long n,
+                      hipStream_t stream);
+/* out = a*b*scalar[0] (b, scalar may be NULL) */
+int tmr_mul(const float* a, const float* b, const float* scalar, float* out, long n,
+            hipStream_t stream);
+
+/* ---------------- NLBlock attention core (head.hip) -------------------------
+ * NLBlock_MutiConv6_3.py:28-34 in GEMV form.  With q = linear1(St) and
+ * u = W2^T q, the reference scores q.(W2 Lt_l + b2) equal Lt_l.u + q.b2; the
+ * q.b2 term is constant over l and cancels in the softmax, so
+ *   p_l = softmax_l(scale * Lt_l . u),  ctx = sum_l p_l Lt_l,
+ * and SLL = linear3 applied to ctx (sum_l p_l = 1).  Lt rows come either from a
+ * dense (B,L,D) tensor (rows == NULL) or straight from the resident LFB bank via
+ * the row table (lt = bank, rows = tmr_lfb_index output). */
+int tmr_nl_attn_fwd(const float* lt, const int32_t* rows, const float* u, float* p, float* ctx,
+                    int b, int l, int d, float scale, hipStream_t stream);
+/* given dctx: dp_l = dctx.Lt_l; ds_l = scale*p_l*(dp_l - sum_k p_k dp_k);
+ * ut = sum_l ds_l Lt_l (= dL/du); dlt (optional, dense Lt only) = p_l*dctx + ds_l*u */
+int tmr_nl_attn_bwd(const float* lt, const int32_t* rows, const float* u, const float* p,
+                    const float* dctx, float* ut, float* dlt, int b, int l, int d, float scale,
+                    hipStream_t stream);
+
+/* ---------------- LSTM cell (head.hip) -------------------------------------
+ * nn.LSTM(2048,512) gates in PyTorch order i,f,g,o (train_only_non-local_pretrained.py:215,
+ * :230-231).  gx: x W_ih^T + b_ih + b_hh for step t (row stride ldgx); ghh: h_{t-1} W_hh^T
+ * (NULL at t=0); c_prev NULL at t=0.  act saves (i,f,g,o) activations [b][4h]. */
+int tmr_lstm_cell_fwd(const float* gx, int ldgx, const float* ghh, const float* c_prev,
+                      float* h_out, int ldh, float* c_out, float* act, int b, int hdim,
+                      hipStream_t stream);
+/* dh = dh_out (row stride lddh) + dh_rec (NULL ok); dc_next (NULL at t=T-1);
+ * writes dgates (pre-activation, row stride lddg) and dc_prev. */
+int tmr_lstm_cell_bwd(const float* dh_out, int lddh, const float* dh_rec, const float* dc_next,
+                      const float* act, const float* c, const float* c_prev, float* dgates,
+                      int lddg, float* dc_prev, int b, int hdim, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMR_H_ */

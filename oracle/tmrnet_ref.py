@@ -1,0 +1,309 @@
+"""CPU oracle: a plain-PyTorch (fp32, CPU) restatement of TMRNet's train-step hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in ``tmrnet_amd/`` imports this module; only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+use it, and only as the checker / the timed CPU baseline.  The product path
+runs the HIP kernels of ``libtmr.so`` and fails loudly without them.
+
+Every function cites the reference code it restates (paths relative to the
+reference checkout, ``code/``):
+
+* ``NLBlockRef``      -- ``Training TMRNet/NLBlock_MutiConv6_3.py:10-40``
+                         (pinned by ``tests/golden/nlblock_L*.npz``)
+* ``TimeConvRef``     -- ``Training TMRNet/NLBlock_MutiConv6_3.py:43-79``,
+                         generalised from the hard-coded L=30 (``:57-77``) to any L;
+                         identical at L=30 (pinned by ``tests/golden/timeconv_L30.npz``)
+* ``ResNet50Ref``     -- torchvision ``resnet50`` as used by
+                         ``Training TMRNet/train_only_non-local_pretrained.py:204-214``.
+                         torchvision is not vendored in the reference nor installed here:
+                         restated from its published v1.5 definition (stride on the 3x3,
+                         kaiming_normal fan_out convs, BN gamma=1 beta=0).  PARITY UNPINNED
+                         for the trunk beyond torch's own Conv2d/BatchNorm2d semantics.
+* ``TMRNetRef``       -- inline ``resnet_lstm`` (``train_only_non-local_pretrained.py:201-240``;
+                         with ``time_conv``: ``train_non-local_mutiConv_resnet.py:208-253``)
+* ``MemoryBankRef``   -- ``Training memory bank model/train_singlenet_phase_1fc.py:201-232``
+* ``get_useful_start_idx`` / ``lfb_index_table`` --
+                         ``train_only_non-local_pretrained.py:273-311`` (+ dict :507-511)
+                         (pinned by ``tests/golden/lfb_index_*.npz``)
+* ``crop_normalize_ref`` -- crop at a per-clip offset + ToTensor + Normalize
+                         (``train_only_non-local_pretrained.py:101-126``, ``:335-341``)
+* ``train_step_ref``  -- the step at ``train_only_non-local_pretrained.py:698-725``
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.nn.init as init
+
+MEAN = (0.41757566, 0.26098573, 0.25888634)
+STD = (0.21938758, 0.1983, 0.19342837)
+
+
+# --------------------------------------------------------------------------
+# NLBlock / TimeConv
+# --------------------------------------------------------------------------
+class NLBlockRef(nn.Module):
+    """NLBlock_MutiConv6_3.py:10-40, op for op."""
+
+    def __init__(self, feature_num=512):
+        super().__init__()
+        self.linear1 = nn.Linear(feature_num, feature_num)
+        self.linear2 = nn.Linear(feature_num, feature_num)
+        self.linear3 = nn.Linear(feature_num, feature_num)
+        self.linear4 = nn.Linear(feature_num, feature_num)
+        self.layer_norm = nn.LayerNorm([1, 512])
+        self.dropout = nn.Dropout(0.2)
+        for lin in (self.linear1, self.linear2, self.linear3, self.linear4):
+            init.xavier_uniform_(lin.weight)
+
+    def forward(self, St, Lt, drop_mask=None):
+        St_1 = self.linear1(St.view(-1, 1, 512))
+        Lt_1 = self.linear2(Lt).transpose(1, 2)
+        SL = torch.matmul(St_1, Lt_1) * ((1 / 512) ** 0.5)
+        SL = F.softmax(SL, dim=2)
+        SLL = torch.matmul(SL, self.linear3(Lt))
+        SLL = F.relu(self.layer_norm(SLL))
+        SLL = self.linear4(SLL)
+        if drop_mask is not None:          # externally supplied dropout mask (already scaled)
+            SLL = SLL * drop_mask.view(-1, 1, 512)
+        else:
+            SLL = self.dropout(SLL)
+        return St + SLL.view(-1, 512)
+
+
+class TimeConvRef(nn.Module):
+    """NLBlock_MutiConv6_3.py:43-79 generalised to any L.
+
+    y = max(x, conv3(x), conv5(x), conv7(x), maxpool2(pad_left0(x))) elementwise;
+    the reference's AdaptiveMaxPool2d((512,1)) over the 5 stacked branches (:75-76)
+    is exactly that max (verified against the golden fixture at L=30).
+    """
+
+    def __init__(self):
+        super().__init__()
+        self.timeconv1 = nn.Conv1d(512, 512, kernel_size=3, padding=1)
+        self.timeconv2 = nn.Conv1d(512, 512, kernel_size=5, padding=2)
+        self.timeconv3 = nn.Conv1d(512, 512, kernel_size=7, padding=3)
+        self.maxpool_m = nn.MaxPool1d(2, stride=1)
+
+    def forward(self, x):
+        xt = x.transpose(1, 2)                       # (B,512,L)
+        y1 = self.timeconv1(xt)
+        y2 = self.timeconv2(xt)
+        y3 = self.timeconv3(xt)
+        y4 = self.maxpool_m(F.pad(xt, (1, 0), mode="constant", value=0))
+        y = torch.stack((xt, y1, y2, y3, y4), dim=3).amax(dim=3)
+        return y.transpose(1, 2).contiguous()
+
+
+# --------------------------------------------------------------------------
+# ResNet-50 v1.5 (torchvision definition, torchvision state_dict keys)
+# --------------------------------------------------------------------------
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return self.relu(out + identity)
+
+
+def make_layer(inplanes, planes, blocks, stride):
+    downsample = None
+    if stride != 1 or inplanes != planes * 4:
+        downsample = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False),
+                                   nn.BatchNorm2d(planes * 4))
+    layers = [Bottleneck(inplanes, planes, stride, downsample)]
+    for _ in range(1, blocks):
+        layers.append(Bottleneck(planes * 4, planes))
+    return nn.Sequential(*layers)
+
+
+def resnet50_share():
+    """nn.Sequential with the reference's `share.*` module names (:204-214)."""
+    share = nn.Sequential()
+    share.add_module("conv1", nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False))
+    share.add_module("bn1", nn.BatchNorm2d(64))
+    share.add_module("relu", nn.ReLU(inplace=True))
+    share.add_module("maxpool", nn.MaxPool2d(3, stride=2, padding=1))
+    share.add_module("layer1", make_layer(64, 64, 3, 1))
+    share.add_module("layer2", make_layer(256, 128, 4, 2))
+    share.add_module("layer3", make_layer(512, 256, 6, 2))
+    share.add_module("layer4", make_layer(1024, 512, 3, 2))
+    share.add_module("avgpool", nn.AdaptiveAvgPool2d((1, 1)))
+    for m in share.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        elif isinstance(m, nn.BatchNorm2d):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+    return share
+
+
+# --------------------------------------------------------------------------
+# TMRNet / memory-bank model
+# --------------------------------------------------------------------------
+class TMRNetRef(nn.Module):
+    """Inline `resnet_lstm` (train_only_non-local_pretrained.py:201-240); with
+    time_conv=True the mutiConv variant (train_non-local_mutiConv_resnet.py:208-253)."""
+
+    def __init__(self, seq_len=10, num_classes=7, time_conv=False):
+        super().__init__()
+        self.seq_len = seq_len
+        self.share = resnet50_share()
+        self.lstm = nn.LSTM(2048, 512, batch_first=True)
+        self.fc_c = nn.Linear(512, num_classes)
+        self.fc_h_c = nn.Linear(1024, 512)
+        self.nl_block = NLBlockRef()
+        self.dropout = nn.Dropout(p=0.5)
+        if time_conv:
+            self.time_conv = TimeConvRef()
+        init.xavier_normal_(self.lstm.all_weights[0][0])
+        init.xavier_normal_(self.lstm.all_weights[0][1])
+        init.xavier_uniform_(self.fc_c.weight)
+        init.xavier_uniform_(self.fc_h_c.weight)
+
+    def forward(self, x, long_feature, masks=None):
+        T = self.seq_len
+        x = self.share(x.reshape(-1, 3, 224, 224)).reshape(-1, T, 2048)
+        y, _ = self.lstm(x)
+        y = y.contiguous().view(-1, 512)[T - 1::T]
+        Lt = self.time_conv(long_feature) if hasattr(self, "time_conv") else long_feature
+        if masks is None:
+            y_1 = self.nl_block(y, Lt)
+            h = self.dropout(self.fc_h_c(torch.cat([y, y_1], dim=1)))
+        else:
+            y_1 = self.nl_block(y, Lt, drop_mask=masks["nl"])
+            h = self.fc_h_c(torch.cat([y, y_1], dim=1)) * masks["head"]
+        return self.fc_c(F.relu(h))
+
+
+class MemoryBankRef(nn.Module):
+    """train_singlenet_phase_1fc.py:201-232: trunk -> LSTM -> dropout(0.2) -> fc on all frames."""
+
+    def __init__(self, seq_len=10, num_classes=7):
+        super().__init__()
+        self.seq_len = seq_len
+        self.share = resnet50_share()
+        self.lstm = nn.LSTM(2048, 512, batch_first=True)
+        self.fc = nn.Linear(512, num_classes)
+        self.dropout = nn.Dropout(p=0.2)
+        init.xavier_normal_(self.lstm.all_weights[0][0])
+        init.xavier_normal_(self.lstm.all_weights[0][1])
+        init.xavier_uniform_(self.fc.weight)
+
+    def forward(self, x, mask=None):
+        x = self.share(x.reshape(-1, 3, 224, 224)).reshape(-1, self.seq_len, 2048)
+        y, _ = self.lstm(x)
+        y = y.contiguous().view(-1, 512)
+        y = y * mask if mask is not None else self.dropout(y)
+        return self.fc(y)
+
+
+# --------------------------------------------------------------------------
+# LFB index rule, input transform, loss, step
+# --------------------------------------------------------------------------
+def get_useful_start_idx(seq_len, lengths):
+    """train_only_non-local_pretrained.py:273-280."""
+    idx, count = [], 0
+    for n in lengths:
+        idx.extend(range(count, count + (n + 1 - seq_len)))
+        count += n
+    return idx
+
+
+def lfb_index_table(starts_query, valid_starts, L):
+    """Row table of get_long_feature (train_only_non-local_pretrained.py:293-311)
+    with the start->row dict of :507-511: out[j][k] is the bank row for the
+    k-th most recent earlier start of clip j, falling back to the last row that
+    existed (own row at k=0), crossing video boundaries as the reference does."""
+    row_of = {s: r for r, s in enumerate(valid_starts)}
+    out = []
+    for s in starts_query:
+        s = int(s)
+        last = row_of[s]
+        rows = []
+        for k in range(L):
+            p = s - k - 1
+            if p in row_of:
+                last = row_of[p]
+            rows.append(last)
+        out.append(rows)
+    return out
+
+
+def crop_normalize_ref(frames_u8, offsets, seq_len):
+    """frames (F,250,250,3) uint8 HWC, offsets (B,2) int (x1,y1) per clip ->
+    (F,3,224,224) fp32: PIL crop((x1,y1,x1+224,y1+224)) then ToTensor+Normalize."""
+    Fn = frames_u8.shape[0]
+    out = torch.empty(Fn, 3, 224, 224, dtype=torch.float32)
+    mean = torch.tensor(MEAN).view(3, 1, 1)
+    std = torch.tensor(STD).view(3, 1, 1)
+    for f in range(Fn):
+        x1, y1 = (int(v) for v in offsets[f // seq_len])
+        crop = frames_u8[f, y1:y1 + 224, x1:x1 + 224, :].permute(2, 0, 1).float() / 255.0
+        out[f] = (crop - mean) / std
+    return out
+
+
+def ce_sum_ref(logits, labels, weight=None):
+    """nn.CrossEntropyLoss(size_average=False) / reduction='sum' (:631, mutiConv :780)."""
+    return F.cross_entropy(logits, labels, weight=weight, reduction="sum")
+
+
+def sgd_param_groups(model, lr):
+    """Param groups of train_only_non-local_pretrained.py:646-655 (multi_optim=1)."""
+    groups = [{"params": list(model.share.parameters())},
+              {"params": list(model.lstm.parameters())}]
+    if hasattr(model, "time_conv"):
+        groups.append({"params": list(model.time_conv.parameters()), "lr": lr})
+    for name in ("nl_block", "fc_h_c", "fc_c"):
+        groups.append({"params": list(getattr(model, name).parameters()), "lr": lr})
+    return groups
+
+
+def train_step_ref(model, opt, frames, long_feature, labels, masks=None, weight=None):
+    opt.zero_grad()
+    out = model(frames, long_feature, masks=masks)
+    loss = ce_sum_ref(out, labels, weight)
+    loss.backward()
+    opt.step()
+    return out.detach(), loss.detach()
+
+
+def trunk_gmacs_per_frame():
+    """Algorithmic MACs of the ResNet-50 trunk at 224x224 (fwd), for the roofline."""
+    total = 0
+    h = 112
+    total += h * h * 64 * 3 * 49
+    h = 56
+    cin = 64
+    for planes, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            ho = h // s
+            total += h * h * cin * planes            # 1x1 (at input res)
+            total += ho * ho * planes * planes * 9   # 3x3 (stride here)
+            total += ho * ho * planes * planes * 4   # 1x1 expand
+            if b == 0:
+                total += ho * ho * cin * planes * 4  # downsample
+            cin = planes * 4
+            h = ho
+    return total / 1e9

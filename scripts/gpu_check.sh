@@ -1,0 +1,19 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, short bench.  Stops at the first crash/timeout
+# (exit codes other than 0/1 from pytest); plain test failures (1) still run the bench.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+STEPS=${STEPS:-5}
+timeout -k 10 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc2=$?
+echo "smoke rc=$rc2"; tail -3 gpurun_out/smoke.log
+if [ $rc2 -ne 0 ] && [ $rc2 -ne 1 ]; then exit $rc2; fi
+timeout -k 10 900 python bench.py --steps $STEPS --warmup 2 ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
+rc3=$?
+echo "bench rc=$rc3"; tail -3 gpurun_out/bench.log
+exit $rc3

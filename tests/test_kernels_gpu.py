@@ -1,0 +1,211 @@
+"""Kernel-level parity: each libtmr entry point against a float64 CPU torch computation of
+the same op (the reference's own ops: nn.Conv2d / BatchNorm2d / MaxPool2d / LSTM / Linear).
+fp32 tolerances are stated per test, scaled by the magnitude of the result."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tmrnet_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+CONV_CASES = [
+    # n, h, w, cin, cout, r, stride, pad
+    (2, 16, 16, 64, 64, 1, 1, 0),
+    (2, 15, 13, 64, 128, 3, 1, 1),
+    (3, 14, 14, 128, 128, 3, 2, 1),
+    (2, 14, 14, 256, 512, 1, 2, 0),
+    (2, 9, 9, 512, 2048, 1, 1, 0),
+    (2, 7, 7, 2048, 512, 1, 1, 0),
+    (1, 28, 28, 3, 64, 7, 2, 3),     # stem: 3 channels stored as 4
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(dev, case):
+    n, h, w, cin, cout, r, st, pad = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, r, r, generator=g, dtype=torch.float64) / np.sqrt(cin * r * r)
+    y_ref = F.conv2d(x, wt, stride=st, padding=pad)
+    dy = torch.randn(y_ref.shape, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=st, padding=pad).backward(dy)
+    cs = 4 if cin == 3 else cin
+    x4 = ops.nchw_to_nhwc(x.float().to(dev), cpad=cs)
+    wk = ops.weight_to_krsc(wt.float().to(dev).contiguous(), cpad=cs)
+    y = ops.conv_fwd(x4, wk, st, pad)
+    assert rel_err(y.permute(0, 3, 1, 2), y_ref) < 2e-6
+    dyd = dy.float().permute(0, 2, 3, 1).contiguous().to(dev)
+    if cin != 3:
+        dx = ops.conv_dgrad(dyd, wk, (h, w), st, pad)
+        assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 2e-6
+        # beta accumulate
+        dx2 = ops.conv_dgrad(dyd, wk, (h, w), st, pad, out=dx.clone(), beta=1.0)
+        assert rel_err(dx2, 2 * dx) < 1e-6
+    dw = ops.conv_wgrad(x4, dyd, r, r, st, pad, c_real=cin)
+    assert rel_err(dw, wr.grad) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 2048, 2048), (7, 512, 64), (64, 7, 512), (33, 65, 17),
+                                   (640, 512, 1024)])
+def test_gemms(dev, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    a = torch.randn(M, K, generator=g, dtype=torch.float64)
+    b = torch.randn(N, K, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    ad, bd = a.float().to(dev), b.float().to(dev)
+    out = ops.gemm_nt(ad, bd, bias=bias.float().to(dev))
+    assert rel_err(out, a @ b.t() + bias) < 2e-6
+    bkn = b.t().contiguous()
+    out = ops.gemm_nn(ad, bkn.float().to(dev))
+    assert rel_err(out, a @ bkn) < 2e-6
+    # gemm_tn: out[K][N] = a^T @ c2 with a (M,K) read as [K'=M][M'=K]
+    c2 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    out = ops.gemm_tn(ad, c2.float().to(dev))
+    assert rel_err(out, a.t() @ c2) < 2e-6
+
+
+@pytest.mark.parametrize("rows,c,relu,res", [(20000, 64, True, False), (3000, 256, True, True),
+                                             (980, 2048, False, False), (4096, 128, True, True)])
+def test_batchnorm(dev, rows, c, relu, res):
+    g = torch.Generator().manual_seed(rows + c)
+    y = (torch.randn(rows, c, generator=g, dtype=torch.float64) * 3 + 5)
+    gamma = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(c, generator=g, dtype=torch.float64)
+    r = torch.randn(rows, c, generator=g, dtype=torch.float64) if res else None
+    rm = torch.randn(c, generator=g, dtype=torch.float64)
+    rv = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    # reference: torch batch_norm train mode (double)
+    yr = y.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+    o = F.batch_norm(yr, rm_ref, rv_ref, gr, br, training=True, momentum=0.1, eps=1e-5)
+    if res:
+        o = o + r
+    if relu:
+        o = torch.relu(o)
+    dz = torch.randn(rows, c, generator=g, dtype=torch.float64)
+    o.backward(dz)
+    yd = y.float().to(dev)
+    rmd, rvd = rm.float().to(dev), rv.float().to(dev)
+    mean, inv, scale, shift = ops.bn_fwd_train(yd, gamma.float().to(dev), beta.float().to(dev),
+                                               rmd, rvd, 0.1, 1e-5)
+    z = ops.bn_apply(yd, scale, shift, r.float().to(dev) if res else None, relu)
+    assert rel_err(z, o) < 3e-6
+    assert rel_err(rmd, rm_ref) < 1e-6 and rel_err(rvd, rv_ref) < 1e-6
+    dy, dres, dgm, dbt = ops.bn_bwd(dz.float().to(dev), yd, z, mean, inv, gamma.float().to(dev),
+                                    relu, want_dres=res)
+    assert rel_err(dy, yr.grad) < 1e-5
+    assert rel_err(dgm, gr.grad) < 1e-5
+    assert rel_err(dbt, br.grad) < 1e-5
+
+
+def test_pools(dev):
+    g = torch.Generator().manual_seed(3)
+    x = torch.relu(torch.randn(2, 64, 112, 112, generator=g, dtype=torch.float64))
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    dy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(dy)
+    xd = x.float().permute(0, 2, 3, 1).contiguous().to(dev)
+    y, am = ops.maxpool_fwd(xd)
+    assert rel_err(y.permute(0, 3, 1, 2), yr) == 0.0
+    dx = ops.maxpool_bwd(dy.float().permute(0, 2, 3, 1).contiguous().to(dev), am, (112, 112))
+    assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-6
+    x = torch.randn(3, 2048, 7, 7, generator=g, dtype=torch.float64)
+    xd = x.float().permute(0, 2, 3, 1).contiguous().to(dev)
+    y = ops.avgpool_fwd(xd)
+    assert rel_err(y, x.mean((2, 3))) < 1e-6
+    dx = ops.avgpool_bwd(y, (7, 7))
+    assert rel_err(dx[:, 3, 4, :], x.mean((2, 3)) / 49) < 1e-6
+
+
+def test_lstm_matches_torch(dev):
+    from tmrnet_amd.lstm import LSTM
+    torch.manual_seed(0)
+    B, T, I, H = 3, 5, 64, 32
+    ref = torch.nn.LSTM(I, H, batch_first=True).double()
+    m = LSTM(I, H).to(dev)
+    m.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = torch.randn(B, T, I, dtype=torch.float64)
+    dy = torch.randn(B, T, H, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    yr, _ = ref(xr)
+    yr.backward(dy)
+    xd = x.float().to(dev).requires_grad_(True)
+    y, (hn, cn) = m(xd)
+    assert rel_err(y, yr) < 2e-6
+    y.backward(dy.float().to(dev))
+    assert rel_err(xd.grad, xr.grad) < 1e-5
+    for (n1, p1), (n2, p2) in zip(m.named_parameters(), ref.named_parameters()):
+        assert n1 == n2
+        assert rel_err(p1.grad, p2.grad) < 1e-5, n1
+
+
+def test_crop_normalize_matches_oracle(dev):
+    from oracle.tmrnet_ref import crop_normalize_ref
+    g = torch.Generator().manual_seed(1)
+    fr = torch.randint(0, 256, (6, 250, 250, 3), generator=g, dtype=torch.uint8)
+    off = torch.randint(0, 27, (2, 2), generator=g, dtype=torch.int32)
+    ref = crop_normalize_ref(fr, off, 3)
+    out = ops.crop_normalize(fr.to(dev), off.to(dev), 3)
+    assert torch.equal(out[..., :3].permute(0, 3, 1, 2).cpu(), ref)   # bit-exact
+    assert out[..., 3].abs().max().item() == 0.0
+
+
+def test_ce_sum(dev):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(64, 7, generator=g, dtype=torch.float64)
+    y = torch.randint(0, 7, (64,), generator=g)
+    w = torch.rand(7, generator=g, dtype=torch.float64) + 0.5
+    for wt in (None, w):
+        xr = x.clone().requires_grad_(True)
+        lr = F.cross_entropy(xr, y, weight=wt, reduction="sum")
+        lr.backward()
+        loss, dl, preds = ops.ce_sum(x.float().to(dev), y.to(dev),
+                                     wt.float().to(dev) if wt is not None else None)
+        assert abs(loss.item() - lr.item()) / abs(lr.item()) < 1e-6
+        assert rel_err(dl, xr.grad) < 1e-6
+        assert torch.equal(preds.cpu(), x.float().argmax(1))
+
+
+def test_sgd_matches_torch(dev):
+    g = torch.Generator().manual_seed(9)
+    p0 = torch.randn(1000, generator=g)
+    grads = [torch.randn(1000, generator=g) for _ in range(3)]
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.SGD([pr], lr=0.1, momentum=0.9, weight_decay=5e-4)
+    from tmrnet_amd.optim import SGD
+    pd = p0.to(dev).requires_grad_(True)
+    opt2 = SGD([pd], lr=0.1, momentum=0.9, weight_decay=5e-4)
+    for gr in grads:
+        pr.grad = gr.clone()
+        opt.step()
+        pd.grad = gr.to(dev)
+        opt2.step()
+    assert rel_err(pd, pr) < 1e-6
+
+
+def test_lfb_index_and_gather_golden(dev):
+    import os
+    for name in ("tiny", "ragged", "c2", "c5"):
+        z = np.load(os.path.join(os.path.dirname(__file__), "golden", "lfb_index_%s.npz" % name))
+        starts = torch.from_numpy(z["starts"]).to(dev)
+        q = torch.from_numpy(z["query"]).to(dev)
+        rows = ops.lfb_index(starts, q, int(z["L"]))
+        assert np.array_equal(rows.cpu().numpy(), z["table"]), name
+    bank = torch.randn(50, 512, device=dev)
+    rows = torch.randint(0, 50, (4, 7), device=dev, dtype=torch.int32)
+    out = ops.lfb_gather(bank, rows)
+    assert torch.equal(out, bank[rows.long()])

@@ -1,0 +1,181 @@
+"""End-to-end parity of the HIP path against the CPU oracle (oracle/tmrnet_ref.py) and the
+reference-generated golden fixtures (tests/golden/).
+
+Contract (BASELINE.json north_star / SURVEY.md §8c): fp32 logits within 1e-4 absolute and
+bit-identical argmax phase ids on identical inputs and weights, in train mode (batch-stat BN,
+dropout masks injected so both sides use the same mask) and in eval mode.  Gradients are
+compared per parameter with a relative tolerance (fp32, different summation order).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import tmrnet_amd
+from tmrnet_amd import ops
+from oracle import tmrnet_ref as ref
+from tests.golden.golden_inputs import (nlblock_params, nlblock_inputs, projection_probes,
+                                        project, timeconv_params, timeconv_inputs, NL_CASES)
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("case", NL_CASES, ids=lambda c: "L%d" % c["L"])
+@pytest.mark.parametrize("lfb_rows", [False, True])
+def test_nlblock_golden(dev, case, lfb_rows):
+    """HIP NLBlock vs outputs/grads of the reference module (NLBlock_MutiConv6_3.py:10-40)."""
+    B, L, seed = case["B"], case["L"], case["seed"]
+    z = np.load(os.path.join(GOLD, "nlblock_L%d.npz" % L))
+    m = tmrnet_amd.NLBlock().to(dev).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in nlblock_params(seed).items()})
+    St_np, Lt_np, g_np = nlblock_inputs(seed, B, L)
+    St = torch.from_numpy(St_np).to(dev).requires_grad_(True)
+    if lfb_rows:
+        # the same Lt served as rows of a resident bank (rows permuted + duplicated bank)
+        bank = torch.from_numpy(Lt_np.reshape(B * L, 512)).to(dev)
+        perm = torch.randperm(B * L)
+        bank2 = torch.empty_like(bank)
+        bank2[perm.to(dev)] = bank
+        rows = perm.view(B, L).to(torch.int32).to(dev)
+        Lt = tmrnet_amd.LFBRows(bank2, rows)
+    else:
+        Lt = torch.from_numpy(Lt_np).to(dev).requires_grad_(True)
+    out = m(St, Lt)
+    out.backward(torch.from_numpy(g_np).to(dev))
+    assert np.abs(out.detach().cpu().numpy() - z["out"]).max() < 1e-5
+    assert rel_err(St.grad, torch.from_numpy(z["dSt"])) < 1e-5
+    if not lfb_rows:
+        assert rel_err(Lt.grad, torch.from_numpy(z["dLt"])) < 1e-5
+    probes = projection_probes(seed, (512, 512), 16)
+    for name, p in m.named_parameters():
+        key = "d_" + name.replace(".", "_")
+        g = p.grad.detach().cpu().numpy()
+        if g.shape == (512, 512):
+            pr = project(g, probes)
+            ex = z[key + "_proj"]
+            assert np.abs(pr - ex).max() <= 1e-5 * np.abs(ex).max() + 1e-6, name
+            assert np.abs(g[0] - z[key + "_row0"]).max() <= 1e-5 * np.abs(z[key + "_row0"]).max() + 1e-7
+        else:
+            ex = z[key]
+            assert np.abs(g.reshape(ex.shape) - ex).max() <= 1e-5 * np.abs(ex).max() + 1e-6, name
+
+
+def _make_pair(dev, seq_len, seed=0):
+    torch.manual_seed(seed)
+    m = tmrnet_amd.resnet_lstm(seq_len=seq_len).to(dev)
+    r = ref.TMRNetRef(seq_len=seq_len)
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    return m, r
+
+
+def _inputs(B, T, L, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32)
+    lt = torch.rand(B, L, 512, generator=g) * 2 - 1
+    labels = torch.randint(0, 7, (B,), generator=g)
+    return frames, off, lt, labels
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_tmrnet_step_parity(dev, train):
+    B, T, L = 2, 3, 5
+    m, r = _make_pair(dev, T)
+    frames, off, lt, labels = _inputs(B, T, L)
+    x_ref = ref.crop_normalize_ref(frames, off, T)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    assert torch.equal(x4[..., :3].permute(0, 3, 1, 2).cpu(), x_ref)
+    g = torch.Generator().manual_seed(7)
+    masks = {"nl": (torch.rand(B, 512, generator=g) >= 0.2).float() / 0.8,
+             "head": (torch.rand(B, 512, generator=g) >= 0.5).float() / 0.5}
+    m.train(train); r.train(train)
+    if train:
+        m.nl_block.forced_mask = masks["nl"].to(dev)
+        m.forced_head_mask = masks["head"].to(dev)
+    out = m(x4, lt.to(dev))
+    out_r = r(x_ref.view(B, T, 3, 224, 224), lt, masks=masks if train else None)
+    err = (out.detach().cpu() - out_r.detach()).abs().max().item()
+    assert err < 1e-4, err
+    assert torch.equal(out.detach().cpu().argmax(1), out_r.detach().argmax(1))
+    if not train:
+        return
+    crit = tmrnet_amd.CrossEntropyLoss(size_average=False)
+    loss = crit(out, labels.to(dev))
+    loss_r = ref.ce_sum_ref(out_r, labels)
+    assert abs(loss.item() - loss_r.item()) <= 1e-4 * max(1.0, abs(loss_r.item()))
+    loss.backward()
+    loss_r.backward()
+    rp = dict(r.named_parameters())
+    worst = []
+    for name, p in m.named_parameters():
+        e = rel_err(p.grad, rp[name].grad)
+        worst.append((e, name))
+        assert e < 5e-3, (name, e)
+    # running statistics after one train-mode forward
+    rb = dict(r.named_buffers())
+    for name, b in m.named_buffers():
+        if b.dtype.is_floating_point:
+            assert rel_err(b, rb[name]) < 1e-4, name
+        else:
+            assert torch.equal(b.cpu(), rb[name]), name
+
+
+def test_sgd_step_after_backward_parity(dev):
+    """One full step (forward, CE-sum, backward, SGD with the reference's param groups)."""
+    B, T, L = 2, 3, 5
+    m, r = _make_pair(dev, T, seed=3)
+    frames, off, lt, labels = _inputs(B, T, L, seed=4)
+    m.train(); r.train()
+    masks = {"nl": torch.ones(B, 512), "head": torch.ones(B, 512)}
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    lr = 1e-3
+    opt = tmrnet_amd.SGD(ref.sgd_param_groups(m, lr), lr=lr / 10, momentum=0.9,
+                         weight_decay=5e-4)
+    opt_r = torch.optim.SGD(ref.sgd_param_groups(r, lr), lr=lr / 10, momentum=0.9,
+                            weight_decay=5e-4)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    x_ref = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
+    crit = tmrnet_amd.CrossEntropyLoss(size_average=False)
+    for _ in range(2):
+        opt.zero_grad()
+        loss = crit(m(x4, lt.to(dev)), labels.to(dev))
+        loss.backward()
+        opt.step()
+        ref.train_step_ref(r, opt_r, x_ref, lt, labels, masks=masks)
+    rp = dict(r.named_parameters())
+    for name, p in m.named_parameters():
+        d = (p.detach().cpu() - rp[name].detach()).abs().max().item()
+        assert d < 1e-5, (name, d)
+
+
+def test_memory_bank_model_parity(dev):
+    """Config 1 model (train_singlenet_phase_1fc.py:201-232) on the HIP path vs the oracle."""
+    B, T = 2, 3
+    torch.manual_seed(5)
+    m = tmrnet_amd.MemoryBankModel(seq_len=T).to(dev)
+    r = ref.MemoryBankRef(seq_len=T)
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    frames, off, _, labels = _inputs(B, T, 1, seed=6)
+    mask = (torch.rand(B * T, 512) >= 0.2).float() / 0.8
+    m.forced_mask = mask.to(dev)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    x_ref = ref.crop_normalize_ref(frames, off, T)
+    out = m(x4)
+    out_r = r(x_ref, mask=mask)
+    assert (out.detach().cpu() - out_r.detach()).abs().max().item() < 1e-4
+    sel = out[T - 1::T]
+    loss = tmrnet_amd.CrossEntropyLoss(size_average=False)(sel, labels.to(dev))
+    loss.backward()
+    ref.ce_sum_ref(out_r[T - 1::T], labels).backward()
+    rp = dict(r.named_parameters())
+    for name, p in m.named_parameters():
+        assert rel_err(p.grad, rp[name].grad) < 5e-3, name

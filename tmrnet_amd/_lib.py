@@ -1,0 +1,121 @@
+"""ctypes binding of libtmr.so, the C-ABI kernel library (include/tmr.h).
+
+The product path has no fallback: if the library is missing or a call fails,
+this raises.  ``call(name, *args)`` converts torch tensors to device pointers,
+checks the returned status and raises ``RuntimeError(tmr_last_error())``.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtmr.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+U64 = ctypes.c_uint64
+SZ = ctypes.c_size_t
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo")]
+
+
+DP = ctypes.POINTER(ConvDesc)
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+SIGNATURES = {
+    "tmr_abi_version": [],
+    "tmr_last_error": [],
+    "tmr_conv2d_fwd": [DP, P, P, P, P, F, P],
+    "tmr_conv2d_dgrad": [DP, P, P, P, F, P],
+    "tmr_conv2d_wgrad_ws_bytes": [DP],
+    "tmr_conv2d_wgrad": [DP, P, P, P, I, F, P, SZ, P],
+    "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
+    "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],
+    "tmr_gemm_tn": [I, I, I, P, I, P, I, P, I, F, P],
+    "tmr_weight_oihw_to_krsc": [P, P, I, I, I, I, I, P],
+    "tmr_nchw_to_nhwc": [P, P, I, I, I, I, I, P],
+    "tmr_nhwc_to_nchw": [P, P, I, I, I, I, I, P],
+    "tmr_crop_normalize": [P, P, P, I, I, I, I, I, F, F, F, F, F, F, P],
+    "tmr_bn_ws_bytes": [I, I],
+    "tmr_bn_fwd_stats": [P, I, I, P, P, P, P, F, F, P, P, P, P, P, SZ, P],
+    "tmr_bn_eval_params": [P, P, P, P, F, I, P, P, P],
+    "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
+    "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
+    "tmr_maxpool2d_fwd": [P, P, P, I, I, I, I, I, I, P],
+    "tmr_maxpool2d_bwd": [P, P, P, I, I, I, I, I, I, P],
+    "tmr_avgpool_fwd": [P, P, I, I, I, P],
+    "tmr_avgpool_bwd": [P, P, I, I, I, P],
+    "tmr_col_sum": [P, I, I, I, P, F, P],
+    "tmr_dropout_mask": [P, L, F, U64, U64, P],
+    "tmr_ce_sum": [P, P, P, I, I, F, P, P, P, P],
+    "tmr_sgd_step": [P, P, P, L, F, F, F, F, I, I, P],
+    "tmr_lfb_index": [P, I, P, I, I, P, P],
+    "tmr_lfb_gather": [P, P, P, L, I, P],
+    "tmr_layernorm_relu_fwd": [P, P, P, P, P, P, I, I, F, P],
+    "tmr_layernorm_relu_bwd": [P, P, P, P, P, P, P, P, P, I, I, P],
+    "tmr_residual_mask": [P, P, P, P, L, P],
+    "tmr_mask_relu_fwd": [P, P, P, L, P],
+    "tmr_mask_relu_bwd": [P, P, P, P, L, P],
+    "tmr_mul": [P, P, P, P, L, P],
+    "tmr_nl_attn_fwd": [P, P, P, P, P, I, I, I, F, P],
+    "tmr_nl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, F, P],
+    "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],
+    "tmr_lstm_cell_bwd": [P, I, P, P, P, P, P, P, I, P, I, I, P],
+}
+_RESTYPES = {
+    "tmr_last_error": ctypes.c_char_p,
+    "tmr_conv2d_wgrad_ws_bytes": SZ,
+    "tmr_bn_ws_bytes": SZ,
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "libtmr.so not found at %s: build it with `make` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
+                % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def _conv(a):
+    if isinstance(a, torch.Tensor):
+        return ctypes.c_void_p(a.data_ptr())
+    return a
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def call(name, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*[_conv(a) for a in args])
+    if rc != 0:
+        raise RuntimeError("%s failed (%d): %s" % (name, rc, lib().tmr_last_error().decode()))
+    return rc
+
+
+def query(name, *args):
+    fn = getattr(lib(), name)
+    return fn(*[_conv(a) for a in args])

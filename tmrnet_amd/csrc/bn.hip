@@ -1,0 +1,356 @@
+// BatchNorm2d (train-mode batch statistics) + ReLU + residual for NHWC fp32.
+//
+// Replaces nn.BatchNorm2d / ReLU / the residual add inside torchvision's
+// resnet50 Bottleneck (the `share` trunk of
+// code/Training TMRNet/train_only_non-local_pretrained.py:204-214).
+// Statistics: per-thread fp32 sums of (y - shift_c) (shift = first row, removes
+// the mean bias), per-block double partials, fixed-order double reduction ->
+// deterministic and accurate for rows up to millions.  HBM-bound kernels:
+// float4 loads/stores along channels, grid sized to fill 256 CUs.
+#include "common.h"
+#include "tmr.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+struct Plan {
+  int cthreads;  // threads across channels (each 4 channels)
+  int rthreads;  // threads across rows
+  int cblocks;   // gridDim.y
+  int rpb;       // rows per block
+  int nrb;       // row blocks (gridDim.x)
+};
+
+Plan make_plan(int rows, int c) {
+  Plan p;
+  int c4 = c / 4;
+  p.cthreads = c4 < 64 ? c4 : 64;
+  p.rthreads = NT / p.cthreads;
+  p.cblocks = c4 / p.cthreads;
+  // ~1024 row blocks for large inputs, >= 8 rows per thread
+  int rpb = rows / 1024;
+  int minr = p.rthreads * 8;
+  if (rpb < minr) rpb = minr;
+  rpb = (rpb + p.rthreads - 1) / p.rthreads * p.rthreads;
+  p.rpb = rpb;
+  p.nrb = (rows + rpb - 1) / rpb;
+  return p;
+}
+
+// layout of the double workspace: [nrb][c][2] partials, then float coeffs [3][c]
+size_t ws_need(int rows, int c) {
+  Plan p = make_plan(rows, c);
+  return (size_t)p.nrb * c * 2 * sizeof(double) + (size_t)3 * c * sizeof(float) + 64;
+}
+
+__global__ __launch_bounds__(NT) void bn_stats_partial(const float* __restrict__ y, int rows, int c,
+                                                       int rpb, int cthreads,
+                                                       double* __restrict__ part) {
+  const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
+  const int rthreads = NT / cthreads;
+  const int ch = (blockIdx.y * cthreads + tc) * 4;
+  const float4 sh = *reinterpret_cast<const float4*>(y + ch);
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  for (int r = r0 + tr; r < r1; r += rthreads) {
+    float4 v = *reinterpret_cast<const float4*>(y + (long)r * c + ch);
+    float a = v.x - sh.x, b = v.y - sh.y, cc = v.z - sh.z, d = v.w - sh.w;
+    s.x += a; s.y += b; s.z += cc; s.w += d;
+    q.x += a * a; q.y += b * b; q.z += cc * cc; q.w += d * d;
+  }
+  __shared__ double red[NT][8];
+  red[threadIdx.x][0] = s.x; red[threadIdx.x][1] = s.y; red[threadIdx.x][2] = s.z;
+  red[threadIdx.x][3] = s.w; red[threadIdx.x][4] = q.x; red[threadIdx.x][5] = q.y;
+  red[threadIdx.x][6] = q.z; red[threadIdx.x][7] = q.w;
+  __syncthreads();
+  if (tr == 0) {
+    double acc[8];
+    for (int e = 0; e < 8; ++e) acc[e] = 0.0;
+    for (int k = 0; k < rthreads; ++k)
+      for (int e = 0; e < 8; ++e) acc[e] += red[k * cthreads + tc][e];
+    double* o = part + ((long)blockIdx.x * c + ch) * 2;
+    for (int e = 0; e < 4; ++e) {
+      o[2 * e] = acc[e];
+      o[2 * e + 1] = acc[4 + e];
+    }
+  }
+}
+
+// one block per 64 channels; 4 groups of partial rows summed in fixed order
+__global__ __launch_bounds__(NT) void bn_stats_final(const float* __restrict__ y, const double* __restrict__ part, int nrb,
+                                                     int rows, int c, const float* gamma,
+                                                     const float* beta, float* rmean, float* rvar,
+                                                     float momentum, float eps, float* smean,
+                                                     float* sinv, float* scale, float* shift) {
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lc;
+  double s = 0.0, q = 0.0;
+  if (ch < c) {
+    for (int b = g; b < nrb; b += 4) {
+      s += part[((long)b * c + ch) * 2];
+      q += part[((long)b * c + ch) * 2 + 1];
+    }
+  }
+  __shared__ double red[4][64][2];
+  red[g][lc][0] = s;
+  red[g][lc][1] = q;
+  __syncthreads();
+  if (g == 0 && ch < c) {
+    s = red[0][lc][0] + red[1][lc][0] + red[2][lc][0] + red[3][lc][0];
+    q = red[0][lc][1] + red[1][lc][1] + red[2][lc][1] + red[3][lc][1];
+    const double n = (double)rows;
+    const double ms = s / n;
+    double var = q / n - ms * ms;
+    if (var < 0) var = 0;
+    const double mean = (double)y[ch] + ms;
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    smean[ch] = (float)mean;
+    sinv[ch] = (float)inv;
+    const double gm = gamma ? gamma[ch] : 1.0;
+    const double bt = beta ? beta[ch] : 0.0;
+    scale[ch] = (float)(gm * inv);
+    shift[ch] = (float)(bt - mean * gm * inv);
+    if (rmean) {
+      const double unb = rows > 1 ? var * n / (n - 1.0) : var;
+      rmean[ch] = (float)((1.0 - momentum) * rmean[ch] + momentum * mean);
+      rvar[ch] = (float)((1.0 - momentum) * rvar[ch] + momentum * unb);
+    }
+  }
+}
+
+__global__ void bn_eval_params_k(const float* gamma, const float* beta, const float* rm,
+                                 const float* rv, float eps, int c, float* scale, float* shift) {
+  int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  float inv = 1.0f / sqrtf(rv[ch] + eps);
+  float g = gamma ? gamma[ch] : 1.f;
+  float b = beta ? beta[ch] : 0.f;
+  scale[ch] = g * inv;
+  shift[ch] = b - rm[ch] * g * inv;
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, const float* __restrict__ scale,
+                                                 const float* __restrict__ shift,
+                                                 const float* __restrict__ res, float* __restrict__ z,
+                                                 long n4, int c4) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    const int cc = (int)(i % c4) * 4;
+    float4 v = reinterpret_cast<const float4*>(y)[i];
+    const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
+    const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
+    v.x = fmaf(v.x, sc.x, sf.x);
+    v.y = fmaf(v.y, sc.y, sf.y);
+    v.z = fmaf(v.z, sc.z, sf.z);
+    v.w = fmaf(v.w, sc.w, sf.w);
+    if (RES) {
+      const float4 r = reinterpret_cast<const float4*>(res)[i];
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    if (RELU) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    reinterpret_cast<float4*>(z)[i] = v;
+  }
+}
+
+template <bool RELU>
+__global__ __launch_bounds__(NT) void bn_bwd_partial(const float* __restrict__ dz, const float* __restrict__ y,
+                                                     const float* __restrict__ z,
+                                                     const float* __restrict__ mean, int rows, int c,
+                                                     int rpb, int cthreads, double* __restrict__ part) {
+  const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
+  const int rthreads = NT / cthreads;
+  const int ch = (blockIdx.y * cthreads + tc) * 4;
+  const float4 mu = *reinterpret_cast<const float4*>(mean + ch);
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  for (int r = r0 + tr; r < r1; r += rthreads) {
+    const long o = (long)r * c + ch;
+    float4 g = *reinterpret_cast<const float4*>(dz + o);
+    const float4 v = *reinterpret_cast<const float4*>(y + o);
+    if (RELU) {
+      const float4 zz = *reinterpret_cast<const float4*>(z + o);
+      g.x = zz.x > 0.f ? g.x : 0.f; g.y = zz.y > 0.f ? g.y : 0.f;
+      g.z = zz.z > 0.f ? g.z : 0.f; g.w = zz.w > 0.f ? g.w : 0.f;
+    }
+    s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
+    q.x = fmaf(g.x, v.x - mu.x, q.x); q.y = fmaf(g.y, v.y - mu.y, q.y);
+    q.z = fmaf(g.z, v.z - mu.z, q.z); q.w = fmaf(g.w, v.w - mu.w, q.w);
+  }
+  __shared__ double red[NT][8];
+  red[threadIdx.x][0] = s.x; red[threadIdx.x][1] = s.y; red[threadIdx.x][2] = s.z;
+  red[threadIdx.x][3] = s.w; red[threadIdx.x][4] = q.x; red[threadIdx.x][5] = q.y;
+  red[threadIdx.x][6] = q.z; red[threadIdx.x][7] = q.w;
+  __syncthreads();
+  if (tr == 0) {
+    double acc[8];
+    for (int e = 0; e < 8; ++e) acc[e] = 0.0;
+    for (int k = 0; k < rthreads; ++k)
+      for (int e = 0; e < 8; ++e) acc[e] += red[k * cthreads + tc][e];
+    double* o = part + ((long)blockIdx.x * c + ch) * 2;
+    for (int e = 0; e < 4; ++e) {
+      o[2 * e] = acc[e];
+      o[2 * e + 1] = acc[4 + e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ part, int nrb, int rows, int c,
+                                                   const float* mean, const float* inv,
+                                                   const float* gamma, float* dgamma,
+                                                   float* dbeta, float* coef) {
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lc;
+  double s = 0.0, q = 0.0;
+  if (ch < c) {
+    for (int b = g; b < nrb; b += 4) {
+      s += part[((long)b * c + ch) * 2];
+      q += part[((long)b * c + ch) * 2 + 1];
+    }
+  }
+  __shared__ double red[4][64][2];
+  red[g][lc][0] = s;
+  red[g][lc][1] = q;
+  __syncthreads();
+  if (g == 0 && ch < c) {
+    s = red[0][lc][0] + red[1][lc][0] + red[2][lc][0] + red[3][lc][0];
+    q = red[0][lc][1] + red[1][lc][1] + red[2][lc][1] + red[3][lc][1];
+    const double iv = inv[ch];
+    const double dbt = s;
+    const double dgm = q * iv;  // sum dzh * xhat
+    if (dgamma) dgamma[ch] = (float)dgm;
+    if (dbeta) dbeta[ch] = (float)dbt;
+    const double n = (double)rows;
+    const double gm = gamma ? gamma[ch] : 1.0;
+    const double A = gm * iv;
+    const double mdz = dbt / n, mdx = dgm / n;
+    const double B = -gm * iv * iv * mdx;
+    const double C = -A * mdz - B * (double)mean[ch];
+    coef[ch] = (float)A;
+    coef[c + ch] = (float)B;
+    coef[2 * c + ch] = (float)C;
+  }
+}
+
+template <bool RELU, bool DRES>
+__global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const float* __restrict__ y,
+                                                   const float* __restrict__ z,
+                                                   const float* __restrict__ coef, float* __restrict__ dy,
+                                                   float* __restrict__ dres, long n4, int c4) {
+  const int c = c4 * 4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    const int cc = (int)(i % c4) * 4;
+    float4 g = reinterpret_cast<const float4*>(dz)[i];
+    const float4 v = reinterpret_cast<const float4*>(y)[i];
+    if (RELU) {
+      const float4 zz = reinterpret_cast<const float4*>(z)[i];
+      g.x = zz.x > 0.f ? g.x : 0.f; g.y = zz.y > 0.f ? g.y : 0.f;
+      g.z = zz.z > 0.f ? g.z : 0.f; g.w = zz.w > 0.f ? g.w : 0.f;
+    }
+    if (DRES) reinterpret_cast<float4*>(dres)[i] = g;
+    const float4 A = *reinterpret_cast<const float4*>(coef + cc);
+    const float4 B = *reinterpret_cast<const float4*>(coef + c + cc);
+    const float4 C = *reinterpret_cast<const float4*>(coef + 2 * c + cc);
+    float4 o;
+    o.x = fmaf(A.x, g.x, fmaf(B.x, v.x, C.x));
+    o.y = fmaf(A.y, g.y, fmaf(B.y, v.y, C.y));
+    o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
+    o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
+    reinterpret_cast<float4*>(dy)[i] = o;
+  }
+}
+
+int ew_blocks(long n4) {
+  long b = (n4 + NT - 1) / NT;
+  if (b > 2048 * 4) b = 2048 * 4;
+  return (int)(b > 0 ? b : 1);
+}
+
+}  // namespace
+
+TMR_API size_t tmr_bn_ws_bytes(int rows, int c) { return ws_need(rows, c); }
+
+TMR_API int tmr_bn_fwd_stats(const float* y, int rows, int c, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var,
+                             float momentum, float eps, float* save_mean, float* save_invstd,
+                             float* scale, float* shift, void* ws, size_t ws_bytes,
+                             hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4, "tmr_bn_fwd_stats: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(rows > 0, "tmr_bn_fwd_stats: empty input");
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_fwd_stats: workspace too small");
+  Plan p = make_plan(rows, c);
+  TMR_CHECK_ARG((c / 4) % p.cthreads == 0, "tmr_bn_fwd_stats: unsupported channel count %d", c);
+  double* part = (double*)ws;
+  hipLaunchKernelGGL(bn_stats_partial, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, y, rows, c,
+                     p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_stats_partial");
+  hipLaunchKernelGGL(bn_stats_final, dim3(cdiv(c, 64)), dim3(NT), 0, stream, y, part, p.nrb, rows,
+                     c, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+                     save_invstd, scale, shift);
+  TMR_CHECK_LAUNCH("bn_stats_final");
+  return 0;
+}
+
+TMR_API int tmr_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
+                               const float* running_var, float eps, int c, float* scale,
+                               float* shift, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_eval_params_k, dim3(cdiv(c, 256)), dim3(256), 0, stream, gamma, beta,
+                     running_mean, running_var, eps, c, scale, shift);
+  TMR_CHECK_LAUNCH("bn_eval_params");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply(const float* y, const float* scale, const float* shift,
+                         const float* residual, float* z, int rows, int c, int relu,
+                         hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_bn_apply: channels %d must be a multiple of 4", c);
+  long n4 = (long)rows * c / 4;
+  int nb = ew_blocks(n4);
+  int c4 = c / 4;
+  if (residual) {
+    if (relu) hipLaunchKernelGGL((bn_apply_k<true, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
+    else hipLaunchKernelGGL((bn_apply_k<true, false>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_apply_k<false, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
+    else hipLaunchKernelGGL((bn_apply_k<false, false>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
+  }
+  TMR_CHECK_LAUNCH("bn_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* save_mean,
+                       const float* save_invstd, const float* gamma, float* dy, float* dres,
+                       float* dgamma, float* dbeta, int rows, int c, int relu, void* ws,
+                       size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4, "tmr_bn_bwd: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(rows > 0, "tmr_bn_bwd: empty input");
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd: workspace too small");
+  TMR_CHECK_ARG(!relu || z, "tmr_bn_bwd: relu backward needs the saved output z");
+  Plan p = make_plan(rows, c);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
+  if (relu)
+    hipLaunchKernelGGL((bn_bwd_partial<true>), dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, dz, y, z, save_mean, rows, c, p.rpb, p.cthreads, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial<false>), dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, dz, y, z, save_mean, rows, c, p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_bwd_partial");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(cdiv(c, 64)), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  long n4 = (long)rows * c / 4;
+  int nb = ew_blocks(n4);
+  int c4 = c / 4;
+  if (relu) {
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
+    else hipLaunchKernelGGL((bn_bwd_apply<true, false>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
+  } else {
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply<false, true>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
+    else hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
+  }
+  TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}

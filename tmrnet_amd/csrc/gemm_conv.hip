@@ -1,0 +1,601 @@
+// Implicit-GEMM convolution / GEMM engine, fp32 in / fp32 accumulate on the
+// gfx950 f32-input matrix cores (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain).
+//
+// One templated kernel serves three GEMM views of a 2-D convolution on NHWC
+// activations (and plain GEMMs as the 1x1 / 1-pixel special case):
+//
+//   FWD   : C[m=(n,ho,wo)][j=co]  = sum_{k=(tap,c)}  X[src(m,tap)][c]  * W[co][tap][c]
+//   DGRAD : C[m=(n,h,w)][j=ci]    = sum_{k=(tap,co)} dY[src(m,tap)][co] * W[co][tap][ci]
+//           (one launch per stride-parity class, so no zero taps are multiplied)
+//   WGRAD : C[i=co][j=(tap,c)]    = sum_{m=(n,ho,wo)} dY[m][co] * X[src(m,tap)][c]
+//           (reduction split over blockIdx.y into fp32 partial slabs, reduced in
+//            a fixed order afterwards -> deterministic)
+//
+// Replaces the cuDNN Conv2d fwd/dgrad/wgrad and cuBLAS Linear GEMMs the
+// reference reaches through torchvision resnet50 / nn.Linear / nn.LSTM
+// (code/Training TMRNet/train_only_non-local_pretrained.py:204-240).
+//
+// Block = 256 threads = 4 waves, tile BM x BN x 16, each wave a
+// (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA tiles.  Global->register prefetch of
+// tile t+1 overlaps the MFMAs on tile t (double-buffered LDS, one barrier per
+// k-tile).  LDS tiles are k-major ([16][BM+pad]) so each MFMA operand read is a
+// conflict-free ds_read_b32 of 32 consecutive floats per half-wave.
+#include "common.h"
+#include "tmr.h"
+
+namespace {
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+constexpr int BK = 16;
+constexpr int NT = 256;
+
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  int M, N, K;
+  // K-index (FWD/DGRAD) or column-index (WGRAD) decomposition into (tap, channel)
+  int log2C, ntaps, tapS, tapSinv;
+  int oy0, ox0, dyr, dxs;   // source offset of tap (ri,si) = (oy0 + dyr*ri, ox0 + dxs*si)
+  int wr0, ws0, wst, wS;    // DGRAD weight tap index = (wr0 + wst*ri)*wS + (ws0 + wst*si)
+  // gather geometry: row -> (n,y,x) on the grid, source pixel (y*sy+oy, x*sx+ox)
+  FastDiv dHW, dW;
+  int Hs, Ws, sy, sx;
+  int lds;   // source pixel stride (elements)
+  int ldb;   // FWD: B row stride; DGRAD: stride per co; WGRAD: dY row stride
+  // output
+  int ldc;
+  float beta;
+  int oH, oW, osy, osx, oyc, oxc;  // DGRAD output-pixel map (osy==0: rows contiguous)
+  // WGRAD split-K
+  int kchunk;
+  long slab;
+};
+
+struct RowGeo {
+  int nHs, yb, xb;  // n*Hs, y*sy, x*sx
+  bool ok;
+};
+
+__device__ __forceinline__ RowGeo row_geo(const GemmArgs& a, int m, int mlimit) {
+  RowGeo g;
+  g.ok = m < mlimit;
+  uint32_t mm = g.ok ? (uint32_t)m : 0u;
+  uint32_t n = fdiv(mm, a.dHW);
+  uint32_t rem = mm - n * a.dHW.d;
+  uint32_t y = fdiv(rem, a.dW);
+  uint32_t x = rem - y * a.dW.d;
+  g.nHs = (int)n * a.Hs;
+  g.yb = (int)y * a.sy;
+  g.xb = (int)x * a.sx;
+  return g;
+}
+
+__device__ __forceinline__ void tap_split(const GemmArgs& a, int tap, int& ri, int& si) {
+  ri = (tap * a.tapSinv) >> 16;
+  si = tap - ri * a.tapS;
+}
+
+// Gathered source pointer for (row geometry, k) or nullptr when padded/out of range.
+__device__ __forceinline__ const float* gather_ptr(const GemmArgs& a, const float* base,
+                                                   const RowGeo& g, int kidx) {
+  int tap, c;
+  if (a.ntaps == 1) {
+    tap = 0;
+    c = kidx;
+  } else {
+    tap = kidx >> a.log2C;
+    c = kidx & ((1 << a.log2C) - 1);
+  }
+  int ri, si;
+  tap_split(a, tap, ri, si);
+  int ys = g.yb + a.oy0 + a.dyr * ri;
+  int xs = g.xb + a.ox0 + a.dxs * si;
+  bool ok = g.ok && tap < a.ntaps && ys >= 0 && ys < a.Hs && xs >= 0 && xs < a.Ws;
+  if (!ok) return nullptr;
+  long pix = ((long)(g.nHs + ys) * a.Ws + xs);
+  return base + pix * a.lds + c;
+}
+
+template <bool AL>
+__device__ __forceinline__ float4 ld4(const float* p, int valid_elems) {
+  if (AL) {
+    return *reinterpret_cast<const float4*>(p);
+  } else {
+    float4 v;
+    v.x = valid_elems > 0 ? p[0] : 0.f;
+    v.y = valid_elems > 1 ? p[1] : 0.f;
+    v.z = valid_elems > 2 ? p[2] : 0.f;
+    v.w = valid_elems > 3 ? p[3] : 0.f;
+    return v;
+  }
+}
+
+template <int MODE, int BM, int BN, int WM, bool AL>
+__global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int RA = BM / 64;  // float4 loads per thread per k-tile for A
+  constexpr int RB = BN / 64;
+  // A tile k-major [BK][LDA]; K-contiguous loaders scatter 4 scalars -> pad 2,
+  // M/N-contiguous loaders write float4 -> pad 4.
+  constexpr bool A_KC = (MODE != MODE_WGRAD);
+  constexpr bool B_KC = (MODE == MODE_FWD);
+  constexpr int LDA = BM + (A_KC ? 2 : 4);
+  constexpr int LDB = BN + (B_KC ? 2 : 4);
+  __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
+  float* As0 = smem;
+  float* Bs0 = smem + 2 * BK * LDA;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, hh = lane >> 5;
+
+  // XCD-aware tile order: consecutive logical tiles share an XCD (and its L2);
+  // n-tiles of one m-tile are consecutive so the gathered A rows are reused.
+  const int nmt = (a.M + BM - 1) / BM;
+  const int nnt = (a.N + BN - 1) / BN;
+  const int nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    int xcd = bid & 7, loc = bid >> 3;
+    int q = nwg >> 3, r = nwg & 7;
+    int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    bid = (nwg >= 8) ? wg : bid;
+  }
+  const int m0 = (bid / nnt) * BM;
+  const int n0 = (bid % nnt) * BN;
+
+  // reduction range
+  int kbeg = 0, kend = a.K;
+  if (MODE == MODE_WGRAD) {
+    kbeg = blockIdx.y * a.kchunk;
+    kend = min(a.K, kbeg + a.kchunk);
+  }
+  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  // ---- per-thread loader state ----
+  RowGeo ga[RA];
+  if (A_KC) {
+#pragma unroll
+    for (int q = 0; q < RA; ++q) ga[q] = row_geo(a, m0 + (tid >> 2) + 64 * q, a.M);
+  }
+
+  float4 ra[RA], rb[RB];
+
+  auto load_tile = [&](int kt) {
+    const int kb = kbeg + kt * BK;
+    // ---- A ----
+    if (A_KC) {
+      const int k = kb + (tid & 3) * 4;
+#pragma unroll
+      for (int q = 0; q < RA; ++q) {
+        const float* p = (k < kend) ? gather_ptr(a, a.A, ga[q], k) : nullptr;
+        ra[q] = p ? ld4<AL>(p, kend - k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {  // WGRAD: A[i][kk] = dY[m][co], co contiguous
+#pragma unroll
+      for (int q = 0; q < RA; ++q) {
+        const int lin = tid + NT * q;
+        const int krow = lin / (BM / 4), c4 = lin % (BM / 4);
+        const int m = kb + krow, i = m0 + c4 * 4;
+        bool ok = (m < kend) && (i < a.M);
+        ra[q] = ok ? ld4<AL>(a.A + (long)m * a.ldb + i, a.M - i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    // ---- B ----
+    if (MODE == MODE_FWD) {  // B[j][k], k contiguous
+      const int k = kb + (tid & 3) * 4;
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        const int j = n0 + (tid >> 2) + 64 * q;
+        bool ok = (j < a.N) && (k < kend);
+        rb[q] = ok ? ld4<AL>(a.B + (long)j * a.ldb + k, kend - k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else if (MODE == MODE_DGRAD) {  // B[k=(tap,co)][j=ci], ci contiguous
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        const int lin = tid + NT * q;
+        const int krow = lin / (BN / 4), c4 = lin % (BN / 4);
+        const int k = kb + krow, j = n0 + c4 * 4;
+        bool ok = (k < kend) && (j < a.N);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) {
+          int tap, co;
+          if (a.ntaps == 1) { tap = 0; co = k; }
+          else { tap = k >> a.log2C; co = k & ((1 << a.log2C) - 1); }
+          int ri, si;
+          tap_split(a, tap, ri, si);
+          int rs = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
+          v = ld4<AL>(a.B + (long)co * a.ldb + (long)rs * a.N + j, a.N - j);
+        }
+        rb[q] = v;
+      }
+    } else {  // WGRAD: B[kk=m][j=(tap,c)] gathered from X
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        const int lin = tid + NT * q;
+        const int krow = lin / (BN / 4), c4 = lin % (BN / 4);
+        const int m = kb + krow, j = n0 + c4 * 4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < kend && j < a.N) {
+          RowGeo g = row_geo(a, m, kend);
+          const float* p = gather_ptr(a, a.B, g, j);
+          if (p) v = ld4<AL>(p, a.N - j);
+        }
+        rb[q] = v;
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    float* As = As0 + buf * BK * LDA;
+    float* Bs = Bs0 + buf * BK * LDB;
+    if (A_KC) {
+      const int kq = (tid & 3) * 4;
+#pragma unroll
+      for (int q = 0; q < RA; ++q) {
+        const int row = (tid >> 2) + 64 * q;
+        As[(kq + 0) * LDA + row] = ra[q].x;
+        As[(kq + 1) * LDA + row] = ra[q].y;
+        As[(kq + 2) * LDA + row] = ra[q].z;
+        As[(kq + 3) * LDA + row] = ra[q].w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < RA; ++q) {
+        const int lin = tid + NT * q;
+        const int krow = lin / (BM / 4), c4 = lin % (BM / 4);
+        *reinterpret_cast<float4*>(&As[krow * LDA + c4 * 4]) = ra[q];
+      }
+    }
+    if (B_KC) {
+      const int kq = (tid & 3) * 4;
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        const int row = (tid >> 2) + 64 * q;
+        Bs[(kq + 0) * LDB + row] = rb[q].x;
+        Bs[(kq + 1) * LDB + row] = rb[q].y;
+        Bs[(kq + 2) * LDB + row] = rb[q].z;
+        Bs[(kq + 3) * LDB + row] = rb[q].w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        const int lin = tid + NT * q;
+        const int krow = lin / (BN / 4), c4 = lin % (BN / 4);
+        *reinterpret_cast<float4*>(&Bs[krow * LDB + c4 * 4]) = rb[q];
+      }
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int aoff = wm * (BM / WM) + l31;
+  const int boff = wn * (BN / WN) + l31;
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < ntiles) load_tile(kt + 1);
+      const float* As = As0 + cur * BK * LDA;
+      const float* Bs = Bs0 + cur * BK * LDB;
+#pragma unroll
+      for (int s = 0; s < BK / 2; ++s) {
+        const int kr = 2 * s + hh;
+        float av[TM], bv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA + aoff + 32 * i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB + boff + 32 * j];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+      if (kt + 1 < ntiles) store_tile(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+  float* Cb = a.C;
+  if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (row >= a.M) continue;
+      long rbase;
+      if (MODE == MODE_DGRAD && a.osy != 0) {
+        uint32_t n = fdiv((uint32_t)row, a.dHW);
+        uint32_t rem = row - n * a.dHW.d;
+        uint32_t y = fdiv(rem, a.dW);
+        uint32_t x = rem - y * a.dW.d;
+        long pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
+        rbase = pix * a.ldc;
+      } else {
+        rbase = (long)row * a.ldc;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * (BN / WN) + 32 * j + l31;
+        if (col >= a.N) continue;
+        float v = acc[i][j][r];
+        if (MODE == MODE_FWD && a.bias) v += a.bias[col];
+        float* cp = Cb + rbase + col;
+        if (a.beta != 0.f) v += a.beta * *cp;
+        *cp = v;
+      }
+    }
+  }
+}
+
+// WGRAD split reduction: dW[co][tap][c] (KRSC with c < creal) summed over splits in
+// split order, written to OIHW (co, c, r, s) of the real weight.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit, long slab,
+                                    float* __restrict__ out, int Cout, int ntaps, int Cpad,
+                                    int creal, float beta) {
+  long total = (long)Cout * ntaps * creal;
+  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total;
+       o += (long)gridDim.x * blockDim.x) {
+    // o indexes OIHW: co, c, tap
+    int tap = (int)(o % ntaps);
+    long t2 = o / ntaps;
+    int c = (int)(t2 % creal);
+    int co = (int)(t2 / creal);
+    long src = ((long)co * ntaps + tap) * Cpad + c;
+    float s = 0.f;
+    for (int p = 0; p < nsplit; ++p) s += slabs[p * slab + src];
+    out[o] = beta != 0.f ? s + beta * out[o] : s;
+  }
+}
+
+template <int MODE, int BM, int BN, int WM>
+int launch_cfg(const GemmArgs& a, bool al, dim3 grid, hipStream_t st) {
+  if (al)
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, true>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, false>), grid, dim3(NT), 0, st, a);
+  TMR_CHECK_LAUNCH("gemm_kernel");
+  return 0;
+}
+
+// Tile selection: keep both tile dims useful; prefer 128x128.
+template <int MODE>
+int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
+  const long M = a.M, N = a.N;
+  int cfg;  // 0: 128x128, 1: 256x64, 2: 64x256, 3: 64x64
+  if (N <= 64 && M >= 256) cfg = 1;
+  else if (M <= 64 && N >= 256) cfg = 2;
+  else if (M <= 64 || N <= 64) cfg = 3;
+  else cfg = 0;
+  const int BMs[4] = {128, 256, 64, 64}, BNs[4] = {128, 64, 256, 64};
+  dim3 grid(cdiv(M, BMs[cfg]) * cdiv(N, BNs[cfg]), splits, 1);
+  if (grid.x == 0) return 0;
+  switch (cfg) {
+    case 0: return launch_cfg<MODE, 128, 128, 2>(a, al, grid, st);
+    case 1: return launch_cfg<MODE, 256, 64, 4>(a, al, grid, st);
+    case 2: return launch_cfg<MODE, 64, 256, 1>(a, al, grid, st);
+    default: return launch_cfg<MODE, 64, 64, 2>(a, al, grid, st);
+  }
+}
+
+int ilog2_exact(int v) {
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+void set_taps(GemmArgs& a, int nR, int nS) {
+  a.ntaps = nR * nS;
+  a.tapS = nS > 0 ? nS : 1;
+  a.tapSinv = (65536 + a.tapS - 1) / a.tapS;
+}
+
+void set_grid(GemmArgs& a, int n, int hg, int wg) {
+  (void)n;
+  a.dHW = make_fastdiv((uint32_t)(hg * wg));
+  a.dW = make_fastdiv((uint32_t)wg);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                           const float* bias, float* y, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
+  const int lc = ilog2_exact(d->c);
+  TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
+  GemmArgs a{};
+  a.A = x; a.B = w_krsc; a.C = y; a.bias = bias;
+  a.M = d->n * d->ho * d->wo; a.N = d->k; a.K = d->r * d->s * d->c;
+  a.log2C = lc;
+  set_taps(a, d->r, d->s);
+  a.oy0 = -d->pad; a.ox0 = -d->pad; a.dyr = 1; a.dxs = 1;
+  set_grid(a, d->n, d->ho, d->wo);
+  a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
+  a.lds = d->c; a.ldb = a.K; a.ldc = d->k; a.beta = beta;
+  bool al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0);
+  return launch_gemm<MODE_FWD>(a, al, 1, stream);
+}
+
+TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                             float* dx, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_dgrad: null descriptor");
+  const int lk = ilog2_exact(d->k);
+  TMR_CHECK_ARG(lk >= 2, "tmr_conv2d_dgrad: output channels %d must be a power of two >= 4", d->k);
+  TMR_CHECK_ARG(d->c % 4 == 0, "tmr_conv2d_dgrad: input channels %d must be a multiple of 4", d->c);
+  const int st = d->stride;
+  // one launch per stride-parity class (ph,pw): rows h = st*y + ph
+  for (int ph = 0; ph < st; ++ph) {
+    for (int pw = 0; pw < st; ++pw) {
+      // valid kernel rows r with (ph + pad - r) % st == 0
+      int r0 = -1, nR = 0, s0 = -1, nS = 0;
+      for (int r = 0; r < d->r; ++r)
+        if (((ph + d->pad - r) % st + st) % st == 0) { if (r0 < 0) r0 = r; ++nR; }
+      for (int s = 0; s < d->s; ++s)
+        if (((pw + d->pad - s) % st + st) % st == 0) { if (s0 < 0) s0 = s; ++nS; }
+      const int hg = (d->h - ph + st - 1) / st, wg = (d->w - pw + st - 1) / st;
+      if (hg <= 0 || wg <= 0) continue;
+      GemmArgs a{};
+      a.A = dy; a.B = w_krsc; a.C = dx; a.bias = nullptr;
+      a.M = d->n * hg * wg; a.N = d->c; a.K = nR * nS * d->k;
+      a.log2C = lk;
+      set_taps(a, nR, nS);
+      if (nR == 0 || nS == 0) { a.K = 0; a.ntaps = 0; }
+      // ho = (h + pad - r)/st = y + (ph + pad - r0)/st - ri
+      a.oy0 = nR ? (ph + d->pad - r0) / st : 0;
+      a.ox0 = nS ? (pw + d->pad - s0) / st : 0;
+      a.dyr = -1; a.dxs = -1;
+      a.wr0 = r0 < 0 ? 0 : r0; a.ws0 = s0 < 0 ? 0 : s0; a.wst = st; a.wS = d->s;
+      set_grid(a, d->n, hg, wg);
+      a.Hs = d->ho; a.Ws = d->wo; a.sy = 1; a.sx = 1;
+      a.lds = d->k; a.ldb = d->r * d->s * d->c; a.ldc = d->c; a.beta = beta;
+      if (st == 1) {
+        a.osy = 0;
+      } else {
+        a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
+      }
+      if (a.K == 0 && beta == 1.f) continue;  // nothing to add
+      bool al = aligned16(dy) && aligned16(w_krsc) && aligned16(dx);
+      int rc = launch_gemm<MODE_DGRAD>(a, al, 1, stream);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
+static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* slab) {
+  const long Mred = (long)d->n * d->ho * d->wo;
+  const long Mo = d->k, No = (long)d->r * d->s * d->c;
+  const long tiles = (long)cdiv(Mo, 128) * cdiv(No, 128);
+  // aim for ~2048 workgroups; at least 512 reduction rows per split
+  long sp = 2048 / (tiles > 0 ? tiles : 1);
+  if (sp < 1) sp = 1;
+  long maxsp = Mred / 512;
+  if (maxsp < 1) maxsp = 1;
+  if (sp > maxsp) sp = maxsp;
+  long kc = (Mred + sp - 1) / sp;
+  kc = (kc + BK - 1) / BK * BK;
+  sp = (Mred + kc - 1) / kc;
+  *splits = (int)sp;
+  *kchunk = (int)kc;
+  *slab = Mo * No;
+  return 0;
+}
+
+TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
+  int sp, kc;
+  long slab;
+  wgrad_plan(d, &sp, &kc, &slab);
+  return (size_t)sp * slab * sizeof(float);
+}
+
+TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float* dy,
+                             float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
+                             hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_wgrad: null descriptor");
+  const int lc = ilog2_exact(d->c);
+  TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_wgrad: stored input channels %d must be a power of two >= 4", d->c);
+  TMR_CHECK_ARG(c_real >= 1 && c_real <= d->c, "tmr_conv2d_wgrad: bad c_real %d", c_real);
+  int sp, kc;
+  long slab;
+  wgrad_plan(d, &sp, &kc, &slab);
+  TMR_CHECK_ARG(ws && ws_bytes >= (size_t)sp * slab * sizeof(float),
+                "tmr_conv2d_wgrad: workspace too small (%zu < %zu)", ws_bytes,
+                (size_t)sp * slab * sizeof(float));
+  GemmArgs a{};
+  a.A = dy; a.B = x; a.C = ws; a.bias = nullptr;
+  a.M = d->k; a.N = d->r * d->s * d->c; a.K = d->n * d->ho * d->wo;
+  a.log2C = lc;
+  set_taps(a, d->r, d->s);
+  a.oy0 = -d->pad; a.ox0 = -d->pad; a.dyr = 1; a.dxs = 1;
+  set_grid(a, d->n, d->ho, d->wo);
+  a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
+  a.lds = d->c; a.ldb = d->k; a.ldc = a.N; a.beta = 0.f;
+  a.kchunk = kc; a.slab = slab;
+  bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0);
+  int rc = launch_gemm<MODE_WGRAD>(a, al, sp, stream);
+  if (rc) return rc;
+  long total = (long)d->k * d->r * d->s * c_real;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, ws, sp, slab,
+                     dw_oihw, d->k, d->r * d->s, d->c, c_real, beta);
+  TMR_CHECK_LAUNCH("wgrad_reduce_kernel");
+  return 0;
+}
+
+// Plain GEMMs on the same engine ---------------------------------------------
+// C[M][N] (row stride ldc) = beta*C + A[M][K] (row stride lda) * B^T, B = [N][K] (ldb) (+bias[N])
+TMR_API int tmr_gemm_nt(int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+                        const float* bias, float* C, int ldc, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "tmr_gemm_nt: negative size");
+  GemmArgs a{};
+  a.A = A; a.B = B; a.C = C; a.bias = bias;
+  a.M = M; a.N = N; a.K = K; a.log2C = 0;
+  set_taps(a, 1, 1);
+  a.dyr = 1; a.dxs = 1;
+  set_grid(a, M, 1, 1);
+  a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
+  a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta;
+  bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && K % 4 == 0;
+  return launch_gemm<MODE_FWD>(a, al, 1, stream);
+}
+
+// C[M][N] = beta*C + A[M][K] (lda) * B[K][N] (ldb)
+TMR_API int tmr_gemm_nn(int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+                        float* C, int ldc, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "tmr_gemm_nn: negative size");
+  GemmArgs a{};
+  a.A = A; a.B = B; a.C = C; a.bias = nullptr;
+  a.M = M; a.N = N; a.K = K; a.log2C = 0;
+  set_taps(a, 1, 1);
+  a.oy0 = 0; a.ox0 = 0; a.dyr = -1; a.dxs = -1;
+  a.wr0 = 0; a.ws0 = 0; a.wst = 1; a.wS = 1;
+  set_grid(a, M, 1, 1);
+  a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
+  a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta; a.osy = 0;
+  bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && K % 4 == 0 &&
+            N % 4 == 0;
+  return launch_gemm<MODE_DGRAD>(a, al, 1, stream);
+}
+
+// C[M][N] = beta*C + A^T B, A = [K][M] (lda), B = [K][N] (ldb)   (no split: small K)
+TMR_API int tmr_gemm_tn(int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+                        float* C, int ldc, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "tmr_gemm_tn: negative size");
+  GemmArgs a{};
+  a.A = A; a.B = B; a.C = C; a.bias = nullptr;
+  a.M = M; a.N = N; a.K = K; a.log2C = 0;
+  set_taps(a, 1, 1);
+  a.dyr = 1; a.dxs = 1;
+  set_grid(a, K, 1, 1);
+  a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
+  a.lds = ldb; a.ldb = lda; a.ldc = ldc; a.beta = beta;
+  a.kchunk = K > 0 ? K : 1; a.slab = 0;
+  bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && M % 4 == 0 &&
+            N % 4 == 0;
+  return launch_gemm<MODE_WGRAD>(a, al, 1, stream);
+}

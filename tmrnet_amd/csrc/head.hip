@@ -1,0 +1,555 @@
+// Clip-level kernels after the frame encoder: LSTM cell, NLBlock attention core,
+// LayerNorm+ReLU, LFB index/gather, dropout, cross-entropy, bias grads, SGD.
+//
+// Reference (paths under code/):
+//   LSTM            nn.LSTM(2048,512) -- Training TMRNet/train_only_non-local_pretrained.py:215,:230-233
+//   NLBlock         Training TMRNet/NLBlock_MutiConv6_3.py:25-40
+//   LFB gather      train_only_non-local_pretrained.py:293-311 (dict :507-511), call :707-713
+//   head + loss     train_only_non-local_pretrained.py:236-239, :631, :720-721
+//   SGD             torch.optim.SGD, :646-655, :725
+#include "common.h"
+#include "tmr.h"
+
+namespace {
+constexpr int NT = 256;
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---------------------------------------------------------------- LSTM cell
+__global__ void lstm_cell_fwd_k(const float* __restrict__ gx, int ldgx,
+                                const float* __restrict__ ghh, const float* __restrict__ cp,
+                                float* __restrict__ h, int ldh, float* __restrict__ c,
+                                float* __restrict__ act, int b, int hd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b * hd) return;
+  const int bb = i / hd, j = i % hd;
+  const float* g = gx + (long)bb * ldgx;
+  float ai = g[j], af = g[hd + j], ag = g[2 * hd + j], ao = g[3 * hd + j];
+  if (ghh) {
+    const float* q = ghh + (long)bb * 4 * hd;
+    ai += q[j]; af += q[hd + j]; ag += q[2 * hd + j]; ao += q[3 * hd + j];
+  }
+  const float ig = sigm(ai), fg = sigm(af), gg = tanhf(ag), og = sigm(ao);
+  const float cprev = cp ? cp[i] : 0.f;
+  const float cn = fg * cprev + ig * gg;
+  c[i] = cn;
+  h[(long)bb * ldh + j] = og * tanhf(cn);
+  float* a = act + (long)bb * 4 * hd;
+  a[j] = ig; a[hd + j] = fg; a[2 * hd + j] = gg; a[3 * hd + j] = og;
+}
+
+__global__ void lstm_cell_bwd_k(const float* __restrict__ dho, int lddh,
+                                const float* __restrict__ dhr, const float* __restrict__ dcn,
+                                const float* __restrict__ act, const float* __restrict__ c,
+                                const float* __restrict__ cp, float* __restrict__ dg, int lddg,
+                                float* __restrict__ dcp, int b, int hd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b * hd) return;
+  const int bb = i / hd, j = i % hd;
+  float dh = dho ? dho[(long)bb * lddh + j] : 0.f;
+  if (dhr) dh += dhr[i];
+  const float* a = act + (long)bb * 4 * hd;
+  const float ig = a[j], fg = a[hd + j], gg = a[2 * hd + j], og = a[3 * hd + j];
+  const float tc = tanhf(c[i]);
+  float dc = dh * og * (1.f - tc * tc);
+  if (dcn) dc += dcn[i];
+  const float dor = dh * tc;
+  const float cprev = cp ? cp[i] : 0.f;
+  float* d = dg + (long)bb * lddg;
+  d[j] = dc * gg * ig * (1.f - ig);
+  d[hd + j] = dc * cprev * fg * (1.f - fg);
+  d[2 * hd + j] = dc * ig * (1.f - gg * gg);
+  d[3 * hd + j] = dor * og * (1.f - og);
+  dcp[i] = dc * fg;
+}
+
+// ------------------------------------------------------ NLBlock attention core
+// one workgroup per clip; wave-per-row dot products, LDS softmax over L
+__global__ __launch_bounds__(NT) void nl_attn_fwd_k(const float* __restrict__ lt,
+                                                    const int32_t* __restrict__ rows,
+                                                    const float* __restrict__ u,
+                                                    float* __restrict__ p, float* __restrict__ ctx,
+                                                    int L, int D, float scale) {
+  extern __shared__ float sm[];  // [L]
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* ub = u + (long)b * D;
+  for (int l = wave; l < L; l += NT / 64) {
+    const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
+    const float* row = lt + r * D;
+    float s = 0.f;
+    for (int c = lane * 4; c < D; c += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(row + c);
+      const float4 w = *reinterpret_cast<const float4*>(ub + c);
+      s = fmaf(v.x, w.x, s); s = fmaf(v.y, w.y, s); s = fmaf(v.z, w.z, s); s = fmaf(v.w, w.w, s);
+    }
+    s = warp_sum(s);
+    if (lane == 0) sm[l] = s * scale;
+  }
+  __syncthreads();
+  // softmax over L (every wave computes the same max/sum; L is small)
+  float mx = -INFINITY;
+  for (int l = lane; l < L; l += 64) mx = fmaxf(mx, sm[l]);
+  mx = warp_max(mx);
+  float den = 0.f;
+  for (int l = lane; l < L; l += 64) den += expf(sm[l] - mx);
+  den = warp_sum(den);
+  __syncthreads();
+  const float inv = 1.0f / den;
+  // every wave has finished reading the scores (barrier above): overwrite in place
+  for (int l = threadIdx.x; l < L; l += NT) {
+    const float e = expf(sm[l] - mx) * inv;
+    p[(long)b * L + l] = e;
+    sm[l] = e;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x * 2; c < D; c += NT * 2) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int l = 0; l < L; ++l) {
+      const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
+      const float2 v = *reinterpret_cast<const float2*>(lt + r * D + c);
+      a0 = fmaf(sm[l], v.x, a0);
+      a1 = fmaf(sm[l], v.y, a1);
+    }
+    ctx[(long)b * D + c] = a0;
+    ctx[(long)b * D + c + 1] = a1;
+  }
+}
+
+__global__ __launch_bounds__(NT) void nl_attn_bwd_k(const float* __restrict__ lt,
+                                                    const int32_t* __restrict__ rows,
+                                                    const float* __restrict__ u,
+                                                    const float* __restrict__ p,
+                                                    const float* __restrict__ dctx,
+                                                    float* __restrict__ ut,
+                                                    float* __restrict__ dlt, int L, int D,
+                                                    float scale) {
+  extern __shared__ float sm[];  // [2L]: dp, ds
+  float* dps = sm;
+  float* dss = sm + L;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* gb = dctx + (long)b * D;
+  for (int l = wave; l < L; l += NT / 64) {
+    const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
+    const float* row = lt + r * D;
+    float s = 0.f;
+    for (int c = lane * 4; c < D; c += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(row + c);
+      const float4 w = *reinterpret_cast<const float4*>(gb + c);
+      s = fmaf(v.x, w.x, s); s = fmaf(v.y, w.y, s); s = fmaf(v.z, w.z, s); s = fmaf(v.w, w.w, s);
+    }
+    s = warp_sum(s);
+    if (lane == 0) dps[l] = s;
+  }
+  __syncthreads();
+  float t = 0.f;
+  for (int l = lane; l < L; l += 64) t = fmaf(p[(long)b * L + l], dps[l], t);
+  t = warp_sum(t);
+  __syncthreads();
+  for (int l = threadIdx.x; l < L; l += NT) {
+    const float pl = p[(long)b * L + l];
+    dss[l] = scale * pl * (dps[l] - t);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x * 2; c < D; c += NT * 2) {
+    float a0 = 0.f, a1 = 0.f;
+    const float g0 = gb[c], g1 = gb[c + 1];
+    const float u0 = u[(long)b * D + c], u1 = u[(long)b * D + c + 1];
+    for (int l = 0; l < L; ++l) {
+      const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
+      const float2 v = *reinterpret_cast<const float2*>(lt + r * D + c);
+      a0 = fmaf(dss[l], v.x, a0);
+      a1 = fmaf(dss[l], v.y, a1);
+      if (dlt) {
+        const float pl = p[(long)b * L + l];
+        float* o = dlt + ((long)b * L + l) * D + c;
+        o[0] = fmaf(pl, g0, dss[l] * u0);
+        o[1] = fmaf(pl, g1, dss[l] * u1);
+      }
+    }
+    ut[(long)b * D + c] = a0;
+    ut[(long)b * D + c + 1] = a1;
+  }
+}
+
+// ------------------------------------------------------------ LayerNorm+ReLU
+// one wave per row
+__global__ __launch_bounds__(NT) void ln_relu_fwd_k(const float* __restrict__ x,
+                                                    const float* __restrict__ g,
+                                                    const float* __restrict__ bt,
+                                                    float* __restrict__ y, float* __restrict__ mean,
+                                                    float* __restrict__ rstd, int rows, int D,
+                                                    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + (long)r * D;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += xr[c];
+  s = warp_sum(s);
+  const float mu = s / (float)D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float d = xr[c] - mu;
+    q = fmaf(d, d, q);
+  }
+  q = warp_sum(q);
+  const float rs = 1.0f / sqrtf(q / (float)D + eps);
+  for (int c = lane; c < D; c += 64) {
+    const float v = (xr[c] - mu) * rs * g[c] + bt[c];
+    y[(long)r * D + c] = fmaxf(v, 0.f);
+  }
+  if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
+}
+
+__global__ __launch_bounds__(NT) void ln_relu_bwd_k(const float* __restrict__ dy,
+                                                    const float* __restrict__ x,
+                                                    const float* __restrict__ y,
+                                                    const float* __restrict__ g,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd,
+                                                    float* __restrict__ dx, int rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float mu = mean[r], rs = rstd[r];
+  const long o = (long)r * D;
+  float s1 = 0.f, s2 = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float gy = y[o + c] > 0.f ? dy[o + c] : 0.f;
+    const float dxh = gy * g[c];
+    const float xh = (x[o + c] - mu) * rs;
+    s1 += dxh;
+    s2 = fmaf(dxh, xh, s2);
+  }
+  s1 = warp_sum(s1) / (float)D;
+  s2 = warp_sum(s2) / (float)D;
+  for (int c = lane; c < D; c += 64) {
+    const float gy = y[o + c] > 0.f ? dy[o + c] : 0.f;
+    const float dxh = gy * g[c];
+    const float xh = (x[o + c] - mu) * rs;
+    dx[o + c] = rs * (dxh - s1 - xh * s2);
+  }
+}
+
+// per-column parameter grads (fixed row order -> deterministic)
+__global__ void ln_relu_param_k(const float* __restrict__ dy, const float* __restrict__ x,
+                                const float* __restrict__ y, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, float* __restrict__ dg,
+                                float* __restrict__ db, int rows, int D) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float sg = 0.f, sb = 0.f;
+  for (int r = 0; r < rows; ++r) {
+    const long o = (long)r * D + c;
+    const float gy = y[o] > 0.f ? dy[o] : 0.f;
+    sb += gy;
+    sg = fmaf(gy, (x[o] - mean[r]) * rstd[r], sg);
+  }
+  if (dg) dg[c] = sg;
+  if (db) db[c] = sb;
+}
+
+// ---------------------------------------------------------------- LFB table
+__global__ void lfb_index_k(const int64_t* __restrict__ vs, int ns, const int64_t* __restrict__ st,
+                            int b, int L, int32_t* __restrict__ rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b * L) return;
+  const int bb = i / L, k = i % L;
+  long q = st[bb] - k - 1;
+  if (q < 0) q = 0;
+  // lower_bound(vs, q)
+  int lo = 0, hi = ns;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (vs[mid] < q) lo = mid + 1;
+    else hi = mid;
+  }
+  rows[i] = lo < ns ? lo : ns - 1;
+}
+
+__global__ void lfb_gather_k(const float* __restrict__ bank, const int32_t* __restrict__ rows,
+                             float* __restrict__ out, long n, int d4) {
+  const long total = n * d4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d4;
+    const int c = (int)(i % d4);
+    reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(bank)[(long)rows[r] * d4 + c];
+  }
+}
+
+// ------------------------------------------------------------------ dropout
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ void dropout_mask_k(float* __restrict__ m, long n, float p, float keep_scale,
+                               uint64_t seed, uint64_t off) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const uint64_t h = mix64(seed * 0x9e3779b97f4a7c15ull + off + (uint64_t)i);
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0,1)
+    m[i] = u >= p ? keep_scale : 0.f;
+  }
+}
+
+// --------------------------------------------------------------------- loss
+__global__ void ce_sum_k(const float* __restrict__ x, const int64_t* __restrict__ y,
+                         const float* __restrict__ w, int b, int k, float gscale,
+                         float* __restrict__ loss, float* __restrict__ dx,
+                         int64_t* __restrict__ preds) {
+  extern __shared__ float ls[];  // [b]
+  for (int i = threadIdx.x; i < b; i += blockDim.x) {
+    const float* xr = x + (long)i * k;
+    float mx = xr[0];
+    int am = 0;
+    for (int j = 1; j < k; ++j)
+      if (xr[j] > mx) { mx = xr[j]; am = j; }
+    float s = 0.f;
+    for (int j = 0; j < k; ++j) s += expf(xr[j] - mx);
+    const float lse = mx + logf(s);
+    const int lab = (int)y[i];
+    const float wi = w ? w[lab] : 1.f;
+    ls[i] = wi * (lse - xr[lab]);
+    if (preds) preds[i] = am;
+    if (dx) {
+      const float inv = 1.0f / s;
+      for (int j = 0; j < k; ++j) {
+        const float sm = expf(xr[j] - mx) * inv;
+        dx[(long)i * k + j] = gscale * wi * (sm - (j == lab ? 1.f : 0.f));
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < b; ++i) t += ls[i];
+    loss[0] = t;
+  }
+}
+
+// ------------------------------------------------------------ column sums
+__global__ void col_sum_k(const float* __restrict__ x, int rows, int cols, int ld,
+                          float* __restrict__ out, float beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += x[(long)r * ld + c];
+  out[c] = beta != 0.f ? s + beta * out[c] : s;
+}
+
+// --------------------------------------------------------------------- SGD
+__global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                      long n, float lr, float mom, float damp, float wd, int nesterov, int first) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float pv = p[i];
+    float d = g[i];
+    if (wd != 0.f) d = d + wd * pv;
+    if (mom != 0.f) {
+      float bv = first ? d : mom * buf[i] + (1.f - damp) * d;
+      buf[i] = bv;
+      d = nesterov ? d + mom * bv : bv;
+    }
+    p[i] = pv - lr * d;
+  }
+}
+
+int blocks_for(long n, int bs) {
+  long b = (n + bs - 1) / bs;
+  if (b > 8192) b = 8192;
+  return (int)(b > 0 ? b : 1);
+}
+
+}  // namespace
+
+TMR_API int tmr_lstm_cell_fwd(const float* gx, int ldgx, const float* ghh, const float* c_prev,
+                              float* h_out, int ldh, float* c_out, float* act, int b, int hdim,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(lstm_cell_fwd_k, dim3(cdiv((long)b * hdim, NT)), dim3(NT), 0, stream, gx,
+                     ldgx, ghh, c_prev, h_out, ldh, c_out, act, b, hdim);
+  TMR_CHECK_LAUNCH("lstm_cell_fwd");
+  return 0;
+}
+
+TMR_API int tmr_lstm_cell_bwd(const float* dh_out, int lddh, const float* dh_rec,
+                              const float* dc_next, const float* act, const float* c,
+                              const float* c_prev, float* dgates, int lddg, float* dc_prev, int b,
+                              int hdim, hipStream_t stream) {
+  hipLaunchKernelGGL(lstm_cell_bwd_k, dim3(cdiv((long)b * hdim, NT)), dim3(NT), 0, stream, dh_out,
+                     lddh, dh_rec, dc_next, act, c, c_prev, dgates, lddg, dc_prev, b, hdim);
+  TMR_CHECK_LAUNCH("lstm_cell_bwd");
+  return 0;
+}
+
+TMR_API int tmr_nl_attn_fwd(const float* lt, const int32_t* rows, const float* u, float* p,
+                            float* ctx, int b, int l, int d, float scale, hipStream_t stream) {
+  TMR_CHECK_ARG(d % 256 == 0, "tmr_nl_attn_fwd: feature dim %d must be a multiple of 256", d);
+  TMR_CHECK_ARG(l >= 1 && l <= 16384, "tmr_nl_attn_fwd: bad L %d", l);
+  if (b == 0) return 0;
+  hipLaunchKernelGGL(nl_attn_fwd_k, dim3(b), dim3(NT), l * sizeof(float), stream, lt, rows, u, p,
+                     ctx, l, d, scale);
+  TMR_CHECK_LAUNCH("nl_attn_fwd");
+  return 0;
+}
+
+TMR_API int tmr_nl_attn_bwd(const float* lt, const int32_t* rows, const float* u, const float* p,
+                            const float* dctx, float* ut, float* dlt, int b, int l, int d,
+                            float scale, hipStream_t stream) {
+  TMR_CHECK_ARG(d % 256 == 0, "tmr_nl_attn_bwd: feature dim %d must be a multiple of 256", d);
+  TMR_CHECK_ARG(!(dlt && rows), "tmr_nl_attn_bwd: dLt only for a dense Lt");
+  if (b == 0) return 0;
+  hipLaunchKernelGGL(nl_attn_bwd_k, dim3(b), dim3(NT), 2 * l * sizeof(float), stream, lt, rows, u,
+                     p, dctx, ut, dlt, l, d, scale);
+  TMR_CHECK_LAUNCH("nl_attn_bwd");
+  return 0;
+}
+
+TMR_API int tmr_layernorm_relu_fwd(const float* x, const float* gamma, const float* beta,
+                                   float* y, float* mean, float* rstd, int rows, int d, float eps,
+                                   hipStream_t stream) {
+  hipLaunchKernelGGL(ln_relu_fwd_k, dim3(cdiv(rows, NT / 64)), dim3(NT), 0, stream, x, gamma, beta,
+                     y, mean, rstd, rows, d, eps);
+  TMR_CHECK_LAUNCH("layernorm_relu_fwd");
+  return 0;
+}
+
+TMR_API int tmr_layernorm_relu_bwd(const float* dy, const float* x, const float* y,
+                                   const float* gamma, const float* mean, const float* rstd,
+                                   float* dx, float* dgamma, float* dbeta, int rows, int d,
+                                   hipStream_t stream) {
+  hipLaunchKernelGGL(ln_relu_bwd_k, dim3(cdiv(rows, NT / 64)), dim3(NT), 0, stream, dy, x, y, gamma,
+                     mean, rstd, dx, rows, d);
+  TMR_CHECK_LAUNCH("layernorm_relu_bwd");
+  if (dgamma || dbeta) {
+    hipLaunchKernelGGL(ln_relu_param_k, dim3(cdiv(d, 256)), dim3(256), 0, stream, dy, x, y, mean,
+                       rstd, dgamma, dbeta, rows, d);
+    TMR_CHECK_LAUNCH("layernorm_relu_param");
+  }
+  return 0;
+}
+
+TMR_API int tmr_lfb_index(const int64_t* valid_starts, int nstarts, const int64_t* clip_starts,
+                          int b, int l, int32_t* rows, hipStream_t stream) {
+  TMR_CHECK_ARG(nstarts > 0, "tmr_lfb_index: empty valid-start list");
+  if (b * l == 0) return 0;
+  hipLaunchKernelGGL(lfb_index_k, dim3(cdiv((long)b * l, NT)), dim3(NT), 0, stream, valid_starts,
+                     nstarts, clip_starts, b, l, rows);
+  TMR_CHECK_LAUNCH("lfb_index");
+  return 0;
+}
+
+TMR_API int tmr_lfb_gather(const float* bank, const int32_t* rows, float* out, long nrows, int d,
+                           hipStream_t stream) {
+  TMR_CHECK_ARG(d % 4 == 0, "tmr_lfb_gather: feature dim must be a multiple of 4");
+  if (nrows == 0) return 0;
+  hipLaunchKernelGGL(lfb_gather_k, dim3(blocks_for(nrows * (d / 4), NT)), dim3(NT), 0, stream, bank,
+                     rows, out, nrows, d / 4);
+  TMR_CHECK_LAUNCH("lfb_gather");
+  return 0;
+}
+
+TMR_API int tmr_dropout_mask(float* mask, long n, float p, uint64_t seed, uint64_t offset,
+                             hipStream_t stream) {
+  TMR_CHECK_ARG(p >= 0.f && p < 1.f, "tmr_dropout_mask: p must be in [0,1)");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dropout_mask_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, mask, n, p,
+                     1.0f / (1.0f - p), seed, offset);
+  TMR_CHECK_LAUNCH("dropout_mask");
+  return 0;
+}
+
+TMR_API int tmr_ce_sum(const float* logits, const int64_t* labels, const float* weight, int b,
+                       int k, float gscale, float* loss, float* dlogits, int64_t* preds,
+                       hipStream_t stream) {
+  TMR_CHECK_ARG(b >= 1 && b <= 65536 && k >= 1, "tmr_ce_sum: bad shape b=%d k=%d", b, k);
+  hipLaunchKernelGGL(ce_sum_k, dim3(1), dim3(256), b * sizeof(float), stream, logits, labels,
+                     weight, b, k, gscale, loss, dlogits, preds);
+  TMR_CHECK_LAUNCH("ce_sum");
+  return 0;
+}
+
+TMR_API int tmr_col_sum(const float* x, int rows, int cols, int ld, float* out, float beta,
+                        hipStream_t stream) {
+  if (cols == 0) return 0;
+  hipLaunchKernelGGL(col_sum_k, dim3(cdiv(cols, 256)), dim3(256), 0, stream, x, rows, cols, ld, out,
+                     beta);
+  TMR_CHECK_LAUNCH("col_sum");
+  return 0;
+}
+
+TMR_API int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr, float momentum,
+                         float dampening, float weight_decay, int nesterov, int first_step,
+                         hipStream_t stream) {
+  if (n == 0) return 0;
+  TMR_CHECK_ARG(momentum == 0.f || buf, "tmr_sgd_step: momentum needs a buffer");
+  hipLaunchKernelGGL(sgd_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, p, g, buf, n, lr,
+                     momentum, dampening, weight_decay, nesterov, first_step);
+  TMR_CHECK_LAUNCH("sgd_step");
+  return 0;
+}
+
+// --------------------------------------------------- small elementwise glue
+namespace {
+__global__ void residual_mask_k(const float* __restrict__ base, const float* __restrict__ z,
+                                const float* __restrict__ m, float* __restrict__ out, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    out[i] = base[i] + (m ? z[i] * m[i] : z[i]);
+}
+__global__ void mask_relu_fwd_k(const float* __restrict__ h, const float* __restrict__ m,
+                                float* __restrict__ a, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    a[i] = fmaxf(m ? h[i] * m[i] : h[i], 0.f);
+}
+__global__ void mask_relu_bwd_k(const float* __restrict__ da, const float* __restrict__ a,
+                                const float* __restrict__ m, float* __restrict__ dh, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float g = a[i] > 0.f ? da[i] : 0.f;
+    dh[i] = m ? g * m[i] : g;
+  }
+}
+__global__ void mul_k(const float* __restrict__ a, const float* __restrict__ b,
+                      const float* __restrict__ s, float* __restrict__ out, long n) {
+  const float sc = s ? s[0] : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    out[i] = (b ? a[i] * b[i] : a[i]) * sc;
+}
+}  // namespace
+
+TMR_API int tmr_residual_mask(const float* base, const float* z, const float* mask, float* out,
+                              long n, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(residual_mask_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, base, z, mask,
+                     out, n);
+  TMR_CHECK_LAUNCH("residual_mask");
+  return 0;
+}
+TMR_API int tmr_mask_relu_fwd(const float* h, const float* mask, float* a, long n,
+                              hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mask_relu_fwd_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, h, mask, a, n);
+  TMR_CHECK_LAUNCH("mask_relu_fwd");
+  return 0;
+}
+TMR_API int tmr_mask_relu_bwd(const float* da, const float* a, const float* mask, float* dh,
+                              long n, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mask_relu_bwd_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, da, a, mask,
+                     dh, n);
+  TMR_CHECK_LAUNCH("mask_relu_bwd");
+  return 0;
+}
+TMR_API int tmr_mul(const float* a, const float* b, const float* scalar, float* out, long n,
+                    hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mul_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, a, b, scalar, out, n);
+  TMR_CHECK_LAUNCH("mul");
+  return 0;
+}

@@ -1,0 +1,250 @@
+// Pooling, layout conversion and the input transform (HBM-bound kernels).
+//
+//  * MaxPool2d(3,2,1) / AdaptiveAvgPool2d(1) of torchvision resnet50 as used by
+//    the `share` trunk (code/Training TMRNet/train_only_non-local_pretrained.py:207,:214)
+//  * per-clip RandomCrop + ToTensor + Normalize of the train transform
+//    (train_only_non-local_pretrained.py:101-126 crop with per-clip seed,
+//    :335-341 Normalize constants), producing the NHWC4 layout the stem conv reads.
+#include "common.h"
+#include "tmr.h"
+
+namespace {
+constexpr int NT = 256;
+
+int ew_blocks(long n) {
+  long b = (n + NT - 1) / NT;
+  if (b > 8192) b = 8192;
+  return (int)(b > 0 ? b : 1);
+}
+
+__global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x, float* __restrict__ y,
+                                                    uchar4* __restrict__ am, int n, int h, int w,
+                                                    int c4, int ho, int wo) {
+  const long total = (long)n * ho * wo * c4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cq = (int)(i % c4);
+    long p = i / c4;
+    const int ox = (int)(p % wo);
+    p /= wo;
+    const int oy = (int)(p % ho);
+    const int nn = (int)(p / ho);
+    float4 best = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    uchar4 bi = make_uchar4(0, 0, 0, 0);
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iy = oy * 2 - 1 + dy;
+      if (iy < 0 || iy >= h) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int ix = ox * 2 - 1 + dx;
+        if (ix < 0 || ix >= w) continue;
+        const float4 v = reinterpret_cast<const float4*>(x)[(((long)nn * h + iy) * w + ix) * c4 + cq];
+        const unsigned char id = (unsigned char)(dy * 3 + dx);
+        // first maximum in scan order wins (PyTorch: val > max || isnan(val))
+        if (v.x > best.x || isnan(v.x)) { best.x = v.x; bi.x = id; }
+        if (v.y > best.y || isnan(v.y)) { best.y = v.y; bi.y = id; }
+        if (v.z > best.z || isnan(v.z)) { best.z = v.z; bi.z = id; }
+        if (v.w > best.w || isnan(v.w)) { best.w = v.w; bi.w = id; }
+      }
+    }
+    reinterpret_cast<float4*>(y)[i] = best;
+    am[i] = bi;
+  }
+}
+
+__global__ __launch_bounds__(NT) void maxpool_bwd_k(const float* __restrict__ dy, const uchar4* __restrict__ am,
+                                                    float* __restrict__ dx, int n, int h, int w,
+                                                    int c4, int ho, int wo) {
+  const long total = (long)n * h * w * c4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cq = (int)(i % c4);
+    long p = i / c4;
+    const int ix = (int)(p % w);
+    p /= w;
+    const int iy = (int)(p % h);
+    const int nn = (int)(p / h);
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int oy0 = iy / 2, oy1 = min((iy + 1) / 2, ho - 1);
+    const int ox0 = ix / 2, ox1 = min((ix + 1) / 2, wo - 1);
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const long o = (((long)nn * ho + oy) * wo + ox) * c4 + cq;
+        const unsigned char id = (unsigned char)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
+        const uchar4 a = am[o];
+        const float4 d = reinterpret_cast<const float4*>(dy)[o];
+        if (a.x == id) g.x += d.x;
+        if (a.y == id) g.y += d.y;
+        if (a.z == id) g.z += d.z;
+        if (a.w == id) g.w += d.w;
+      }
+    }
+    reinterpret_cast<float4*>(dx)[i] = g;
+  }
+}
+
+__global__ __launch_bounds__(NT) void avgpool_fwd_k(const float* __restrict__ x, float* __restrict__ y, int n,
+                                                    int hw, int c4) {
+  const long total = (long)n * c4;
+  const float inv = 1.0f / (float)hw;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cq = (int)(i % c4);
+    const long nn = i / c4;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* px = reinterpret_cast<const float4*>(x) + nn * hw * c4 + cq;
+    for (int p = 0; p < hw; ++p) {
+      const float4 v = px[(long)p * c4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    s.x *= inv; s.y *= inv; s.z *= inv; s.w *= inv;
+    reinterpret_cast<float4*>(y)[i] = s;
+  }
+}
+
+__global__ __launch_bounds__(NT) void avgpool_bwd_k(const float* __restrict__ dy, float* __restrict__ dx, int n,
+                                                    int hw, int c4) {
+  const long total = (long)n * hw * c4;
+  const float inv = 1.0f / (float)hw;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cq = (int)(i % c4);
+    const long nn = i / ((long)hw * c4);
+    float4 d = reinterpret_cast<const float4*>(dy)[nn * c4 + cq];
+    d.x *= inv; d.y *= inv; d.z *= inv; d.w *= inv;
+    reinterpret_cast<float4*>(dx)[i] = d;
+  }
+}
+
+__global__ void oihw_to_krsc_k(const float* __restrict__ w, float* __restrict__ wk, int k, int c,
+                               int rs, int cpad) {
+  const long total = (long)k * rs * cpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cpad);
+    const long t = i / cpad;
+    const int tap = (int)(t % rs);
+    const int ko = (int)(t / rs);
+    wk[i] = ci < c ? w[((long)ko * c + ci) * rs + tap] : 0.f;
+  }
+}
+
+__global__ void nchw_to_nhwc_k(const float* __restrict__ x, float* __restrict__ y, int n, int c,
+                               int h, int w, int cpad) {
+  const long total = (long)n * h * w * cpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cpad);
+    const long p = i / cpad;
+    const long hw = p % ((long)h * w);
+    const long nn = p / ((long)h * w);
+    y[i] = ci < c ? x[(nn * c + ci) * h * w + hw] : 0.f;
+  }
+}
+
+__global__ void nhwc_to_nchw_k(const float* __restrict__ x, float* __restrict__ y, int n, int c,
+                               int cs, int h, int w) {
+  const long total = (long)n * c * h * w;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long hw = i % ((long)h * w);
+    const long t = i / ((long)h * w);
+    const int ci = (int)(t % c);
+    const long nn = t / c;
+    y[i] = x[(nn * h * w + hw) * cs + ci];
+  }
+}
+
+__global__ __launch_bounds__(NT) void crop_normalize_k(const uint8_t* __restrict__ fr,
+                                                       const int32_t* __restrict__ off,
+                                                       float4* __restrict__ out, int f, int hin,
+                                                       int win, int seq, int crop, float m0,
+                                                       float m1, float m2, float s0, float s1,
+                                                       float s2) {
+  const long total = (long)f * crop * crop;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int x = (int)(i % crop);
+    const long t = i / crop;
+    const int y = (int)(t % crop);
+    const int fi = (int)(t / crop);
+    const int clip = fi / seq;
+    // clamp keeps a bad offset from reading outside the frame
+    const int x1 = min(max(off[2 * clip], 0), win - crop);
+    const int y1 = min(max(off[2 * clip + 1], 0), hin - crop);
+    const uint8_t* px = fr + (((long)fi * hin + (y + y1)) * win + (x + x1)) * 3;
+    // ToTensor: u8 -> float / 255; Normalize: (v - mean) / std
+    const float r = (float)px[0] / 255.0f, g = (float)px[1] / 255.0f, b = (float)px[2] / 255.0f;
+    out[i] = make_float4((r - m0) / s0, (g - m1) / s1, (b - m2) / s2, 0.f);
+  }
+}
+
+}  // namespace
+
+TMR_API int tmr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int n, int h, int w,
+                              int c, int ho, int wo, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd: channels %d must be a multiple of 4", c);
+  const long total = (long)n * ho * wo * (c / 4);
+  hipLaunchKernelGGL(maxpool_fwd_k, dim3(ew_blocks(total)), dim3(NT), 0, stream, x, y,
+                     (uchar4*)argmax, n, h, w, c / 4, ho, wo);
+  TMR_CHECK_LAUNCH("maxpool_fwd");
+  return 0;
+}
+
+TMR_API int tmr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int n, int h,
+                              int w, int c, int ho, int wo, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_bwd: channels %d must be a multiple of 4", c);
+  const long total = (long)n * h * w * (c / 4);
+  hipLaunchKernelGGL(maxpool_bwd_k, dim3(ew_blocks(total)), dim3(NT), 0, stream, dy,
+                     (const uchar4*)argmax, dx, n, h, w, c / 4, ho, wo);
+  TMR_CHECK_LAUNCH("maxpool_bwd");
+  return 0;
+}
+
+TMR_API int tmr_avgpool_fwd(const float* x, float* y, int n, int hw, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool_fwd: channels %d must be a multiple of 4", c);
+  hipLaunchKernelGGL(avgpool_fwd_k, dim3(ew_blocks((long)n * c / 4)), dim3(NT), 0, stream, x, y, n,
+                     hw, c / 4);
+  TMR_CHECK_LAUNCH("avgpool_fwd");
+  return 0;
+}
+
+TMR_API int tmr_avgpool_bwd(const float* dy, float* dx, int n, int hw, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool_bwd: channels %d must be a multiple of 4", c);
+  hipLaunchKernelGGL(avgpool_bwd_k, dim3(ew_blocks((long)n * hw * c / 4)), dim3(NT), 0, stream, dy,
+                     dx, n, hw, c / 4);
+  TMR_CHECK_LAUNCH("avgpool_bwd");
+  return 0;
+}
+
+TMR_API int tmr_weight_oihw_to_krsc(const float* w, float* wk, int k, int c, int r, int s,
+                                    int cpad, hipStream_t stream) {
+  TMR_CHECK_ARG(cpad >= c, "tmr_weight_oihw_to_krsc: cpad < c");
+  hipLaunchKernelGGL(oihw_to_krsc_k, dim3(ew_blocks((long)k * r * s * cpad)), dim3(NT), 0, stream,
+                     w, wk, k, c, r * s, cpad);
+  TMR_CHECK_LAUNCH("oihw_to_krsc");
+  return 0;
+}
+
+TMR_API int tmr_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, int cpad,
+                             hipStream_t stream) {
+  TMR_CHECK_ARG(cpad >= c, "tmr_nchw_to_nhwc: cpad < c");
+  hipLaunchKernelGGL(nchw_to_nhwc_k, dim3(ew_blocks((long)n * h * w * cpad)), dim3(NT), 0, stream,
+                     x, y, n, c, h, w, cpad);
+  TMR_CHECK_LAUNCH("nchw_to_nhwc");
+  return 0;
+}
+
+TMR_API int tmr_nhwc_to_nchw(const float* x, float* y, int n, int c, int cstore, int h, int w,
+                             hipStream_t stream) {
+  hipLaunchKernelGGL(nhwc_to_nchw_k, dim3(ew_blocks((long)n * h * w * c)), dim3(NT), 0, stream, x,
+                     y, n, c, cstore, h, w);
+  TMR_CHECK_LAUNCH("nhwc_to_nchw");
+  return 0;
+}
+
+TMR_API int tmr_crop_normalize(const uint8_t* frames, const int32_t* offsets, float* out, int f,
+                               int hin, int win, int seq_len, int crop, float m0, float m1,
+                               float m2, float s0, float s1, float s2, hipStream_t stream) {
+  TMR_CHECK_ARG(seq_len > 0 && f % seq_len == 0, "tmr_crop_normalize: frames %d not a multiple of seq_len %d", f, seq_len);
+  TMR_CHECK_ARG(crop <= hin && crop <= win, "tmr_crop_normalize: crop larger than frame");
+  hipLaunchKernelGGL(crop_normalize_k, dim3(ew_blocks((long)f * crop * crop)), dim3(NT), 0, stream,
+                     frames, offsets, (float4*)out, f, hin, win, seq_len, crop, m0, m1, m2, s0, s1,
+                     s2);
+  TMR_CHECK_LAUNCH("crop_normalize");
+  return 0;
+}

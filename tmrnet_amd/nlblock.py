@@ -1,0 +1,136 @@
+"""NLBlock (the temporal-variation layer) on libtmr kernels.
+
+Drop-in for ``NLBlock`` of code/Training TMRNet/NLBlock_MutiConv6_3.py:10-40
+(identical class in code/eval/python/NLBlock.py:10-40): same constructor,
+parameter names (linear1..4, layer_norm with weight/bias of shape (1,512)),
+xavier_uniform init, Dropout(0.2) in train mode, ``forward(St, Lt)``.
+
+The single-query attention runs in re-associated GEMV form (see
+include/tmr.h, tmr_nl_attn_fwd): u = W2^T (W1 St + b1) once per clip, then one
+pass over the L long-term rows for the scores and one for the context, so the
+L x 512 x 512 projections of the reference (linear2/linear3 applied to every
+LFB row) are never materialised.  ``Lt`` can be a dense (B,L,512) tensor or an
+``LFBRows`` view (resident bank + device row table), in which case the rows are
+read straight from the bank in HBM.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.init as init
+
+from . import ops
+
+
+class LFBRows:
+    """Lt given as rows of the resident long-term feature bank: bank (N,D) fp32 on the
+    device, rows (B,L) int32 (tmr_lfb_index output)."""
+
+    def __init__(self, bank, rows):
+        self.bank = bank
+        self.rows = rows
+
+    @property
+    def shape(self):
+        return (self.rows.shape[0], self.rows.shape[1], self.bank.shape[1])
+
+    def dense(self):
+        return ops.lfb_gather(self.bank, self.rows)
+
+
+class _DropoutRNG:
+    """Counter-based dropout masks (tmr_dropout_mask): seed from torch's generator, a new
+    offset per call."""
+
+    def __init__(self):
+        self.seed = None
+        self.offset = 0
+
+    def mask(self, n, p, like):
+        if self.seed is None:
+            self.seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFF
+        m = ops.dropout_mask(n, p, self.seed, self.offset, like)
+        self.offset += n
+        return m
+
+
+class NLBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, St, lt, rows, mask, L, w1, b1, w2, b2, w3, b3, g, bt, w4, b4):
+        B = St.shape[0]
+        St = St.contiguous()
+        scale = (1.0 / 512) ** 0.5
+        q = ops.gemm_nt(St, w1.detach(), bias=b1.detach())                 # linear1
+        u = ops.gemm_nn(q, w2.detach())                                    # W2^T q
+        p, c = ops.nl_attn_fwd(lt, rows, u, B, L, scale)                   # softmax, ctx
+        sll = ops.gemm_nt(c, w3.detach(), bias=b3.detach())                # linear3 (sum p = 1)
+        a, mu, rs = ops.layernorm_relu_fwd(sll, g.detach().reshape(-1).contiguous(),
+                                           bt.detach().reshape(-1).contiguous(), 1e-5)
+        z = ops.gemm_nt(a, w4.detach(), bias=b4.detach())                  # linear4
+        out = ops.residual_mask(St, z, mask)                               # dropout + residual
+        ctx.save_for_backward(St, lt, rows, mask, q, u, p, c, sll, a, mu, rs,
+                              w1, w2, w3, g, w4)
+        ctx.dims = (B, L)
+        ctx.lt_grad = ctx.needs_input_grad[1] and rows is None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (St, lt, rows, mask, q, u, p, c, sll, a, mu, rs, w1, w2, w3, g, w4) = ctx.saved_tensors
+        B, L = ctx.dims
+        dout = dout.contiguous()
+        scale = (1.0 / 512) ** 0.5
+        dz = ops.mul(dout, mask) if mask is not None else dout
+        dw4 = ops.gemm_tn(dz, a)
+        db4 = ops.col_sum(dz, B, 512, 512)
+        da = ops.gemm_nn(dz, w4.detach())
+        dsll, dg, dbt = ops.layernorm_relu_bwd(da, sll, a, g.detach().reshape(-1).contiguous(),
+                                               mu, rs)
+        dw3 = ops.gemm_tn(dsll, c)
+        db3 = ops.col_sum(dsll, B, 512, 512)
+        dc = ops.gemm_nn(dsll, w3.detach())
+        ut, dlt = ops.nl_attn_bwd(lt, rows, u, p, dc, B, L, scale, ctx.lt_grad)
+        dq = ops.gemm_nt(ut, w2.detach())                                  # W2 ut
+        dw2 = ops.gemm_tn(q, ut)                                           # q ut^T
+        db2 = torch.zeros_like(db3)  # sum_l dscore_l == 0: q.b2 cancels in the softmax
+        dw1 = ops.gemm_tn(dq, St)
+        db1 = ops.col_sum(dq, B, 512, 512)
+        dSt = ops.gemm_nn(dq, w1.detach(), out=ops.mul(dout), beta=1.0)   # dout + W1^T dq
+        return (dSt, dlt, None, None, None, dw1, db1, dw2, db2, dw3, db3,
+                dg.view_as(g), dbt.view_as(g), dw4, db4)
+
+
+class NLBlock(nn.Module):
+    def __init__(self, feature_num=512):
+        super().__init__()
+        if feature_num != 512:
+            raise ValueError("NLBlock is fixed at 512 features (LayerNorm([1,512]) in the reference)")
+        self.linear1 = nn.Linear(feature_num, feature_num)
+        self.linear2 = nn.Linear(feature_num, feature_num)
+        self.linear3 = nn.Linear(feature_num, feature_num)
+        self.linear4 = nn.Linear(feature_num, feature_num)
+        self.layer_norm = nn.LayerNorm([1, 512])
+        self.dropout = nn.Dropout(0.2)
+        init.xavier_uniform_(self.linear1.weight)
+        init.xavier_uniform_(self.linear2.weight)
+        init.xavier_uniform_(self.linear3.weight)
+        init.xavier_uniform_(self.linear4.weight)
+        self._rng = _DropoutRNG()
+        self.forced_mask = None  # parity tests: externally supplied scaled mask (B,512)
+
+    def forward(self, St, Lt):
+        B = St.shape[0]
+        if isinstance(Lt, LFBRows):
+            lt, rows, L = Lt.bank, Lt.rows, Lt.rows.shape[1]
+        else:
+            lt, rows, L = Lt.contiguous(), None, Lt.shape[1]
+        mask = None
+        if self.training and self.dropout.p > 0:
+            mask = (self.forced_mask if self.forced_mask is not None
+                    else self._rng.mask(B * 512, self.dropout.p, St).view(B, 512))
+        return NLBlockFn.apply(St, lt, rows, mask, L,
+                               self.linear1.weight, self.linear1.bias,
+                               self.linear2.weight, self.linear2.bias,
+                               self.linear3.weight, self.linear3.bias,
+                               self.layer_norm.weight, self.layer_norm.bias,
+                               self.linear4.weight, self.linear4.bias)

@@ -1,0 +1,388 @@
+"""Tensor-level wrappers over the libtmr C ABI.
+
+Every function takes CUDA(HIP) tensors, allocates outputs with torch's caching
+allocator (the library never allocates), passes raw pointers plus the current
+stream, and raises RuntimeError on a failed call.  No function here computes
+anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
+"""
+import torch
+
+from ._lib import call, query, stream_ptr, ConvDesc
+import ctypes
+
+f32 = torch.float32
+
+# Optional live instrumentation (bench.py): when a list, every conv launch appends
+# (kind, algorithmic_flops, start_event, end_event) recorded on the launching stream.
+PROF = None
+
+
+class _prof:
+    def __init__(self, kind, flops):
+        self.kind, self.flops = kind, flops
+
+    def __enter__(self):
+        if PROF is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *a):
+        if PROF is not None:
+            self.e1.record()
+            PROF.append((self.kind, self.flops, self.e0, self.e1))
+        return False
+
+
+def _req(t, name, dtype=f32):
+    if not t.is_cuda:
+        raise RuntimeError("%s must be a GPU tensor (libtmr has no CPU path)" % name)
+    if t.dtype != dtype:
+        raise RuntimeError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise RuntimeError("%s must be contiguous" % name)
+    return t
+
+
+def _empty(shape, like, dtype=f32):
+    return torch.empty(shape, dtype=dtype, device=like.device)
+
+
+# ----------------------------------------------------------------- conv / gemm
+def conv_desc(n, h, w, c, k, r, s, stride, pad):
+    ho = (h + 2 * pad - r) // stride + 1
+    wo = (w + 2 * pad - s) // stride + 1
+    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo)
+
+
+def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None):
+    """x (N,H,W,C) NHWC, w_krsc (K,R,S,C) -> y (N,Ho,Wo,K)."""
+    _req(x, "x"); _req(w_krsc, "w")
+    n, h, w, c = x.shape
+    k, r, s, c2 = w_krsc.shape
+    assert c == c2, (x.shape, w_krsc.shape)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    if out is None:
+        out = _empty((n, d.ho, d.wo, k), x)
+    with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c)):
+        call("tmr_conv2d_fwd", ctypes.byref(d), x, w_krsc, bias if bias is not None else None,
+             out, float(beta), stream_ptr())
+    return out
+
+
+def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0):
+    """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C)."""
+    _req(dy, "dy"); _req(w_krsc, "w")
+    n, ho, wo, k = dy.shape
+    k2, r, s, c = w_krsc.shape
+    h, w = in_hw
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
+    if out is None:
+        out = _empty((n, h, w, c), dy)
+    with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c):
+        call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
+    return out
+
+
+def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0):
+    """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW."""
+    _req(x, "x"); _req(dy, "dy")
+    n, h, w, c = x.shape
+    k = dy.shape[3]
+    c_real = c if c_real is None else c_real
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    assert (d.ho, d.wo) == tuple(dy.shape[1:3])
+    if out is None:
+        out = _empty((k, c_real, r, s), x)
+    ws_bytes = query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d))
+    ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
+    with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * c_real):
+        call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,
+             ctypes.c_size_t(ws.numel() * 4), stream_ptr())
+    return out
+
+
+def gemm_nt(a, b, bias=None, out=None, beta=0.0, M=None, N=None, K=None, lda=None, ldb=None,
+            ldc=None):
+    """out[M][N] = beta*out + a[M][K] @ b[N][K]^T (+bias)."""
+    M = a.shape[0] if M is None else M
+    K = a.shape[1] if K is None else K
+    N = b.shape[0] if N is None else N
+    lda = a.stride(0) if lda is None else lda
+    ldb = b.stride(0) if ldb is None else ldb
+    if out is None:
+        out = _empty((M, N), a)
+    ldc = out.stride(0) if ldc is None else ldc
+    call("tmr_gemm_nt", M, N, K, a, lda, b, ldb, bias, out, ldc, float(beta), stream_ptr())
+    return out
+
+
+def gemm_nn(a, b, out=None, beta=0.0, M=None, N=None, K=None, lda=None, ldb=None, ldc=None):
+    """out[M][N] = beta*out + a[M][K] @ b[K][N]."""
+    M = a.shape[0] if M is None else M
+    K = a.shape[1] if K is None else K
+    N = b.shape[1] if N is None else N
+    lda = a.stride(0) if lda is None else lda
+    ldb = b.stride(0) if ldb is None else ldb
+    if out is None:
+        out = _empty((M, N), a)
+    ldc = out.stride(0) if ldc is None else ldc
+    call("tmr_gemm_nn", M, N, K, a, lda, b, ldb, out, ldc, float(beta), stream_ptr())
+    return out
+
+
+def gemm_tn(a, b, out=None, beta=0.0, M=None, N=None, K=None, lda=None, ldb=None, ldc=None):
+    """out[M][N] = beta*out + a[K][M]^T @ b[K][N]."""
+    K = a.shape[0] if K is None else K
+    M = a.shape[1] if M is None else M
+    N = b.shape[1] if N is None else N
+    lda = a.stride(0) if lda is None else lda
+    ldb = b.stride(0) if ldb is None else ldb
+    if out is None:
+        out = _empty((M, N), a)
+    ldc = out.stride(0) if ldc is None else ldc
+    call("tmr_gemm_tn", M, N, K, a, lda, b, ldb, out, ldc, float(beta), stream_ptr())
+    return out
+
+
+def col_sum(x, rows, cols, ld, out=None, beta=0.0):
+    if out is None:
+        out = _empty((cols,), x)
+    call("tmr_col_sum", x, rows, cols, ld, out, float(beta), stream_ptr())
+    return out
+
+
+# --------------------------------------------------------------------- layout
+def weight_to_krsc(w, cpad=None):
+    k, c, r, s = w.shape
+    cpad = c if cpad is None else cpad
+    out = _empty((k, r, s, cpad), w)
+    call("tmr_weight_oihw_to_krsc", _req(w, "w"), out, k, c, r, s, cpad, stream_ptr())
+    return out
+
+
+def nchw_to_nhwc(x, cpad=None):
+    n, c, h, w = x.shape
+    cpad = c if cpad is None else cpad
+    out = _empty((n, h, w, cpad), x)
+    call("tmr_nchw_to_nhwc", _req(x, "x"), out, n, c, h, w, cpad, stream_ptr())
+    return out
+
+
+def nhwc_to_nchw(x, c=None):
+    n, h, w, cs = x.shape
+    c = cs if c is None else c
+    out = _empty((n, c, h, w), x)
+    call("tmr_nhwc_to_nchw", _req(x, "x"), out, n, c, cs, h, w, stream_ptr())
+    return out
+
+
+MEAN = (0.41757566, 0.26098573, 0.25888634)
+STD = (0.21938758, 0.1983, 0.19342837)
+
+
+def crop_normalize(frames_u8, offsets_i32, seq_len, crop=224, mean=MEAN, std=STD, out=None):
+    """frames (F,Hin,Win,3) uint8, offsets (F/seq,2) int32 (x1,y1) -> (F,crop,crop,4) fp32 NHWC4."""
+    _req(frames_u8, "frames", torch.uint8)
+    _req(offsets_i32, "offsets", torch.int32)
+    f, hin, win, _ = frames_u8.shape
+    if out is None:
+        out = _empty((f, crop, crop, 4), frames_u8)
+    call("tmr_crop_normalize", frames_u8, offsets_i32, out, f, hin, win, seq_len, crop,
+         *[float(v) for v in mean], *[float(v) for v in std], stream_ptr())
+    return out
+
+
+# ---------------------------------------------------------------- batch norm
+def _bn_ws(rows, c, device):
+    nb = query("tmr_bn_ws_bytes", rows, c)
+    return torch.empty((nb + 7) // 8, dtype=torch.float64, device=device), nb
+
+
+def bn_fwd_train(y2d, gamma, beta, running_mean, running_var, momentum, eps):
+    rows, c = y2d.shape
+    ws, nb = _bn_ws(rows, c, y2d.device)
+    mean = _empty((c,), y2d); inv = _empty((c,), y2d)
+    scale = _empty((c,), y2d); shift = _empty((c,), y2d)
+    call("tmr_bn_fwd_stats", y2d, rows, c, gamma, beta, running_mean, running_var,
+         float(momentum), float(eps), mean, inv, scale, shift, ws, ctypes.c_size_t(nb),
+         stream_ptr())
+    return mean, inv, scale, shift
+
+
+def bn_eval_params(gamma, beta, running_mean, running_var, eps):
+    c = running_mean.numel()
+    scale = _empty((c,), running_mean); shift = _empty((c,), running_mean)
+    call("tmr_bn_eval_params", gamma, beta, running_mean, running_var, float(eps), c, scale, shift,
+         stream_ptr())
+    return scale, shift
+
+
+def bn_apply(y, scale, shift, residual=None, relu=True, out=None):
+    c = y.shape[-1]
+    rows = y.numel() // c
+    if out is None:
+        out = torch.empty_like(y)
+    call("tmr_bn_apply", y, scale, shift, residual, out, rows, c, int(relu), stream_ptr())
+    return out
+
+
+def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None):
+    c = y.shape[-1]
+    rows = y.numel() // c
+    ws, nb = _bn_ws(rows, c, y.device)
+    dy = torch.empty_like(y)
+    dres = None
+    if want_dres:
+        dres = torch.empty_like(y) if dres_out is None else dres_out
+    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
+    call("tmr_bn_bwd", dz, y, z if relu else None, mean, inv, gamma, dy, dres, dgamma, dbeta,
+         rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
+    return dy, dres, dgamma, dbeta
+
+
+# ------------------------------------------------------------------- pooling
+def maxpool_fwd(x):
+    n, h, w, c = x.shape
+    ho = (h + 2 - 3) // 2 + 1
+    wo = (w + 2 - 3) // 2 + 1
+    y = _empty((n, ho, wo, c), x)
+    am = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
+    call("tmr_maxpool2d_fwd", x, y, am, n, h, w, c, ho, wo, stream_ptr())
+    return y, am
+
+
+def maxpool_bwd(dy, am, in_hw):
+    n, ho, wo, c = dy.shape
+    h, w = in_hw
+    dx = _empty((n, h, w, c), dy)
+    call("tmr_maxpool2d_bwd", dy, am, dx, n, h, w, c, ho, wo, stream_ptr())
+    return dx
+
+
+def avgpool_fwd(x):
+    n, h, w, c = x.shape
+    y = _empty((n, c), x)
+    call("tmr_avgpool_fwd", x, y, n, h * w, c, stream_ptr())
+    return y
+
+
+def avgpool_bwd(dy, hw):
+    n, c = dy.shape
+    h, w = hw
+    dx = _empty((n, h, w, c), dy)
+    call("tmr_avgpool_bwd", dy, dx, n, h * w, c, stream_ptr())
+    return dx
+
+
+# ----------------------------------------------------------------- head ops
+def dropout_mask(n, p, seed, offset, like):
+    m = _empty((n,), like)
+    call("tmr_dropout_mask", m, n, float(p), ctypes.c_uint64(seed), ctypes.c_uint64(offset),
+         stream_ptr())
+    return m
+
+
+def ce_sum(logits, labels, weight=None, gscale=1.0, want_grad=True):
+    b, k = logits.shape
+    loss = _empty((1,), logits)
+    dl = _empty((b, k), logits) if want_grad else None
+    preds = torch.empty((b,), dtype=torch.int64, device=logits.device)
+    call("tmr_ce_sum", _req(logits, "logits"), _req(labels, "labels", torch.int64), weight, b, k,
+         float(gscale), loss, dl, preds, stream_ptr())
+    return loss, dl, preds
+
+
+def sgd_step(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step):
+    call("tmr_sgd_step", p, g, buf, p.numel(), float(lr), float(momentum), float(dampening),
+         float(weight_decay), int(nesterov), int(first_step), stream_ptr())
+
+
+def lfb_index(valid_starts_i64, clip_starts_i64, L):
+    b = clip_starts_i64.numel()
+    rows = torch.empty((b, L), dtype=torch.int32, device=clip_starts_i64.device)
+    call("tmr_lfb_index", _req(valid_starts_i64, "valid_starts", torch.int64),
+         valid_starts_i64.numel(), _req(clip_starts_i64, "clip_starts", torch.int64), b, L, rows,
+         stream_ptr())
+    return rows
+
+
+def lfb_gather(bank, rows):
+    d = bank.shape[1]
+    out = _empty(tuple(rows.shape) + (d,), bank)
+    call("tmr_lfb_gather", _req(bank, "bank"), _req(rows, "rows", torch.int32), out, rows.numel(),
+         d, stream_ptr())
+    return out
+
+
+def layernorm_relu_fwd(x, gamma, beta, eps):
+    rows, d = x.shape
+    y = torch.empty_like(x)
+    mean = _empty((rows,), x); rstd = _empty((rows,), x)
+    call("tmr_layernorm_relu_fwd", x, gamma, beta, y, mean, rstd, rows, d, float(eps),
+         stream_ptr())
+    return y, mean, rstd
+
+
+def layernorm_relu_bwd(dy, x, y, gamma, mean, rstd):
+    rows, d = x.shape
+    dx = torch.empty_like(x)
+    dg = _empty((d,), x); db = _empty((d,), x)
+    call("tmr_layernorm_relu_bwd", dy, x, y, gamma, mean, rstd, dx, dg, db, rows, d,
+         stream_ptr())
+    return dx, dg, db
+
+
+def residual_mask(base, z, mask):
+    out = torch.empty_like(base)
+    call("tmr_residual_mask", base, z, mask, out, base.numel(), stream_ptr())
+    return out
+
+
+def mask_relu_fwd(h, mask):
+    a = torch.empty_like(h)
+    call("tmr_mask_relu_fwd", h, mask, a, h.numel(), stream_ptr())
+    return a
+
+
+def mask_relu_bwd(da, a, mask):
+    dh = torch.empty_like(da)
+    call("tmr_mask_relu_bwd", da, a, mask, dh, da.numel(), stream_ptr())
+    return dh
+
+
+def mul(a, b=None, scalar=None, out=None):
+    out = torch.empty_like(a) if out is None else out
+    call("tmr_mul", a, b, scalar, out, a.numel(), stream_ptr())
+    return out
+
+
+def nl_attn_fwd(lt, rows, u, B, L, scale):
+    d = u.shape[1]
+    p = _empty((B, L), u)
+    ctx = _empty((B, d), u)
+    call("tmr_nl_attn_fwd", lt, rows, u, p, ctx, B, L, d, float(scale), stream_ptr())
+    return p, ctx
+
+
+def nl_attn_bwd(lt, rows, u, p, dctx, B, L, scale, want_dlt):
+    d = u.shape[1]
+    ut = _empty((B, d), u)
+    dlt = _empty((B, L, d), u) if want_dlt else None
+    call("tmr_nl_attn_bwd", lt, rows, u, p, dctx, ut, dlt, B, L, d, float(scale), stream_ptr())
+    return ut, dlt
+
+
+def lstm_cell_fwd(gx_t, ghh, c_prev, h_t, c_t, act_t):
+    """gx_t (B,4H) row-strided view, h_t (B,H) row-strided view of y[:, t]."""
+    B, H = c_t.shape
+    call("tmr_lstm_cell_fwd", gx_t, gx_t.stride(0), ghh, c_prev, h_t, h_t.stride(0), c_t, act_t,
+         B, H, stream_ptr())
+
+
+def lstm_cell_bwd(dh_out_t, dh_rec, dc_next, act_t, c_t, c_prev, dg_t, dc_prev):
+    B, H = c_t.shape
+    call("tmr_lstm_cell_bwd", dh_out_t, dh_out_t.stride(0), dh_rec, dc_next, act_t, c_t, c_prev,
+         dg_t, dg_t.stride(0), dc_prev, B, H, stream_ptr())

@@ -1,0 +1,219 @@
+"""ResNet-50 frame encoder (`share`) on libtmr's NHWC implicit-GEMM kernels.
+
+Drop-in for the `share` nn.Sequential of the reference's inline TMRNet model
+(code/Training TMRNet/train_only_non-local_pretrained.py:204-214, built from
+torchvision resnet50): same child names (conv1, bn1, relu, maxpool,
+layer1..4, avgpool), same Bottleneck sub-module names and therefore identical
+``state_dict`` keys ("share.layer1.0.conv1.weight", "share.bn1.running_mean",
+...).  nn.Conv2d / nn.BatchNorm2d modules are kept as parameter/buffer
+containers only (their torch forward is never called); the whole trunk runs
+as ONE autograd node (`TrunkFn`) that keeps activations NHWC in HBM and drives
+conv -> BN(batch stats) -> ReLU(+residual) on the HIP kernels, with the
+backward pass (BN backward, dgrad, wgrad) in reverse layer order.
+
+BN semantics follow nn.BatchNorm2d in train mode: batch mean / biased variance
+for normalisation, running stats updated with momentum and the unbiased
+variance, num_batches_tracked += 1; eval mode uses running stats.
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+class Bottleneck(nn.Module):
+    """torchvision v1.5 Bottleneck (stride on the 3x3) as a parameter container."""
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+
+def _make_layer(inplanes, planes, blocks, stride):
+    downsample = None
+    if stride != 1 or inplanes != planes * 4:
+        downsample = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False),
+                                   nn.BatchNorm2d(planes * 4))
+    layers = [Bottleneck(inplanes, planes, stride, downsample)]
+    for _ in range(1, blocks):
+        layers.append(Bottleneck(planes * 4, planes))
+    return nn.Sequential(*layers)
+
+
+# --------------------------------------------------------------------- engine
+def _bn_momentum(bn):
+    if bn.momentum is None:
+        raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative average) is not supported")
+    return bn.momentum
+
+
+def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None):
+    """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z."""
+    w = conv.weight
+    k, c, r, s = w.shape
+    cs = x.shape[3]
+    if r == 1 and s == 1 and c == cs:
+        wk = w.detach().contiguous()          # OIHW == KRSC for 1x1
+    else:
+        wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs)
+    y = ops.conv_fwd(x, wk, stride, pad, c_real=c)
+    y2 = y.view(-1, k)
+    if training:
+        mean, inv, scale, shift = ops.bn_fwd_train(
+            y2, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var,
+            _bn_momentum(bn), bn.eps)
+        bn.num_batches_tracked.add_(1)
+    else:
+        mean = inv = None
+        scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                          bn.running_var, bn.eps)
+    z = ops.bn_apply(y, scale, shift, residual, relu)
+    if recs is not None:
+        recs.append({"x": x, "wk": wk, "y": y, "z": z, "mean": mean, "inv": inv,
+                     "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
+                     "c_real": c})
+    return z
+
+
+def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True):
+    conv, bn = rec["conv"], rec["bn"]
+    dy, dres, dg, db = ops.bn_bwd(dz, rec["y"], rec["z"], rec["mean"], rec["inv"],
+                                  bn.weight.detach(), rec["relu"], want_dres=want_dres)
+    grads[bn.weight] = dg
+    grads[bn.bias] = db
+    x = rec["x"]
+    k, c, r, s = conv.weight.shape
+    grads[conv.weight] = ops.conv_wgrad(x, dy, r, s, rec["stride"], rec["pad"],
+                                        c_real=rec["c_real"])
+    dx = None
+    if need_dx:
+        dx = ops.conv_dgrad(dy, rec["wk"], (x.shape[1], x.shape[2]), rec["stride"], rec["pad"],
+                            out=dx_out, beta=dx_beta)
+    return dx, dres
+
+
+class TrunkFn(torch.autograd.Function):
+    """Whole ResNet-50 trunk as one autograd node: x NHWC4 (F,224,224,4) -> (F,2048)."""
+
+    @staticmethod
+    def forward(ctx, x4, share, *params):
+        training = share.training
+        keep = training and torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        recs = [] if keep else None
+        conv1, bn1, layers = share.trunk_parts()
+        z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs)
+        p, am = ops.maxpool_fwd(z)
+        stem_hw = (z.shape[1], z.shape[2])
+        h = p
+        blocks = []
+        for layer in layers:
+            for blk in layer:
+                brec = [] if keep else None
+                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec)
+                z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec)
+                if blk.downsample is not None:
+                    idn = _conv_bn(h, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
+                                   training, recs=brec)
+                else:
+                    idn = h
+                h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, residual=idn,
+                             recs=brec)
+                blocks.append((blk, brec))
+        feat = ops.avgpool_fwd(h)
+        ctx.keep = keep
+        if keep:
+            ctx.share = share
+            ctx.params = params
+            ctx.stem = recs
+            ctx.pool = (am, stem_hw)
+            ctx.blocks = blocks
+            ctx.last_hw = (h.shape[1], h.shape[2])
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        if not ctx.keep:
+            raise RuntimeError("trunk backward needs train mode and a forward with grad enabled")
+        grads = {}
+        dh = ops.avgpool_bwd(dfeat.contiguous(), ctx.last_hw)
+        blocks = ctx.blocks
+        while blocks:
+            blk, brec = blocks.pop()
+            has_ds = blk.downsample is not None
+            r1, r2 = brec[0], brec[1]
+            rd = brec[2] if has_ds else None
+            r3 = brec[-1]
+            dz2, dres = _conv_bn_bwd(r3, dh, grads, want_dres=True)
+            dz1, _ = _conv_bn_bwd(r2, dz2, grads)
+            del dz2
+            if has_ds:
+                dx, _ = _conv_bn_bwd(r1, dz1, grads)
+                _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0)
+            else:
+                dx, _ = _conv_bn_bwd(r1, dz1, grads, dx_out=dres, dx_beta=1.0)
+            del dz1, brec
+            dh = dx
+        am, stem_hw = ctx.pool
+        dz = ops.maxpool_bwd(dh, am, stem_hw)
+        _conv_bn_bwd(ctx.stem[0], dz, grads, need_dx=False)
+        out = [grads.get(p) for p in ctx.params]
+        ctx.blocks = ctx.stem = None
+        return (None, None) + tuple(out)
+
+
+_CHILD_NAMES = ("conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4",
+                "avgpool")
+
+
+class ResNet50Share(nn.Sequential):
+    """The reference's `share` Sequential (keys identical to torchvision's resnet50 children).
+
+    ``indexed=True`` names the children "0".."8" instead, which is the
+    ``Sequential(*list(resnet50().children())[:-1])`` layout of code/models.py:26-28
+    (keys ``res.0.weight``, ``res.4.0.conv1.weight``, ...).
+    """
+
+    def __init__(self, indexed=False):
+        super().__init__()
+        mods = (nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64),
+                nn.ReLU(inplace=True), nn.MaxPool2d(3, stride=2, padding=1),
+                _make_layer(64, 64, 3, 1), _make_layer(256, 128, 4, 2),
+                _make_layer(512, 256, 6, 2), _make_layer(1024, 512, 3, 2),
+                nn.AdaptiveAvgPool2d((1, 1)))
+        for i, (name, m) in enumerate(zip(_CHILD_NAMES, mods)):
+            self.add_module(str(i) if indexed else name, m)
+        # torchvision init: kaiming_normal fan_out for convs, BN gamma=1 beta=0
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def trunk_parts(self):
+        ch = list(self.children())
+        return ch[0], ch[1], ch[4:8]
+
+    def features_nhwc4(self, x4):
+        """x4: (F,224,224,4) fp32 NHWC, 4th channel zero -> (F,2048)."""
+        return TrunkFn.apply(x4, self, *self.parameters())
+
+    def forward(self, x):
+        """x: (F,3,224,224) fp32 NCHW (reference layout) -> (F,2048,1,1)."""
+        x = x.reshape(-1, 3, x.shape[-2], x.shape[-1]).contiguous()
+        x4 = ops.nchw_to_nhwc(x, cpad=4)
+        feat = self.features_nhwc4(x4)
+        return feat.view(feat.shape[0], feat.shape[1], 1, 1)
+
+
+def resnet50_share():
+    return ResNet50Share()
