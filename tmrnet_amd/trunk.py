@@ -62,7 +62,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None)
     k, c, r, s = w.shape
     cs = x.shape[3]
     if r == 1 and s == 1 and c == cs:
-        wk = w.detach().contiguous()          # OIHW == KRSC for 1x1
+        wk = w.detach().contiguous().view(k, 1, 1, c)   # OIHW == KRSC for 1x1
     else:
         wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs)
     y = ops.conv_fwd(x, wk, stride, pad, c_real=c)
