@@ -105,9 +105,9 @@ class TrunkFn(torch.autograd.Function):
     """Whole ResNet-50 trunk as one autograd node: x NHWC4 (F,224,224,4) -> (F,2048)."""
 
     @staticmethod
-    def forward(ctx, x4, share, *params):
+    def forward(ctx, x4, share, keep, *params):
         training = share.training
-        keep = training and torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        keep = keep and training
         recs = [] if keep else None
         conv1, bn1, layers = share.trunk_parts()
         z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs)
@@ -167,7 +167,7 @@ class TrunkFn(torch.autograd.Function):
         _conv_bn_bwd(ctx.stem[0], dz, grads, need_dx=False)
         out = [grads.get(p) for p in ctx.params]
         ctx.blocks = ctx.stem = None
-        return (None, None) + tuple(out)
+        return (None, None, None) + tuple(out)
 
 
 _CHILD_NAMES = ("conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4",
@@ -205,7 +205,10 @@ class ResNet50Share(nn.Sequential):
 
     def features_nhwc4(self, x4):
         """x4: (F,224,224,4) fp32 NHWC, 4th channel zero -> (F,2048)."""
-        return TrunkFn.apply(x4, self, *self.parameters())
+        params = list(self.parameters())
+        # grad mode is off inside autograd.Function.forward: decide here whether to save
+        keep = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        return TrunkFn.apply(x4, self, keep, *params)
 
     def forward(self, x):
         """x: (F,3,224,224) fp32 NCHW (reference layout) -> (F,2048,1,1)."""
