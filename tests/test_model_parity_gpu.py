@@ -76,6 +76,24 @@ def _make_pair(dev, seq_len, seed=0):
     return m, r
 
 
+def _double_copy(r, masks, B, T, L):
+    import copy
+    m64 = copy.deepcopy(r).double()
+    m64.load_state_dict({k: v.double() if v.is_floating_point() else v
+                         for k, v in r.state_dict().items()})
+    # running stats were already updated by r's forward: restore the pre-forward values
+    for (n, b) in m64.named_buffers():
+        if n.endswith("running_mean"):
+            b.zero_()
+        elif n.endswith("running_var"):
+            b.fill_(1.0)
+        elif n.endswith("num_batches_tracked"):
+            b.zero_()
+    for p in m64.parameters():
+        p.grad = None
+    return m64
+
+
 def _inputs(B, T, L, seed=1):
     g = torch.Generator().manual_seed(seed)
     frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8)
@@ -113,12 +131,17 @@ def test_tmrnet_step_parity(dev, train):
     assert abs(loss.item() - loss_r.item()) <= 1e-4 * max(1.0, abs(loss_r.item()))
     loss.backward()
     loss_r.backward()
+    # float64 oracle: the fp32 CPU oracle's own rounding error sets the scale for the HIP path's
+    m64 = _double_copy(r, masks, B, T, L)
+    out64 = m64(x_ref.double().view(B, T, 3, 224, 224), lt.double(),
+                masks={k: v.double() for k, v in masks.items()})
+    ref.ce_sum_ref(out64, labels).backward()
     rp = dict(r.named_parameters())
-    worst = []
+    p64 = dict(m64.named_parameters())
     for name, p in m.named_parameters():
-        e = rel_err(p.grad, rp[name].grad)
-        worst.append((e, name))
-        assert e < 5e-3, (name, e)
+        e_hip = rel_err(p.grad, p64[name].grad)
+        e_cpu = rel_err(rp[name].grad, p64[name].grad)
+        assert e_hip < max(2e-3, 4 * e_cpu), (name, e_hip, e_cpu)
     # running statistics after one train-mode forward
     rb = dict(r.named_buffers())
     for name, b in m.named_buffers():
