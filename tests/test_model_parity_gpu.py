@@ -136,12 +136,8 @@ def test_tmrnet_step_parity(dev, train):
     out64 = m64(x_ref.double().view(B, T, 3, 224, 224), lt.double(),
                 masks={k: v.double() for k, v in masks.items()})
     ref.ce_sum_ref(out64, labels).backward()
-    rp = dict(r.named_parameters())
-    p64 = dict(m64.named_parameters())
-    for name, p in m.named_parameters():
-        e_hip = rel_err(p.grad, p64[name].grad)
-        e_cpu = rel_err(rp[name].grad, p64[name].grad)
-        assert e_hip < max(2e-3, 4 * e_cpu), (name, e_hip, e_cpu)
+    g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
+    _assert_vs_fp64(g(m), g(r), g(m64), 2e-3, "grad")
     # running statistics after one train-mode forward
     rb = dict(r.named_buffers())
     for name, b in m.named_buffers():
@@ -151,12 +147,21 @@ def test_tmrnet_step_parity(dev, train):
             assert torch.equal(b.cpu(), rb[name]), name
 
 
+def l2_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
 def _assert_vs_fp64(ours, ref32, ref64, floor, what):
-    """HIP result no further from the float64 oracle than 4x the fp32 CPU oracle is (or floor)."""
+    """HIP result no further (relative L2) from the float64 oracle than 3x the fp32 CPU oracle
+    is, or `floor`.  At random init with a handful of frames per BN batch the trunk gradients
+    are ill-conditioned: the fp32 CPU oracle itself is ~2% (L2) away from float64 there, so a
+    fixed tight tolerance against the fp32 oracle would test rounding noise, not correctness."""
     for name, t in ours.items():
-        e_hip = rel_err(t, ref64[name])
-        e_cpu = rel_err(ref32[name], ref64[name])
-        assert e_hip < max(floor, 4 * e_cpu), (what, name, e_hip, e_cpu)
+        e_hip = l2_err(t, ref64[name])
+        e_cpu = l2_err(ref32[name], ref64[name])
+        assert e_hip < max(floor, 3 * e_cpu), (what, name, e_hip, e_cpu)
 
 
 def test_sgd_step_after_backward_parity(dev):
