@@ -1,0 +1,12 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of a short bench run (no PMC here: counters go in their own pass)
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/${PROF_NAME:-prof}
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
+  python3 "$R/bench.py" --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$OUT/bench.log" 2>&1
+rc=$?
+echo "rocprof rc=$rc"; tail -2 "$OUT/bench.log"
+find "$OUT" -name "*stats*" | head
+exit $rc
