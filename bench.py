@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--lfb", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--conv-table", action="store_true", help="per-launch conv table on stderr")
     ap.add_argument("--cpu-clips", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=2)
     return ap.parse_args()
@@ -139,11 +140,16 @@ def main():
         step(i)
         torch.cuda.synchronize()
         recs, ops.PROF = ops.PROF, None
-        tot_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in recs)
-        tot_flops = sum(f for _, f, _, _ in recs)
+        tot_ms = sum(r[2].elapsed_time(r[3]) for r in recs)
+        tot_flops = sum(r[1] for r in recs)
+        if args.conv_table and rank == 0:
+            for kind, f, e0, e1, shp in recs:
+                t = e0.elapsed_time(e1)
+                print("%-10s %-34s %8.3f ms %7.1f TF" % (kind, shp, t, f / (t * 1e-3) / 1e12),
+                      file=sys.stderr)
         achieved = tot_flops / (tot_ms * 1e-3) / 1e12
         per_kind = {}
-        for kind, f, e0, e1 in recs:
+        for kind, f, e0, e1, _ in recs:
             a = per_kind.setdefault(kind, [0, 0.0, 0.0])
             a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
         roof = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, f32 MFMA)",

@@ -18,8 +18,8 @@ PROF = None
 
 
 class _prof:
-    def __init__(self, kind, flops):
-        self.kind, self.flops = kind, flops
+    def __init__(self, kind, flops, shape=None):
+        self.kind, self.flops, self.shape = kind, flops, shape
 
     def __enter__(self):
         if PROF is not None:
@@ -31,7 +31,7 @@ class _prof:
     def __exit__(self, *a):
         if PROF is not None:
             self.e1.record()
-            PROF.append((self.kind, self.flops, self.e0, self.e1))
+            PROF.append((self.kind, self.flops, self.e0, self.e1, self.shape))
         return False
 
 
@@ -65,7 +65,8 @@ def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None)
     d = conv_desc(n, h, w, c, k, r, s, stride, pad)
     if out is None:
         out = _empty((n, d.ho, d.wo, k), x)
-    with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c)):
+    with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
+               (n, h, w, c, k, r, stride)):
         call("tmr_conv2d_fwd", ctypes.byref(d), x, w_krsc, bias if bias is not None else None,
              out, float(beta), stream_ptr())
     return out
@@ -81,7 +82,7 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0):
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
-    with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c):
+    with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride)):
         call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
     return out
 
@@ -98,7 +99,8 @@ def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0):
         out = _empty((k, c_real, r, s), x)
     ws_bytes = query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d))
     ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
-    with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * c_real):
+    with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * c_real,
+               (n, h, w, c, k, r, stride)):
         call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,
              ctypes.c_size_t(ws.numel() * 4), stream_ptr())
     return out
