@@ -1,0 +1,89 @@
+"""Microbenchmark of the implicit-GEMM conv kernels on every distinct ResNet-50 conv shape
+(F frames), weighted by how often each shape occurs in one train step.
+
+usage: python scripts/convbench.py [--frames 640] [--reps 5] [--kinds fwd,dgrad,wgrad]
+Env TMR_GEMM_CFG=<i> forces a tile config (experiments; see gemm_conv.hip kCfgs).
+"""
+import argparse
+import json
+import os
+import sys
+from collections import Counter
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tmrnet_amd import ops  # noqa: E402
+
+
+def resnet50_convs(F):
+    """(n, h, w, cin, cout, r, stride, pad) of every conv in the trunk, in order."""
+    out = [(F, 224, 224, 3, 64, 7, 2, 3)]
+    h, cin = 56, 64
+    for planes, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            out.append((F, h, h, cin, planes, 1, 1, 0))
+            out.append((F, h, h, planes, planes, 3, s, 1))
+            ho = h // s
+            out.append((F, ho, ho, planes, planes * 4, 1, 1, 0))
+            if b == 0:
+                out.append((F, h, h, cin, planes * 4, 1, s, 0))
+            cin, h = planes * 4, ho
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=640)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    shapes = Counter(resnet50_convs(args.frames))
+    kinds = args.kinds.split(",")
+    res = []
+    tot = {k: [0.0, 0.0] for k in kinds}
+    for shp, cnt in shapes.items():
+        n, h, w, cin, cout, r, st, pad = shp
+        cs = 4 if cin == 3 else cin
+        x = torch.randn(n, h, w, cs, device=dev)
+        wk = torch.randn(cout, r, r, cs, device=dev)
+        y = ops.conv_fwd(x, wk, st, pad)
+        dy = torch.randn_like(y)
+        for kind in kinds:
+            if kind == "dgrad" and cin == 3:
+                continue
+            fn = {"fwd": lambda: ops.conv_fwd(x, wk, st, pad, out=y),
+                  "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x),
+                  "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin)}[kind]
+            fn()
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            flops = 2.0 * n * y.shape[1] * y.shape[2] * cout * r * r * cin
+            tf = flops / (ms * 1e-3) / 1e12
+            res.append({"kind": kind, "shape": shp, "count": cnt, "ms": ms, "tflops": tf})
+            tot[kind][0] += ms * cnt
+            tot[kind][1] += flops * cnt
+            print("%-6s %-34s x%d %8.3f ms %7.1f TF" % (kind, shp, cnt, ms, tf), flush=True)
+    allms = sum(v[0] for v in tot.values())
+    allf = sum(v[1] for v in tot.values())
+    summ = {k: {"ms": round(v[0], 2), "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 1)}
+            for k, v in tot.items()}
+    print("TOTAL per step: %.2f ms, %.1f TF  %s  cfg=%s" % (allms, allf / (allms * 1e-3) / 1e12,
+                                                            json.dumps(summ),
+                                                            os.environ.get("TMR_GEMM_CFG", "auto")))
+    if args.json:
+        json.dump({"rows": res, "summary": summ, "total_ms": allms}, open(args.json, "w"))
+
+
+if __name__ == "__main__":
+    main()

@@ -22,11 +22,11 @@
 // conflict-free ds_read_b32 of 32 consecutive floats per half-wave.
 #include "common.h"
 #include "tmr.h"
+#include <stdlib.h>
 
 namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
-constexpr int BK = 16;
 constexpr int NT = 256;
 
 struct GemmArgs {
@@ -112,13 +112,15 @@ __device__ __forceinline__ float4 ld4(const float* p, int valid_elems) {
   }
 }
 
-template <int MODE, int BM, int BN, int WM, bool AL>
+template <int MODE, int BM, int BN, int WM, int BK, bool AL>
 __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
-  constexpr int RA = BM / 64;  // float4 loads per thread per k-tile for A
-  constexpr int RB = BN / 64;
+  constexpr int KQ = BK / 4;             // float4 per row of a K-contiguous tile
+  constexpr int RA = BM * BK / 1024;     // float4 loads per thread per k-tile for A
+  constexpr int RB = BN * BK / 1024;
+  static_assert(RA >= 1 && RB >= 1, "tile too small for 256 threads");
   // A tile k-major [BK][LDA]; K-contiguous loaders scatter 4 scalars -> pad 2,
   // M/N-contiguous loaders write float4 -> pad 4.
   constexpr bool A_KC = (MODE != MODE_WGRAD);
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
   RowGeo ga[RA];
   if (A_KC) {
 #pragma unroll
-    for (int q = 0; q < RA; ++q) ga[q] = row_geo(a, m0 + (tid >> 2) + 64 * q, a.M);
+    for (int q = 0; q < RA; ++q) ga[q] = row_geo(a, m0 + (tid + NT * q) / KQ, a.M);
   }
 
   float4 ra[RA], rb[RB];
@@ -171,9 +173,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
     const int kb = kbeg + kt * BK;
     // ---- A ----
     if (A_KC) {
-      const int k = kb + (tid & 3) * 4;
 #pragma unroll
       for (int q = 0; q < RA; ++q) {
+        const int k = kb + ((tid + NT * q) % KQ) * 4;
         const float* p = (k < kend) ? gather_ptr(a, a.A, ga[q], k) : nullptr;
         ra[q] = p ? ld4<AL>(p, kend - k) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -189,10 +191,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
     }
     // ---- B ----
     if (MODE == MODE_FWD) {  // B[j][k], k contiguous
-      const int k = kb + (tid & 3) * 4;
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
-        const int j = n0 + (tid >> 2) + 64 * q;
+        const int lin = tid + NT * q;
+        const int j = n0 + lin / KQ;
+        const int k = kb + (lin % KQ) * 4;
         bool ok = (j < a.N) && (k < kend);
         rb[q] = ok ? ld4<AL>(a.B + (long)j * a.ldb + k, kend - k) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -236,10 +239,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
     float* As = As0 + buf * BK * LDA;
     float* Bs = Bs0 + buf * BK * LDB;
     if (A_KC) {
-      const int kq = (tid & 3) * 4;
 #pragma unroll
       for (int q = 0; q < RA; ++q) {
-        const int row = (tid >> 2) + 64 * q;
+        const int lin = tid + NT * q;
+        const int row = lin / KQ, kq = (lin % KQ) * 4;
         As[(kq + 0) * LDA + row] = ra[q].x;
         As[(kq + 1) * LDA + row] = ra[q].y;
         As[(kq + 2) * LDA + row] = ra[q].z;
@@ -254,10 +257,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
       }
     }
     if (B_KC) {
-      const int kq = (tid & 3) * 4;
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
-        const int row = (tid >> 2) + 64 * q;
+        const int lin = tid + NT * q;
+        const int row = lin / KQ, kq = (lin % KQ) * 4;
         Bs[(kq + 0) * LDB + row] = rb[q].x;
         Bs[(kq + 1) * LDB + row] = rb[q].y;
         Bs[(kq + 2) * LDB + row] = rb[q].z;
@@ -315,35 +318,54 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
   // ---- epilogue ----
   float* Cb = a.C;
   if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
+  const int col0 = n0 + wn * (BN / WN) + l31;
+  // output row offset for accumulator register r of row-tile i (-1: outside M)
+  auto row_off = [&](int i, int r) -> long {
+    const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    if (row >= a.M) return -1;
+    if (MODE == MODE_DGRAD && a.osy != 0) {
+      uint32_t n = fdiv((uint32_t)row, a.dHW);
+      uint32_t rem = row - n * a.dHW.d;
+      uint32_t y = fdiv(rem, a.dW);
+      uint32_t x = rem - y * a.dW.d;
+      long pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
+      return pix * a.ldc;
+    }
+    return (long)row * a.ldc;
+  };
+  // (1) all reads of the old output first (beta), so they are issued back to back
+  if (a.beta != 0.f) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long ro = row_off(i, r);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = col0 + 32 * j;
+          if (ro >= 0 && col < a.N) acc[i][j][r] += a.beta * Cb[ro + col];
+        }
+      }
+  }
+  // (2) bias + stores
+  float bvals[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col0 + 32 * j;
+    bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      if (row >= a.M) continue;
-      long rbase;
-      if (MODE == MODE_DGRAD && a.osy != 0) {
-        uint32_t n = fdiv((uint32_t)row, a.dHW);
-        uint32_t rem = row - n * a.dHW.d;
-        uint32_t y = fdiv(rem, a.dW);
-        uint32_t x = rem - y * a.dW.d;
-        long pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
-        rbase = pix * a.ldc;
-      } else {
-        rbase = (long)row * a.ldc;
-      }
+      const long ro = row_off(i, r);
+      if (ro < 0) continue;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * (BN / WN) + 32 * j + l31;
-        if (col >= a.N) continue;
-        float v = acc[i][j][r];
-        if (MODE == MODE_FWD && a.bias) v += a.bias[col];
-        float* cp = Cb + rbase + col;
-        if (a.beta != 0.f) v += a.beta * *cp;
-        *cp = v;
+        const int col = col0 + 32 * j;
+        if (col < a.N) Cb[ro + col] = acc[i][j][r] + bvals[j];
       }
     }
-  }
 }
 
 // WGRAD split reduction: dW[co][tap][c] (KRSC with c < creal) summed over splits in
@@ -366,33 +388,56 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit,
   }
 }
 
-template <int MODE, int BM, int BN, int WM>
+template <int MODE, int BM, int BN, int WM, int BKT>
 int launch_cfg(const GemmArgs& a, bool al, dim3 grid, hipStream_t st) {
   if (al)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, true>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, BKT, true>), grid, dim3(NT), 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, false>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, BKT, false>), grid, dim3(NT), 0, st, a);
   TMR_CHECK_LAUNCH("gemm_kernel");
   return 0;
 }
 
-// Tile selection: keep both tile dims useful; prefer 128x128.
+// Tile configurations (BM, BN, WM, BK).  Selection keeps both tile dims useful.
+struct TileCfg { int bm, bn; };
+constexpr TileCfg kCfgs[] = {{128, 128}, {256, 64}, {64, 256}, {64, 64},
+                             {128, 128}, {256, 64}, {64, 256}, {256, 128}, {128, 256}};
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+int pick_cfg(long M, long N) {
+  static const int forced = env_int("TMR_GEMM_CFG", -1);  // experiments only
+  if (forced >= 0) {
+    if (forced <= 3 || forced == 7 || forced == 8 || (forced >= 4 && forced <= 6)) {
+      const TileCfg c = kCfgs[forced];
+      if (M >= c.bm / 2 && N >= c.bn / 2) return forced;
+    }
+  }
+  if (N <= 64 && M >= 256) return 1;
+  if (M <= 64 && N >= 256) return 2;
+  if (M <= 64 || N <= 64) return 3;
+  return 0;
+}
+
 template <int MODE>
 int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
-  const long M = a.M, N = a.N;
-  int cfg;  // 0: 128x128, 1: 256x64, 2: 64x256, 3: 64x64
-  if (N <= 64 && M >= 256) cfg = 1;
-  else if (M <= 64 && N >= 256) cfg = 2;
-  else if (M <= 64 || N <= 64) cfg = 3;
-  else cfg = 0;
-  const int BMs[4] = {128, 256, 64, 64}, BNs[4] = {128, 64, 256, 64};
-  dim3 grid(cdiv(M, BMs[cfg]) * cdiv(N, BNs[cfg]), splits, 1);
+  const int cfg = pick_cfg(a.M, a.N);
+  const TileCfg c = kCfgs[cfg];
+  dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   switch (cfg) {
-    case 0: return launch_cfg<MODE, 128, 128, 2>(a, al, grid, st);
-    case 1: return launch_cfg<MODE, 256, 64, 4>(a, al, grid, st);
-    case 2: return launch_cfg<MODE, 64, 256, 1>(a, al, grid, st);
-    default: return launch_cfg<MODE, 64, 64, 2>(a, al, grid, st);
+    case 0: return launch_cfg<MODE, 128, 128, 2, 16>(a, al, grid, st);
+    case 1: return launch_cfg<MODE, 256, 64, 4, 16>(a, al, grid, st);
+    case 2: return launch_cfg<MODE, 64, 256, 1, 16>(a, al, grid, st);
+    case 3: return launch_cfg<MODE, 64, 64, 2, 16>(a, al, grid, st);
+    case 4: return launch_cfg<MODE, 128, 128, 2, 32>(a, al, grid, st);
+    case 5: return launch_cfg<MODE, 256, 64, 4, 32>(a, al, grid, st);
+    case 6: return launch_cfg<MODE, 64, 256, 1, 32>(a, al, grid, st);
+    case 7: return launch_cfg<MODE, 256, 128, 2, 16>(a, al, grid, st);
+    default: return launch_cfg<MODE, 128, 256, 2, 16>(a, al, grid, st);
   }
 }
 
@@ -497,7 +542,7 @@ static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* sl
   if (maxsp < 1) maxsp = 1;
   if (sp > maxsp) sp = maxsp;
   long kc = (Mred + sp - 1) / sp;
-  kc = (kc + BK - 1) / BK * BK;
+  kc = (kc + 31) / 32 * 32;  // multiple of every BK
   sp = (Mred + kc - 1) / kc;
   *splits = (int)sp;
   *kchunk = (int)kc;
