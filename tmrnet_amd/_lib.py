@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtmr.so")
+LIB_PATH = os.environ.get("TMR_LIB_PATH") or os.path.join(_HERE, "libtmr.so")  # override: experiments
 
 P = ctypes.c_void_p
 I = ctypes.c_int

@@ -27,7 +27,14 @@
 namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
-constexpr int NT = 256;
+#ifndef TMR_GEMM_WAVES
+#define TMR_GEMM_WAVES 3
+#endif
+#if TMR_GEMM_WAVES > 0
+#define TMR_GEMM_LB __launch_bounds__(64 * WM * WN, TMR_GEMM_WAVES)
+#else
+#define TMR_GEMM_LB __launch_bounds__(64 * WM * WN)
+#endif
 
 struct GemmArgs {
   const float* A;
@@ -112,14 +119,14 @@ __device__ __forceinline__ float4 ld4(const float* p, int valid_elems) {
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int BK, bool AL>
-__global__ __launch_bounds__(NT) void gemm_kernel(const GemmArgs a) {
-  constexpr int WN = 4 / WM;
+template <int MODE, int BM, int BN, int WM, int WN, int BK, bool AL>
+__global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
+  constexpr int NT = 64 * WM * WN;       // threads per workgroup
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   constexpr int KQ = BK / 4;             // float4 per row of a K-contiguous tile
-  constexpr int RA = BM * BK / 1024;     // float4 loads per thread per k-tile for A
-  constexpr int RB = BN * BK / 1024;
+  constexpr int RA = BM * BK / (4 * NT); // float4 loads per thread per k-tile for A
+  constexpr int RB = BN * BK / (4 * NT);
   static_assert(RA >= 1 && RB >= 1, "tile too small for 256 threads");
   // A tile k-major [BK][LDA]; K-contiguous loaders scatter 4 scalars -> pad 2,
   // M/N-contiguous loaders write float4 -> pad 4.
@@ -388,20 +395,21 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit,
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int BKT>
+template <int MODE, int BM, int BN, int WM, int WN, int BKT>
 int launch_cfg(const GemmArgs& a, bool al, dim3 grid, hipStream_t st) {
   if (al)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, BKT, true>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, true>), grid, dim3(64 * WM * WN), 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, BKT, false>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, false>), grid, dim3(64 * WM * WN), 0, st, a);
   TMR_CHECK_LAUNCH("gemm_kernel");
   return 0;
 }
 
-// Tile configurations (BM, BN, WM, BK).  Selection keeps both tile dims useful.
+// Tile configurations (BM, BN).  Selection keeps both tile dims useful.
 struct TileCfg { int bm, bn; };
 constexpr TileCfg kCfgs[] = {{128, 128}, {256, 64}, {64, 256}, {64, 64},
-                             {128, 128}, {256, 64}, {64, 256}, {256, 128}, {128, 256}};
+                             {256, 128}, {128, 256}, {256, 256}};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
@@ -410,11 +418,9 @@ int env_int(const char* name, int dflt) {
 
 int pick_cfg(long M, long N) {
   static const int forced = env_int("TMR_GEMM_CFG", -1);  // experiments only
-  if (forced >= 0) {
-    if (forced <= 3 || forced == 7 || forced == 8 || (forced >= 4 && forced <= 6)) {
-      const TileCfg c = kCfgs[forced];
-      if (M >= c.bm / 2 && N >= c.bn / 2) return forced;
-    }
+  if (forced >= 0 && forced < kNumCfgs) {
+    const TileCfg c = kCfgs[forced];
+    if (M >= c.bm && N >= c.bn) return forced;
   }
   if (N <= 64 && M >= 256) return 1;
   if (M <= 64 && N >= 256) return 2;
@@ -429,15 +435,13 @@ int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   switch (cfg) {
-    case 0: return launch_cfg<MODE, 128, 128, 2, 16>(a, al, grid, st);
-    case 1: return launch_cfg<MODE, 256, 64, 4, 16>(a, al, grid, st);
-    case 2: return launch_cfg<MODE, 64, 256, 1, 16>(a, al, grid, st);
-    case 3: return launch_cfg<MODE, 64, 64, 2, 16>(a, al, grid, st);
-    case 4: return launch_cfg<MODE, 128, 128, 2, 32>(a, al, grid, st);
-    case 5: return launch_cfg<MODE, 256, 64, 4, 32>(a, al, grid, st);
-    case 6: return launch_cfg<MODE, 64, 256, 1, 32>(a, al, grid, st);
-    case 7: return launch_cfg<MODE, 256, 128, 2, 16>(a, al, grid, st);
-    default: return launch_cfg<MODE, 128, 256, 2, 16>(a, al, grid, st);
+    case 0: return launch_cfg<MODE, 128, 128, 2, 2, 16>(a, al, grid, st);
+    case 1: return launch_cfg<MODE, 256, 64, 4, 1, 16>(a, al, grid, st);
+    case 2: return launch_cfg<MODE, 64, 256, 1, 4, 16>(a, al, grid, st);
+    case 3: return launch_cfg<MODE, 64, 64, 2, 2, 16>(a, al, grid, st);
+    case 4: return launch_cfg<MODE, 256, 128, 4, 2, 16>(a, al, grid, st);
+    case 5: return launch_cfg<MODE, 128, 256, 2, 4, 16>(a, al, grid, st);
+    default: return launch_cfg<MODE, 256, 256, 4, 4, 16>(a, al, grid, st);
   }
 }
 
