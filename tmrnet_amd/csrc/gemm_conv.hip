@@ -174,9 +174,9 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     for (int q = 0; q < RA; ++q) ga[q] = row_geo(a, m0 + (tid + NT * q) / KQ, a.M);
   }
 
-  float4 ra[RA], rb[RB];
+  float4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];  // two prefetch register sets
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, float4 (&ra)[RA], float4 (&rb)[RB]) {
     const int kb = kbeg + kt * BK;
     // ---- A ----
     if (A_KC) {
@@ -242,7 +242,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const float4 (&ra)[RA], const float4 (&rb)[RB]) {
     float* As = As0 + buf * BK * LDA;
     float* Bs = Bs0 + buf * BK * LDB;
     if (A_KC) {
@@ -294,30 +294,44 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   const int aoff = wm * (BM / WM) + l31;
   const int boff = wn * (BN / WN) + l31;
 
+  auto compute = [&](int cur) {
+    const float* As = As0 + cur * BK * LDA;
+    const float* Bs = Bs0 + cur * BK * LDB;
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      const int kr = 2 * s + hh;
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA + aoff + 32 * i];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB + boff + 32 * j];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // Software pipeline, prefetch distance 2: while the MFMAs run on LDS buffer kt&1, the
+  // registers of one set hold tile kt+1 (written to the other LDS buffer after the MFMAs)
+  // and the other set has tile kt+2's global loads in flight.
   if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0);
+    load_tile(0, ra0, rb0);
+    if (ntiles > 1) load_tile(1, ra1, rb1);
+    store_tile(0, ra0, rb0);
     __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < ntiles) load_tile(kt + 1);
-      const float* As = As0 + cur * BK * LDA;
-      const float* Bs = Bs0 + cur * BK * LDB;
-#pragma unroll
-      for (int s = 0; s < BK / 2; ++s) {
-        const int kr = 2 * s + hh;
-        float av[TM], bv[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA + aoff + 32 * i];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB + boff + 32 * j];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
-      if (kt + 1 < ntiles) store_tile(cur ^ 1);
+    for (int kt = 0; kt < ntiles; kt += 2) {
+      // even step: compute buffer 0; set1 = tile kt+1; set0 <- tile kt+2
+      if (kt + 2 < ntiles) load_tile(kt + 2, ra0, rb0);
+      compute(0);
+      if (kt + 1 < ntiles) store_tile(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 1 >= ntiles) break;
+      // odd step: compute buffer 1; set0 = tile kt+2; set1 <- tile kt+3
+      if (kt + 3 < ntiles) load_tile(kt + 3, ra1, rb1);
+      compute(1);
+      if (kt + 2 < ntiles) store_tile(0, ra0, rb0);
       __syncthreads();
     }
   }
