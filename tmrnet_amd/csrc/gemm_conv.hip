@@ -436,6 +436,8 @@ int pick_cfg(long M, long N) {
     const TileCfg c = kCfgs[forced];
     if (M >= c.bm && N >= c.bn) return forced;
   }
+  if (M >= 256 && N >= 256) return 6;   // 256x256, 16 waves (measured best, convbench)
+  if (M >= 256 && N >= 128) return 4;   // 256x128, 8 waves
   if (N <= 64 && M >= 256) return 1;
   if (M <= 64 && N >= 256) return 2;
   if (M <= 64 || N <= 64) return 3;
@@ -552,11 +554,14 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
 static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* slab) {
   const long Mred = (long)d->n * d->ho * d->wo;
   const long Mo = d->k, No = (long)d->r * d->s * d->c;
-  const long tiles = (long)cdiv(Mo, 128) * cdiv(No, 128);
-  // aim for ~2048 workgroups; at least 512 reduction rows per split
-  long sp = 2048 / (tiles > 0 ? tiles : 1);
+  const TileCfg tc = kCfgs[pick_cfg(Mo, No)];
+  const long tiles = (long)cdiv(Mo, tc.bm) * cdiv(No, tc.bn);
+  // aim for ~target workgroups; at least minrows reduction rows per split
+  static const long target = env_int("TMR_WGRAD_TARGET", 1024);
+  static const long minrows = env_int("TMR_WGRAD_MINROWS", 1024);
+  long sp = target / (tiles > 0 ? tiles : 1);
   if (sp < 1) sp = 1;
-  long maxsp = Mred / 512;
+  long maxsp = Mred / minrows;
   if (maxsp < 1) maxsp = 1;
   if (sp > maxsp) sp = maxsp;
   long kc = (Mred + sp - 1) / sp;
