@@ -48,6 +48,12 @@ typedef struct tmr_conv_desc {
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
 int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
                    const float* bias, float* y, float beta, hipStream_t stream);
+/* Forward conv whose epilogue also emits BatchNorm batch-statistic partials of y:
+ * stats = float4 [tmr_conv2d_fwd_stats_parts(d)][k] of (count, mean, M2, 0) per output-row
+ * tile, consumed by tmr_bn_finalize (fuses the separate statistics pass of nn.BatchNorm2d). */
+int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d);
+int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const float* w_krsc, float* y,
+                           void* stats, size_t stats_bytes, hipStream_t stream);
 /* dx[n,h,w,c] = beta*dx + conv_transpose(dy, w_krsc) */
 int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
                      float beta, hipStream_t stream);
@@ -93,6 +99,11 @@ int tmr_bn_fwd_stats(const float* y, int rows, int c, const float* gamma, const 
                      float* running_mean, float* running_var, float momentum, float eps,
                      float* save_mean, float* save_invstd, float* scale, float* shift, void* ws,
                      size_t ws_bytes, hipStream_t stream);
+/* combine (count, mean, M2) partials (float4 [nparts][c]) -> the outputs of tmr_bn_fwd_stats */
+int tmr_bn_finalize(const void* partials, int nparts, int c, const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, float momentum, float eps,
+                    float* save_mean, float* save_invstd, float* scale, float* shift,
+                    hipStream_t stream);
 /* eval mode: scale/shift from running stats */
 int tmr_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, int c, float* scale, float* shift,

@@ -209,3 +209,30 @@ def test_lfb_index_and_gather_golden(dev):
     rows = torch.randint(0, 50, (4, 7), device=dev, dtype=torch.int32)
     out = ops.lfb_gather(bank, rows)
     assert torch.equal(out, bank[rows.long()])
+
+
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 1, 1, 0), (3, 14, 14, 128, 256, 3, 2, 1),
+                                  (1, 28, 28, 3, 64, 7, 2, 3), (5, 7, 7, 512, 2048, 1, 1, 0)])
+def test_conv_fused_bn_stats(dev, case):
+    """conv epilogue BN partials + tmr_bn_finalize == torch batch_norm statistics."""
+    n, h, w, cin, cout, r, st, pad = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.relu(torch.randn(n, cin, h, w, generator=g)) + 0.5   # non-zero-mean input
+    wt = torch.randn(cout, cin, r, r, generator=g) / np.sqrt(cin * r * r)
+    cs = 4 if cin == 3 else cin
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=cs)
+    wk = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=cs)
+    y, stats, nparts = ops.conv_fwd_bnstats(x4, wk, st, pad, c_real=cin)
+    y_ref = ops.conv_fwd(x4, wk, st, pad)
+    assert torch.equal(y, y_ref)
+    yd = y_ref.double().view(-1, cout).cpu()
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = torch.randn(cout, generator=g)
+    rm, rv = torch.zeros(cout), torch.ones(cout)
+    rmd, rvd = rm.to(dev), rv.to(dev)
+    mean, inv, scale, shift = ops.bn_finalize(stats, nparts, gamma.to(dev), beta.to(dev), rmd, rvd,
+                                              0.1, 1e-5)
+    assert rel_err(mean, yd.mean(0)) < 1e-6
+    var = yd.var(0, unbiased=False)
+    assert rel_err(inv, 1 / torch.sqrt(var + 1e-5)) < 1e-5
+    assert rel_err(rvd, 0.9 + 0.1 * yd.var(0, unbiased=True)) < 1e-6

@@ -32,6 +32,8 @@ SIGNATURES = {
     "tmr_abi_version": [],
     "tmr_last_error": [],
     "tmr_conv2d_fwd": [DP, P, P, P, P, F, P],
+    "tmr_conv2d_fwd_stats_parts": [DP],
+    "tmr_conv2d_fwd_bnstats": [DP, P, P, P, P, SZ, P],
     "tmr_conv2d_dgrad": [DP, P, P, P, F, P],
     "tmr_conv2d_wgrad_ws_bytes": [DP],
     "tmr_conv2d_wgrad": [DP, P, P, P, I, F, P, SZ, P],
@@ -44,6 +46,7 @@ SIGNATURES = {
     "tmr_crop_normalize": [P, P, P, I, I, I, I, I, F, F, F, F, F, F, P],
     "tmr_bn_ws_bytes": [I, I],
     "tmr_bn_fwd_stats": [P, I, I, P, P, P, P, F, F, P, P, P, P, P, SZ, P],
+    "tmr_bn_finalize": [P, I, I, P, P, P, P, F, F, P, P, P, P, P],
     "tmr_bn_eval_params": [P, P, P, P, F, I, P, P, P],
     "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
     "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],

@@ -46,13 +46,14 @@ size_t ws_need(int rows, int c) {
 
 __global__ __launch_bounds__(NT) void bn_stats_partial(const float* __restrict__ y, int rows, int c,
                                                        int rpb, int cthreads,
-                                                       double* __restrict__ part) {
+                                                       float4* __restrict__ part) {
   const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
   const int rthreads = NT / cthreads;
   const int ch = (blockIdx.y * cthreads + tc) * 4;
-  const float4 sh = *reinterpret_cast<const float4*>(y + ch);
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(rows, r0 + rpb);
+  // shift by the block's first row: removes the mean from the fp32 sums
+  const float4 sh = *reinterpret_cast<const float4*>(y + (long)r0 * c + ch);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
   for (int r = r0 + tr; r < r1; r += rthreads) {
     float4 v = *reinterpret_cast<const float4*>(y + (long)r * c + ch);
@@ -70,41 +71,49 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const float* __restrict__
     for (int e = 0; e < 8; ++e) acc[e] = 0.0;
     for (int k = 0; k < rthreads; ++k)
       for (int e = 0; e < 8; ++e) acc[e] += red[k * cthreads + tc][e];
-    double* o = part + ((long)blockIdx.x * c + ch) * 2;
+    const double n = (double)(r1 - r0);
+    const float shv[4] = {sh.x, sh.y, sh.z, sh.w};
     for (int e = 0; e < 4; ++e) {
-      o[2 * e] = acc[e];
-      o[2 * e + 1] = acc[4 + e];
+      const double ms = acc[e] / n;
+      double m2 = acc[4 + e] - acc[e] * ms;
+      if (m2 < 0) m2 = 0;
+      part[(long)blockIdx.x * c + ch + e] = make_float4((float)n, (float)(shv[e] + ms), (float)m2, 0.f);
     }
   }
 }
 
-// one block per 64 channels; 4 groups of partial rows summed in fixed order
-__global__ __launch_bounds__(NT) void bn_stats_final(const float* __restrict__ y, const double* __restrict__ part, int nrb,
-                                                     int rows, int c, const float* gamma,
-                                                     const float* beta, float* rmean, float* rvar,
-                                                     float momentum, float eps, float* smean,
-                                                     float* sinv, float* scale, float* shift) {
-  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int ch = blockIdx.x * 64 + lc;
-  double s = 0.0, q = 0.0;
-  if (ch < c) {
-    for (int b = g; b < nrb; b += 4) {
-      s += part[((long)b * c + ch) * 2];
-      q += part[((long)b * c + ch) * 2 + 1];
+// Chan/Welford combine of (n, mean, M2) partials in double, fixed order -> deterministic.
+// 8 channels per workgroup x 32 groups of partial rows.
+__device__ __forceinline__ void chan_add(double& n, double& mean, double& m2, double nb,
+                                         double mb, double m2b) {
+  if (nb <= 0) return;
+  const double nn = n + nb;
+  const double d = mb - mean;
+  mean += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+__global__ __launch_bounds__(NT) void bn_finalize_k(const float4* __restrict__ part, int nparts,
+                                                    int c, const float* gamma, const float* beta,
+                                                    float* rmean, float* rvar, float momentum,
+                                                    float eps, float* smean, float* sinv,
+                                                    float* scale, float* shift) {
+  const int lc = threadIdx.x & 7, g = threadIdx.x >> 3;
+  const int ch = blockIdx.x * 8 + lc;
+  double n = 0, mean = 0, m2 = 0;
+  if (ch < c)
+    for (int b = g; b < nparts; b += 32) {
+      const float4 p = part[(long)b * c + ch];
+      chan_add(n, mean, m2, p.x, p.y, p.z);
     }
-  }
-  __shared__ double red[4][64][2];
-  red[g][lc][0] = s;
-  red[g][lc][1] = q;
+  __shared__ double red[32][8][3];
+  red[g][lc][0] = n; red[g][lc][1] = mean; red[g][lc][2] = m2;
   __syncthreads();
   if (g == 0 && ch < c) {
-    s = red[0][lc][0] + red[1][lc][0] + red[2][lc][0] + red[3][lc][0];
-    q = red[0][lc][1] + red[1][lc][1] + red[2][lc][1] + red[3][lc][1];
-    const double n = (double)rows;
-    const double ms = s / n;
-    double var = q / n - ms * ms;
-    if (var < 0) var = 0;
-    const double mean = (double)y[ch] + ms;
+    n = 0; mean = 0; m2 = 0;
+    for (int k = 0; k < 32; ++k) chan_add(n, mean, m2, red[k][lc][0], red[k][lc][1], red[k][lc][2]);
+    const double var = n > 0 ? m2 / n : 0.0;
     const double inv = 1.0 / sqrt(var + (double)eps);
     smean[ch] = (float)mean;
     sinv[ch] = (float)inv;
@@ -113,7 +122,7 @@ __global__ __launch_bounds__(NT) void bn_stats_final(const float* __restrict__ y
     scale[ch] = (float)(gm * inv);
     shift[ch] = (float)(bt - mean * gm * inv);
     if (rmean) {
-      const double unb = rows > 1 ? var * n / (n - 1.0) : var;
+      const double unb = n > 1 ? m2 / (n - 1.0) : var;
       rmean[ch] = (float)((1.0 - momentum) * rmean[ch] + momentum * mean);
       rvar[ch] = (float)((1.0 - momentum) * rvar[ch] + momentum * unb);
     }
@@ -203,22 +212,22 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
                                                    const float* mean, const float* inv,
                                                    const float* gamma, float* dgamma,
                                                    float* dbeta, float* coef) {
-  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int ch = blockIdx.x * 64 + lc;
+  const int lc = threadIdx.x & 7, g = threadIdx.x >> 3;
+  const int ch = blockIdx.x * 8 + lc;
   double s = 0.0, q = 0.0;
   if (ch < c) {
-    for (int b = g; b < nrb; b += 4) {
+    for (int b = g; b < nrb; b += 32) {
       s += part[((long)b * c + ch) * 2];
       q += part[((long)b * c + ch) * 2 + 1];
     }
   }
-  __shared__ double red[4][64][2];
+  __shared__ double red[32][8][2];
   red[g][lc][0] = s;
   red[g][lc][1] = q;
   __syncthreads();
   if (g == 0 && ch < c) {
-    s = red[0][lc][0] + red[1][lc][0] + red[2][lc][0] + red[3][lc][0];
-    q = red[0][lc][1] + red[1][lc][1] + red[2][lc][1] + red[3][lc][1];
+    s = 0.0; q = 0.0;
+    for (int k = 0; k < 32; ++k) { s += red[k][lc][0]; q += red[k][lc][1]; }
     const double iv = inv[ch];
     const double dbt = s;
     const double dgm = q * iv;  // sum dzh * xhat
@@ -284,14 +293,23 @@ TMR_API int tmr_bn_fwd_stats(const float* y, int rows, int c, const float* gamma
   TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_fwd_stats: workspace too small");
   Plan p = make_plan(rows, c);
   TMR_CHECK_ARG((c / 4) % p.cthreads == 0, "tmr_bn_fwd_stats: unsupported channel count %d", c);
-  double* part = (double*)ws;
+  float4* part = (float4*)ws;
   hipLaunchKernelGGL(bn_stats_partial, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, y, rows, c,
                      p.rpb, p.cthreads, part);
   TMR_CHECK_LAUNCH("bn_stats_partial");
-  hipLaunchKernelGGL(bn_stats_final, dim3(cdiv(c, 64)), dim3(NT), 0, stream, y, part, p.nrb, rows,
-                     c, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+  return tmr_bn_finalize(part, p.nrb, c, gamma, beta, running_mean, running_var, momentum, eps,
+                         save_mean, save_invstd, scale, shift, stream);
+}
+
+TMR_API int tmr_bn_finalize(const void* partials, int nparts, int c, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            float momentum, float eps, float* save_mean, float* save_invstd,
+                            float* scale, float* shift, hipStream_t stream) {
+  TMR_CHECK_ARG(nparts > 0 && c > 0, "tmr_bn_finalize: empty partials");
+  hipLaunchKernelGGL(bn_finalize_k, dim3(cdiv(c, 8)), dim3(NT), 0, stream, (const float4*)partials,
+                     nparts, c, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd, scale, shift);
-  TMR_CHECK_LAUNCH("bn_stats_final");
+  TMR_CHECK_LAUNCH("bn_finalize");
   return 0;
 }
 
@@ -338,7 +356,7 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
   else
     hipLaunchKernelGGL((bn_bwd_partial<false>), dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, dz, y, z, save_mean, rows, c, p.rpb, p.cthreads, part);
   TMR_CHECK_LAUNCH("bn_bwd_partial");
-  hipLaunchKernelGGL(bn_bwd_final, dim3(cdiv(c, 64)), dim3(NT), 0, stream, part, p.nrb, rows, c,
+  hipLaunchKernelGGL(bn_bwd_final, dim3(cdiv(c, 8)), dim3(NT), 0, stream, part, p.nrb, rows, c,
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");
   long n4 = (long)rows * c / 4;

@@ -58,6 +58,8 @@ struct GemmArgs {
   // WGRAD split-K
   int kchunk;
   long slab;
+  // FWD: optional per-(m-tile, column) BatchNorm partials (n, mean, M2, 0)
+  float4* stats;
 };
 
 struct RowGeo {
@@ -375,6 +377,68 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     const int col = col0 + 32 * j;
     bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
   }
+  // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
+  // then M2 about it; combined across tiles by tmr_bn_finalize (Chan, double, fixed order).
+  if (MODE == MODE_FWD && a.stats != nullptr) {
+    float* red = smem;  // main loop ended with a barrier: LDS is free
+    const int nrows = min(BM, a.M - m0);
+    const int rbase_w = m0 + wm * (BM / WM) + 4 * hh;
+    auto valid = [&](int i, int r) {
+      return rbase_w + 32 * i + (r & 3) + 8 * (r >> 2) < a.M;
+    };
+    float cs[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += valid(i, r) ? acc[i][j][r] + bvals[j] : 0.f;
+      t += __shfl_xor(t, 32, 64);
+      cs[j] = t;
+    }
+    if (hh == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
+    __syncthreads();
+    float mj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
+      mj[j] = t / (float)nrows;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[i][j][r] + bvals[j] - mj[j];
+          t += valid(i, r) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 32, 64);
+      cs[j] = t;
+    }
+    if (hh == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col0 + 32 * j;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
+        if (col < a.N)
+          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -487,12 +551,12 @@ void set_grid(GemmArgs& a, int n, int hg, int wg) {
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
-                           const float* bias, float* y, float beta, hipStream_t stream) {
+static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                         const float* bias, float* y, float beta, GemmArgs& a, bool& al) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
-  GemmArgs a{};
+  a = GemmArgs{};
   a.A = x; a.B = w_krsc; a.C = y; a.bias = bias;
   a.M = d->n * d->ho * d->wo; a.N = d->k; a.K = d->r * d->s * d->c;
   a.log2C = lc;
@@ -501,7 +565,34 @@ TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* 
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = d->c; a.ldb = a.K; a.ldc = d->k; a.beta = beta;
-  bool al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0);
+  al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0);
+  return 0;
+}
+
+TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                           const float* bias, float* y, float beta, hipStream_t stream) {
+  GemmArgs a;
+  bool al;
+  int rc = conv_fwd_args(d, x, w_krsc, bias, y, beta, a, al);
+  if (rc) return rc;
+  return launch_gemm<MODE_FWD>(a, al, 1, stream);
+}
+
+TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
+  const long M = (long)d->n * d->ho * d->wo;
+  return cdiv(M, kCfgs[pick_cfg(M, d->k)].bm);
+}
+
+TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                                   float* y, void* stats, size_t stats_bytes, hipStream_t stream) {
+  GemmArgs a;
+  bool al;
+  int rc = conv_fwd_args(d, x, w_krsc, nullptr, y, 0.f, a, al);
+  if (rc) return rc;
+  const size_t need = (size_t)tmr_conv2d_fwd_stats_parts(d) * d->k * sizeof(float4);
+  TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
+                stats_bytes, need);
+  a.stats = (float4*)stats;
   return launch_gemm<MODE_FWD>(a, al, 1, stream);
 }
 
@@ -557,7 +648,7 @@ static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* sl
   const TileCfg tc = kCfgs[pick_cfg(Mo, No)];
   const long tiles = (long)cdiv(Mo, tc.bm) * cdiv(No, tc.bn);
   // aim for ~target workgroups; at least minrows reduction rows per split
-  static const long target = env_int("TMR_WGRAD_TARGET", 1024);
+  static const long target = env_int("TMR_WGRAD_TARGET", 512);
   static const long minrows = env_int("TMR_WGRAD_MINROWS", 1024);
   long sp = target / (tiles > 0 ? tiles : 1);
   if (sp < 1) sp = 1;

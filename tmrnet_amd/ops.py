@@ -72,6 +72,32 @@ def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None)
     return out
 
 
+def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None):
+    """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts)."""
+    _req(x, "x"); _req(w_krsc, "w")
+    n, h, w, c = x.shape
+    k, r, s, c2 = w_krsc.shape
+    assert c == c2, (x.shape, w_krsc.shape)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    out = _empty((n, d.ho, d.wo, k), x)
+    nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
+    stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
+    with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
+               (n, h, w, c, k, r, stride)):
+        call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
+             ctypes.c_size_t(stats.numel() * 4), stream_ptr())
+    return out, stats, nparts
+
+
+def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum, eps):
+    c = stats.shape[1]
+    mean = _empty((c,), stats); inv = _empty((c,), stats)
+    scale = _empty((c,), stats); shift = _empty((c,), stats)
+    call("tmr_bn_finalize", stats, nparts, c, gamma, beta, running_mean, running_var,
+         float(momentum), float(eps), mean, inv, scale, shift, stream_ptr())
+    return mean, inv, scale, shift
+
+
 def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0):
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C)."""
     _req(dy, "dy"); _req(w_krsc, "w")

@@ -65,14 +65,15 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None)
         wk = w.detach().contiguous().view(k, 1, 1, c)   # OIHW == KRSC for 1x1
     else:
         wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs)
-    y = ops.conv_fwd(x, wk, stride, pad, c_real=c)
-    y2 = y.view(-1, k)
     if training:
-        mean, inv, scale, shift = ops.bn_fwd_train(
-            y2, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var,
-            _bn_momentum(bn), bn.eps)
+        # batch statistics come out of the conv epilogue (no separate pass over y)
+        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c)
+        mean, inv, scale, shift = ops.bn_finalize(
+            stats, nparts, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+            bn.running_var, _bn_momentum(bn), bn.eps)
         bn.num_batches_tracked.add_(1)
     else:
+        y = ops.conv_fwd(x, wk, stride, pad, c_real=c)
         mean = inv = None
         scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                                           bn.running_var, bn.eps)
