@@ -41,8 +41,9 @@ const char* tmr_last_error(void);
 typedef struct tmr_conv_desc {
   int n, h, w, c; /* input NHWC; c = stored channels (power of two >= 4) */
   int k;          /* output channels */
-  int r, s, stride, pad;
-  int ho, wo; /* output spatial size */
+  int r, s, stride, pad; /* pad = padding along h */
+  int ho, wo;             /* output spatial size */
+  int pad_w;              /* padding along w */
 } tmr_conv_desc;
 
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
@@ -189,6 +190,15 @@ int tmr_nl_attn_fwd(const float* lt, const int32_t* rows, const float* u, float*
 int tmr_nl_attn_bwd(const float* lt, const int32_t* rows, const float* u, const float* p,
                     const float* dctx, float* ut, float* dlt, int b, int l, int d, float scale,
                     hipStream_t stream);
+
+/* TimeConv (NLBlock_MutiConv6_3.py:43-79, generalised in L): the three Conv1d branches run
+ * on tmr_conv2d_* (L as H, W=1); these kernels take the elementwise max of
+ * (x, conv3, conv5, conv7, maxpool2(pad_left0(x))) with the reference's first-max tie rule,
+ * and route the gradient back.  code: uint8 [b][l][c]. */
+int tmr_timeconv_max5_fwd(const float* x, const float* y1, const float* y2, const float* y3,
+                          float* out, uint8_t* code, int b, int l, int c, hipStream_t stream);
+int tmr_timeconv_max5_bwd(const float* dy, const uint8_t* code, float* d1, float* d2, float* d3,
+                          float* dx, int b, int l, int c, hipStream_t stream);
 
 /* ---------------- LSTM cell (head.hip) -------------------------------------
  * nn.LSTM(2048,512) gates in PyTorch order i,f,g,o (train_only_non-local_pretrained.py:215,

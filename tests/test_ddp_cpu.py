@@ -1,0 +1,59 @@
+"""Multi-process (world_size 2, gloo, CPU) check of the data-parallel gradient exchange:
+tmrnet_amd.ddp.GradAllReduce must SUM gradients across ranks (the reference's DataParallel
+reduce-adds onto cuda:0 under CrossEntropyLoss(reduction='sum')) and
+broadcast rank 0's initial weights."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tmrnet_amd.ddp import GradAllReduce
+    torch.manual_seed(100 + rank)           # different init per rank -> broadcast must fix it
+    m = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.Linear(200, 7))
+    red = GradAllReduce(m, dist, bucket_bytes=4 * 1024)
+    for i, p in enumerate(m.parameters()):
+        p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
+    red.all_reduce_sum()
+    out = [p.grad.clone() for p in m.parameters()]
+    w = [p.detach().clone() for p in m.parameters()]
+    q.put((rank, out, w, len(red.buckets)))
+    dist.destroy_process_group()
+
+
+def test_grad_all_reduce_sum_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, grads, weights, nb = q.get(timeout=120)
+        res[rank] = (grads, weights, nb)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][2] > 1                       # several buckets exercised
+    for i, g in enumerate(res[0][0]):
+        expect = (1 + 2) * (i + 1)             # sum over ranks, not mean
+        assert torch.all(g == expect)
+        assert torch.equal(g, res[1][0][i])
+    for w0, w1 in zip(res[0][1], res[1][1]):
+        assert torch.equal(w0, w1)

@@ -224,3 +224,56 @@ def test_memory_bank_model_parity(dev):
     ref.ce_sum_ref(out64[T - 1::T], labels).backward()
     g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
     _assert_vs_fp64(g(m), g(r), g(r64), 2e-3, "grad")
+
+
+def test_timeconv_golden(dev):
+    """HIP TimeConv vs the reference module's outputs/grads at L=30 (NLBlock_MutiConv6_3.py:43-79)."""
+    from tmrnet_amd.timeconv import TimeConv
+    from tests.golden.golden_inputs import TC_CASES
+    case = TC_CASES[0]
+    B, L, seed = case["B"], case["L"], case["seed"]
+    z = np.load(os.path.join(GOLD, "timeconv_L%d.npz" % L))
+    m = TimeConv().to(dev)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in timeconv_params(seed).items()})
+    x_np, g_np = timeconv_inputs(seed, B, L)
+    x = torch.from_numpy(x_np).to(dev).requires_grad_(True)
+    y = m(x)
+    y.backward(torch.from_numpy(g_np).to(dev))
+    assert np.abs(y.detach().cpu().numpy() - z["out"]).max() < 1e-5
+    assert rel_err(x.grad, torch.from_numpy(z["dx"])) < 1e-5
+    for name, p in m.named_parameters():
+        key = "d_" + name.replace(".", "_")
+        g = p.grad.detach().cpu().numpy()
+        if g.ndim == 3:
+            probes = projection_probes(seed + 7, g.shape, 16)
+            ex = z[key + "_proj"]
+            assert np.abs(project(g, probes) - ex).max() <= 1e-5 * np.abs(ex).max(), name
+        else:
+            assert np.abs(g - z[key]).max() <= 1e-5 * np.abs(z[key]).max(), name
+
+
+@pytest.mark.parametrize("L", [1, 7, 40])
+def test_timeconv_generalised_L(dev, L):
+    from tmrnet_amd.timeconv import TimeConv
+    torch.manual_seed(L)
+    m = TimeConv().to(dev)
+    r = ref.TimeConvRef()
+    r.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    x = torch.rand(3, L, 512) * 2 - 1
+    y = m(x.to(dev))
+    assert (y.cpu() - r(x)).abs().max().item() < 1e-5
+
+
+def test_tmrnet_muticonv_parity(dev):
+    """resnet_lstm with TimeConv (train_non-local_mutiConv_resnet.py:208-253), L=40."""
+    B, T, L = 2, 3, 40
+    torch.manual_seed(2)
+    m = tmrnet_amd.resnet_lstm(seq_len=T, num_classes=6, time_conv=True).to(dev).eval()
+    r = ref.TMRNetRef(seq_len=T, num_classes=6, time_conv=True).eval()
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    frames, off, lt, labels = _inputs(B, T, L, seed=8)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    out = m(x4, lt.to(dev))
+    out_r = r(ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224), lt)
+    assert (out.detach().cpu() - out_r.detach()).abs().max().item() < 1e-4
+    assert torch.equal(out.detach().cpu().argmax(1), out_r.argmax(1))

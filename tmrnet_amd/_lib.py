@@ -22,7 +22,7 @@ SZ = ctypes.c_size_t
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
-                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo")]
+                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "pad_w")]
 
 
 DP = ctypes.POINTER(ConvDesc)
@@ -68,6 +68,8 @@ SIGNATURES = {
     "tmr_mul": [P, P, P, P, L, P],
     "tmr_nl_attn_fwd": [P, P, P, P, P, I, I, I, F, P],
     "tmr_nl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, F, P],
+    "tmr_timeconv_max5_fwd": [P, P, P, P, P, P, I, I, I, P],
+    "tmr_timeconv_max5_bwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],
     "tmr_lstm_cell_bwd": [P, I, P, P, P, P, P, P, I, P, I, I, P],
 }

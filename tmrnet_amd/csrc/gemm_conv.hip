@@ -561,7 +561,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.M = d->n * d->ho * d->wo; a.N = d->k; a.K = d->r * d->s * d->c;
   a.log2C = lc;
   set_taps(a, d->r, d->s);
-  a.oy0 = -d->pad; a.ox0 = -d->pad; a.dyr = 1; a.dxs = 1;
+  a.oy0 = -d->pad; a.ox0 = -d->pad_w; a.dyr = 1; a.dxs = 1;
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = d->c; a.ldb = a.K; a.ldc = d->k; a.beta = beta;
@@ -611,7 +611,7 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
       for (int r = 0; r < d->r; ++r)
         if (((ph + d->pad - r) % st + st) % st == 0) { if (r0 < 0) r0 = r; ++nR; }
       for (int s = 0; s < d->s; ++s)
-        if (((pw + d->pad - s) % st + st) % st == 0) { if (s0 < 0) s0 = s; ++nS; }
+        if (((pw + d->pad_w - s) % st + st) % st == 0) { if (s0 < 0) s0 = s; ++nS; }
       const int hg = (d->h - ph + st - 1) / st, wg = (d->w - pw + st - 1) / st;
       if (hg <= 0 || wg <= 0) continue;
       GemmArgs a{};
@@ -622,7 +622,7 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
       if (nR == 0 || nS == 0) { a.K = 0; a.ntaps = 0; }
       // ho = (h + pad - r)/st = y + (ph + pad - r0)/st - ri
       a.oy0 = nR ? (ph + d->pad - r0) / st : 0;
-      a.ox0 = nS ? (pw + d->pad - s0) / st : 0;
+      a.ox0 = nS ? (pw + d->pad_w - s0) / st : 0;
       a.dyr = -1; a.dxs = -1;
       a.wr0 = r0 < 0 ? 0 : r0; a.ws0 = s0 < 0 ? 0 : s0; a.wst = st; a.wS = d->s;
       set_grid(a, d->n, hg, wg);
@@ -689,7 +689,7 @@ TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float
   a.M = d->k; a.N = d->r * d->s * d->c; a.K = d->n * d->ho * d->wo;
   a.log2C = lc;
   set_taps(a, d->r, d->s);
-  a.oy0 = -d->pad; a.ox0 = -d->pad; a.dyr = 1; a.dxs = 1;
+  a.oy0 = -d->pad; a.ox0 = -d->pad_w; a.dyr = 1; a.dxs = 1;
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = d->c; a.ldb = d->k; a.ldc = a.N; a.beta = 0.f;

@@ -553,3 +553,72 @@ TMR_API int tmr_mul(const float* a, const float* b, const float* scalar, float* 
   TMR_CHECK_LAUNCH("mul");
   return 0;
 }
+
+// ------------------------------------------------------------ TimeConv max-of-5
+// NLBlock_MutiConv6_3.py:52-79: y = max over (x, conv3(x), conv5(x), conv7(x),
+// maxpool2(pad_left0(x))) with the first maximum winning (AdaptiveMaxPool2d / MaxPool1d
+// tie rule).  code: 0 identity, 1..3 conv branches, 4 maxpool -> x[t-1] (or the zero pad).
+namespace {
+__global__ void max5_fwd_k(const float* __restrict__ x, const float* __restrict__ y1,
+                           const float* __restrict__ y2, const float* __restrict__ y3,
+                           float* __restrict__ out, uint8_t* __restrict__ code, int L, int C,
+                           long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)((i / C) % L);
+    const float xv = x[i];
+    const float prev = t > 0 ? x[i - C] : 0.f;
+    // MaxPool1d(2,1) over (prev, x): first max wins -> prev on ties
+    const bool mp_prev = !(xv > prev);
+    const float mp = mp_prev ? prev : xv;
+    float best = xv;
+    uint8_t c = 0;
+    const float v1 = y1[i], v2 = y2[i], v3 = y3[i];
+    if (v1 > best) { best = v1; c = 1; }
+    if (v2 > best) { best = v2; c = 2; }
+    if (v3 > best) { best = v3; c = 3; }
+    if (mp > best) { best = mp; c = mp_prev ? 4 : 0; }
+    out[i] = best;
+    code[i] = c;
+  }
+}
+__global__ void max5_bwd_k(const float* __restrict__ dy, const uint8_t* __restrict__ code,
+                           float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ d3,
+                           float* __restrict__ dx, int L, int C, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const uint8_t c = code[i];
+    const float g = dy[i];
+    d1[i] = c == 1 ? g : 0.f;
+    d2[i] = c == 2 ? g : 0.f;
+    d3[i] = c == 3 ? g : 0.f;
+    if (dx) {
+      const int t = (int)((i / C) % L);
+      float v = c == 0 ? g : 0.f;
+      if (t + 1 < L && code[i + C] == 4) v += dy[i + C];  // maxpool of step t+1 chose x[t]
+      dx[i] = v;
+    }
+  }
+}
+}  // namespace
+
+TMR_API int tmr_timeconv_max5_fwd(const float* x, const float* y1, const float* y2,
+                                  const float* y3, float* out, uint8_t* code, int b, int l, int c,
+                                  hipStream_t stream) {
+  const long n = (long)b * l * c;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(max5_fwd_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, x, y1, y2, y3, out,
+                     code, l, c, n);
+  TMR_CHECK_LAUNCH("timeconv_max5_fwd");
+  return 0;
+}
+
+TMR_API int tmr_timeconv_max5_bwd(const float* dy, const uint8_t* code, float* d1, float* d2,
+                                  float* d3, float* dx, int b, int l, int c, hipStream_t stream) {
+  const long n = (long)b * l * c;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(max5_bwd_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, dy, code, d1, d2,
+                     d3, dx, l, c, n);
+  TMR_CHECK_LAUNCH("timeconv_max5_bwd");
+  return 0;
+}

@@ -50,19 +50,20 @@ def _empty(shape, like, dtype=f32):
 
 
 # ----------------------------------------------------------------- conv / gemm
-def conv_desc(n, h, w, c, k, r, s, stride, pad):
+def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None):
+    pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
-    wo = (w + 2 * pad - s) // stride + 1
-    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo)
+    wo = (w + 2 * pad_w - s) // stride + 1
+    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w)
 
 
-def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None):
+def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None, pad_w=None):
     """x (N,H,W,C) NHWC, w_krsc (K,R,S,C) -> y (N,Ho,Wo,K)."""
     _req(x, "x"); _req(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
     if out is None:
         out = _empty((n, d.ho, d.wo, k), x)
     with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
@@ -72,13 +73,13 @@ def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None)
     return out
 
 
-def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None):
+def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None):
     """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts)."""
     _req(x, "x"); _req(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
     out = _empty((n, d.ho, d.wo, k), x)
     nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
@@ -98,13 +99,13 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
     return mean, inv, scale, shift
 
 
-def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0):
+def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None):
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C)."""
     _req(dy, "dy"); _req(w_krsc, "w")
     n, ho, wo, k = dy.shape
     k2, r, s, c = w_krsc.shape
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
@@ -113,13 +114,13 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0):
     return out
 
 
-def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0):
+def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None):
     """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW."""
     _req(x, "x"); _req(dy, "dy")
     n, h, w, c = x.shape
     k = dy.shape[3]
     c_real = c if c_real is None else c_real
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
     assert (d.ho, d.wo) == tuple(dy.shape[1:3])
     if out is None:
         out = _empty((k, c_real, r, s), x)
