@@ -60,25 +60,37 @@ struct GemmArgs {
   long slab;
   // FWD: optional per-(m-tile, column) BatchNorm partials (n, mean, M2, 0)
   float4* stats;
+  // byte extents of A and B (buffer-descriptor range checks)
+  uint32_t Abytes, Bbytes;
 };
 
-struct RowGeo {
-  int nHs, yb, xb;  // n*Hs, y*sy, x*sx
-  bool ok;
-};
+// Buffer loads: 32-bit byte offsets against a per-tensor descriptor; an out-of-range
+// offset returns zeros, so padding / tails / masked rows need no branches (the compiler
+// can then count vmcnt exactly across the software pipeline).
+constexpr uint32_t OOB = 0x80000000u;  // tensors are < 2^31 bytes (checked on the host)
 
-__device__ __forceinline__ RowGeo row_geo(const GemmArgs& a, int m, int mlimit) {
-  RowGeo g;
-  g.ok = m < mlimit;
-  uint32_t mm = g.ok ? (uint32_t)m : 0u;
-  uint32_t n = fdiv(mm, a.dHW);
-  uint32_t rem = mm - n * a.dHW.d;
-  uint32_t y = fdiv(rem, a.dW);
-  uint32_t x = rem - y * a.dW.d;
-  g.nHs = (int)n * a.Hs;
-  g.yb = (int)y * a.sy;
-  g.xb = (int)x * a.sx;
-  return g;
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__builtin_bit_cast(float, v[0]), __builtin_bit_cast(float, v[1]),
+                     __builtin_bit_cast(float, v[2]), __builtin_bit_cast(float, v[3]));
+}
+__device__ __forceinline__ float bld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+// 4 consecutive elements at byte offset `off`; `nvalid` of them in range (AL: all or none)
+template <bool AL>
+__device__ __forceinline__ float4 ld4v(__amdgpu_buffer_rsrc_t r, uint32_t off, bool ok, int nvalid) {
+  if (AL) return bld4(r, ok ? off : OOB);
+  float4 v;
+  v.x = bld1(r, ok && nvalid > 0 ? off : OOB);
+  v.y = bld1(r, ok && nvalid > 1 ? off + 4 : OOB);
+  v.z = bld1(r, ok && nvalid > 2 ? off + 8 : OOB);
+  v.w = bld1(r, ok && nvalid > 3 ? off + 12 : OOB);
+  return v;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
 
 __device__ __forceinline__ void tap_split(const GemmArgs& a, int tap, int& ri, int& si) {
@@ -86,50 +98,19 @@ __device__ __forceinline__ void tap_split(const GemmArgs& a, int tap, int& ri, i
   si = tap - ri * a.tapS;
 }
 
-// Gathered source pointer for (row geometry, k) or nullptr when padded/out of range.
-__device__ __forceinline__ const float* gather_ptr(const GemmArgs& a, const float* base,
-                                                   const RowGeo& g, int kidx) {
-  int tap, c;
-  if (a.ntaps == 1) {
-    tap = 0;
-    c = kidx;
-  } else {
-    tap = kidx >> a.log2C;
-    c = kidx & ((1 << a.log2C) - 1);
-  }
-  int ri, si;
-  tap_split(a, tap, ri, si);
-  int ys = g.yb + a.oy0 + a.dyr * ri;
-  int xs = g.xb + a.ox0 + a.dxs * si;
-  bool ok = g.ok && tap < a.ntaps && ys >= 0 && ys < a.Hs && xs >= 0 && xs < a.Ws;
-  if (!ok) return nullptr;
-  long pix = ((long)(g.nHs + ys) * a.Ws + xs);
-  return base + pix * a.lds + c;
-}
-
-template <bool AL>
-__device__ __forceinline__ float4 ld4(const float* p, int valid_elems) {
-  if (AL) {
-    return *reinterpret_cast<const float4*>(p);
-  } else {
-    float4 v;
-    v.x = valid_elems > 0 ? p[0] : 0.f;
-    v.y = valid_elems > 1 ? p[1] : 0.f;
-    v.z = valid_elems > 2 ? p[2] : 0.f;
-    v.w = valid_elems > 3 ? p[3] : 0.f;
-    return v;
-  }
-}
-
-template <int MODE, int BM, int BN, int WM, int WN, int BK, bool AL>
+// VAR: 0 = aligned float4 loads, one tap per k-tile (channels per tap >= BK, or a plain GEMM)
+//      1 = aligned, tap varies inside a k-tile (the 4-channel stem)
+//      2 = unaligned scalar loads (GEMMs with odd leading dimensions), one tap
+template <int MODE, int BM, int BN, int WM, int WN, int BK, int VAR>
 __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
+  constexpr bool AL = (VAR != 2);
   constexpr int NT = 64 * WM * WN;       // threads per workgroup
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   constexpr int KQ = BK / 4;             // float4 per row of a K-contiguous tile
   constexpr int RA = BM * BK / (4 * NT); // float4 loads per thread per k-tile for A
   constexpr int RB = BN * BK / (4 * NT);
-  static_assert(RA >= 1 && RB >= 1, "tile too small for 256 threads");
+  static_assert(RA >= 1 && RB >= 1, "tile too small for the workgroup");
   // A tile k-major [BK][LDA]; K-contiguous loaders scatter 4 scalars -> pad 2,
   // M/N-contiguous loaders write float4 -> pad 4.
   constexpr bool A_KC = (MODE != MODE_WGRAD);
@@ -169,11 +150,48 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   }
   const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  // ---- per-thread loader state ----
-  RowGeo ga[RA];
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.A, a.Abytes);
+  const __amdgpu_buffer_rsrc_t rB = make_rsrc(a.B, a.Bbytes);
+  const int cmask = (1 << a.log2C) - 1;
+
+  // ---- per-thread loader state (fixed across k-tiles) ----
+  // A_KC (FWD/DGRAD): gathered rows -> (pixel byte offset, y, x, in-range)
+  uint32_t apix[A_KC ? RA : 1];
+  int ay[A_KC ? RA : 1], ax[A_KC ? RA : 1];
+  bool aok[A_KC ? RA : 1];
   if (A_KC) {
 #pragma unroll
-    for (int q = 0; q < RA; ++q) ga[q] = row_geo(a, m0 + (tid + NT * q) / KQ, a.M);
+    for (int q = 0; q < RA; ++q) {
+      const int m = m0 + (tid + NT * q) / KQ;
+      aok[q] = m < a.M;
+      const uint32_t mm = aok[q] ? (uint32_t)m : 0u;
+      const uint32_t n = fdiv(mm, a.dHW);
+      const uint32_t rem = mm - n * a.dHW.d;
+      const uint32_t y = fdiv(rem, a.dW);
+      const uint32_t x = rem - y * a.dW.d;
+      ay[q] = (int)y * a.sy;
+      ax[q] = (int)x * a.sx;
+      apix[q] = ((uint32_t)(((int)n * a.Hs + ay[q]) * a.Ws + ax[q]) * (uint32_t)a.lds) * 4u;
+    }
+  }
+  // WGRAD B: this thread's columns j -> (tap offset, channel), fixed for the whole kernel
+  int bdy[MODE == MODE_WGRAD ? RB : 1], bdx[MODE == MODE_WGRAD ? RB : 1];
+  uint32_t bcoff[MODE == MODE_WGRAD ? RB : 1];
+  bool bjok[MODE == MODE_WGRAD ? RB : 1];
+  if (MODE == MODE_WGRAD) {
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      const int j = n0 + ((tid + NT * q) % (BN / 4)) * 4;
+      int tap, c;
+      if (a.ntaps == 1) { tap = 0; c = j; }
+      else { tap = j >> a.log2C; c = j & cmask; }
+      int ri, si;
+      tap_split(a, tap, ri, si);
+      bdy[q] = a.oy0 + a.dyr * ri;
+      bdx[q] = a.ox0 + a.dxs * si;
+      bcoff[q] = (uint32_t)c * 4u;
+      bjok[q] = j < a.N && tap < a.ntaps;
+    }
   }
 
   float4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];  // two prefetch register sets
@@ -182,11 +200,34 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     const int kb = kbeg + kt * BK;
     // ---- A ----
     if (A_KC) {
+      // tap of this k-tile (uniform unless VAR==1)
+      int tapU = 0, cbU = kb, dyU = a.oy0, dxU = a.ox0;
+      if (VAR != 1 && a.ntaps != 1) {
+        tapU = kb >> a.log2C;
+        cbU = kb & cmask;
+        int ri, si;
+        tap_split(a, tapU, ri, si);
+        dyU = a.oy0 + a.dyr * ri;
+        dxU = a.ox0 + a.dxs * si;
+      }
 #pragma unroll
       for (int q = 0; q < RA; ++q) {
-        const int k = kb + ((tid + NT * q) % KQ) * 4;
-        const float* p = (k < kend) ? gather_ptr(a, a.A, ga[q], k) : nullptr;
-        ra[q] = p ? ld4<AL>(p, kend - k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int kq4 = ((tid + NT * q) % KQ) * 4;
+        const int k = kb + kq4;
+        int tap = tapU, c = cbU + kq4, dy = dyU, dx = dxU;
+        if (VAR == 1) {
+          tap = k >> a.log2C;
+          c = k & cmask;
+          int ri, si;
+          tap_split(a, tap, ri, si);
+          dy = a.oy0 + a.dyr * ri;
+          dx = a.ox0 + a.dxs * si;
+        }
+        const int ys = ay[q] + dy, xs = ax[q] + dx;
+        const bool ok = aok[q] && k < kend && tap < a.ntaps && (unsigned)ys < (unsigned)a.Hs &&
+                        (unsigned)xs < (unsigned)a.Ws;
+        const uint32_t off = apix[q] + (uint32_t)(((dy * a.Ws + dx) * a.lds + c) * 4);
+        ra[q] = ld4v<AL>(rA, off, ok, kend - k);
       }
     } else {  // WGRAD: A[i][kk] = dY[m][co], co contiguous
 #pragma unroll
@@ -194,8 +235,8 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const int lin = tid + NT * q;
         const int krow = lin / (BM / 4), c4 = lin % (BM / 4);
         const int m = kb + krow, i = m0 + c4 * 4;
-        bool ok = (m < kend) && (i < a.M);
-        ra[q] = ok ? ld4<AL>(a.A + (long)m * a.ldb + i, a.M - i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = (m < kend) && (i < a.M);
+        ra[q] = ld4v<AL>(rA, ((uint32_t)m * (uint32_t)a.ldb + (uint32_t)i) * 4u, ok, a.M - i);
       }
     }
     // ---- B ----
@@ -205,41 +246,46 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const int lin = tid + NT * q;
         const int j = n0 + lin / KQ;
         const int k = kb + (lin % KQ) * 4;
-        bool ok = (j < a.N) && (k < kend);
-        rb[q] = ok ? ld4<AL>(a.B + (long)j * a.ldb + k, kend - k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = (j < a.N) && (k < kend);
+        rb[q] = ld4v<AL>(rB, ((uint32_t)j * (uint32_t)a.ldb + (uint32_t)k) * 4u, ok, kend - k);
       }
     } else if (MODE == MODE_DGRAD) {  // B[k=(tap,co)][j=ci], ci contiguous
+      int tapU = 0, cbU = kb, rsU = 0;
+      if (a.ntaps != 1) {
+        tapU = kb >> a.log2C;
+        cbU = kb & cmask;
+        int ri, si;
+        tap_split(a, tapU, ri, si);
+        rsU = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
+      }
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
         const int lin = tid + NT * q;
         const int krow = lin / (BN / 4), c4 = lin % (BN / 4);
         const int k = kb + krow, j = n0 + c4 * 4;
-        bool ok = (k < kend) && (j < a.N);
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) {
-          int tap, co;
-          if (a.ntaps == 1) { tap = 0; co = k; }
-          else { tap = k >> a.log2C; co = k & ((1 << a.log2C) - 1); }
-          int ri, si;
-          tap_split(a, tap, ri, si);
-          int rs = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
-          v = ld4<AL>(a.B + (long)co * a.ldb + (long)rs * a.N + j, a.N - j);
-        }
-        rb[q] = v;
+        const bool ok = (k < kend) && (j < a.N);
+        const uint32_t co = (uint32_t)(cbU + krow);
+        rb[q] = ld4v<AL>(rB, (co * (uint32_t)a.ldb + (uint32_t)rsU * (uint32_t)a.N + (uint32_t)j) * 4u,
+                         ok, a.N - j);
       }
     } else {  // WGRAD: B[kk=m][j=(tap,c)] gathered from X
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
         const int lin = tid + NT * q;
-        const int krow = lin / (BN / 4), c4 = lin % (BN / 4);
-        const int m = kb + krow, j = n0 + c4 * 4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < kend && j < a.N) {
-          RowGeo g = row_geo(a, m, kend);
-          const float* p = gather_ptr(a, a.B, g, j);
-          if (p) v = ld4<AL>(p, a.N - j);
-        }
-        rb[q] = v;
+        const int krow = lin / (BN / 4);
+        const int m = kb + krow;
+        const uint32_t mm = m < kend ? (uint32_t)m : 0u;
+        const uint32_t n = fdiv(mm, a.dHW);
+        const uint32_t rem = mm - n * a.dHW.d;
+        const uint32_t y = fdiv(rem, a.dW);
+        const uint32_t x = rem - y * a.dW.d;
+        const int ys = (int)y * a.sy + bdy[q], xs = (int)x * a.sx + bdx[q];
+        const bool ok = m < kend && bjok[q] && (unsigned)ys < (unsigned)a.Hs &&
+                        (unsigned)xs < (unsigned)a.Ws;
+        const uint32_t off =
+            ((uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds) * 4u + bcoff[q];
+        const int j = n0 + (lin % (BN / 4)) * 4;
+        rb[q] = ld4v<AL>(rB, off, ok, a.N - j);
       }
     }
   };
@@ -474,11 +520,14 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit,
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int BKT>
-int launch_cfg(const GemmArgs& a, bool al, dim3 grid, hipStream_t st) {
-  if (al)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, true>), grid, dim3(64 * WM * WN), 0, st, a);
+int launch_cfg(const GemmArgs& a, int var, dim3 grid, hipStream_t st) {
+  const dim3 blk(64 * WM * WN);
+  if (var == 2)
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 2>), grid, blk, 0, st, a);
+  else if (MODE == MODE_FWD && var == 1)
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, (MODE == MODE_FWD ? 1 : 0)>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, false>), grid, dim3(64 * WM * WN), 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0>), grid, blk, 0, st, a);
   TMR_CHECK_LAUNCH("gemm_kernel");
   return 0;
 }
@@ -510,19 +559,30 @@ int pick_cfg(long M, long N) {
 
 template <int MODE>
 int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
+  TMR_CHECK_ARG(a.Abytes < 0x80000000u && a.Bbytes < 0x80000000u,
+                "gemm: operand larger than 2 GiB (split the batch)");
+  const bool uniform = a.ntaps <= 1 || (1 << a.log2C) >= 16;
+  int var = al ? (uniform ? 0 : 1) : 2;
+  TMR_CHECK_ARG(uniform || (al && MODE == MODE_FWD),
+                "gemm: per-element taps need aligned channels and the forward view");
   const int cfg = pick_cfg(a.M, a.N);
   const TileCfg c = kCfgs[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   switch (cfg) {
-    case 0: return launch_cfg<MODE, 128, 128, 2, 2, 16>(a, al, grid, st);
-    case 1: return launch_cfg<MODE, 256, 64, 4, 1, 16>(a, al, grid, st);
-    case 2: return launch_cfg<MODE, 64, 256, 1, 4, 16>(a, al, grid, st);
-    case 3: return launch_cfg<MODE, 64, 64, 2, 2, 16>(a, al, grid, st);
-    case 4: return launch_cfg<MODE, 256, 128, 4, 2, 16>(a, al, grid, st);
-    case 5: return launch_cfg<MODE, 128, 256, 2, 4, 16>(a, al, grid, st);
-    default: return launch_cfg<MODE, 256, 256, 4, 4, 16>(a, al, grid, st);
+    case 0: return launch_cfg<MODE, 128, 128, 2, 2, 16>(a, var, grid, st);
+    case 1: return launch_cfg<MODE, 256, 64, 4, 1, 16>(a, var, grid, st);
+    case 2: return launch_cfg<MODE, 64, 256, 1, 4, 16>(a, var, grid, st);
+    case 3: return launch_cfg<MODE, 64, 64, 2, 2, 16>(a, var, grid, st);
+    case 4: return launch_cfg<MODE, 256, 128, 4, 2, 16>(a, var, grid, st);
+    case 5: return launch_cfg<MODE, 128, 256, 2, 4, 16>(a, var, grid, st);
+    default: return launch_cfg<MODE, 256, 256, 4, 4, 16>(a, var, grid, st);
   }
+}
+
+static uint32_t clamp_bytes(long elems) {
+  long b = elems * 4;
+  return b >= 0x80000000L ? 0x80000000u : (uint32_t)b;
 }
 
 int ilog2_exact(int v) {
@@ -565,6 +625,8 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = d->c; a.ldb = a.K; a.ldc = d->k; a.beta = beta;
+  a.Abytes = clamp_bytes((long)d->n * d->h * d->w * d->c);
+  a.Bbytes = clamp_bytes((long)d->k * a.K);
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0);
   return 0;
 }
@@ -628,6 +690,8 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
       set_grid(a, d->n, hg, wg);
       a.Hs = d->ho; a.Ws = d->wo; a.sy = 1; a.sx = 1;
       a.lds = d->k; a.ldb = d->r * d->s * d->c; a.ldc = d->c; a.beta = beta;
+      a.Abytes = clamp_bytes((long)d->n * d->ho * d->wo * d->k);
+      a.Bbytes = clamp_bytes((long)d->k * d->r * d->s * d->c);
       if (st == 1) {
         a.osy = 0;
       } else {
@@ -694,6 +758,8 @@ TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = d->c; a.ldb = d->k; a.ldc = a.N; a.beta = 0.f;
   a.kchunk = kc; a.slab = slab;
+  a.Abytes = clamp_bytes((long)d->n * d->ho * d->wo * d->k);
+  a.Bbytes = clamp_bytes((long)d->n * d->h * d->w * d->c);
   bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0);
   int rc = launch_gemm<MODE_WGRAD>(a, al, sp, stream);
   if (rc) return rc;
@@ -719,6 +785,8 @@ TMR_API int tmr_gemm_nt(int M, int N, int K, const float* A, int lda, const floa
   set_grid(a, M, 1, 1);
   a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
   a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta;
+  a.Abytes = clamp_bytes(M > 0 ? (long)(M - 1) * lda + K : 0);
+  a.Bbytes = clamp_bytes(N > 0 ? (long)(N - 1) * ldb + K : 0);
   bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && K % 4 == 0;
   return launch_gemm<MODE_FWD>(a, al, 1, stream);
 }
@@ -736,6 +804,8 @@ TMR_API int tmr_gemm_nn(int M, int N, int K, const float* A, int lda, const floa
   set_grid(a, M, 1, 1);
   a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
   a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta; a.osy = 0;
+  a.Abytes = clamp_bytes(M > 0 ? (long)(M - 1) * lda + K : 0);
+  a.Bbytes = clamp_bytes(K > 0 ? (long)(K - 1) * ldb + N : 0);
   bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && K % 4 == 0 &&
             N % 4 == 0;
   return launch_gemm<MODE_DGRAD>(a, al, 1, stream);
@@ -754,6 +824,8 @@ TMR_API int tmr_gemm_tn(int M, int N, int K, const float* A, int lda, const floa
   a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
   a.lds = ldb; a.ldb = lda; a.ldc = ldc; a.beta = beta;
   a.kchunk = K > 0 ? K : 1; a.slab = 0;
+  a.Abytes = clamp_bytes(K > 0 ? (long)(K - 1) * lda + M : 0);
+  a.Bbytes = clamp_bytes(K > 0 ? (long)(K - 1) * ldb + N : 0);
   bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && M % 4 == 0 &&
             N % 4 == 0;
   return launch_gemm<MODE_WGRAD>(a, al, 1, stream);
