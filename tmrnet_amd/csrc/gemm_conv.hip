@@ -69,10 +69,12 @@ struct GemmArgs {
 // can then count vmcnt exactly across the software pipeline).
 constexpr uint32_t OOB = 0x80000000u;  // tensors are < 2^31 bytes (checked on the host)
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  return make_float4(__builtin_bit_cast(float, v[0]), __builtin_bit_cast(float, v[1]),
-                     __builtin_bit_cast(float, v[2]), __builtin_bit_cast(float, v[3]));
+  // whole-vector bit_cast: extracting v[0..3] one by one makes hipcc (ROCm 7.2) emit a
+  // single buffer_load_dword and replicate it (miscompile, checked in the .s)
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return __builtin_bit_cast(float4, v);
 }
 __device__ __forceinline__ float bld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
@@ -250,14 +252,15 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         rb[q] = ld4v<AL>(rB, ((uint32_t)j * (uint32_t)a.ldb + (uint32_t)k) * 4u, ok, kend - k);
       }
     } else if (MODE == MODE_DGRAD) {  // B[k=(tap,co)][j=ci], ci contiguous
-      int tapU = 0, cbU = kb, rsU = 0;
+      int tapU = 0, cbU = kb;
       if (a.ntaps != 1) {
         tapU = kb >> a.log2C;
         cbU = kb & cmask;
-        int ri, si;
-        tap_split(a, tapU, ri, si);
-        rsU = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
       }
+      int ri, si;
+      tap_split(a, tapU, ri, si);
+      // weight tap of this k-tile (a one-tap parity class still sits at (wr0, ws0))
+      const int rsU = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
         const int lin = tid + NT * q;
@@ -561,7 +564,8 @@ template <int MODE>
 int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   TMR_CHECK_ARG(a.Abytes < 0x80000000u && a.Bbytes < 0x80000000u,
                 "gemm: operand larger than 2 GiB (split the batch)");
-  const bool uniform = a.ntaps <= 1 || (1 << a.log2C) >= 16;
+  // WGRAD resolves taps per column (fixed per thread); FWD/DGRAD per k-tile when uniform
+  const bool uniform = MODE == MODE_WGRAD || a.ntaps <= 1 || (1 << a.log2C) >= 16;
   int var = al ? (uniform ? 0 : 1) : 2;
   TMR_CHECK_ARG(uniform || (al && MODE == MODE_FWD),
                 "gemm: per-element taps need aligned channels and the forward view");
