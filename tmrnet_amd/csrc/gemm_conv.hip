@@ -27,6 +27,9 @@
 namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+#ifndef TMR_PF
+#define TMR_PF 2
+#endif
 #ifndef TMR_GEMM_WAVES
 #define TMR_GEMM_WAVES 3
 #endif
@@ -364,28 +367,43 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     }
   };
 
-  // Software pipeline, prefetch distance 2: while the MFMAs run on LDS buffer kt&1, the
-  // registers of one set hold tile kt+1 (written to the other LDS buffer after the MFMAs)
-  // and the other set has tile kt+2's global loads in flight.
+  // Software pipeline.  Loads past the last k-tile are issued anyway: their offsets are out
+  // of range (k >= kend) so they return zeros, and the loop has no load/store branches, which
+  // lets the compiler place exact (counted) vmcnt waits.
+#if TMR_PF == 2
+  // prefetch distance 2: while the MFMAs run on LDS buffer kt&1, one register set holds
+  // tile kt+1 (written to the other buffer after the MFMAs) and the other set has tile
+  // kt+2's loads in flight.
   if (ntiles > 0) {
     load_tile(0, ra0, rb0);
-    if (ntiles > 1) load_tile(1, ra1, rb1);
+    load_tile(1, ra1, rb1);
     store_tile(0, ra0, rb0);
     __syncthreads();
     for (int kt = 0; kt < ntiles; kt += 2) {
-      // even step: compute buffer 0; set1 = tile kt+1; set0 <- tile kt+2
-      if (kt + 2 < ntiles) load_tile(kt + 2, ra0, rb0);
+      load_tile(kt + 2, ra0, rb0);
       compute(0);
-      if (kt + 1 < ntiles) store_tile(1, ra1, rb1);
+      store_tile(1, ra1, rb1);
       __syncthreads();
       if (kt + 1 >= ntiles) break;
-      // odd step: compute buffer 1; set0 = tile kt+2; set1 <- tile kt+3
-      if (kt + 3 < ntiles) load_tile(kt + 3, ra1, rb1);
+      load_tile(kt + 3, ra1, rb1);
       compute(1);
-      if (kt + 2 < ntiles) store_tile(0, ra0, rb0);
+      store_tile(0, ra0, rb0);
       __syncthreads();
     }
   }
+#else
+  if (ntiles > 0) {
+    load_tile(0, ra0, rb0);
+    store_tile(0, ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+      load_tile(kt + 1, ra0, rb0);
+      compute(kt & 1);
+      store_tile((kt & 1) ^ 1, ra0, rb0);
+      __syncthreads();
+    }
+  }
+#endif
 
   // ---- epilogue ----
   float* Cb = a.C;
@@ -538,7 +556,7 @@ int launch_cfg(const GemmArgs& a, int var, dim3 grid, hipStream_t st) {
 // Tile configurations (BM, BN).  Selection keeps both tile dims useful.
 struct TileCfg { int bm, bn; };
 constexpr TileCfg kCfgs[] = {{128, 128}, {256, 64}, {64, 256}, {64, 64},
-                             {256, 128}, {128, 256}, {256, 256}};
+                             {256, 128}, {128, 256}, {256, 256}, {256, 256}, {256, 128}};
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int env_int(const char* name, int dflt) {
@@ -580,7 +598,9 @@ int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
     case 3: return launch_cfg<MODE, 64, 64, 2, 2, 16>(a, var, grid, st);
     case 4: return launch_cfg<MODE, 256, 128, 4, 2, 16>(a, var, grid, st);
     case 5: return launch_cfg<MODE, 128, 256, 2, 4, 16>(a, var, grid, st);
-    default: return launch_cfg<MODE, 256, 256, 4, 4, 16>(a, var, grid, st);
+    case 6: return launch_cfg<MODE, 256, 256, 4, 4, 16>(a, var, grid, st);
+    case 7: return launch_cfg<MODE, 256, 256, 4, 4, 32>(a, var, grid, st);
+    default: return launch_cfg<MODE, 256, 128, 4, 2, 32>(a, var, grid, st);
   }
 }
 
@@ -724,7 +744,7 @@ static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* sl
   if (maxsp < 1) maxsp = 1;
   if (sp > maxsp) sp = maxsp;
   long kc = (Mred + sp - 1) / sp;
-  kc = (kc + 31) / 32 * 32;  // multiple of every BK
+  kc = (kc + 31) / 32 * 32;  // multiple of every BK (16, 32)
   sp = (Mred + kc - 1) / kc;
   *splits = (int)sp;
   *kchunk = (int)kc;
