@@ -44,6 +44,8 @@ typedef struct tmr_conv_desc {
   int r, s, stride, pad; /* pad = padding along h */
   int ho, wo;             /* output spatial size */
   int pad_w;              /* padding along w */
+  int x_ld, y_ld;         /* pixel strides (elements) of x/dx and y/dy; 0 = dense (c, k).
+                             A channel slice of a wider tensor = grouped convolution. */
 } tmr_conv_desc;
 
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
@@ -128,6 +130,27 @@ int tmr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int n, 
 /* AdaptiveAvgPool2d(1) of share.avgpool (:214): x [n][hw][c] -> y [n][c] */
 int tmr_avgpool_fwd(const float* x, float* y, int n, int hw, int c, hipStream_t stream);
 int tmr_avgpool_bwd(const float* dy, float* dx, int n, int hw, int c, hipStream_t stream);
+
+/* ---------------- ResNeSt-50 blocks (resnest.hip) --------------------------
+ * SplAtConv2d (radix 2, cardinality 1) of the resnest50() trunk used at
+ * Training TMRNet/train_non-local_mutiConv_resnest.py:210-220.  x: [n][hw][2c] (after the
+ * grouped conv + bn0 + ReLU), z: fc2 logits [n][2c], att: r-softmax [n][2c]. */
+/* gap[n][c] = mean_hw(x[:, :, c] + x[:, :, c+C]) */
+int tmr_splat_gap(const float* x, float* gap, int n, int hw, int c, hipStream_t stream);
+/* att = softmax over the radix pair of z; out[n,hw,c] = att0*x0 + att1*x1 (att may be NULL) */
+int tmr_splat_combine(const float* x, const float* z, float* att, float* out, int n, int hw, int c,
+                      hipStream_t stream);
+/* dz = softmax-backward of (sum_hw dout * x_r) */
+int tmr_splat_bwd(const float* dout, const float* x, const float* att, float* dz, int n, int hw,
+                  int c, hipStream_t stream);
+/* dx[n,hw,r*C+c] = att_r*dout[n,hw,c] + dgap[n][c]/hw */
+int tmr_splat_bwd_apply(const float* dout, const float* att, const float* dgap, float* dx, int n,
+                        int hw, int c, hipStream_t stream);
+/* AvgPool2d(k, s, p) NHWC; divisor k*k (count_include_pad) or the number of valid cells */
+int tmr_avgpool2d_fwd(const float* x, float* y, int n, int h, int w, int c, int ho, int wo, int k,
+                      int s, int p, int count_include_pad, hipStream_t stream);
+int tmr_avgpool2d_bwd(const float* dy, float* dx, int n, int h, int w, int c, int ho, int wo, int k,
+                      int s, int p, int count_include_pad, hipStream_t stream);
 
 /* ---------------- misc (head.hip) ------------------------------------------ */
 /* out[j] = beta*out[j] + sum_i x[i*ld + j]   (Linear bias grads) */

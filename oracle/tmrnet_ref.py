@@ -158,16 +158,119 @@ def resnet50_share():
 
 
 # --------------------------------------------------------------------------
+# ResNeSt-50 (radix 2, cardinality 1, deep stem 32, avg_down, avd) -- the
+# third-party `resnest` package's resnest50() used at
+# Training TMRNet/train_non-local_mutiConv_resnest.py:210-220.  The package is
+# neither vendored in the reference nor installed here: restated from its
+# published definition.  PARITY UNPINNED (checked by parameter count
+# 25,434,240 and 5.369 GMAC/frame).
+# --------------------------------------------------------------------------
+class SplAtConv2d(nn.Module):
+    def __init__(self, in_channels, channels, stride=1, radix=2, reduction_factor=4):
+        super().__init__()
+        inter = max(in_channels * radix // reduction_factor, 32)
+        self.radix = radix
+        self.channels = channels
+        self.conv = nn.Conv2d(in_channels, channels * radix, 3, stride, 1, groups=radix, bias=False)
+        self.bn0 = nn.BatchNorm2d(channels * radix)
+        self.relu = nn.ReLU(inplace=True)
+        self.fc1 = nn.Conv2d(channels, inter, 1, groups=1)
+        self.bn1 = nn.BatchNorm2d(inter)
+        self.fc2 = nn.Conv2d(inter, channels * radix, 1, groups=1)
+
+    def forward(self, x):
+        x = self.relu(self.bn0(self.conv(x)))
+        b = x.shape[0]
+        splits = torch.split(x, self.channels, dim=1)
+        gap = F.adaptive_avg_pool2d(sum(splits), 1)
+        gap = self.relu(self.bn1(self.fc1(gap)))
+        att = self.fc2(gap).view(b, 1, self.radix, -1).transpose(1, 2)
+        att = F.softmax(att, dim=1).reshape(b, -1, 1, 1)
+        atts = torch.split(att, self.channels, dim=1)
+        return sum(a * s_ for a, s_ in zip(atts, splits))
+
+
+class BottleneckS(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, is_first=False):
+        super().__init__()
+        gw = planes
+        self.conv1 = nn.Conv2d(inplanes, gw, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(gw)
+        self.avd = stride > 1 or is_first
+        if self.avd:
+            self.avd_layer = nn.AvgPool2d(3, stride, padding=1)
+            stride = 1
+        self.conv2 = SplAtConv2d(gw, gw, stride=stride)
+        self.conv3 = nn.Conv2d(gw, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.conv2(out)
+        if self.avd:
+            out = self.avd_layer(out)
+        out = self.bn3(self.conv3(out))
+        res = self.downsample(x) if self.downsample is not None else x
+        return self.relu(out + res)
+
+
+def _make_layer_s(inplanes, planes, blocks, stride):
+    downsample = None
+    if stride != 1 or inplanes != planes * 4:
+        pool = (nn.AvgPool2d(stride, stride, ceil_mode=True, count_include_pad=False) if stride != 1
+                else nn.AvgPool2d(1, 1, ceil_mode=True, count_include_pad=False))
+        downsample = nn.Sequential(pool, nn.Conv2d(inplanes, planes * 4, 1, bias=False),
+                                   nn.BatchNorm2d(planes * 4))
+    layers = [BottleneckS(inplanes, planes, stride, downsample)]
+    for _ in range(1, blocks):
+        layers.append(BottleneckS(planes * 4, planes))
+    return nn.Sequential(*layers)
+
+
+class GlobalAvgPool2d(nn.Module):
+    def forward(self, x):
+        return F.adaptive_avg_pool2d(x, 1).view(x.size(0), -1)
+
+
+def resnest50_share():
+    share = nn.Sequential()
+    share.add_module("conv1", nn.Sequential(
+        nn.Conv2d(3, 32, 3, 2, 1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+        nn.Conv2d(32, 32, 3, 1, 1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+        nn.Conv2d(32, 64, 3, 1, 1, bias=False)))
+    share.add_module("bn1", nn.BatchNorm2d(64))
+    share.add_module("relu", nn.ReLU(inplace=True))
+    share.add_module("maxpool", nn.MaxPool2d(3, 2, 1))
+    share.add_module("layer1", _make_layer_s(64, 64, 3, 1))
+    share.add_module("layer2", _make_layer_s(256, 128, 4, 2))
+    share.add_module("layer3", _make_layer_s(512, 256, 6, 2))
+    share.add_module("layer4", _make_layer_s(1024, 512, 3, 2))
+    share.add_module("avgpool", GlobalAvgPool2d())
+    for m in share.modules():   # resnest ResNet.__init__ init
+        if isinstance(m, nn.Conv2d):
+            n = m.kernel_size[0] * m.kernel_size[1] * m.out_channels
+            m.weight.data.normal_(0, math.sqrt(2.0 / n))
+        elif isinstance(m, nn.BatchNorm2d):
+            m.weight.data.fill_(1)
+            m.bias.data.zero_()
+    return share
+
+
+# --------------------------------------------------------------------------
 # TMRNet / memory-bank model
 # --------------------------------------------------------------------------
 class TMRNetRef(nn.Module):
     """Inline `resnet_lstm` (train_only_non-local_pretrained.py:201-240); with
     time_conv=True the mutiConv variant (train_non-local_mutiConv_resnet.py:208-253)."""
 
-    def __init__(self, seq_len=10, num_classes=7, time_conv=False):
+    def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50"):
         super().__init__()
         self.seq_len = seq_len
-        self.share = resnet50_share()
+        self.share = resnet50_share() if backbone == "resnet50" else resnest50_share()
         self.lstm = nn.LSTM(2048, 512, batch_first=True)
         self.fc_c = nn.Linear(512, num_classes)
         self.fc_h_c = nn.Linear(1024, 512)

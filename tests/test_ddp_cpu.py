@@ -29,8 +29,9 @@ def _worker(rank, world, port, q):
     for i, p in enumerate(m.parameters()):
         p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
     red.all_reduce_sum()
-    out = [p.grad.clone() for p in m.parameters()]
-    w = [p.detach().clone() for p in m.parameters()]
+    # numpy copies: torch tensors would travel as shared-memory fds that vanish with the child
+    out = [p.grad.numpy().copy() for p in m.parameters()]
+    w = [p.detach().numpy().copy() for p in m.parameters()]
     q.put((rank, out, w, len(red.buckets)))
     dist.destroy_process_group()
 
@@ -53,7 +54,7 @@ def test_grad_all_reduce_sum_world2():
     assert res[0][2] > 1                       # several buckets exercised
     for i, g in enumerate(res[0][0]):
         expect = (1 + 2) * (i + 1)             # sum over ranks, not mean
-        assert torch.all(g == expect)
-        assert torch.equal(g, res[1][0][i])
+        assert (g == expect).all()
+        assert (g == res[1][0][i]).all()
     for w0, w1 in zip(res[0][1], res[1][1]):
-        assert torch.equal(w0, w1)
+        assert (w0 == w1).all()

@@ -119,6 +119,28 @@ def test_oracle_model_shapes_and_counts():
     assert out.shape == (2, 7)
 
 
+def test_resnest_oracle_counts_and_keys():
+    """ResNeSt restatement (parity unpinned: the resnest package is not in the reference):
+    25,434,240 trunk parameters, 5.369 conv GMAC/frame, TMRNet-ResNeSt+TimeConv 36,194,951
+    (SURVEY.md §8a-5); the HIP module tree carries exactly the same state_dict keys/shapes."""
+    share = ref.resnest50_share().eval()
+    assert sum(p.numel() for p in share.parameters()) == 25434240
+    macs = []
+    hook = lambda mod, inp, out: macs.append(out.numel() * mod.weight[0].numel())
+    for mod in share.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.register_forward_hook(hook)
+    with torch.no_grad():
+        assert share(torch.randn(1, 3, 224, 224)).shape == (1, 2048)
+    assert abs(sum(macs) / 1e9 - 5.369) < 1e-3
+    m = ref.TMRNetRef(seq_len=2, num_classes=7, time_conv=True, backbone="resnest50")
+    assert sum(p.numel() for p in m.parameters()) == 36194951
+    from tmrnet_amd.resnest import ResNeSt50Share
+    ours = {k: v.shape for k, v in ResNeSt50Share().state_dict().items()}
+    theirs = {k: v.shape for k, v in share.state_dict().items()}
+    assert ours == theirs
+
+
 def test_timeconv_generalised_L():
     m = ref.TimeConvRef()
     for L in (1, 7, 40):

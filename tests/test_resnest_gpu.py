@@ -1,0 +1,152 @@
+"""ResNeSt-50 backbone (train_non-local_mutiConv_resnest.py:204-249) on the HIP path.
+
+Kernel level: split attention and the general average pools against float64 torch CPU
+computations of the reference's ops.  Model level: the ResNeSt trunk and the ResNeSt TMRNet
+(TimeConv head) against oracle/tmrnet_ref.py (resnest50_share / TMRNetRef(backbone=...)) --
+logits within 1e-4 and identical argmax; gradients against the float64 oracle with the same
+criterion as tests/test_model_parity_gpu.py.  The resnest package is absent from the
+reference and from this image, so the ResNeSt restatement itself is "parity unpinned"
+(pinned only by its parameter count and GMAC, tests/test_oracle_cpu.py)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import tmrnet_amd
+from tmrnet_amd import ops
+from tmrnet_amd.resnest import AvgPoolFn, SplAtFn, ResNeSt50Share
+from oracle import tmrnet_ref as ref
+from tests.test_model_parity_gpu import (_assert_vs_fp64, _double_copy, _inputs, rel_err)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", [(2, 56, 56, 64, 3, 2, 1, True, False),
+                                  (2, 56, 56, 256, 2, 2, 0, False, True),
+                                  (3, 7, 7, 32, 3, 1, 1, True, False),
+                                  (2, 15, 13, 8, 2, 2, 0, False, True),    # ragged + ceil
+                                  (2, 15, 13, 8, 3, 2, 1, True, False)])
+def test_avgpool2d(dev, case):
+    n, h, w, c, k, s, p, incl, ceil = case
+    g = torch.Generator().manual_seed(sum(case[:4]))
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    yr = F.avg_pool2d(xr, k, s, p, ceil_mode=ceil, count_include_pad=incl)
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(gy)
+    xd = x.float().permute(0, 2, 3, 1).contiguous().to(dev).requires_grad_(True)
+    y = AvgPoolFn.apply(xd, k, s, p, incl, ceil)
+    assert y.shape[1:3] == yr.shape[2:]
+    y.backward(gy.float().permute(0, 2, 3, 1).contiguous().to(dev))
+    assert rel_err(y.permute(0, 3, 1, 2), yr) < 1e-6
+    assert rel_err(xd.grad.permute(0, 3, 1, 2), xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("n,h,w,C", [(4, 56, 56, 64), (6, 7, 7, 512), (3, 5, 3, 32)])
+def test_split_attention(dev, n, h, w, C):
+    """SplAtFn vs the reference SplAtConv2d tail (after conv+bn0+relu) in float64."""
+    torch.manual_seed(C + h)
+    m = ref.SplAtConv2d(C, C).double().train()
+    x2 = torch.rand(n, 2 * C, h, w, dtype=torch.float64)
+    xr = x2.clone().requires_grad_(True)
+    b = n
+    splits = torch.split(xr, C, dim=1)
+    gap = F.adaptive_avg_pool2d(sum(splits), 1)
+    gap = F.relu(m.bn1(m.fc1(gap)))
+    att = m.fc2(gap).view(b, 1, 2, -1).transpose(1, 2)
+    att = F.softmax(att, dim=1).reshape(b, -1, 1, 1)
+    atts = torch.split(att, C, dim=1)
+    yr = sum(a * s_ for a, s_ in zip(atts, splits))
+    gy = torch.randn(yr.shape, dtype=torch.float64)
+    yr.backward(gy)
+    from tmrnet_amd.resnest import SplAtConv2d
+    md = SplAtConv2d(C, C).to(dev).train()
+    md.load_state_dict({k: v.float() for k, v in m.state_dict().items()}, strict=False)
+    md.bn1.running_mean.zero_(); md.bn1.running_var.fill_(1.0)
+    xd = x2.float().permute(0, 2, 3, 1).contiguous().to(dev).requires_grad_(True)
+    y = SplAtFn.apply(xd, md.fc1.weight, md.fc1.bias, md.bn1.weight, md.bn1.bias, md.fc2.weight,
+                      md.fc2.bias, md.bn1)
+    y.backward(gy.float().permute(0, 2, 3, 1).contiguous().to(dev))
+    assert rel_err(y.permute(0, 3, 1, 2), yr) < 1e-5
+    assert rel_err(xd.grad.permute(0, 3, 1, 2), xr.grad) < 1e-4
+    for name in ("fc1.weight", "fc1.bias", "bn1.weight", "bn1.bias", "fc2.weight", "fc2.bias"):
+        pd = dict(md.named_parameters())[name]
+        pr = dict(m.named_parameters())[name]
+        assert rel_err(pd.grad, pr.grad) < 1e-3, name
+
+
+def test_resnest_trunk_parity(dev):
+    """share = resnest50 children (train_non-local_mutiConv_resnest.py:210-220), train mode."""
+    torch.manual_seed(11)
+    m = ResNeSt50Share().to(dev).train()
+    r = ref.resnest50_share().train()
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    r64 = _double_copy(r, None, 0, 0, 0)
+    g = torch.Generator().manual_seed(12)
+    x = torch.rand(4, 3, 224, 224, generator=g) * 4 - 2
+    feat = m(x.to(dev))
+    feat_r = r(x)
+    assert feat.shape == (4, 2048)
+    assert (feat.detach().cpu() - feat_r.detach()).abs().max().item() < 1e-4 * max(
+        1.0, feat_r.abs().max().item())
+    gy = torch.randn(4, 2048, generator=g)
+    feat.backward(gy.to(dev))
+    feat_r.backward(gy)
+    r64(x.double()).backward(gy.double())
+    grads = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
+    _assert_vs_fp64(grads(m), grads(r), grads(r64), 2e-3, "grad")
+    rb = dict(r.named_buffers())
+    for name, b in m.named_buffers():
+        if b.dtype.is_floating_point:
+            assert rel_err(b, rb[name]) < 1e-4, name
+        else:
+            assert torch.equal(b.cpu(), rb[name]), name
+
+
+def test_resnest_trunk_eval(dev):
+    torch.manual_seed(13)
+    m = ResNeSt50Share().to(dev)
+    for mod in m.modules():     # non-trivial running statistics
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.1, 0.1)
+            mod.running_var.uniform_(0.5, 2.0)
+    m.eval()
+    r = ref.resnest50_share().eval()
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    x = torch.rand(3, 3, 224, 224) * 4 - 2
+    with torch.no_grad():
+        f = m(x.to(dev)).cpu()
+        fr = r(x)
+    assert (f - fr).abs().max().item() < 1e-4 * max(1.0, fr.abs().max().item())
+
+
+def test_tmrnet_resnest_parity(dev):
+    """resnet_lstm of train_non-local_mutiConv_resnest.py (ResNeSt + LSTM + NLBlock + TimeConv),
+    one train-mode step: logits, CE-sum and gradients vs the oracle."""
+    B, T, L = 2, 3, 7
+    torch.manual_seed(14)
+    m = tmrnet_amd.resnet_lstm(seq_len=T, num_classes=7, time_conv=True,
+                               backbone="resnest50").to(dev).train()
+    r = ref.TMRNetRef(seq_len=T, num_classes=7, time_conv=True, backbone="resnest50").train()
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    frames, off, lt, _ = _inputs(B, T, L, seed=15)
+    labels = torch.tensor([1, 5])
+    g = torch.Generator().manual_seed(16)
+    masks = {"nl": (torch.rand(B, 512, generator=g) >= 0.2).float() / 0.8,
+             "head": (torch.rand(B, 512, generator=g) >= 0.5).float() / 0.5}
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    x_ref = ref.crop_normalize_ref(frames, off, T)
+    out = m(x4, lt.to(dev))
+    out_r = r(x_ref.view(B, T, 3, 224, 224), lt, masks=masks)
+    assert (out.detach().cpu() - out_r.detach()).abs().max().item() < 1e-4
+    assert torch.equal(out.detach().cpu().argmax(1), out_r.detach().argmax(1))
+    loss = tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels.to(dev))
+    loss.backward()
+    ref.ce_sum_ref(out_r, labels).backward()
+    m64 = _double_copy(r, masks, B, T, L)
+    out64 = m64(x_ref.double().view(B, T, 3, 224, 224), lt.double(),
+                masks={k: v.double() for k, v in masks.items()})
+    ref.ce_sum_ref(out64, labels).backward()
+    grads = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
+    _assert_vs_fp64(grads(m), grads(r), grads(m64), 2e-3, "grad")

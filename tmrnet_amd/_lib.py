@@ -22,7 +22,8 @@ SZ = ctypes.c_size_t
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
-                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "pad_w")]
+                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "pad_w",
+                 "x_ld", "y_ld")]
 
 
 DP = ctypes.POINTER(ConvDesc)
@@ -54,6 +55,12 @@ SIGNATURES = {
     "tmr_maxpool2d_bwd": [P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd": [P, P, I, I, I, P],
     "tmr_avgpool_bwd": [P, P, I, I, I, P],
+    "tmr_splat_gap": [P, P, I, I, I, P],
+    "tmr_splat_combine": [P, P, P, P, I, I, I, P],
+    "tmr_splat_bwd": [P, P, P, P, I, I, I, P],
+    "tmr_splat_bwd_apply": [P, P, P, P, I, I, I, P],
+    "tmr_avgpool2d_fwd": [P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "tmr_avgpool2d_bwd": [P, P, I, I, I, I, I, I, I, I, I, I, P],
     "tmr_col_sum": [P, I, I, I, P, F, P],
     "tmr_dropout_mask": [P, L, F, U64, U64, P],
     "tmr_ce_sum": [P, P, P, I, I, F, P, P, P, P],

@@ -604,6 +604,10 @@ int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   }
 }
 
+static inline int xld_of(const tmr_conv_desc* d) { return d->x_ld ? d->x_ld : d->c; }
+static inline int yld_of(const tmr_conv_desc* d) { return d->y_ld ? d->y_ld : d->k; }
+static inline long span(long pixels, int ld, int width) { return pixels > 0 ? (pixels - 1) * ld + width : 0; }
+
 static uint32_t clamp_bytes(long elems) {
   long b = elems * 4;
   return b >= 0x80000000L ? 0x80000000u : (uint32_t)b;
@@ -648,10 +652,10 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.oy0 = -d->pad; a.ox0 = -d->pad_w; a.dyr = 1; a.dxs = 1;
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
-  a.lds = d->c; a.ldb = a.K; a.ldc = d->k; a.beta = beta;
-  a.Abytes = clamp_bytes((long)d->n * d->h * d->w * d->c);
+  a.lds = xld_of(d); a.ldb = a.K; a.ldc = yld_of(d); a.beta = beta;
+  a.Abytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
   a.Bbytes = clamp_bytes((long)d->k * a.K);
-  al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0);
+  al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
 }
 
@@ -675,6 +679,7 @@ TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const
   bool al;
   int rc = conv_fwd_args(d, x, w_krsc, nullptr, y, 0.f, a, al);
   if (rc) return rc;
+  TMR_CHECK_ARG(yld_of(d) == d->k, "tmr_conv2d_fwd_bnstats: output must be dense (y_ld == k)");
   const size_t need = (size_t)tmr_conv2d_fwd_stats_parts(d) * d->k * sizeof(float4);
   TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
                 stats_bytes, need);
@@ -713,8 +718,8 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
       a.wr0 = r0 < 0 ? 0 : r0; a.ws0 = s0 < 0 ? 0 : s0; a.wst = st; a.wS = d->s;
       set_grid(a, d->n, hg, wg);
       a.Hs = d->ho; a.Ws = d->wo; a.sy = 1; a.sx = 1;
-      a.lds = d->k; a.ldb = d->r * d->s * d->c; a.ldc = d->c; a.beta = beta;
-      a.Abytes = clamp_bytes((long)d->n * d->ho * d->wo * d->k);
+      a.lds = yld_of(d); a.ldb = d->r * d->s * d->c; a.ldc = xld_of(d); a.beta = beta;
+      a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.lds, d->k));
       a.Bbytes = clamp_bytes((long)d->k * d->r * d->s * d->c);
       if (st == 1) {
         a.osy = 0;
@@ -722,7 +727,7 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
         a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
       }
       if (a.K == 0 && beta == 1.f) continue;  // nothing to add
-      bool al = aligned16(dy) && aligned16(w_krsc) && aligned16(dx);
+      bool al = aligned16(dy) && aligned16(w_krsc) && aligned16(dx) && a.lds % 4 == 0;
       int rc = launch_gemm<MODE_DGRAD>(a, al, 1, stream);
       if (rc) return rc;
     }
@@ -780,11 +785,11 @@ TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float
   a.oy0 = -d->pad; a.ox0 = -d->pad_w; a.dyr = 1; a.dxs = 1;
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
-  a.lds = d->c; a.ldb = d->k; a.ldc = a.N; a.beta = 0.f;
+  a.lds = xld_of(d); a.ldb = yld_of(d); a.ldc = a.N; a.beta = 0.f;
   a.kchunk = kc; a.slab = slab;
-  a.Abytes = clamp_bytes((long)d->n * d->ho * d->wo * d->k);
-  a.Bbytes = clamp_bytes((long)d->n * d->h * d->w * d->c);
-  bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0);
+  a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldb, d->k));
+  a.Bbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
+  bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0) && a.lds % 4 == 0 && a.ldb % 4 == 0;
   int rc = launch_gemm<MODE_WGRAD>(a, al, sp, stream);
   if (rc) return rc;
   long total = (long)d->k * d->r * d->s * c_real;

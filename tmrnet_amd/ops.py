@@ -45,27 +45,41 @@ def _req(t, name, dtype=f32):
     return t
 
 
+def _nhwc_ld(t, name):
+    """Pixel stride of an NHWC tensor or channel-slice view of one (0 when dense)."""
+    if t.is_contiguous():
+        return 0
+    n, h, w, c = t.shape
+    ld = t.stride(2)
+    if t.stride(3) != 1 or t.stride(1) != w * ld or t.stride(0) != h * w * ld:
+        raise RuntimeError("%s must be NHWC or a channel slice of an NHWC tensor" % name)
+    return ld
+
+
 def _empty(shape, like, dtype=f32):
     return torch.empty(shape, dtype=dtype, device=like.device)
 
 
 # ----------------------------------------------------------------- conv / gemm
-def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None):
+def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0):
     pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
     wo = (w + 2 * pad_w - s) // stride + 1
-    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w)
+    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld)
 
 
 def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None, pad_w=None):
-    """x (N,H,W,C) NHWC, w_krsc (K,R,S,C) -> y (N,Ho,Wo,K)."""
-    _req(x, "x"); _req(w_krsc, "w")
+    """x (N,H,W,C) NHWC (or channel-slice view), w_krsc (K,R,S,C) -> y (N,Ho,Wo,K);
+    `out` may be a channel-slice view of a wider NHWC tensor (grouped convolution)."""
+    _req(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
     d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
     if out is None:
         out = _empty((n, d.ho, d.wo, k), x)
+    d.x_ld = _nhwc_ld(x, "x")
+    d.y_ld = _nhwc_ld(out, "out")
     with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
                (n, h, w, c, k, r, stride)):
         call("tmr_conv2d_fwd", ctypes.byref(d), x, w_krsc, bias if bias is not None else None,
@@ -100,8 +114,8 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
 
 
 def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None):
-    """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C)."""
-    _req(dy, "dy"); _req(w_krsc, "w")
+    """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices)."""
+    _req(w_krsc, "w")
     n, ho, wo, k = dy.shape
     k2, r, s, c = w_krsc.shape
     h, w = in_hw
@@ -109,18 +123,21 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None):
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
+    d.x_ld = _nhwc_ld(out, "dx")
+    d.y_ld = _nhwc_ld(dy, "dy")
     with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride)):
         call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
     return out
 
 
 def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None):
-    """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW."""
-    _req(x, "x"); _req(dy, "dy")
+    """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW (x/dy may be channel slices)."""
     n, h, w, c = x.shape
     k = dy.shape[3]
     c_real = c if c_real is None else c_real
     d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
+    d.x_ld = _nhwc_ld(x, "x")
+    d.y_ld = _nhwc_ld(dy, "dy")
     assert (d.ho, d.wo) == tuple(dy.shape[1:3])
     if out is None:
         out = _empty((k, c_real, r, s), x)

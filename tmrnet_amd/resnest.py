@@ -1,0 +1,306 @@
+"""ResNeSt-50 frame encoder (`share` of the ResNeSt TMRNet) on libtmr kernels.
+
+Drop-in for the `share` Sequential of code/Training TMRNet/train_non-local_mutiConv_resnest.py:210-220
+built from the third-party ``resnest50()`` (radix 2, cardinality 1, deep stem of width 32,
+avg_down shortcut, avd pooling on strided blocks): same child names and state_dict keys
+(``share.conv1.0.weight``, ``share.layer1.0.conv2.conv.weight``, ``...conv2.fc1.bias``, ...),
+25,434,240 parameters.
+
+Each stage is an autograd node over HIP kernels, activations NHWC:
+  * ConvBNActFn   -- (grouped) implicit-GEMM conv + BatchNorm (batch stats) + residual + ReLU
+  * SplAtFn       -- split attention: radix-summed GAP, fc1 -> BN -> ReLU -> fc2 GEMMs,
+                     r-softmax and weighted sum (and their backward)
+  * AvgPoolFn / MaxPoolFn / GlobalPoolFn
+Grouped convolutions run one GEMM launch per group on channel slices (pixel strides in
+tmr_conv_desc), so no channel shuffles are materialised.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import call, stream_ptr
+
+
+def _bn_train_or_eval(y, bn, training):
+    k = y.shape[-1]
+    if training:
+        mean, inv, scale, shift = ops.bn_fwd_train(y.view(-1, k), bn.weight.detach(), bn.bias.detach(),
+                                                   bn.running_mean, bn.running_var, bn.momentum, bn.eps)
+        bn.num_batches_tracked.add_(1)
+        return mean, inv, scale, shift
+    scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                      bn.running_var, bn.eps)
+    return None, None, scale, shift
+
+
+class ConvBNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, residual, bn, stride, pad, groups, relu, c_real):
+        x = x.contiguous()
+        n, h, wd, cs = x.shape
+        k, cg, r, s = w.shape
+        kg = k // groups
+        cgs = cs // groups                       # stored channels per group
+        training = bn.training
+        wks = [ops.weight_to_krsc(w.detach()[g * kg:(g + 1) * kg].contiguous(), cpad=cgs)
+               for g in range(groups)]
+        if groups == 1 and training:
+            y, stats, nparts = ops.conv_fwd_bnstats(x, wks[0], stride, pad, c_real=c_real)
+            mean, inv, scale, shift = ops.bn_finalize(stats, nparts, gamma.detach(), beta.detach(),
+                                                      bn.running_mean, bn.running_var, bn.momentum,
+                                                      bn.eps)
+            bn.num_batches_tracked.add_(1)
+        else:
+            ho = (h + 2 * pad - r) // stride + 1
+            wo = (wd + 2 * pad - s) // stride + 1
+            y = torch.empty((n, ho, wo, k), dtype=x.dtype, device=x.device)
+            for g in range(groups):
+                ops.conv_fwd(x[..., g * cgs:(g + 1) * cgs], wks[g], stride, pad,
+                             out=y[..., g * kg:(g + 1) * kg], c_real=min(cg, c_real))
+            mean, inv, scale, shift = _bn_train_or_eval(y, bn, training)
+        z = ops.bn_apply(y, scale, shift, residual.contiguous() if residual is not None else None,
+                         relu)
+        ctx.save_for_backward(x, y, z, mean, inv, gamma, *wks)
+        ctx.cfg = (stride, pad, groups, relu, c_real, residual is not None, r, s)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, y, z, mean, inv, gamma, *wks = ctx.saved_tensors
+        stride, pad, groups, relu, c_real, has_res, r, s = ctx.cfg
+        if mean is None:
+            raise RuntimeError("backward through eval-mode BatchNorm is not supported")
+        dz = dz.contiguous()
+        dy, dres, dg, db = ops.bn_bwd(dz, y, z, mean, inv, gamma.detach(), relu, want_dres=has_res)
+        n, h, wd, cs = x.shape
+        k = y.shape[-1]
+        kg, cgs = k // groups, cs // groups
+        creal_g = min(c_real, cgs)
+        dw = torch.empty((k, creal_g, r, s), dtype=x.dtype, device=x.device)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        for g in range(groups):
+            dyg = dy[..., g * kg:(g + 1) * kg]
+            ops.conv_wgrad(x[..., g * cgs:(g + 1) * cgs], dyg, r, s, stride, pad, c_real=creal_g,
+                           out=dw[g * kg:(g + 1) * kg])
+            if dx is not None:
+                ops.conv_dgrad(dyg, wks[g], (h, wd), stride, pad, out=dx[..., g * cgs:(g + 1) * cgs])
+        return dx, dw, dg, db, dres, None, None, None, None, None, None
+
+
+class SplAtFn(torch.autograd.Function):
+    """Split attention after the grouped conv + bn0 + ReLU: x2 (N,H,W,2C) -> (N,H,W,C)."""
+
+    @staticmethod
+    def forward(ctx, x2, w1, b1, g1, bt1, w2, b2, bn1):
+        x2 = x2.contiguous()
+        n, h, w, c2 = x2.shape
+        C = c2 // 2
+        hw = h * w
+        gap = torch.empty((n, C), dtype=x2.dtype, device=x2.device)
+        call("tmr_splat_gap", x2, gap, n, hw, C, stream_ptr())
+        inter = w1.shape[0]
+        w1d = w1.detach().reshape(inter, C)
+        w2d = w2.detach().reshape(c2, inter)
+        h1 = ops.gemm_nt(gap, w1d, bias=b1.detach())
+        mean, inv, scale, shift = _bn_train_or_eval(h1, bn1, bn1.training)
+        a1 = ops.bn_apply(h1, scale, shift, None, True)
+        zl = ops.gemm_nt(a1, w2d, bias=b2.detach())
+        att = torch.empty((n, c2), dtype=x2.dtype, device=x2.device)
+        out = torch.empty((n, h, w, C), dtype=x2.dtype, device=x2.device)
+        call("tmr_splat_combine", x2, zl, att, out, n, hw, C, stream_ptr())
+        ctx.save_for_backward(x2, gap, h1, a1, att, mean, inv, w1, w2, g1)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, gap, h1, a1, att, mean, inv, w1, w2, g1 = ctx.saved_tensors
+        if mean is None:
+            raise RuntimeError("backward through eval-mode BatchNorm is not supported")
+        dout = dout.contiguous()
+        n, h, w, c2 = x2.shape
+        C = c2 // 2
+        hw = h * w
+        inter = w1.shape[0]
+        dzl = torch.empty((n, c2), dtype=x2.dtype, device=x2.device)
+        call("tmr_splat_bwd", dout, x2, att, dzl, n, hw, C, stream_ptr())
+        dw2 = ops.gemm_tn(dzl, a1).view_as(w2)
+        db2 = ops.col_sum(dzl, n, c2, c2)
+        da1 = ops.gemm_nn(dzl, w2.detach().reshape(c2, inter))
+        dh1, _, dg1, dbt1 = ops.bn_bwd(da1, h1, a1, mean, inv, g1.detach(), True)
+        dw1 = ops.gemm_tn(dh1, gap).view_as(w1)
+        db1 = ops.col_sum(dh1, n, inter, inter)
+        dgap = ops.gemm_nn(dh1, w1.detach().reshape(inter, C))
+        dx2 = torch.empty_like(x2)
+        call("tmr_splat_bwd_apply", dout, att, dgap, dx2, n, hw, C, stream_ptr())
+        return dx2, dw1, db1, dg1, dbt1, dw2, db2, None
+
+
+def _pool_out(h, k, s, p, ceil):
+    if not ceil:
+        return (h + 2 * p - k) // s + 1
+    o = -(-(h + 2 * p - k) // s) + 1
+    if (o - 1) * s >= h + p:   # last window must start inside the input (PyTorch rule)
+        o -= 1
+    return o
+
+
+class AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, incl, ceil):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        ho, wo = _pool_out(h, k, s, p, ceil), _pool_out(w, k, s, p, ceil)
+        y = torch.empty((n, ho, wo, c), dtype=x.dtype, device=x.device)
+        call("tmr_avgpool2d_fwd", x, y, n, h, w, c, ho, wo, k, s, p, int(incl), stream_ptr())
+        ctx.cfg = (n, h, w, c, ho, wo, k, s, p, incl)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c, ho, wo, k, s, p, incl = ctx.cfg
+        dx = torch.empty((n, h, w, c), dtype=dy.dtype, device=dy.device)
+        call("tmr_avgpool2d_bwd", dy.contiguous(), dx, n, h, w, c, ho, wo, k, s, p, int(incl),
+             stream_ptr())
+        return dx, None, None, None, None, None
+
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y, am = ops.maxpool_fwd(x.contiguous())
+        ctx.save_for_backward(am)
+        ctx.hw = (x.shape[1], x.shape[2])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        return ops.maxpool_bwd(dy.contiguous(), am, ctx.hw)
+
+
+class GlobalPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return ops.avgpool_fwd(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ops.avgpool_bwd(dy.contiguous(), ctx.hw)
+
+
+def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=None):
+    return ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, residual, bn, stride, pad, groups,
+                             relu, c_real if c_real is not None else conv.weight.shape[1] * groups)
+
+
+# ------------------------------------------------------------------ modules
+class SplAtConv2d(nn.Module):
+    """resnest SplAtConv2d(radix=2, groups=1, reduction_factor=4): parameter container."""
+
+    def __init__(self, in_channels, channels, stride=1, radix=2):
+        super().__init__()
+        inter = max(in_channels * radix // 4, 32)
+        self.radix, self.channels, self.stride = radix, channels, stride
+        self.conv = nn.Conv2d(in_channels, channels * radix, 3, stride, 1, groups=radix, bias=False)
+        self.bn0 = nn.BatchNorm2d(channels * radix)
+        self.relu = nn.ReLU(inplace=True)
+        self.fc1 = nn.Conv2d(channels, inter, 1, groups=1)
+        self.bn1 = nn.BatchNorm2d(inter)
+        self.fc2 = nn.Conv2d(inter, channels * radix, 1, groups=1)
+
+    def forward(self, x):
+        x2 = conv_bn_act(x, self.conv, self.bn0, self.stride, 1, True, groups=self.radix)
+        return SplAtFn.apply(x2, self.fc1.weight, self.fc1.bias, self.bn1.weight, self.bn1.bias,
+                             self.fc2.weight, self.fc2.bias, self.bn1)
+
+
+class BottleneckS(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, is_first=False):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.avd = stride > 1 or is_first
+        self.avd_stride = stride
+        if self.avd:
+            self.avd_layer = nn.AvgPool2d(3, stride, padding=1)
+            stride = 1
+        self.conv2 = SplAtConv2d(planes, planes, stride=stride)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        out = conv_bn_act(x, self.conv1, self.bn1, 1, 0, True)
+        out = self.conv2(out)
+        if self.avd:
+            out = AvgPoolFn.apply(out, 3, self.avd_stride, 1, True, False)
+        res = x
+        if self.downsample is not None:
+            pool, conv, bn = self.downsample[0], self.downsample[1], self.downsample[2]
+            if pool.kernel_size != 1:
+                res = AvgPoolFn.apply(x, pool.kernel_size, pool.stride, 0, False, True)
+            res = conv_bn_act(res, conv, bn, 1, 0, False)
+        return conv_bn_act(out, self.conv3, self.bn3, 1, 0, True, residual=res)
+
+
+def _make_layer(inplanes, planes, blocks, stride):
+    downsample = None
+    if stride != 1 or inplanes != planes * 4:
+        pool = (nn.AvgPool2d(stride, stride, ceil_mode=True, count_include_pad=False) if stride != 1
+                else nn.AvgPool2d(1, 1, ceil_mode=True, count_include_pad=False))
+        downsample = nn.Sequential(pool, nn.Conv2d(inplanes, planes * 4, 1, bias=False),
+                                   nn.BatchNorm2d(planes * 4))
+    layers = [BottleneckS(inplanes, planes, stride, downsample)]
+    for _ in range(1, blocks):
+        layers.append(BottleneckS(planes * 4, planes))
+    return nn.Sequential(*layers)
+
+
+class GlobalAvgPool2d(nn.Module):
+    def forward(self, x):  # unused (the engine pools NHWC); kept for the module tree
+        raise RuntimeError("use ResNeSt50Share.forward")
+
+
+class ResNeSt50Share(nn.Sequential):
+    def __init__(self):
+        super().__init__()
+        self.add_module("conv1", nn.Sequential(
+            nn.Conv2d(3, 32, 3, 2, 1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+            nn.Conv2d(32, 32, 3, 1, 1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+            nn.Conv2d(32, 64, 3, 1, 1, bias=False)))
+        self.add_module("bn1", nn.BatchNorm2d(64))
+        self.add_module("relu", nn.ReLU(inplace=True))
+        self.add_module("maxpool", nn.MaxPool2d(3, 2, 1))
+        self.add_module("layer1", _make_layer(64, 64, 3, 1))
+        self.add_module("layer2", _make_layer(256, 128, 4, 2))
+        self.add_module("layer3", _make_layer(512, 256, 6, 2))
+        self.add_module("layer4", _make_layer(1024, 512, 3, 2))
+        self.add_module("avgpool", GlobalAvgPool2d())
+        for m in self.modules():   # resnest ResNet.__init__ init
+            if isinstance(m, nn.Conv2d):
+                nk = m.kernel_size[0] * m.kernel_size[1] * m.out_channels
+                m.weight.data.normal_(0, math.sqrt(2.0 / nk))
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+
+    def features_nhwc4(self, x4):
+        c = self.conv1
+        h = conv_bn_act(x4, c[0], c[1], 2, 1, True, c_real=3)
+        h = conv_bn_act(h, c[3], c[4], 1, 1, True)
+        h = conv_bn_act(h, c[6], self.bn1, 1, 1, True)
+        h = MaxPoolFn.apply(h)
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                h = blk(h)
+        return GlobalPoolFn.apply(h)
+
+    def forward(self, x):
+        x = x.reshape(-1, 3, x.shape[-2], x.shape[-1]).contiguous()
+        return self.features_nhwc4(ops.nchw_to_nhwc(x, cpad=4))
