@@ -146,6 +146,14 @@ int tmr_splat_bwd(const float* dout, const float* x, const float* att, float* dz
 /* dx[n,hw,r*C+c] = att_r*dout[n,hw,c] + dgap[n][c]/hw */
 int tmr_splat_bwd_apply(const float* dout, const float* att, const float* dgap, float* dx, int n,
                         int hw, int c, hipStream_t stream);
+/* center[j] = mean_i x[i][j] (double accumulation); xc[i][j] = x[i][j] - center[j].
+ * The fc1 -> BatchNorm of SplAtConv2d runs on centered GAP rows: BN removes any per-channel
+ * constant exactly, and the GAP rows of a batch agree to ~1%, so centering first keeps fp32
+ * rounding relative to the batch spread instead of the magnitude. */
+int tmr_center_cols(const float* x, int rows, int cols, float* center, float* xc,
+                    hipStream_t stream);
+/* y[i] += alpha * x[i] */
+int tmr_axpy(int n, float alpha, const float* x, float* y, hipStream_t stream);
 /* AvgPool2d(k, s, p) NHWC; divisor k*k (count_include_pad) or the number of valid cells */
 int tmr_avgpool2d_fwd(const float* x, float* y, int n, int h, int w, int c, int ho, int wo, int k,
                       int s, int p, int count_include_pad, hipStream_t stream);

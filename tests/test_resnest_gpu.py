@@ -7,6 +7,8 @@ logits within 1e-4 and identical argmax; gradients against the float64 oracle wi
 criterion as tests/test_model_parity_gpu.py.  The resnest package is absent from the
 reference and from this image, so the ResNeSt restatement itself is "parity unpinned"
 (pinned only by its parameter count and GMAC, tests/test_oracle_cpu.py)."""
+import copy
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -15,7 +17,8 @@ import tmrnet_amd
 from tmrnet_amd import ops
 from tmrnet_amd.resnest import AvgPoolFn, SplAtFn, ResNeSt50Share
 from oracle import tmrnet_ref as ref
-from tests.test_model_parity_gpu import (_assert_vs_fp64, _double_copy, _inputs, rel_err)
+from tests.test_model_parity_gpu import (_assert_vs_fp64, _double_copy, _inputs, l2_err,
+                                         rel_err)
 
 pytestmark = pytest.mark.gpu
 
@@ -41,14 +44,17 @@ def test_avgpool2d(dev, case):
     assert rel_err(xd.grad.permute(0, 3, 1, 2), xr.grad) < 1e-6
 
 
-@pytest.mark.parametrize("n,h,w,C", [(4, 56, 56, 64), (6, 7, 7, 512), (3, 5, 3, 32)])
-def test_split_attention(dev, n, h, w, C):
-    """SplAtFn vs the reference SplAtConv2d tail (after conv+bn0+relu) in float64."""
-    torch.manual_seed(C + h)
-    m = ref.SplAtConv2d(C, C).double().train()
-    x2 = torch.rand(n, 2 * C, h, w, dtype=torch.float64)
+def _zero_grad_scales(g64):
+    """fc1.bias feeds batch-stat BatchNorm: its exact gradient is 0; judge it on the scale of
+    the fc1.weight gradient instead of its own (rounding-noise) magnitude."""
+    return {n: g64[n[:-4] + "weight"].double().norm().item()
+            for n in g64 if n.endswith("fc1.bias")}
+
+
+def _splat_ref(m, x2, C, gy):
+    """The reference SplAtConv2d tail (after conv+bn0+relu), in m's dtype."""
     xr = x2.clone().requires_grad_(True)
-    b = n
+    b = x2.shape[0]
     splits = torch.split(xr, C, dim=1)
     gap = F.adaptive_avg_pool2d(sum(splits), 1)
     gap = F.relu(m.bn1(m.fc1(gap)))
@@ -56,22 +62,37 @@ def test_split_attention(dev, n, h, w, C):
     att = F.softmax(att, dim=1).reshape(b, -1, 1, 1)
     atts = torch.split(att, C, dim=1)
     yr = sum(a * s_ for a, s_ in zip(atts, splits))
-    gy = torch.randn(yr.shape, dtype=torch.float64)
     yr.backward(gy)
+    return yr, xr.grad, {n: p.grad for n, p in m.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("n,h,w,C", [(4, 56, 56, 64), (6, 7, 7, 512), (3, 5, 3, 32)])
+def test_split_attention(dev, n, h, w, C):
+    """SplAtFn vs the reference SplAtConv2d tail in float64; the fp32 CPU run of the same
+    module sets the error scale (BN over n rows amplifies rounding when n is tiny)."""
+    torch.manual_seed(C + h)
+    m32 = ref.SplAtConv2d(C, C).train()
+    m64 = copy.deepcopy(m32).double()
+    x2 = torch.rand(n, 2 * C, h, w, dtype=torch.float64)
+    gy = torch.randn(n, C, h, w, dtype=torch.float64)
+    y64, dx64, g64 = _splat_ref(m64, x2, C, gy)
+    y32, dx32, g32 = _splat_ref(m32, x2.float(), C, gy.float())
     from tmrnet_amd.resnest import SplAtConv2d
     md = SplAtConv2d(C, C).to(dev).train()
-    md.load_state_dict({k: v.float() for k, v in m.state_dict().items()}, strict=False)
+    md.load_state_dict(m32.state_dict())
     md.bn1.running_mean.zero_(); md.bn1.running_var.fill_(1.0)
     xd = x2.float().permute(0, 2, 3, 1).contiguous().to(dev).requires_grad_(True)
     y = SplAtFn.apply(xd, md.fc1.weight, md.fc1.bias, md.bn1.weight, md.bn1.bias, md.fc2.weight,
                       md.fc2.bias, md.bn1)
     y.backward(gy.float().permute(0, 2, 3, 1).contiguous().to(dev))
-    assert rel_err(y.permute(0, 3, 1, 2), yr) < 1e-5
-    assert rel_err(xd.grad.permute(0, 3, 1, 2), xr.grad) < 1e-4
-    for name in ("fc1.weight", "fc1.bias", "bn1.weight", "bn1.bias", "fc2.weight", "fc2.bias"):
-        pd = dict(md.named_parameters())[name]
-        pr = dict(m.named_parameters())[name]
-        assert rel_err(pd.grad, pr.grad) < 1e-3, name
+    ok = lambda ours, r32, r64, floor, sc=None: (l2_err(ours, r64, sc)
+                                                 <= max(floor, 3 * l2_err(r32, r64, sc)))
+    assert ok(y.permute(0, 3, 1, 2), y32, y64, 1e-6)
+    assert ok(xd.grad.permute(0, 3, 1, 2), dx32, dx64, 1e-5)
+    sc = _zero_grad_scales(g64)
+    for name, p in md.named_parameters():
+        if name in g64:
+            assert ok(p.grad, g32[name], g64[name], 1e-5, sc.get(name)), name
 
 
 def test_resnest_trunk_parity(dev):
@@ -85,15 +106,19 @@ def test_resnest_trunk_parity(dev):
     x = torch.rand(4, 3, 224, 224, generator=g) * 4 - 2
     feat = m(x.to(dev))
     feat_r = r(x)
+    feat64 = r64(x.double())
     assert feat.shape == (4, 2048)
-    assert (feat.detach().cpu() - feat_r.detach()).abs().max().item() < 1e-4 * max(
-        1.0, feat_r.abs().max().item())
+    # train-mode BN over 4 frames: judge the fp32 error against the float64 oracle, scaled by
+    # the fp32 CPU oracle's own error (same criterion as the gradients below)
+    e_hip = l2_err(feat, feat64)
+    e_cpu = l2_err(feat_r, feat64)
+    assert e_hip < max(1e-5, 3 * e_cpu), (e_hip, e_cpu)
     gy = torch.randn(4, 2048, generator=g)
     feat.backward(gy.to(dev))
     feat_r.backward(gy)
-    r64(x.double()).backward(gy.double())
+    feat64.backward(gy.double())
     grads = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
-    _assert_vs_fp64(grads(m), grads(r), grads(r64), 2e-3, "grad")
+    _assert_vs_fp64(grads(m), grads(r), grads(r64), 2e-3, "grad", _zero_grad_scales(grads(r64)))
     rb = dict(r.named_buffers())
     for name, b in m.named_buffers():
         if b.dtype.is_floating_point:
@@ -149,4 +174,4 @@ def test_tmrnet_resnest_parity(dev):
                 masks={k: v.double() for k, v in masks.items()})
     ref.ce_sum_ref(out64, labels).backward()
     grads = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
-    _assert_vs_fp64(grads(m), grads(r), grads(m64), 2e-3, "grad")
+    _assert_vs_fp64(grads(m), grads(r), grads(m64), 2e-3, "grad", _zero_grad_scales(grads(m64)))

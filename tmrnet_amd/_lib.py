@@ -59,6 +59,8 @@ SIGNATURES = {
     "tmr_splat_combine": [P, P, P, P, I, I, I, P],
     "tmr_splat_bwd": [P, P, P, P, I, I, I, P],
     "tmr_splat_bwd_apply": [P, P, P, P, I, I, I, P],
+    "tmr_center_cols": [P, I, I, P, P, P],
+    "tmr_axpy": [I, F, P, P, P],
     "tmr_avgpool2d_fwd": [P, P, I, I, I, I, I, I, I, I, I, I, P],
     "tmr_avgpool2d_bwd": [P, P, I, I, I, I, I, I, I, I, I, I, P],
     "tmr_col_sum": [P, I, I, I, P, F, P],

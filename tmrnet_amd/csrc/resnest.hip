@@ -18,23 +18,64 @@ int blocks_for(long n) {
   return (int)(b > 0 ? b : 1);
 }
 
+// block shape of the per-frame reductions: `cols` float4 columns (power of two <= 64) x NT/cols rows
+void red_shape(int c4, int& cols, int& chunks) {
+  cols = 1;
+  while (cols * 2 <= c4 && cols < 64) cols *= 2;
+  chunks = (c4 + cols - 1) / cols;
+}
+
+// Per-frame channel reductions over hw pixels.  One block per (frame, chunk of up to 64
+// float4 channel columns): thread (col, row) walks pixels row, row+R, ... with coalesced float4
+// loads and double accumulators, then an LDS tree over the R rows.  The sums feed a BatchNorm
+// over N frames whose inputs differ by ~1% of their magnitude, so fp32 sequential sums
+// (error ~ hw*eps) would be amplified ~100x; double keeps them exact to fp32 rounding.
+struct Red4 { double x, y, z, w; };
+
+__device__ __forceinline__ void red_add(Red4& a, float4 v) { a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w; }
+
+__device__ __forceinline__ void red_fma(Red4& a, float4 g, float4 v) {
+  a.x = fma((double)g.x, (double)v.x, a.x); a.y = fma((double)g.y, (double)v.y, a.y);
+  a.z = fma((double)g.z, (double)v.z, a.z); a.w = fma((double)g.w, (double)v.w, a.w);
+}
+
+// tree-reduce `nacc` Red4 accumulators per thread over the block's rows; result in rows 0
+template <int NACC>
+__device__ __forceinline__ void red_rows(Red4 (&acc)[NACC], Red4* lds, int col, int row, int cols, int rows) {
+  for (int k = 0; k < NACC; ++k) lds[(k * rows + row) * cols + col] = acc[k];
+  __syncthreads();
+  for (int half = rows >> 1; half > 0; half >>= 1) {
+    if (row < half)
+      for (int k = 0; k < NACC; ++k) {
+        Red4& d = lds[(k * rows + row) * cols + col];
+        const Red4 o = lds[(k * rows + row + half) * cols + col];
+        d.x += o.x; d.y += o.y; d.z += o.z; d.w += o.w;
+      }
+    __syncthreads();
+  }
+  for (int k = 0; k < NACC; ++k) acc[k] = lds[(k * rows) * cols + col];
+}
+
 // gap[n][c] = mean_hw (x[n,hw,c] + x[n,hw,C+c]),  x: [n][hw][2C]
 __global__ __launch_bounds__(NT) void splat_gap_k(const float* __restrict__ x, float* __restrict__ gap,
-                                                  int n, int hw, int c4) {
-  const long total = (long)n * c4;
-  const float inv = 1.0f / (float)hw;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int cq = (int)(i % c4);
-    const long nn = i / c4;
-    const float4* px = reinterpret_cast<const float4*>(x) + nn * hw * 2 * c4;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int p = 0; p < hw; ++p) {
-      const float4 a = px[(long)p * 2 * c4 + cq];
-      const float4 b = px[(long)p * 2 * c4 + c4 + cq];
-      s.x += a.x + b.x; s.y += a.y + b.y; s.z += a.z + b.z; s.w += a.w + b.w;
+                                                  int hw, int c4, int cols, int chunks) {
+  __shared__ Red4 lds[NT];
+  const int nn = blockIdx.x / chunks, cq = (blockIdx.x % chunks) * cols + threadIdx.x % cols;
+  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = NT / cols;
+  const bool live = cq < c4;
+  Red4 acc[1] = {{0.0, 0.0, 0.0, 0.0}};
+  const float4* px = reinterpret_cast<const float4*>(x) + (long)nn * hw * 2 * c4;
+  if (live)
+    for (int p = row; p < hw; p += rows) {
+      red_add(acc[0], px[(long)p * 2 * c4 + cq]);
+      red_add(acc[0], px[(long)p * 2 * c4 + c4 + cq]);
     }
-    s.x *= inv; s.y *= inv; s.z *= inv; s.w *= inv;
-    reinterpret_cast<float4*>(gap)[i] = s;
+  red_rows<1>(acc, lds, col, row, cols, rows);
+  if (row == 0 && live) {
+    const double inv = 1.0 / (double)hw;
+    reinterpret_cast<float4*>(gap)[(long)nn * c4 + cq] =
+        make_float4((float)(acc[0].x * inv), (float)(acc[0].y * inv), (float)(acc[0].z * inv),
+                    (float)(acc[0].w * inv));
   }
 }
 
@@ -65,23 +106,32 @@ __global__ __launch_bounds__(NT) void splat_combine_k(const float* __restrict__ 
 // dz[n][r*C+c] from da_r = sum_hw dout * x_r  (softmax backward over the radix pair)
 __global__ __launch_bounds__(NT) void splat_bwd_reduce_k(const float* __restrict__ dout, const float* __restrict__ x,
                                                          const float* __restrict__ att, float* __restrict__ dz,
-                                                         int n, int hw, int C) {
-  const long total = (long)n * C;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int c = (int)(i % C);
-    const long nn = i / C;
-    float d0 = 0.f, d1 = 0.f;
-    const float* g = dout + nn * hw * C + c;
-    const float* xp = x + nn * hw * 2 * C + c;
-    for (int p = 0; p < hw; ++p) {
-      const float gv = g[(long)p * C];
-      d0 = fmaf(gv, xp[(long)p * 2 * C], d0);
-      d1 = fmaf(gv, xp[(long)p * 2 * C + C], d1);
+                                                         int hw, int c4, int cols, int chunks) {
+  __shared__ Red4 lds[2 * NT];
+  const int nn = blockIdx.x / chunks, cq = (blockIdx.x % chunks) * cols + threadIdx.x % cols;
+  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = NT / cols;
+  const bool live = cq < c4;
+  Red4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  const float4* g = reinterpret_cast<const float4*>(dout) + (long)nn * hw * c4;
+  const float4* px = reinterpret_cast<const float4*>(x) + (long)nn * hw * 2 * c4;
+  if (live)
+    for (int p = row; p < hw; p += rows) {
+      const float4 gv = g[(long)p * c4 + cq];
+      red_fma(acc[0], gv, px[(long)p * 2 * c4 + cq]);
+      red_fma(acc[1], gv, px[(long)p * 2 * c4 + c4 + cq]);
     }
-    const float a0 = att[nn * 2 * C + c], a1 = att[nn * 2 * C + C + c];
-    const float dot = a0 * d0 + a1 * d1;
-    dz[nn * 2 * C + c] = a0 * (d0 - dot);
-    dz[nn * 2 * C + C + c] = a1 * (d1 - dot);
+  red_rows<2>(acc, lds, col, row, cols, rows);
+  if (row == 0 && live) {
+    const int C = c4 * 4;
+    const double d0[4] = {acc[0].x, acc[0].y, acc[0].z, acc[0].w};
+    const double d1[4] = {acc[1].x, acc[1].y, acc[1].z, acc[1].w};
+    for (int j = 0; j < 4; ++j) {
+      const long i0 = (long)nn * 2 * C + cq * 4 + j;
+      const double a0 = att[i0], a1 = att[i0 + C];
+      const double dot = a0 * d0[j] + a1 * d1[j];
+      dz[i0] = (float)(a0 * (d0[j] - dot));
+      dz[i0 + C] = (float)(a1 * (d1[j] - dot));
+    }
   }
 }
 
@@ -165,12 +215,47 @@ __global__ __launch_bounds__(NT) void avgpool2d_bwd_k(const float* __restrict__ 
   }
 }
 
+// one thread per column: rows are few (frames), columns <= 512
+__global__ __launch_bounds__(NT) void center_cols_k(const float* __restrict__ x, int rows, int cols,
+                                                    float* __restrict__ center, float* __restrict__ xc) {
+  const int j = blockIdx.x * NT + threadIdx.x;
+  if (j >= cols) return;
+  double s = 0.0;
+  for (int i = 0; i < rows; ++i) s += x[(long)i * cols + j];
+  const float m = (float)(s / (double)rows);
+  center[j] = m;
+  for (int i = 0; i < rows; ++i) xc[(long)i * cols + j] = x[(long)i * cols + j] - m;
+}
+
+__global__ __launch_bounds__(NT) void axpy_k(int n, float alpha, const float* __restrict__ x,
+                                             float* __restrict__ y) {
+  for (int i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) y[i] = fmaf(alpha, x[i], y[i]);
+}
+
 }  // namespace
+
+TMR_API int tmr_center_cols(const float* x, int rows, int cols, float* center, float* xc,
+                            hipStream_t stream) {
+  TMR_CHECK_ARG(rows > 0 && cols > 0, "tmr_center_cols: bad shape %dx%d", rows, cols);
+  hipLaunchKernelGGL(center_cols_k, dim3((cols + NT - 1) / NT), dim3(NT), 0, stream, x, rows, cols,
+                     center, xc);
+  TMR_CHECK_LAUNCH("center_cols");
+  return 0;
+}
+
+TMR_API int tmr_axpy(int n, float alpha, const float* x, float* y, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(axpy_k, dim3(blocks_for(n)), dim3(NT), 0, stream, n, alpha, x, y);
+  TMR_CHECK_LAUNCH("axpy");
+  return 0;
+}
 
 TMR_API int tmr_splat_gap(const float* x, float* gap, int n, int hw, int c, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_splat_gap: channels %d must be a multiple of 4", c);
-  hipLaunchKernelGGL(splat_gap_k, dim3(blocks_for((long)n * c / 4)), dim3(NT), 0, stream, x, gap, n,
-                     hw, c / 4);
+  int cols, chunks;
+  red_shape(c / 4, cols, chunks);
+  hipLaunchKernelGGL(splat_gap_k, dim3(n * chunks), dim3(NT), 0, stream, x, gap, hw, c / 4, cols,
+                     chunks);
   TMR_CHECK_LAUNCH("splat_gap");
   return 0;
 }
@@ -185,8 +270,11 @@ TMR_API int tmr_splat_combine(const float* x, const float* z, float* att, float*
 
 TMR_API int tmr_splat_bwd(const float* dout, const float* x, const float* att, float* dz, int n,
                           int hw, int c, hipStream_t stream) {
-  hipLaunchKernelGGL(splat_bwd_reduce_k, dim3(blocks_for((long)n * c)), dim3(NT), 0, stream, dout, x,
-                     att, dz, n, hw, c);
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_splat_bwd: channels %d must be a multiple of 4", c);
+  int cols, chunks;
+  red_shape(c / 4, cols, chunks);
+  hipLaunchKernelGGL(splat_bwd_reduce_k, dim3(n * chunks), dim3(NT), 0, stream, dout, x, att, dz, hw,
+                     c / 4, cols, chunks);
   TMR_CHECK_LAUNCH("splat_bwd_reduce");
   return 0;
 }

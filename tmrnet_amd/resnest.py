@@ -90,7 +90,13 @@ class ConvBNActFn(torch.autograd.Function):
 
 
 class SplAtFn(torch.autograd.Function):
-    """Split attention after the grouped conv + bn0 + ReLU: x2 (N,H,W,2C) -> (N,H,W,C)."""
+    """Split attention after the grouped conv + bn0 + ReLU: x2 (N,H,W,2C) -> (N,H,W,C).
+
+    Train mode runs fc1 on GAP rows centered over the batch (tmr_center_cols): BatchNorm
+    removes any per-channel constant exactly, so BN(W1 gap + b1) = BN(W1 (gap - c)), while the
+    fp32 error then scales with the batch spread of the GAP rows (~1% of their magnitude)
+    instead of the magnitude.  The running mean gets the removed W1 c + b1 back (tmr_axpy).
+    The same identity makes d b1 exactly zero (sum_n dh1 = 0 under batch-stat BN)."""
 
     @staticmethod
     def forward(ctx, x2, w1, b1, g1, bt1, w2, b2, bn1):
@@ -103,8 +109,20 @@ class SplAtFn(torch.autograd.Function):
         inter = w1.shape[0]
         w1d = w1.detach().reshape(inter, C)
         w2d = w2.detach().reshape(c2, inter)
-        h1 = ops.gemm_nt(gap, w1d, bias=b1.detach())
-        mean, inv, scale, shift = _bn_train_or_eval(h1, bn1, bn1.training)
+        training = bn1.training
+        if training:
+            center = torch.empty((1, C), dtype=x2.dtype, device=x2.device)
+            gap_c = torch.empty_like(gap)
+            call("tmr_center_cols", gap, n, C, center, gap_c, stream_ptr())
+            h1 = ops.gemm_nt(gap_c, w1d)
+            mean, inv, scale, shift = _bn_train_or_eval(h1, bn1, True)
+            shift_back = ops.gemm_nt(center, w1d, bias=b1.detach())      # W1 c + b1
+            call("tmr_axpy", inter, float(bn1.momentum), shift_back, bn1.running_mean,
+                 stream_ptr())
+            gap = gap_c
+        else:
+            h1 = ops.gemm_nt(gap, w1d, bias=b1.detach())
+            mean, inv, scale, shift = _bn_train_or_eval(h1, bn1, False)
         a1 = ops.bn_apply(h1, scale, shift, None, True)
         zl = ops.gemm_nt(a1, w2d, bias=b2.detach())
         att = torch.empty((n, c2), dtype=x2.dtype, device=x2.device)
@@ -129,8 +147,8 @@ class SplAtFn(torch.autograd.Function):
         db2 = ops.col_sum(dzl, n, c2, c2)
         da1 = ops.gemm_nn(dzl, w2.detach().reshape(c2, inter))
         dh1, _, dg1, dbt1 = ops.bn_bwd(da1, h1, a1, mean, inv, g1.detach(), True)
-        dw1 = ops.gemm_tn(dh1, gap).view_as(w1)
-        db1 = ops.col_sum(dh1, n, inter, inter)
+        dw1 = ops.gemm_tn(dh1, gap).view_as(w1)          # gap is centered (see class doc)
+        db1 = torch.zeros((inter,), dtype=x2.dtype, device=x2.device)
         dgap = ops.gemm_nn(dh1, w1.detach().reshape(inter, C))
         dx2 = torch.empty_like(x2)
         call("tmr_splat_bwd_apply", dout, att, dgap, dx2, n, hw, C, stream_ptr())
