@@ -26,7 +26,9 @@ sys.path.insert(0, ROOT)
 MFMA_F32_PEAK_TF = 157.3     # MI355X dense f32 MFMA (guides: 256 CU x 2.4 GHz x 256 FLOP/clk)
 MFMA_BF16_PEAK_TF = 2516.6
 HBM_PEAK_GBS = 8000.0
-GFLOP_PER_FRAME = {"c2": 24.33}
+# algorithmic train-step GFLOP per frame: 3 x 2 x trunk GMAC (fwd, dgrad, wgrad; no stem dgrad)
+# + LSTM/NL/TimeConv/head (oracle.tmrnet_ref.trunk_gmacs_per_frame)
+GFLOP_PER_FRAME = {"resnet50": 24.33, "resnest50": 32.3}
 
 
 def parse():
@@ -42,6 +44,9 @@ def parse():
     ap.add_argument("--conv-table", action="store_true", help="per-launch conv table on stderr")
     ap.add_argument("--cpu-clips", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--model", choices=["resnet50", "resnest50"], default="resnet50",
+                    help="resnest50 = C4 model (ResNeSt50 + TimeConv head, fp32 here); the "
+                         "metric line is defined on resnet50")
     return ap.parse_args()
 
 
@@ -87,7 +92,11 @@ def main():
     from oracle.tmrnet_ref import sgd_param_groups
 
     torch.manual_seed(0)
-    model = tmrnet_amd.resnet_lstm(seq_len=args.seq).to(dev).train()
+    if args.model == "resnet50":
+        model = tmrnet_amd.resnet_lstm(seq_len=args.seq).to(dev).train()
+    else:
+        model = tmrnet_amd.resnet_lstm(seq_len=args.seq, time_conv=True,
+                                       backbone="resnest50").to(dev).train()
     lr = 5e-7  # reference default (-l 5e-7), groups at lr/10 and lr (:646-655)
     opt = tmrnet_amd.SGD(sgd_param_groups(model, lr), lr=lr / 10, momentum=0.9,
                          weight_decay=5e-4)
@@ -133,6 +142,7 @@ def main():
 
     # ---- live roofline of the dominant kernel family (implicit-GEMM conv) ----
     roof = None
+    traffic = load_traffic(args.model)
     if not args.no_roofline:
         ops.PROF = []
         torch.cuda.synchronize()
@@ -142,24 +152,30 @@ def main():
         recs, ops.PROF = ops.PROF, None
         tot_ms = sum(r[2].elapsed_time(r[3]) for r in recs)
         tot_flops = sum(r[1] for r in recs)
+        tot_bytes = sum(r[5] for r in recs)
         if args.conv_table and rank == 0:
-            for kind, f, e0, e1, shp in recs:
+            for kind, f, e0, e1, shp, _ in recs:
                 t = e0.elapsed_time(e1)
                 print("%-10s %-34s %8.3f ms %7.1f TF" % (kind, shp, t, f / (t * 1e-3) / 1e12),
                       file=sys.stderr)
         achieved = tot_flops / (tot_ms * 1e-3) / 1e12
         per_kind = {}
-        for kind, f, e0, e1, _ in recs:
+        for kind, f, e0, e1, _, _ in recs:
             a = per_kind.setdefault(kind, [0, 0.0, 0.0])
             a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
         roof = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, f32 MFMA)",
                 "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(achieved / MFMA_F32_PEAK_TF, 4), "traffic": None,
+                "frac": round(achieved / MFMA_F32_PEAK_TF, 4),
+                # HBM bytes per conv call (PMC, per step / calls per step), same unit as achieved
+                "traffic": int(traffic["hbm_bytes_per_step"] / len(recs)) if traffic else None,
+                "traffic_source": traffic.get("source") if traffic else None,
+                "alg_bytes_per_launch": int(tot_bytes / max(1, len(recs))),
+                "flops_per_launch": int(tot_flops / max(1, len(recs))),
                 "launches": len(recs), "avg_launch_ms": round(tot_ms / max(1, len(recs)), 4),
                 "conv_ms_per_step": round(tot_ms, 2),
                 "per_kind": {k: {"launches": v[0], "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
                                  "ms": round(v[2], 2)} for k, v in per_kind.items()},
-                "step_mfma_frac": round(fps / world * GFLOP_PER_FRAME["c2"] * 1e9 /
+                "step_mfma_frac": round(fps / world * GFLOP_PER_FRAME.get(args.model, 0.0) * 1e9 /
                                         (MFMA_F32_PEAK_TF * 1e12), 4)}
 
     cpu = None
@@ -168,13 +184,19 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "train frames/sec, TMRNet ResNet50 seq=10 LFB=40",
+            "metric": ("train frames/sec, TMRNet ResNet50 seq=10 LFB=40" if args.model == "resnet50"
+                       else "train frames/sec, TMRNet ResNeSt50+TimeConv seq=10 LFB=40 (fp32)"),
             "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (uint8 250x250x3 frames, U(-1,1) LFB bank 99640x512, random-init weights)",
-            "config": {"workload": "C2/C3: TMRNet ResNet50+LSTM+NLBlock train step",
-                       "model": "resnet_lstm (train_only_non-local_pretrained)",
+            "config": {"workload": ("C2/C3: TMRNet ResNet50+LSTM+NLBlock train step"
+                                    if args.model == "resnet50" else
+                                    "C4 model at fp32: TMRNet ResNeSt50+LSTM+NLBlock+TimeConv "
+                                    "train step"),
+                       "model": ("resnet_lstm (train_only_non-local_pretrained)"
+                                 if args.model == "resnet50" else
+                                 "resnet_lstm (train_non-local_mutiConv_resnest)"),
                        "global_batch": B * world, "clips_per_gpu": B, "seq_len": T, "lfb_len": L,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
             "loss_last": loss_v,
@@ -186,6 +208,25 @@ def main():
         dist.destroy_process_group()
 
 
+def load_traffic(model):
+    """HBM bytes of the conv kernels per step from the committed rocprofv3 PMC passes of this
+    workload (scripts/pmc.sh -> scripts/pmc_summary.py -> profiles/<round>/pmc_traffic_<model>.json:
+    FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE of gemm_kernel + wgrad_reduce_kernel
+    launches, per train step).  None when no PMC pass has been committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_%s.json" % model)))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    fams = d.get("families", {})
+    if "gemm_kernel" not in fams:
+        return None
+    per_step = sum(fams[k]["hbm_bytes_per_step"] for k in ("gemm_kernel", "wgrad_reduce_kernel")
+                   if k in fams)
+    return {"hbm_bytes_per_step": per_step, "source": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(args):
     """The CPU oracle (pure-torch restatement of the reference step) on the host cores."""
     from oracle import tmrnet_ref as ref
@@ -193,7 +234,8 @@ def cpu_baseline(args):
     torch.set_num_threads(threads)
     B, T, L = args.cpu_clips, args.seq, args.lfb
     torch.manual_seed(0)
-    m = ref.TMRNetRef(seq_len=T).train()
+    m = ref.TMRNetRef(seq_len=T, time_conv=(args.model == "resnest50"),
+                      backbone=args.model).train()
     opt = torch.optim.SGD(ref.sgd_param_groups(m, 5e-7), lr=5e-8, momentum=0.9, weight_decay=5e-4)
     g = torch.Generator().manual_seed(1)
     frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8)

@@ -13,13 +13,15 @@ import ctypes
 f32 = torch.float32
 
 # Optional live instrumentation (bench.py): when a list, every conv launch appends
-# (kind, algorithmic_flops, start_event, end_event) recorded on the launching stream.
+# (kind, algorithmic_flops, start_event, end_event, shape, algorithmic_bytes) recorded on the
+# launching stream.  Algorithmic bytes = each operand read once + the output written once
+# (+ read once more when accumulating with beta != 0).
 PROF = None
 
 
 class _prof:
-    def __init__(self, kind, flops, shape=None):
-        self.kind, self.flops, self.shape = kind, flops, shape
+    def __init__(self, kind, flops, shape=None, nbytes=0):
+        self.kind, self.flops, self.shape, self.nbytes = kind, flops, shape, nbytes
 
     def __enter__(self):
         if PROF is not None:
@@ -31,7 +33,7 @@ class _prof:
     def __exit__(self, *a):
         if PROF is not None:
             self.e1.record()
-            PROF.append((self.kind, self.flops, self.e0, self.e1, self.shape))
+            PROF.append((self.kind, self.flops, self.e0, self.e1, self.shape, self.nbytes))
         return False
 
 
@@ -80,8 +82,10 @@ def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None,
         out = _empty((n, d.ho, d.wo, k), x)
     d.x_ld = _nhwc_ld(x, "x")
     d.y_ld = _nhwc_ld(out, "out")
+    ysz = n * d.ho * d.wo * k
     with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
-               (n, h, w, c, k, r, stride)):
+               (n, h, w, c, k, r, stride),
+               4 * (n * h * w * c + k * r * s * c + ysz * (2 if beta else 1))):
         call("tmr_conv2d_fwd", ctypes.byref(d), x, w_krsc, bias if bias is not None else None,
              out, float(beta), stream_ptr())
     return out
@@ -98,7 +102,8 @@ def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None):
     nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
     with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
-               (n, h, w, c, k, r, stride)):
+               (n, h, w, c, k, r, stride),
+               4 * (n * h * w * c + k * r * s * c + n * d.ho * d.wo * k) + stats.numel() * 4):
         call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
              ctypes.c_size_t(stats.numel() * 4), stream_ptr())
     return out, stats, nparts
@@ -125,7 +130,8 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None):
         out = _empty((n, h, w, c), dy)
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
-    with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride)):
+    with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
+               4 * (n * ho * wo * k + k * r * s * c + n * h * w * c * (2 if beta else 1))):
         call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
     return out
 
@@ -144,7 +150,8 @@ def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=
     ws_bytes = query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d))
     ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
     with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * c_real,
-               (n, h, w, c, k, r, stride)):
+               (n, h, w, c, k, r, stride),
+               4 * (n * h * w * c + n * d.ho * d.wo * k + k * r * s * c_real)):
         call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,
              ctypes.c_size_t(ws.numel() * 4), stream_ptr())
     return out
