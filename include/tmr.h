@@ -115,11 +115,15 @@ int tmr_bn_eval_params(const float* gamma, const float* beta, const float* runni
 int tmr_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
                  float* z, int rows, int c, int relu, hipStream_t stream);
 /* backward of z = act(bn(y) (+res)): dy, optional dres (= grad at the pre-activation),
- * dgamma, dbeta.  z is the saved output (ReLU mask z>0); NULL when relu==0. */
-int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* save_mean,
-               const float* save_invstd, const float* gamma, float* dy, float* dres,
-               float* dgamma, float* dbeta, int rows, int c, int relu, void* ws, size_t ws_bytes,
-               hipStream_t stream);
+ * dgamma, dbeta.  ReLU mask: z > 0 from the saved output z when z != NULL, otherwise
+ * y*scale+shift > 0 recomputed from the forward's scale/shift (valid without a residual;
+ * saves one full read of z).  z/scale/shift unused when relu == 0.  dres may alias dz: the
+ * first pass then overwrites dz with the masked gradient (the residual branch's gradient, in
+ * place) and the second pass reads it back without re-reading the mask source. */
+int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* scale,
+               const float* shift, const float* save_mean, const float* save_invstd,
+               const float* gamma, float* dy, float* dres, float* dgamma, float* dbeta, int rows,
+               int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* ---------------- pooling (pool_layout.hip) --------------------------------------- */
 /* MaxPool2d(3,2,1) of share.maxpool (train_only_non-local_pretrained.py:207), NHWC */

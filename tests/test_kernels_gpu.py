@@ -109,6 +109,19 @@ def test_batchnorm(dev, rows, c, relu, res):
     assert rel_err(dy, yr.grad) < 1e-5
     assert rel_err(dgm, gr.grad) < 1e-5
     assert rel_err(dbt, br.grad) < 1e-5
+    if res:
+        # dres aliasing dz: masked gradient written in place, same dy / dres / dgamma / dbeta
+        dzi = dz.float().to(dev)
+        dy3, dres3, dgm3, dbt3 = ops.bn_bwd(dzi, yd, z, mean, inv, gamma.float().to(dev), relu,
+                                            want_dres=True, dres_out=dzi)
+        assert dres3.data_ptr() == dzi.data_ptr()
+        assert torch.equal(dres3, dres) and torch.equal(dy3, dy)
+        assert torch.equal(dgm3, dgm) and torch.equal(dbt3, dbt)
+    if relu and not res:
+        # mask recomputed from y*scale+shift instead of reading z: bit-identical results
+        dy2, _, dgm2, dbt2 = ops.bn_bwd(dz.float().to(dev), yd, None, mean, inv,
+                                        gamma.float().to(dev), relu, scale=scale, shift=shift)
+        assert torch.equal(dy2, dy) and torch.equal(dgm2, dgm) and torch.equal(dbt2, dbt)
 
 
 def test_pools(dev):

@@ -50,7 +50,7 @@ SIGNATURES = {
     "tmr_bn_finalize": [P, I, I, P, P, P, P, F, F, P, P, P, P, P],
     "tmr_bn_eval_params": [P, P, P, P, F, I, P, P, P],
     "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
-    "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
+    "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_maxpool2d_fwd": [P, P, P, I, I, I, I, I, I, P],
     "tmr_maxpool2d_bwd": [P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd": [P, P, I, I, I, P],

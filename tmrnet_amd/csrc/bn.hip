@@ -165,15 +165,37 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, co
   }
 }
 
-template <bool RELU>
-__global__ __launch_bounds__(NT) void bn_bwd_partial(const float* __restrict__ dz, const float* __restrict__ y,
+// ReLU mask of the backward: MASK 0 = none, 1 = saved output z > 0, 2 = recomputed
+// fmaf(y, scale, shift) > 0 (bit-identical to the forward's z > 0 when there is no residual,
+// and saves reading z)
+__device__ __forceinline__ float4 relu_mask4(float4 g, float4 m) {
+  g.x = m.x > 0.f ? g.x : 0.f; g.y = m.y > 0.f ? g.y : 0.f;
+  g.z = m.z > 0.f ? g.z : 0.f; g.w = m.w > 0.f ? g.w : 0.f;
+  return g;
+}
+__device__ __forceinline__ float4 affine4(float4 v, float4 sc, float4 sf) {
+  return make_float4(fmaf(v.x, sc.x, sf.x), fmaf(v.y, sc.y, sf.y), fmaf(v.z, sc.z, sf.z),
+                     fmaf(v.w, sc.w, sf.w));
+}
+
+// WB: write the masked gradient back over dz (dres aliasing dz: the identity branch of a
+// residual block takes the masked gradient in place, and the apply pass needs no mask)
+template <int MASK, bool WB = false>
+__global__ __launch_bounds__(NT) void bn_bwd_partial(float* dz, const float* __restrict__ y,
                                                      const float* __restrict__ z,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift,
                                                      const float* __restrict__ mean, int rows, int c,
                                                      int rpb, int cthreads, double* __restrict__ part) {
   const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
   const int rthreads = NT / cthreads;
   const int ch = (blockIdx.y * cthreads + tc) * 4;
   const float4 mu = *reinterpret_cast<const float4*>(mean + ch);
+  float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sf = sc;
+  if (MASK == 2) {
+    sc = *reinterpret_cast<const float4*>(scale + ch);
+    sf = *reinterpret_cast<const float4*>(shift + ch);
+  }
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(rows, r0 + rpb);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
@@ -181,11 +203,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const float* __restrict__ d
     const long o = (long)r * c + ch;
     float4 g = *reinterpret_cast<const float4*>(dz + o);
     const float4 v = *reinterpret_cast<const float4*>(y + o);
-    if (RELU) {
-      const float4 zz = *reinterpret_cast<const float4*>(z + o);
-      g.x = zz.x > 0.f ? g.x : 0.f; g.y = zz.y > 0.f ? g.y : 0.f;
-      g.z = zz.z > 0.f ? g.z : 0.f; g.w = zz.w > 0.f ? g.w : 0.f;
-    }
+    if (MASK == 1) g = relu_mask4(g, *reinterpret_cast<const float4*>(z + o));
+    if (MASK == 2) g = relu_mask4(g, affine4(v, sc, sf));
+    if (WB) *reinterpret_cast<float4*>(dz + o) = g;
     s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
     q.x = fmaf(g.x, v.x - mu.x, q.x); q.y = fmaf(g.y, v.y - mu.y, q.y);
     q.z = fmaf(g.z, v.z - mu.z, q.z); q.w = fmaf(g.w, v.w - mu.w, q.w);
@@ -245,9 +265,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
   }
 }
 
-template <bool RELU, bool DRES>
+template <int MASK, bool DRES>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const float* __restrict__ y,
                                                    const float* __restrict__ z,
+                                                   const float* __restrict__ scale,
+                                                   const float* __restrict__ shift,
                                                    const float* __restrict__ coef, float* __restrict__ dy,
                                                    float* __restrict__ dres, long n4, int c4) {
   const int c = c4 * 4;
@@ -255,11 +277,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
     const int cc = (int)(i % c4) * 4;
     float4 g = reinterpret_cast<const float4*>(dz)[i];
     const float4 v = reinterpret_cast<const float4*>(y)[i];
-    if (RELU) {
-      const float4 zz = reinterpret_cast<const float4*>(z)[i];
-      g.x = zz.x > 0.f ? g.x : 0.f; g.y = zz.y > 0.f ? g.y : 0.f;
-      g.z = zz.z > 0.f ? g.z : 0.f; g.w = zz.w > 0.f ? g.w : 0.f;
-    }
+    if (MASK == 1) g = relu_mask4(g, reinterpret_cast<const float4*>(z)[i]);
+    if (MASK == 2)
+      g = relu_mask4(g, affine4(v, *reinterpret_cast<const float4*>(scale + cc),
+                                *reinterpret_cast<const float4*>(shift + cc)));
     if (DRES) reinterpret_cast<float4*>(dres)[i] = g;
     const float4 A = *reinterpret_cast<const float4*>(coef + cc);
     const float4 B = *reinterpret_cast<const float4*>(coef + c + cc);
@@ -340,21 +361,37 @@ TMR_API int tmr_bn_apply(const float* y, const float* scale, const float* shift,
   return 0;
 }
 
-TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* save_mean,
-                       const float* save_invstd, const float* gamma, float* dy, float* dres,
-                       float* dgamma, float* dbeta, int rows, int c, int relu, void* ws,
-                       size_t ws_bytes, hipStream_t stream) {
+TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* scale,
+                       const float* shift, const float* save_mean, const float* save_invstd,
+                       const float* gamma, float* dy, float* dres, float* dgamma, float* dbeta,
+                       int rows, int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0 && c >= 4, "tmr_bn_bwd: channels %d must be a multiple of 4", c);
   TMR_CHECK_ARG(rows > 0, "tmr_bn_bwd: empty input");
   TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd: workspace too small");
-  TMR_CHECK_ARG(!relu || z, "tmr_bn_bwd: relu backward needs the saved output z");
+  TMR_CHECK_ARG(!relu || z || (scale && shift),
+                "tmr_bn_bwd: relu backward needs the saved output z or the forward scale/shift");
+  int mask = relu ? (z ? 1 : 2) : 0;
   Plan p = make_plan(rows, c);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
-  if (relu)
-    hipLaunchKernelGGL((bn_bwd_partial<true>), dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, dz, y, z, save_mean, rows, c, p.rpb, p.cthreads, part);
+  const dim3 pg(p.nrb, p.cblocks);
+  float* dzw = const_cast<float*>(dz);
+  if (dres == dz) {
+    // in-place identity-branch gradient: pass 1 masks dz itself, pass 2 reads it unmasked
+    if (mask == 1)
+      hipLaunchKernelGGL((bn_bwd_partial<1, true>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+    else if (mask == 2)
+      hipLaunchKernelGGL((bn_bwd_partial<2, true>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+    else
+      hipLaunchKernelGGL((bn_bwd_partial<0>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+    mask = 0;
+    dres = nullptr;
+  } else if (mask == 1)
+    hipLaunchKernelGGL((bn_bwd_partial<1>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  else if (mask == 2)
+    hipLaunchKernelGGL((bn_bwd_partial<2>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
   else
-    hipLaunchKernelGGL((bn_bwd_partial<false>), dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, dz, y, z, save_mean, rows, c, p.rpb, p.cthreads, part);
+    hipLaunchKernelGGL((bn_bwd_partial<0>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
   TMR_CHECK_LAUNCH("bn_bwd_partial");
   hipLaunchKernelGGL(bn_bwd_final, dim3(cdiv(c, 8)), dim3(NT), 0, stream, part, p.nrb, rows, c,
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
@@ -362,13 +399,15 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
   long n4 = (long)rows * c / 4;
   int nb = ew_blocks(n4);
   int c4 = c / 4;
-  if (relu) {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
-    else hipLaunchKernelGGL((bn_bwd_apply<true, false>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
+#define TMR_BN_APPLY(M, D)                                                                        \
+  hipLaunchKernelGGL((bn_bwd_apply<M, D>), dim3(nb), dim3(NT), 0, stream, dz, y, z, scale, shift, \
+                     coef, dy, dres, n4, c4)
+  if (dres) {
+    if (mask == 1) TMR_BN_APPLY(1, true); else if (mask == 2) TMR_BN_APPLY(2, true); else TMR_BN_APPLY(0, true);
   } else {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply<false, true>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
-    else hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(nb), dim3(NT), 0, stream, dz, y, z, coef, dy, dres, n4, c4);
+    if (mask == 1) TMR_BN_APPLY(1, false); else if (mask == 2) TMR_BN_APPLY(2, false); else TMR_BN_APPLY(0, false);
   }
+#undef TMR_BN_APPLY
   TMR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }

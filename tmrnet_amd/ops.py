@@ -282,7 +282,10 @@ def bn_apply(y, scale, shift, residual=None, relu=True, out=None):
     return out
 
 
-def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None):
+def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None, scale=None,
+           shift=None):
+    """ReLU mask from the saved output z, or (z=None) recomputed from y with the forward's
+    scale/shift -- only valid when the forward had no residual."""
     c = y.shape[-1]
     rows = y.numel() // c
     ws, nb = _bn_ws(rows, c, y.device)
@@ -291,8 +294,8 @@ def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None):
     if want_dres:
         dres = torch.empty_like(y) if dres_out is None else dres_out
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)
-    call("tmr_bn_bwd", dz, y, z if relu else None, mean, inv, gamma, dy, dres, dgamma, dbeta,
-         rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
+    call("tmr_bn_bwd", dz, y, z if relu else None, scale, shift, mean, inv, gamma, dy, dres,
+         dgamma, dbeta, rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
     return dy, dres, dgamma, dbeta
 
 

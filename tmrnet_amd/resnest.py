@@ -62,18 +62,21 @@ class ConvBNActFn(torch.autograd.Function):
             mean, inv, scale, shift = _bn_train_or_eval(y, bn, training)
         z = ops.bn_apply(y, scale, shift, residual.contiguous() if residual is not None else None,
                          relu)
-        ctx.save_for_backward(x, y, z, mean, inv, gamma, *wks)
+        # without a residual the backward recomputes the ReLU mask from y and scale/shift
+        ctx.save_for_backward(x, y, z if residual is not None else None, scale, shift, mean, inv,
+                              gamma, *wks)
         ctx.cfg = (stride, pad, groups, relu, c_real, residual is not None, r, s)
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        x, y, z, mean, inv, gamma, *wks = ctx.saved_tensors
+        x, y, z, scale, shift, mean, inv, gamma, *wks = ctx.saved_tensors
         stride, pad, groups, relu, c_real, has_res, r, s = ctx.cfg
         if mean is None:
             raise RuntimeError("backward through eval-mode BatchNorm is not supported")
         dz = dz.contiguous()
-        dy, dres, dg, db = ops.bn_bwd(dz, y, z, mean, inv, gamma.detach(), relu, want_dres=has_res)
+        dy, dres, dg, db = ops.bn_bwd(dz, y, z, mean, inv, gamma.detach(), relu, want_dres=has_res,
+                                      scale=scale, shift=shift)
         n, h, wd, cs = x.shape
         k = y.shape[-1]
         kg, cgs = k // groups, cs // groups

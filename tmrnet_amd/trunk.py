@@ -79,16 +79,24 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None)
                                           bn.running_var, bn.eps)
     z = ops.bn_apply(y, scale, shift, residual, relu)
     if recs is not None:
-        recs.append({"x": x, "wk": wk, "y": y, "z": z, "mean": mean, "inv": inv,
+        # without a residual the backward recomputes the ReLU mask from y (scale/shift)
+        recs.append({"x": x, "wk": wk, "y": y, "z": z if residual is not None else None,
+                     "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
                      "c_real": c})
     return z
 
 
-def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True):
+def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
+                 dres_inplace=False):
+    """BN backward (ReLU mask from the saved z, or recomputed from y when there was no
+    residual), wgrad, dgrad (optionally accumulated into dx_out).  dres_inplace: the
+    pre-activation gradient (the identity branch's) overwrites dz and is returned as dres."""
     conv, bn = rec["conv"], rec["bn"]
     dy, dres, dg, db = ops.bn_bwd(dz, rec["y"], rec["z"], rec["mean"], rec["inv"],
-                                  bn.weight.detach(), rec["relu"], want_dres=want_dres)
+                                  bn.weight.detach(), rec["relu"], want_dres=want_dres,
+                                  dres_out=dz if dres_inplace else None,
+                                  scale=rec["scale"], shift=rec["shift"])
     grads[bn.weight] = dg
     grads[bn.bias] = db
     x = rec["x"]
@@ -145,7 +153,7 @@ class TrunkFn(torch.autograd.Function):
         if not ctx.keep:
             raise RuntimeError("trunk backward needs train mode and a forward with grad enabled")
         grads = {}
-        dh = ops.avgpool_bwd(dfeat.contiguous(), ctx.last_hw)
+        g = ops.avgpool_bwd(dfeat.contiguous(), ctx.last_hw)   # grad at the last block output
         blocks = ctx.blocks
         while blocks:
             blk, brec = blocks.pop()
@@ -153,7 +161,8 @@ class TrunkFn(torch.autograd.Function):
             r1, r2 = brec[0], brec[1]
             rd = brec[2] if has_ds else None
             r3 = brec[-1]
-            dz2, dres = _conv_bn_bwd(r3, dh, grads, want_dres=True)
+            # g (owned here) becomes the masked pre-ReLU gradient = the identity-branch grad
+            dz2, dres = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True)
             dz1, _ = _conv_bn_bwd(r2, dz2, grads)
             del dz2
             if has_ds:
@@ -161,8 +170,9 @@ class TrunkFn(torch.autograd.Function):
                 _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0)
             else:
                 dx, _ = _conv_bn_bwd(r1, dz1, grads, dx_out=dres, dx_beta=1.0)
-            del dz1, brec
-            dh = dx
+            del dz1, brec, dres
+            g = dx
+        dh = g
         am, stem_hw = ctx.pool
         dz = ops.maxpool_bwd(dh, am, stem_hw)
         _conv_bn_bwd(ctx.stem[0], dz, grads, need_dx=False)
