@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--model", choices=["resnet50", "resnest50"], default="resnet50",
                     help="resnest50 = C4 model (ResNeSt50 + TimeConv head, fp32 here); the "
                          "metric line is defined on resnet50")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="trunk conv operand precision (bf16 = configs C4/C5; the metric "
+                         "line's config C2 is fp32)")
     return ap.parse_args()
 
 
@@ -93,10 +96,10 @@ def main():
 
     torch.manual_seed(0)
     if args.model == "resnet50":
-        model = tmrnet_amd.resnet_lstm(seq_len=args.seq).to(dev).train()
+        model = tmrnet_amd.resnet_lstm(seq_len=args.seq, precision=args.precision).to(dev).train()
     else:
-        model = tmrnet_amd.resnet_lstm(seq_len=args.seq, time_conv=True,
-                                       backbone="resnest50").to(dev).train()
+        model = tmrnet_amd.resnet_lstm(seq_len=args.seq, time_conv=True, backbone="resnest50",
+                                       precision=args.precision).to(dev).train()
     lr = 5e-7  # reference default (-l 5e-7), groups at lr/10 and lr (:646-655)
     opt = tmrnet_amd.SGD(sgd_param_groups(model, lr), lr=lr / 10, momentum=0.9,
                          weight_decay=5e-4)
@@ -142,7 +145,7 @@ def main():
 
     # ---- live roofline of the dominant kernel family (implicit-GEMM conv) ----
     roof = None
-    traffic = load_traffic(args.model)
+    traffic = load_traffic(args.model + ("" if args.precision == "fp32" else "_bf16"))
     if not args.no_roofline:
         ops.PROF = []
         torch.cuda.synchronize()
@@ -163,9 +166,12 @@ def main():
         for kind, f, e0, e1, _, _ in recs:
             a = per_kind.setdefault(kind, [0, 0.0, 0.0])
             a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
-        roof = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, f32 MFMA)",
-                "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(achieved / MFMA_F32_PEAK_TF, 4),
+        peak = MFMA_F32_PEAK_TF if args.precision == "fp32" else MFMA_BF16_PEAK_TF
+        roof = {"bound": "mfma",
+                "kernel": "gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA)"
+                          % ("f32" if args.precision == "fp32" else "bf16 operands, f32 acc"),
+                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
                 # HBM bytes per conv call (PMC, per step / calls per step), same unit as achieved
                 "traffic": int(traffic["hbm_bytes_per_step"] / len(recs)) if traffic else None,
                 "traffic_source": traffic.get("source") if traffic else None,
@@ -176,7 +182,7 @@ def main():
                 "per_kind": {k: {"launches": v[0], "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
                                  "ms": round(v[2], 2)} for k, v in per_kind.items()},
                 "step_mfma_frac": round(fps / world * GFLOP_PER_FRAME.get(args.model, 0.0) * 1e9 /
-                                        (MFMA_F32_PEAK_TF * 1e12), 4)}
+                                        (peak * 1e12), 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -184,16 +190,14 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": ("train frames/sec, TMRNet ResNet50 seq=10 LFB=40" if args.model == "resnet50"
-                       else "train frames/sec, TMRNet ResNeSt50+TimeConv seq=10 LFB=40 (fp32)"),
+            "metric": ("train frames/sec, TMRNet ResNet50 seq=%d LFB=%d" % (T, L)
+                       if args.model == "resnet50" else
+                       "train frames/sec, TMRNet ResNeSt50+TimeConv seq=%d LFB=%d" % (T, L)),
             "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (uint8 250x250x3 frames, U(-1,1) LFB bank 99640x512, random-init weights)",
-            "config": {"workload": ("C2/C3: TMRNet ResNet50+LSTM+NLBlock train step"
-                                    if args.model == "resnet50" else
-                                    "C4 model at fp32: TMRNet ResNeSt50+LSTM+NLBlock+TimeConv "
-                                    "train step"),
+            "config": {"workload": workload_name(args),
                        "model": ("resnet_lstm (train_only_non-local_pretrained)"
                                  if args.model == "resnet50" else
                                  "resnet_lstm (train_non-local_mutiConv_resnest)"),
@@ -206,6 +210,16 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def workload_name(args):
+    if args.model == "resnest50":
+        return ("C4: TMRNet ResNeSt50+LSTM+NLBlock+TimeConv train step, %s convs"
+                % args.precision)
+    if args.precision == "bf16" or args.seq != 10 or args.lfb != 40:
+        return ("C5-style: TMRNet ResNet50+LSTM+NLBlock train step, seq %d, LFB %d, %s convs"
+                % (args.seq, args.lfb, args.precision))
+    return "C2/C3: TMRNet ResNet50+LSTM+NLBlock train step"
 
 
 def load_traffic(model):

@@ -46,7 +46,13 @@ typedef struct tmr_conv_desc {
   int pad_w;              /* padding along w */
   int x_ld, y_ld;         /* pixel strides (elements) of x/dx and y/dy; 0 = dense (c, k).
                              A channel slice of a wider tensor = grouped convolution. */
+  int math;               /* TMR_MATH_F32: fp32 operands on v_mfma_f32_32x32x2_f32;
+                             TMR_MATH_BF16: operands rounded to bf16 (RNE) when staged to LDS,
+                             v_mfma_f32_32x32x16_bf16, fp32 accumulation and fp32 tensors in HBM
+                             (the bf16 configs C4/C5 of BASELINE.json) */
 } tmr_conv_desc;
+#define TMR_MATH_F32 0
+#define TMR_MATH_BF16 1
 
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
 int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,

@@ -28,6 +28,11 @@ reference checkout, ``code/``):
 * ``crop_normalize_ref`` -- crop at a per-clip offset + ToTensor + Normalize
                          (``train_only_non-local_pretrained.py:101-126``, ``:335-341``)
 * ``train_step_ref``  -- the step at ``train_only_non-local_pretrained.py:698-725``
+* ``emulate_bf16_convs`` -- the bf16 configs (BASELINE.json configs[3], [4]) have no reference
+                         implementation (the reference is fp32 only): this restates the
+                         build's TMR_MATH_BF16 contract on torch ops -- every trunk conv with
+                         operands rounded to bf16 (RNE), exact products, accumulation in the
+                         tensor dtype; fwd rounds (x, w), dgrad (dy, w), wgrad (x, dy).
 """
 import math
 
@@ -263,14 +268,60 @@ def resnest50_share():
 # --------------------------------------------------------------------------
 # TMRNet / memory-bank model
 # --------------------------------------------------------------------------
+def bf16_round(t):
+    """Round to the nearest bf16 (ties to even), returned in t's dtype."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, padding, groups):
+        xb, wb = bf16_round(x), bf16_round(w)
+        ctx.save_for_backward(xb, wb)
+        ctx.cfg = (stride, padding, groups)
+        return F.conv2d(xb, wb, None, stride, padding, 1, groups)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb = ctx.saved_tensors
+        stride, padding, groups = ctx.cfg
+        gyb = bf16_round(gy)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv2d_input(xb.shape, wb, gyb, stride, padding, 1, groups)
+        dw = torch.nn.grad.conv2d_weight(xb, wb.shape, gyb, stride, padding, 1, groups)
+        return dx, dw, None, None, None
+
+
+class Bf16Conv2d(nn.Conv2d):
+    """nn.Conv2d (no bias) whose operands are rounded to bf16 (see emulate_bf16_convs)."""
+
+    def forward(self, x):
+        assert self.bias is None
+        return _Bf16ConvFn.apply(x, self.weight, self.stride, self.padding, self.groups)
+
+
+def emulate_bf16_convs(module, skip=("fc1", "fc2")):
+    """Switch every trunk Conv2d of `module` to bf16-operand math (class swap, so deepcopy
+    and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay."""
+    for name, m in module.named_modules():
+        if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
+            m.__class__ = Bf16Conv2d
+    return module
+
+
 class TMRNetRef(nn.Module):
     """Inline `resnet_lstm` (train_only_non-local_pretrained.py:201-240); with
-    time_conv=True the mutiConv variant (train_non-local_mutiConv_resnet.py:208-253)."""
+    time_conv=True the mutiConv variant (train_non-local_mutiConv_resnet.py:208-253).
+    precision='bf16': trunk convs with bf16 operands (emulate_bf16_convs)."""
 
-    def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50"):
+    def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50",
+                 precision="fp32"):
         super().__init__()
         self.seq_len = seq_len
         self.share = resnet50_share() if backbone == "resnet50" else resnest50_share()
+        if precision == "bf16":
+            emulate_bf16_convs(self.share)
         self.lstm = nn.LSTM(2048, 512, batch_first=True)
         self.fc_c = nn.Linear(512, num_classes)
         self.fc_h_c = nn.Linear(1024, 512)

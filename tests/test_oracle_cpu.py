@@ -145,3 +145,21 @@ def test_timeconv_generalised_L():
     m = ref.TimeConvRef()
     for L in (1, 7, 40):
         assert m(torch.randn(2, L, 512)).shape == (2, L, 512)
+
+
+def test_bf16_conv_emulation():
+    """emulate_bf16_convs: forward = conv of bf16-rounded operands; backward rounds dy and
+    uses the rounded saved operands (the TMR_MATH_BF16 contract of include/tmr.h)."""
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(8, 16, 3, 2, 1, bias=False)
+    emu = ref.emulate_bf16_convs(torch.nn.Sequential(conv))
+    x = torch.randn(2, 8, 9, 7, requires_grad=True)
+    y = emu(x)
+    r = ref.bf16_round
+    assert torch.equal(y, torch.nn.functional.conv2d(r(x), r(conv.weight), None, 2, 1))
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    dx = torch.nn.grad.conv2d_input(x.shape, r(conv.weight), r(gy), 2, 1)
+    dw = torch.nn.grad.conv2d_weight(r(x), conv.weight.shape, r(gy), 2, 1)
+    assert torch.equal(x.grad, dx) and torch.equal(conv.weight.grad, dw)
+    assert not torch.equal(r(x), x)

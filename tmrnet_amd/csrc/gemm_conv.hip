@@ -65,7 +65,17 @@ struct GemmArgs {
   float4* stats;
   // byte extents of A and B (buffer-descriptor range checks)
   uint32_t Abytes, Bbytes;
+  int prec;  // TMR_MATH_F32 / TMR_MATH_BF16
 };
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};   // v_cvt_pk_bf16_f32, round to nearest even
+  return __builtin_bit_cast(uint32_t, v);
+}
 
 // Buffer loads: 32-bit byte offsets against a per-tensor descriptor; an out-of-range
 // offset returns zeros, so padding / tails / masked rows need no branches (the compiler
@@ -106,7 +116,12 @@ __device__ __forceinline__ void tap_split(const GemmArgs& a, int tap, int& ri, i
 // VAR: 0 = aligned float4 loads, one tap per k-tile (channels per tap >= BK, or a plain GEMM)
 //      1 = aligned, tap varies inside a k-tile (the 4-channel stem)
 //      2 = unaligned scalar loads (GEMMs with odd leading dimensions), one tap
-template <int MODE, int BM, int BN, int WM, int WN, int BK, int VAR>
+// PREC: 0 = fp32 operands, LDS k-major, v_mfma_f32_32x32x2_f32
+//       1 = operands rounded to bf16 when written to LDS, LDS row-major [row][BK+8] so each
+//           lane's 8-element k-fragment is one ds_read_b128, v_mfma_f32_32x32x16_bf16.
+//           M/N-contiguous operands are loaded as k-row pairs so the LDS writes are packed
+//           bf16x2 dwords (conflict-free); K-contiguous operands write bf16x4.
+template <int MODE, int BM, int BN, int WM, int WN, int BK, int VAR, int PREC = 0>
 __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   constexpr bool AL = (VAR != 2);
   constexpr int NT = 64 * WM * WN;       // threads per workgroup
@@ -122,15 +137,31 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   constexpr bool B_KC = (MODE == MODE_FWD);
   constexpr int LDA = BM + (A_KC ? 2 : 4);
   constexpr int LDB = BN + (B_KC ? 2 : 4);
-  __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
+  constexpr int LDK = BK + 8;            // bf16 row stride (80 B for BK=32: conflict-free b128)
+  static_assert(PREC == 0 || (BK % 16 == 0 && RA % 2 == 0 && RB % 2 == 0), "bf16 tile shape");
+  constexpr int SMEM_F = PREC ? (2 * (BM + BN) * LDK + 1) / 2 : 2 * BK * (LDA + LDB);
+  __shared__ __attribute__((aligned(16))) float smem[SMEM_F];
   float* As0 = smem;
   float* Bs0 = smem + 2 * BK * LDA;
+  __bf16* Ah0 = reinterpret_cast<__bf16*>(smem);
+  __bf16* Bh0 = Ah0 + 2 * BM * LDK;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int l31 = lane & 31, hh = lane >> 5;
+  // M/N-contiguous operand loads (WGRAD A, DGRAD B, WGRAD B): load q -> (k row, float4 column)
+  // fp32: consecutive threads walk the columns of one k row.  bf16: loads q, q^1 are the k-row
+  // pair (2kp, 2kp+1) of one column group, so the LDS write packs them into bf16x2 dwords.
+  auto mn_krow = [&](int q, int W4) -> int {
+    if (PREC) return 2 * ((tid + NT * (q >> 1)) % (BK / 2)) + (q & 1);
+    return (tid + NT * q) / W4;
+  };
+  auto mn_c4 = [&](int q, int W4) -> int {
+    if (PREC) return (tid + NT * (q >> 1)) / (BK / 2);
+    return (tid + NT * q) % W4;
+  };
 
   // XCD-aware tile order: consecutive logical tiles share an XCD (and its L2);
   // n-tiles of one m-tile are consecutive so the gathered A rows are reused.
@@ -186,7 +217,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   if (MODE == MODE_WGRAD) {
 #pragma unroll
     for (int q = 0; q < RB; ++q) {
-      const int j = n0 + ((tid + NT * q) % (BN / 4)) * 4;
+      const int j = n0 + mn_c4(q, BN / 4) * 4;
       int tap, c;
       if (a.ntaps == 1) { tap = 0; c = j; }
       else { tap = j >> a.log2C; c = j & cmask; }
@@ -237,8 +268,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     } else {  // WGRAD: A[i][kk] = dY[m][co], co contiguous
 #pragma unroll
       for (int q = 0; q < RA; ++q) {
-        const int lin = tid + NT * q;
-        const int krow = lin / (BM / 4), c4 = lin % (BM / 4);
+        const int krow = mn_krow(q, BM / 4), c4 = mn_c4(q, BM / 4);
         const int m = kb + krow, i = m0 + c4 * 4;
         const bool ok = (m < kend) && (i < a.M);
         ra[q] = ld4v<AL>(rA, ((uint32_t)m * (uint32_t)a.ldb + (uint32_t)i) * 4u, ok, a.M - i);
@@ -266,8 +296,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
       const int rsU = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
-        const int lin = tid + NT * q;
-        const int krow = lin / (BN / 4), c4 = lin % (BN / 4);
+        const int krow = mn_krow(q, BN / 4), c4 = mn_c4(q, BN / 4);
         const int k = kb + krow, j = n0 + c4 * 4;
         const bool ok = (k < kend) && (j < a.N);
         const uint32_t co = (uint32_t)(cbU + krow);
@@ -277,8 +306,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     } else {  // WGRAD: B[kk=m][j=(tap,c)] gathered from X
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
-        const int lin = tid + NT * q;
-        const int krow = lin / (BN / 4);
+        const int krow = mn_krow(q, BN / 4);
         const int m = kb + krow;
         const uint32_t mm = m < kend ? (uint32_t)m : 0u;
         const uint32_t n = fdiv(mm, a.dHW);
@@ -290,13 +318,47 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
                         (unsigned)xs < (unsigned)a.Ws;
         const uint32_t off =
             ((uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds) * 4u + bcoff[q];
-        const int j = n0 + (lin % (BN / 4)) * 4;
+        const int j = n0 + mn_c4(q, BN / 4) * 4;
         rb[q] = ld4v<AL>(rB, off, ok, a.N - j);
       }
     }
   };
 
+  auto store_tile_h = [&](int buf, const float4 (&ra)[RA], const float4 (&rb)[RB]) {
+    __bf16* Ah = Ah0 + buf * BM * LDK;
+    __bf16* Bh = Bh0 + buf * BN * LDK;
+    auto kc_store = [&](__bf16* T, int lin, const float4& v) {   // K-contiguous: 4 k of one row
+      const int row = lin / KQ, kq = (lin % KQ) * 4;
+      const uint2 w = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+      *reinterpret_cast<uint2*>(&T[row * LDK + kq]) = w;
+    };
+    auto mn_store = [&](__bf16* T, int q, int W4, const float4& v0, const float4& v1) {
+      // v0/v1: rows k = 2kp, 2kp+1 of columns 4c4..4c4+3 -> T[col][2kp..2kp+1]
+      const int kp = mn_krow(q, W4) >> 1, c4 = mn_c4(q, W4);
+      uint32_t* t = reinterpret_cast<uint32_t*>(T);
+      t[((4 * c4 + 0) * LDK) / 2 + kp] = pack_bf16x2(v0.x, v1.x);
+      t[((4 * c4 + 1) * LDK) / 2 + kp] = pack_bf16x2(v0.y, v1.y);
+      t[((4 * c4 + 2) * LDK) / 2 + kp] = pack_bf16x2(v0.z, v1.z);
+      t[((4 * c4 + 3) * LDK) / 2 + kp] = pack_bf16x2(v0.w, v1.w);
+    };
+    if (A_KC) {
+#pragma unroll
+      for (int q = 0; q < RA; ++q) kc_store(Ah, tid + NT * q, ra[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < RA; q += 2) mn_store(Ah, q, BM / 4, ra[q], ra[q + 1]);
+    }
+    if (B_KC) {
+#pragma unroll
+      for (int q = 0; q < RB; ++q) kc_store(Bh, tid + NT * q, rb[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < RB; q += 2) mn_store(Bh, q, BN / 4, rb[q], rb[q + 1]);
+    }
+  };
+
   auto store_tile = [&](int buf, const float4 (&ra)[RA], const float4 (&rb)[RB]) {
+    if (PREC) { store_tile_h(buf, ra, rb); return; }
     float* As = As0 + buf * BK * LDA;
     float* Bs = Bs0 + buf * BK * LDB;
     if (A_KC) {
@@ -348,7 +410,28 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   const int aoff = wm * (BM / WM) + l31;
   const int boff = wn * (BN / WN) + l31;
 
+  auto compute_h = [&](int cur) {
+    const __bf16* Ah = Ah0 + cur * BM * LDK;
+    const __bf16* Bh = Bh0 + cur * BN * LDK;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        av[i] = *reinterpret_cast<const bf16x8*>(&Ah[(aoff + 32 * i) * LDK + 16 * s + 8 * hh]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = *reinterpret_cast<const bf16x8*>(&Bh[(boff + 32 * j) * LDK + 16 * s + 8 * hh]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
   auto compute = [&](int cur) {
+    if (PREC) { compute_h(cur); return; }
     const float* As = As0 + cur * BK * LDA;
     const float* Bs = Bs0 + cur * BK * LDB;
 #pragma unroll
@@ -370,40 +453,42 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   // Software pipeline.  Loads past the last k-tile are issued anyway: their offsets are out
   // of range (k >= kend) so they return zeros, and the loop has no load/store branches, which
   // lets the compiler place exact (counted) vmcnt waits.
-#if TMR_PF == 2
-  // prefetch distance 2: while the MFMAs run on LDS buffer kt&1, one register set holds
-  // tile kt+1 (written to the other buffer after the MFMAs) and the other set has tile
-  // kt+2's loads in flight.
-  if (ntiles > 0) {
-    load_tile(0, ra0, rb0);
-    load_tile(1, ra1, rb1);
-    store_tile(0, ra0, rb0);
-    __syncthreads();
-    for (int kt = 0; kt < ntiles; kt += 2) {
-      load_tile(kt + 2, ra0, rb0);
-      compute(0);
-      store_tile(1, ra1, rb1);
-      __syncthreads();
-      if (kt + 1 >= ntiles) break;
-      load_tile(kt + 3, ra1, rb1);
-      compute(1);
+  // bf16: one register set (BK=32 tiles are twice as many registers per set)
+  constexpr int PFD = PREC ? 1 : TMR_PF;
+  if constexpr (PFD == 2) {
+    // prefetch distance 2: while the MFMAs run on LDS buffer kt&1, one register set holds
+    // tile kt+1 (written to the other buffer after the MFMAs) and the other set has tile
+    // kt+2's loads in flight.
+    if (ntiles > 0) {
+      load_tile(0, ra0, rb0);
+      load_tile(1, ra1, rb1);
       store_tile(0, ra0, rb0);
       __syncthreads();
+      for (int kt = 0; kt < ntiles; kt += 2) {
+        load_tile(kt + 2, ra0, rb0);
+        compute(0);
+        store_tile(1, ra1, rb1);
+        __syncthreads();
+        if (kt + 1 >= ntiles) break;
+        load_tile(kt + 3, ra1, rb1);
+        compute(1);
+        store_tile(0, ra0, rb0);
+        __syncthreads();
+      }
     }
-  }
-#else
-  if (ntiles > 0) {
-    load_tile(0, ra0, rb0);
-    store_tile(0, ra0, rb0);
-    __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      load_tile(kt + 1, ra0, rb0);
-      compute(kt & 1);
-      store_tile((kt & 1) ^ 1, ra0, rb0);
+  } else {
+    if (ntiles > 0) {
+      load_tile(0, ra0, rb0);
+      store_tile(0, ra0, rb0);
       __syncthreads();
+      for (int kt = 0; kt < ntiles; ++kt) {
+        load_tile(kt + 1, ra0, rb0);
+        compute(kt & 1);
+        store_tile((kt & 1) ^ 1, ra0, rb0);
+        __syncthreads();
+      }
     }
   }
-#endif
 
   // ---- epilogue ----
   float* Cb = a.C;
@@ -540,15 +625,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit,
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int BKT>
+template <int MODE, int BM, int BN, int WM, int WN, int BKT, int PREC = 0>
 int launch_cfg(const GemmArgs& a, int var, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
   if (var == 2)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 2>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 2, PREC>), grid, blk, 0, st, a);
   else if (MODE == MODE_FWD && var == 1)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, (MODE == MODE_FWD ? 1 : 0)>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, (MODE == MODE_FWD ? 1 : 0), PREC>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, PREC>), grid, blk, 0, st, a);
   TMR_CHECK_LAUNCH("gemm_kernel");
   return 0;
 }
@@ -583,7 +668,9 @@ int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   TMR_CHECK_ARG(a.Abytes < 0x80000000u && a.Bbytes < 0x80000000u,
                 "gemm: operand larger than 2 GiB (split the batch)");
   // WGRAD resolves taps per column (fixed per thread); FWD/DGRAD per k-tile when uniform
-  const bool uniform = MODE == MODE_WGRAD || a.ntaps <= 1 || (1 << a.log2C) >= 16;
+  // (a k-tile of BK must not straddle two taps: channels per tap >= BK)
+  const int bk = a.prec == TMR_MATH_BF16 ? 32 : 16;
+  const bool uniform = MODE == MODE_WGRAD || a.ntaps <= 1 || (1 << a.log2C) >= bk;
   int var = al ? (uniform ? 0 : 1) : 2;
   TMR_CHECK_ARG(uniform || (al && MODE == MODE_FWD),
                 "gemm: per-element taps need aligned channels and the forward view");
@@ -591,6 +678,17 @@ int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   const TileCfg c = kCfgs[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
+  if (a.prec == TMR_MATH_BF16) {
+    switch (cfg) {
+      case 0: return launch_cfg<MODE, 128, 128, 2, 2, 32, 1>(a, var, grid, st);
+      case 1: return launch_cfg<MODE, 256, 64, 4, 1, 32, 1>(a, var, grid, st);
+      case 2: return launch_cfg<MODE, 64, 256, 1, 4, 32, 1>(a, var, grid, st);
+      case 3: return launch_cfg<MODE, 64, 64, 2, 2, 32, 1>(a, var, grid, st);
+      case 4: case 8: return launch_cfg<MODE, 256, 128, 4, 2, 32, 1>(a, var, grid, st);
+      case 5: return launch_cfg<MODE, 128, 256, 2, 4, 32, 1>(a, var, grid, st);
+      default: return launch_cfg<MODE, 256, 256, 4, 4, 32, 1>(a, var, grid, st);
+    }
+  }
   switch (cfg) {
     case 0: return launch_cfg<MODE, 128, 128, 2, 2, 16>(a, var, grid, st);
     case 1: return launch_cfg<MODE, 256, 64, 4, 1, 16>(a, var, grid, st);
@@ -642,6 +740,7 @@ void set_grid(GemmArgs& a, int n, int hg, int wg) {
 static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_krsc,
                          const float* bias, float* y, float beta, GemmArgs& a, bool& al) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
+  TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
   a = GemmArgs{};
@@ -654,6 +753,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = xld_of(d); a.ldb = a.K; a.ldc = yld_of(d); a.beta = beta;
   a.Abytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
+  a.prec = d->math;
   a.Bbytes = clamp_bytes((long)d->k * a.K);
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
@@ -690,6 +790,7 @@ TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const
 TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
                              float* dx, float beta, hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad: null descriptor");
+  TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
   const int lk = ilog2_exact(d->k);
   TMR_CHECK_ARG(lk >= 2, "tmr_conv2d_dgrad: output channels %d must be a power of two >= 4", d->k);
   TMR_CHECK_ARG(d->c % 4 == 0, "tmr_conv2d_dgrad: input channels %d must be a multiple of 4", d->c);
@@ -720,6 +821,7 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
       a.Hs = d->ho; a.Ws = d->wo; a.sy = 1; a.sx = 1;
       a.lds = yld_of(d); a.ldb = d->r * d->s * d->c; a.ldc = xld_of(d); a.beta = beta;
       a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.lds, d->k));
+      a.prec = d->math;
       a.Bbytes = clamp_bytes((long)d->k * d->r * d->s * d->c);
       if (st == 1) {
         a.osy = 0;
@@ -768,6 +870,7 @@ TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float
                              float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
                              hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_wgrad: null descriptor");
+  TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_wgrad: stored input channels %d must be a power of two >= 4", d->c);
   TMR_CHECK_ARG(c_real >= 1 && c_real <= d->c, "tmr_conv2d_wgrad: bad c_real %d", c_real);
@@ -788,6 +891,7 @@ TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float
   a.lds = xld_of(d); a.ldb = yld_of(d); a.ldc = a.N; a.beta = 0.f;
   a.kchunk = kc; a.slab = slab;
   a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldb, d->k));
+  a.prec = d->math;
   a.Bbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
   bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0) && a.lds % 4 == 0 && a.ldb % 4 == 0;
   int rc = launch_gemm<MODE_WGRAD>(a, al, sp, stream);

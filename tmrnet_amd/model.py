@@ -87,17 +87,27 @@ def _frames_to_features(share, x):
     return share(x).view(-1, 2048)
 
 
+def _make_trunk(backbone, precision):
+    if precision not in ("fp32", "bf16"):
+        raise ValueError("precision must be 'fp32' or 'bf16', got %r" % precision)
+    if backbone == "resnet50":
+        return ResNet50Share(precision=precision)
+    if backbone == "resnest50":
+        from .resnest import ResNeSt50Share
+        return ResNeSt50Share(precision=precision)
+    raise ValueError("unknown backbone %r" % backbone)
+
+
 class resnet_lstm(nn.Module):  # noqa: N801  (reference class name)
-    def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50"):
+    """precision='bf16' runs the trunk convolutions (fwd, dgrad, wgrad) with bf16 operands on
+    the bf16 matrix cores, fp32 accumulation, fp32 activations/BN/master weights (the bf16
+    configs C4/C5); everything else stays fp32."""
+
+    def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50",
+                 precision="fp32"):
         super().__init__()
         self.seq_len = seq_len
-        if backbone == "resnet50":
-            self.share = ResNet50Share()
-        elif backbone == "resnest50":
-            from .resnest import ResNeSt50Share
-            self.share = ResNeSt50Share()
-        else:
-            raise ValueError("unknown backbone %r" % backbone)
+        self.share = _make_trunk(backbone, precision)
         self.lstm = LSTM(2048, 512, batch_first=True)
         self.fc_c = nn.Linear(512, num_classes)
         self.fc_h_c = nn.Linear(1024, 512)
@@ -135,14 +145,10 @@ class resnet_lstm(nn.Module):  # noqa: N801  (reference class name)
 
 
 class resnet_lstm_LFB(nn.Module):  # noqa: N801
-    def __init__(self, seq_len=10, backbone="resnet50"):
+    def __init__(self, seq_len=10, backbone="resnet50", precision="fp32"):
         super().__init__()
         self.seq_len = seq_len
-        if backbone == "resnet50":
-            self.share = ResNet50Share()
-        else:
-            from .resnest import ResNeSt50Share
-            self.share = ResNeSt50Share()
+        self.share = _make_trunk(backbone, precision)
         self.lstm = LSTM(2048, 512, batch_first=True)
         init.xavier_normal_(self.lstm.all_weights[0][0])
         init.xavier_normal_(self.lstm.all_weights[0][1])

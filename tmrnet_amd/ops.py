@@ -63,27 +63,32 @@ def _empty(shape, like, dtype=f32):
 
 
 # ----------------------------------------------------------------- conv / gemm
-def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0):
+MATH = {"fp32": 0, "bf16": 1}   # tmr_conv_desc.math (TMR_MATH_F32 / TMR_MATH_BF16)
+_SUFFIX = {"fp32": "", "bf16": "_bf16"}
+
+
+def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math="fp32"):
     pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
     wo = (w + 2 * pad_w - s) // stride + 1
-    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld)
+    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math])
 
 
-def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None, pad_w=None):
+def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None, pad_w=None,
+             math="fp32"):
     """x (N,H,W,C) NHWC (or channel-slice view), w_krsc (K,R,S,C) -> y (N,Ho,Wo,K);
     `out` may be a channel-slice view of a wider NHWC tensor (grouped convolution)."""
     _req(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
     if out is None:
         out = _empty((n, d.ho, d.wo, k), x)
     d.x_ld = _nhwc_ld(x, "x")
     d.y_ld = _nhwc_ld(out, "out")
     ysz = n * d.ho * d.wo * k
-    with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
+    with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
                (n, h, w, c, k, r, stride),
                4 * (n * h * w * c + k * r * s * c + ysz * (2 if beta else 1))):
         call("tmr_conv2d_fwd", ctypes.byref(d), x, w_krsc, bias if bias is not None else None,
@@ -91,17 +96,17 @@ def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None,
     return out
 
 
-def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None):
+def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32"):
     """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts)."""
     _req(x, "x"); _req(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
     out = _empty((n, d.ho, d.wo, k), x)
     nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
-    with _prof("conv_fwd", 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
+    with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
                (n, h, w, c, k, r, stride),
                4 * (n * h * w * c + k * r * s * c + n * d.ho * d.wo * k) + stats.numel() * 4):
         call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
@@ -118,30 +123,31 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
     return mean, inv, scale, shift
 
 
-def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None):
+def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, math="fp32"):
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices)."""
     _req(w_krsc, "w")
     n, ho, wo, k = dy.shape
     k2, r, s, c = w_krsc.shape
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
-    with _prof("conv_dgrad", 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
+    with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
                4 * (n * ho * wo * k + k * r * s * c + n * h * w * c * (2 if beta else 1))):
         call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
     return out
 
 
-def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None):
+def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None,
+               math="fp32"):
     """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW (x/dy may be channel slices)."""
     n, h, w, c = x.shape
     k = dy.shape[3]
     c_real = c if c_real is None else c_real
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
     d.x_ld = _nhwc_ld(x, "x")
     d.y_ld = _nhwc_ld(dy, "dy")
     assert (d.ho, d.wo) == tuple(dy.shape[1:3])
@@ -149,7 +155,7 @@ def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=
         out = _empty((k, c_real, r, s), x)
     ws_bytes = query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d))
     ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
-    with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * c_real,
+    with _prof("conv_wgrad" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * c_real,
                (n, h, w, c, k, r, stride),
                4 * (n * h * w * c + n * d.ho * d.wo * k + k * r * s * c_real)):
         call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,

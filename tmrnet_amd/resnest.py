@@ -37,7 +37,7 @@ def _bn_train_or_eval(y, bn, training):
 
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, residual, bn, stride, pad, groups, relu, c_real):
+    def forward(ctx, x, w, gamma, beta, residual, bn, stride, pad, groups, relu, c_real, math):
         x = x.contiguous()
         n, h, wd, cs = x.shape
         k, cg, r, s = w.shape
@@ -47,7 +47,8 @@ class ConvBNActFn(torch.autograd.Function):
         wks = [ops.weight_to_krsc(w.detach()[g * kg:(g + 1) * kg].contiguous(), cpad=cgs)
                for g in range(groups)]
         if groups == 1 and training:
-            y, stats, nparts = ops.conv_fwd_bnstats(x, wks[0], stride, pad, c_real=c_real)
+            y, stats, nparts = ops.conv_fwd_bnstats(x, wks[0], stride, pad, c_real=c_real,
+                                                    math=math)
             mean, inv, scale, shift = ops.bn_finalize(stats, nparts, gamma.detach(), beta.detach(),
                                                       bn.running_mean, bn.running_var, bn.momentum,
                                                       bn.eps)
@@ -58,20 +59,20 @@ class ConvBNActFn(torch.autograd.Function):
             y = torch.empty((n, ho, wo, k), dtype=x.dtype, device=x.device)
             for g in range(groups):
                 ops.conv_fwd(x[..., g * cgs:(g + 1) * cgs], wks[g], stride, pad,
-                             out=y[..., g * kg:(g + 1) * kg], c_real=min(cg, c_real))
+                             out=y[..., g * kg:(g + 1) * kg], c_real=min(cg, c_real), math=math)
             mean, inv, scale, shift = _bn_train_or_eval(y, bn, training)
         z = ops.bn_apply(y, scale, shift, residual.contiguous() if residual is not None else None,
                          relu)
         # without a residual the backward recomputes the ReLU mask from y and scale/shift
         ctx.save_for_backward(x, y, z if residual is not None else None, scale, shift, mean, inv,
                               gamma, *wks)
-        ctx.cfg = (stride, pad, groups, relu, c_real, residual is not None, r, s)
+        ctx.cfg = (stride, pad, groups, relu, c_real, residual is not None, r, s, math)
         return z
 
     @staticmethod
     def backward(ctx, dz):
         x, y, z, scale, shift, mean, inv, gamma, *wks = ctx.saved_tensors
-        stride, pad, groups, relu, c_real, has_res, r, s = ctx.cfg
+        stride, pad, groups, relu, c_real, has_res, r, s, math = ctx.cfg
         if mean is None:
             raise RuntimeError("backward through eval-mode BatchNorm is not supported")
         dz = dz.contiguous()
@@ -86,10 +87,11 @@ class ConvBNActFn(torch.autograd.Function):
         for g in range(groups):
             dyg = dy[..., g * kg:(g + 1) * kg]
             ops.conv_wgrad(x[..., g * cgs:(g + 1) * cgs], dyg, r, s, stride, pad, c_real=creal_g,
-                           out=dw[g * kg:(g + 1) * kg])
+                           out=dw[g * kg:(g + 1) * kg], math=math)
             if dx is not None:
-                ops.conv_dgrad(dyg, wks[g], (h, wd), stride, pad, out=dx[..., g * cgs:(g + 1) * cgs])
-        return dx, dw, dg, db, dres, None, None, None, None, None, None
+                ops.conv_dgrad(dyg, wks[g], (h, wd), stride, pad, out=dx[..., g * cgs:(g + 1) * cgs],
+                               math=math)
+        return dx, dw, dg, db, dres, None, None, None, None, None, None, None
 
 
 class SplAtFn(torch.autograd.Function):
@@ -212,9 +214,11 @@ class GlobalPoolFn(torch.autograd.Function):
         return ops.avgpool_bwd(dy.contiguous(), ctx.hw)
 
 
-def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=None):
+def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=None,
+                math="fp32"):
     return ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, residual, bn, stride, pad, groups,
-                             relu, c_real if c_real is not None else conv.weight.shape[1] * groups)
+                             relu, c_real if c_real is not None else conv.weight.shape[1] * groups,
+                             math)
 
 
 # ------------------------------------------------------------------ modules
@@ -225,6 +229,7 @@ class SplAtConv2d(nn.Module):
         super().__init__()
         inter = max(in_channels * radix // 4, 32)
         self.radix, self.channels, self.stride = radix, channels, stride
+        self.math = "fp32"   # set by ResNeSt50Share(precision=...)
         self.conv = nn.Conv2d(in_channels, channels * radix, 3, stride, 1, groups=radix, bias=False)
         self.bn0 = nn.BatchNorm2d(channels * radix)
         self.relu = nn.ReLU(inplace=True)
@@ -233,7 +238,8 @@ class SplAtConv2d(nn.Module):
         self.fc2 = nn.Conv2d(inter, channels * radix, 1, groups=1)
 
     def forward(self, x):
-        x2 = conv_bn_act(x, self.conv, self.bn0, self.stride, 1, True, groups=self.radix)
+        x2 = conv_bn_act(x, self.conv, self.bn0, self.stride, 1, True, groups=self.radix,
+                         math=self.math)
         return SplAtFn.apply(x2, self.fc1.weight, self.fc1.bias, self.bn1.weight, self.bn1.bias,
                              self.fc2.weight, self.fc2.bias, self.bn1)
 
@@ -255,9 +261,11 @@ class BottleneckS(nn.Module):
         self.bn3 = nn.BatchNorm2d(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
+        self.math = "fp32"
 
     def forward(self, x):
-        out = conv_bn_act(x, self.conv1, self.bn1, 1, 0, True)
+        mt = self.math
+        out = conv_bn_act(x, self.conv1, self.bn1, 1, 0, True, math=mt)
         out = self.conv2(out)
         if self.avd:
             out = AvgPoolFn.apply(out, 3, self.avd_stride, 1, True, False)
@@ -266,8 +274,8 @@ class BottleneckS(nn.Module):
             pool, conv, bn = self.downsample[0], self.downsample[1], self.downsample[2]
             if pool.kernel_size != 1:
                 res = AvgPoolFn.apply(x, pool.kernel_size, pool.stride, 0, False, True)
-            res = conv_bn_act(res, conv, bn, 1, 0, False)
-        return conv_bn_act(out, self.conv3, self.bn3, 1, 0, True, residual=res)
+            res = conv_bn_act(res, conv, bn, 1, 0, False, math=mt)
+        return conv_bn_act(out, self.conv3, self.bn3, 1, 0, True, residual=res, math=mt)
 
 
 def _make_layer(inplanes, planes, blocks, stride):
@@ -289,8 +297,9 @@ class GlobalAvgPool2d(nn.Module):
 
 
 class ResNeSt50Share(nn.Sequential):
-    def __init__(self):
+    def __init__(self, precision="fp32"):
         super().__init__()
+        self.precision = precision
         self.add_module("conv1", nn.Sequential(
             nn.Conv2d(3, 32, 3, 2, 1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
             nn.Conv2d(32, 32, 3, 1, 1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
@@ -310,12 +319,15 @@ class ResNeSt50Share(nn.Sequential):
             elif isinstance(m, nn.BatchNorm2d):
                 m.weight.data.fill_(1)
                 m.bias.data.zero_()
+        for m in self.modules():
+            if isinstance(m, (BottleneckS, SplAtConv2d)):
+                m.math = precision
 
     def features_nhwc4(self, x4):
-        c = self.conv1
-        h = conv_bn_act(x4, c[0], c[1], 2, 1, True, c_real=3)
-        h = conv_bn_act(h, c[3], c[4], 1, 1, True)
-        h = conv_bn_act(h, c[6], self.bn1, 1, 1, True)
+        c, mt = self.conv1, self.precision
+        h = conv_bn_act(x4, c[0], c[1], 2, 1, True, c_real=3, math=mt)
+        h = conv_bn_act(h, c[3], c[4], 1, 1, True, math=mt)
+        h = conv_bn_act(h, c[6], self.bn1, 1, 1, True, math=mt)
         h = MaxPoolFn.apply(h)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:

@@ -56,7 +56,7 @@ def _bn_momentum(bn):
     return bn.momentum
 
 
-def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None):
+def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32"):
     """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z."""
     w = conv.weight
     k, c, r, s = w.shape
@@ -67,13 +67,13 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None)
         wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs)
     if training:
         # batch statistics come out of the conv epilogue (no separate pass over y)
-        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c)
+        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c, math=math)
         mean, inv, scale, shift = ops.bn_finalize(
             stats, nparts, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
             bn.running_var, _bn_momentum(bn), bn.eps)
         bn.num_batches_tracked.add_(1)
     else:
-        y = ops.conv_fwd(x, wk, stride, pad, c_real=c)
+        y = ops.conv_fwd(x, wk, stride, pad, c_real=c, math=math)
         mean = inv = None
         scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                                           bn.running_var, bn.eps)
@@ -83,7 +83,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None)
         recs.append({"x": x, "wk": wk, "y": y, "z": z if residual is not None else None,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
-                     "c_real": c})
+                     "c_real": c, "math": math})
     return z
 
 
@@ -102,11 +102,11 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     x = rec["x"]
     k, c, r, s = conv.weight.shape
     grads[conv.weight] = ops.conv_wgrad(x, dy, r, s, rec["stride"], rec["pad"],
-                                        c_real=rec["c_real"])
+                                        c_real=rec["c_real"], math=rec["math"])
     dx = None
     if need_dx:
         dx = ops.conv_dgrad(dy, rec["wk"], (x.shape[1], x.shape[2]), rec["stride"], rec["pad"],
-                            out=dx_out, beta=dx_beta)
+                            out=dx_out, beta=dx_beta, math=rec["math"])
     return dx, dres
 
 
@@ -119,7 +119,8 @@ class TrunkFn(torch.autograd.Function):
         keep = keep and training
         recs = [] if keep else None
         conv1, bn1, layers = share.trunk_parts()
-        z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs)
+        mt = share.precision
+        z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt)
         p, am = ops.maxpool_fwd(z)
         stem_hw = (z.shape[1], z.shape[2])
         h = p
@@ -127,15 +128,16 @@ class TrunkFn(torch.autograd.Function):
         for layer in layers:
             for blk in layer:
                 brec = [] if keep else None
-                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec)
-                z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec)
+                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt)
+                z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec,
+                              math=mt)
                 if blk.downsample is not None:
                     idn = _conv_bn(h, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
-                                   training, recs=brec)
+                                   training, recs=brec, math=mt)
                 else:
                     idn = h
                 h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, residual=idn,
-                             recs=brec)
+                             recs=brec, math=mt)
                 blocks.append((blk, brec))
         feat = ops.avgpool_fwd(h)
         ctx.keep = keep
@@ -193,8 +195,9 @@ class ResNet50Share(nn.Sequential):
     (keys ``res.0.weight``, ``res.4.0.conv1.weight``, ...).
     """
 
-    def __init__(self, indexed=False):
+    def __init__(self, indexed=False, precision="fp32"):
         super().__init__()
+        self.precision = precision   # conv operand precision: "fp32" | "bf16" (ops.MATH)
         mods = (nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64),
                 nn.ReLU(inplace=True), nn.MaxPool2d(3, stride=2, padding=1),
                 _make_layer(64, 64, 3, 1), _make_layer(256, 128, 4, 2),
