@@ -50,6 +50,9 @@ typedef struct tmr_conv_desc {
                              TMR_MATH_BF16: operands rounded to bf16 (RNE) when staged to LDS,
                              v_mfma_f32_32x32x16_bf16, fp32 accumulation and fp32 tensors in HBM
                              (the bf16 configs C4/C5 of BASELINE.json) */
+  int max_frames;         /* frames per kernel launch, 0 = automatic.  Operands of one launch
+                             must stay < 2 GiB (32-bit buffer offsets): larger batches run as
+                             consecutive frame chunks (wgrad accumulates them in order) */
 } tmr_conv_desc;
 #define TMR_MATH_F32 0
 #define TMR_MATH_BF16 1

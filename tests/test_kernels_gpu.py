@@ -249,3 +249,45 @@ def test_conv_fused_bn_stats(dev, case):
     var = yd.var(0, unbiased=False)
     assert rel_err(inv, 1 / torch.sqrt(var + 1e-5)) < 1e-5
     assert rel_err(rvd, 0.9 + 0.1 * yd.var(0, unbiased=True)) < 1e-6
+
+
+@pytest.mark.parametrize("case", [(5, 14, 14, 64, 128, 3, 2, 1), (4, 9, 9, 256, 64, 1, 1, 0),
+                                  (3, 28, 28, 3, 64, 7, 2, 3)])
+def test_conv_frame_chunks(dev, case):
+    """Batches whose operands exceed 2 GiB run as consecutive frame chunks
+    (tmr_conv_desc.max_frames): forced here at 2 frames per launch, the results equal the
+    single-launch ones (fwd, fused BN partials, dgrad bit-exact; wgrad to summation order)."""
+    n, h, w, cin, cout, r, st, pad = case
+    g = torch.Generator().manual_seed(sum(case))
+    cs = 4 if cin == 3 else cin
+    x = torch.randn(n, h, w, cs, generator=g)
+    if cin == 3:
+        x[..., 3] = 0
+    x = x.to(dev)
+    wk = torch.randn(cout, r, r, cs, generator=g).to(dev) / (cin * r * r) ** 0.5
+    y1 = ops.conv_fwd(x, wk, st, pad)
+    ys, stats, nparts = ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin)
+    dy = torch.randn(y1.shape, generator=g).to(dev)
+    dx1 = ops.conv_dgrad(dy, wk, (h, w), st, pad) if cin != 3 else None
+    dw1 = ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin)
+    old = ops.MAX_FRAMES
+    try:
+        ops.MAX_FRAMES = 2
+        y2 = ops.conv_fwd(x, wk, st, pad)
+        ys2, stats2, nparts2 = ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin)
+        dx2 = ops.conv_dgrad(dy, wk, (h, w), st, pad) if cin != 3 else None
+        dw2 = ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin)
+    finally:
+        ops.MAX_FRAMES = old
+    assert torch.equal(y1, y2) and torch.equal(ys, ys2)
+    assert nparts2 >= nparts
+    if dx1 is not None:
+        assert torch.equal(dx1, dx2)
+    assert rel_err(dw2, dw1) < 1e-6
+    # BN statistics from the chunked partials
+    c = cout
+    outs = []
+    for st_, np_ in ((stats, nparts), (stats2, nparts2)):
+        outs.append(ops.bn_finalize(st_, np_, torch.ones(c, device=dev), torch.zeros(c, device=dev),
+                                    torch.zeros(c, device=dev), torch.ones(c, device=dev), 0.1, 1e-5))
+    assert rel_err(outs[1][0], outs[0][0]) < 1e-5 and rel_err(outs[1][1], outs[0][1]) < 1e-5

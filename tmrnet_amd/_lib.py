@@ -23,7 +23,7 @@ SZ = ctypes.c_size_t
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "pad_w",
-                 "x_ld", "y_ld", "math")]
+                 "x_ld", "y_ld", "math", "max_frames")]
 
 
 DP = ctypes.POINTER(ConvDesc)

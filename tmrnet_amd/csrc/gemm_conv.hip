@@ -759,37 +759,83 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   return 0;
 }
 
-TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
-                           const float* bias, float* y, float beta, hipStream_t stream) {
-  GemmArgs a;
-  bool al;
-  int rc = conv_fwd_args(d, x, w_krsc, bias, y, beta, a, al);
-  if (rc) return rc;
-  return launch_gemm<MODE_FWD>(a, al, 1, stream);
+// Frames per launch: the buffer descriptors take 32-bit byte offsets, so every operand of one
+// launch must stay below 2 GiB; larger batches (e.g. C5's 1920 frames) run as several launches
+// over consecutive frame ranges (d->max_frames caps it further, for tests).
+static int frames_per_launch(const tmr_conv_desc* d) {
+  const long xf = (long)d->h * d->w * xld_of(d) * 4;
+  const long yf = (long)d->ho * d->wo * yld_of(d) * 4;
+  const long mx = xf > yf ? xf : yf;
+  long f = mx > 0 ? 0x7fffffffL / mx : d->n;
+  if (d->max_frames > 0 && d->max_frames < f) f = d->max_frames;
+  if (f > d->n) f = d->n;
+  return (int)(f > 0 ? f : 1);
 }
 
-TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
+static tmr_conv_desc chunk_desc(const tmr_conv_desc* d, int nc) {
+  tmr_conv_desc c = *d;
+  c.n = nc;
+  return c;
+}
+
+static int stats_parts_of(const tmr_conv_desc* d) {
   const long M = (long)d->n * d->ho * d->wo;
   return cdiv(M, kCfgs[pick_cfg(M, d->k)].bm);
 }
 
+static long x_frame(const tmr_conv_desc* d) { return (long)d->h * d->w * xld_of(d); }
+static long y_frame(const tmr_conv_desc* d) { return (long)d->ho * d->wo * yld_of(d); }
+
+TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                           const float* bias, float* y, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
+  const int fc = frames_per_launch(d);
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    GemmArgs a;
+    bool al;
+    int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, bias, y + f0 * y_frame(d), beta, a, al);
+    if (!rc) rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
+  const int fc = frames_per_launch(d);
+  int parts = 0;
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    parts += stats_parts_of(&c);
+  }
+  return parts;
+}
+
 TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const float* w_krsc,
                                    float* y, void* stats, size_t stats_bytes, hipStream_t stream) {
-  GemmArgs a;
-  bool al;
-  int rc = conv_fwd_args(d, x, w_krsc, nullptr, y, 0.f, a, al);
-  if (rc) return rc;
+  TMR_CHECK_ARG(d, "tmr_conv2d_fwd_bnstats: null descriptor");
   TMR_CHECK_ARG(yld_of(d) == d->k, "tmr_conv2d_fwd_bnstats: output must be dense (y_ld == k)");
   const size_t need = (size_t)tmr_conv2d_fwd_stats_parts(d) * d->k * sizeof(float4);
   TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
                 stats_bytes, need);
-  a.stats = (float4*)stats;
-  return launch_gemm<MODE_FWD>(a, al, 1, stream);
+  const int fc = frames_per_launch(d);
+  float4* st = (float4*)stats;
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    GemmArgs a;
+    bool al;
+    int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, nullptr, y + f0 * y_frame(d), 0.f, a, al);
+    if (rc) return rc;
+    a.stats = st;
+    rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
+    if (rc) return rc;
+    st += (long)stats_parts_of(&c) * d->k;
+  }
+  return 0;
 }
 
-TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
-                             float* dx, float beta, hipStream_t stream) {
-  TMR_CHECK_ARG(d, "tmr_conv2d_dgrad: null descriptor");
+static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                           float* dx, float beta, hipStream_t stream) {
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
   const int lk = ilog2_exact(d->k);
   TMR_CHECK_ARG(lk >= 2, "tmr_conv2d_dgrad: output channels %d must be a power of two >= 4", d->k);
@@ -837,6 +883,18 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
   return 0;
 }
 
+TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                             float* dx, float beta, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_dgrad: null descriptor");
+  const int fc = frames_per_launch(d);
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    int rc = conv_dgrad_impl(&c, dy + f0 * y_frame(d), w_krsc, dx + f0 * x_frame(d), beta, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* slab) {
   const long Mred = (long)d->n * d->ho * d->wo;
   const long Mo = d->k, No = (long)d->r * d->s * d->c;
@@ -862,14 +920,33 @@ static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* sl
 TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
   int sp, kc;
   long slab;
-  wgrad_plan(d, &sp, &kc, &slab);
+  const tmr_conv_desc c = chunk_desc(d, frames_per_launch(d));   // the largest chunk
+  wgrad_plan(&c, &sp, &kc, &slab);
   return (size_t)sp * slab * sizeof(float);
 }
 
+static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* dy,
+                           float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
+                           hipStream_t stream);
+
+// frame chunks accumulate into dw in chunk order (beta = 1 after the first): deterministic
 TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float* dy,
                              float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
                              hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_wgrad: null descriptor");
+  const int fc = frames_per_launch(d);
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    int rc = conv_wgrad_impl(&c, x + f0 * x_frame(d), dy + f0 * y_frame(d), dw_oihw, c_real,
+                             f0 == 0 ? beta : 1.f, ws, ws_bytes, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* dy,
+                           float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
+                           hipStream_t stream) {
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_wgrad: stored input channels %d must be a power of two >= 4", d->c);

@@ -65,13 +65,17 @@ def _empty(shape, like, dtype=f32):
 # ----------------------------------------------------------------- conv / gemm
 MATH = {"fp32": 0, "bf16": 1}   # tmr_conv_desc.math (TMR_MATH_F32 / TMR_MATH_BF16)
 _SUFFIX = {"fp32": "", "bf16": "_bf16"}
+# frames per conv launch (tmr_conv_desc.max_frames): 0 = automatic (operands < 2 GiB); tests set
+# a small cap to exercise the frame-chunked launches at small sizes
+MAX_FRAMES = 0
 
 
 def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math="fp32"):
     pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
     wo = (w + 2 * pad_w - s) // stride + 1
-    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math])
+    return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
+                    MAX_FRAMES)
 
 
 def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None, pad_w=None,
