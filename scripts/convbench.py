@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--dgrad-beta", type=float, default=0.0,
+                    help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     shapes = Counter(resnet50_convs(args.frames))
@@ -56,7 +58,8 @@ def main():
             if kind == "dgrad" and cin == 3:
                 continue
             fn = {"fwd": lambda: ops.conv_fwd(x, wk, st, pad, out=y),
-                  "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x),
+                  "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x,
+                                                  beta=args.dgrad_beta),
                   "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin)}[kind]
             fn()
             torch.cuda.synchronize()

@@ -649,12 +649,22 @@ int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-int pick_cfg(long M, long N) {
+// Tile choice per GEMM view, from scripts/convbench.py over the 23 ResNet-50 shapes x 3 views
+// (profiles/r1/convbench_cfgs.txt).  Short reductions (K <= 576: the 1x1 dgrads that accumulate
+// into the residual gradient, the 3x3 ones at 64 channels) are epilogue/latency bound and run
+// best as 64x64 tiles at high occupancy; wgrad prefers 256x128 to 256x256.
+int pick_cfg(long M, long N, long K, int mode) {
   static const int forced = env_int("TMR_GEMM_CFG", -1);  // experiments only
   if (forced >= 0 && forced < kNumCfgs) {
     const TileCfg c = kCfgs[forced];
     if (M >= c.bm && N >= c.bn) return forced;
   }
+  if (mode == MODE_DGRAD && K <= 576 && M >= 4096) return 3;
+  if (mode == MODE_WGRAD) {
+    if (M <= 64 && N >= 512) return 3;
+    if (M >= 256 && N >= 128) return 4;
+  }
+  if (mode == MODE_FWD && N <= 128 && K >= 576 && M >= 4096) return 3;
   if (M >= 256 && N >= 256) return 6;   // 256x256, 16 waves (measured best, convbench)
   if (M >= 256 && N >= 128) return 4;   // 256x128, 8 waves
   if (N <= 64 && M >= 256) return 1;
@@ -674,7 +684,7 @@ int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   int var = al ? (uniform ? 0 : 1) : 2;
   TMR_CHECK_ARG(uniform || (al && MODE == MODE_FWD),
                 "gemm: per-element taps need aligned channels and the forward view");
-  const int cfg = pick_cfg(a.M, a.N);
+  const int cfg = pick_cfg(a.M, a.N, a.K, MODE);
   const TileCfg c = kCfgs[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
@@ -780,7 +790,7 @@ static tmr_conv_desc chunk_desc(const tmr_conv_desc* d, int nc) {
 
 static int stats_parts_of(const tmr_conv_desc* d) {
   const long M = (long)d->n * d->ho * d->wo;
-  return cdiv(M, kCfgs[pick_cfg(M, d->k)].bm);
+  return cdiv(M, kCfgs[pick_cfg(M, d->k, (long)d->r * d->s * d->c, MODE_FWD)].bm);
 }
 
 static long x_frame(const tmr_conv_desc* d) { return (long)d->h * d->w * xld_of(d); }
@@ -898,7 +908,7 @@ TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const floa
 static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* slab) {
   const long Mred = (long)d->n * d->ho * d->wo;
   const long Mo = d->k, No = (long)d->r * d->s * d->c;
-  const TileCfg tc = kCfgs[pick_cfg(Mo, No)];
+  const TileCfg tc = kCfgs[pick_cfg(Mo, No, Mred, MODE_WGRAD)];
   const long tiles = (long)cdiv(Mo, tc.bm) * cdiv(No, tc.bn);
   // aim for ~target workgroups; at least minrows reduction rows per split
   static const long target = env_int("TMR_WGRAD_TARGET", 512);
