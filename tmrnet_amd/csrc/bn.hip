@@ -82,37 +82,43 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const float* __restrict__
   }
 }
 
-// Chan/Welford combine of (n, mean, M2) partials in double, fixed order -> deterministic.
-// 8 channels per workgroup x 32 groups of partial rows.
-__device__ __forceinline__ void chan_add(double& n, double& mean, double& m2, double nb,
-                                         double mb, double m2b) {
-  if (nb <= 0) return;
-  const double nn = n + nb;
-  const double d = mb - mean;
-  mean += d * (nb / nn);
-  m2 += m2b + d * d * (n * nb / nn);
-  n = nn;
-}
-
+// Combine of (n, mean, M2) partials in double, fixed order -> deterministic.  One
+// workgroup per channel (the conv epilogue emits ~8k partials per channel for layer1-sized
+// outputs, so the combine needs the whole chip).  Division-free shifted sums about
+// K = the first partial's mean: N = sum n_b, S1 = sum n_b d_b, S2 = sum (M2_b + n_b d_b^2),
+// d_b = mean_b - K; then mean = K + S1/N and M2 = S2 - S1^2/N (exact in exact arithmetic;
+// the shift keeps the cancellation at the size of the spread of the partial means).
 __global__ __launch_bounds__(NT) void bn_finalize_k(const float4* __restrict__ part, int nparts,
                                                     int c, const float* gamma, const float* beta,
                                                     float* rmean, float* rvar, float momentum,
                                                     float eps, float* smean, float* sinv,
                                                     float* scale, float* shift) {
-  const int lc = threadIdx.x & 7, g = threadIdx.x >> 3;
-  const int ch = blockIdx.x * 8 + lc;
-  double n = 0, mean = 0, m2 = 0;
-  if (ch < c)
-    for (int b = g; b < nparts; b += 32) {
-      const float4 p = part[(long)b * c + ch];
-      chan_add(n, mean, m2, p.x, p.y, p.z);
-    }
-  __shared__ double red[32][8][3];
-  red[g][lc][0] = n; red[g][lc][1] = mean; red[g][lc][2] = m2;
+  const int ch = blockIdx.x;
+  const double K = part[ch].y;
+  double n = 0, s1 = 0, s2 = 0;
+  for (int b = threadIdx.x; b < nparts; b += NT) {
+    const float4 p = part[(long)b * c + ch];
+    const double nb = p.x, d = (double)p.y - K;
+    n += nb;
+    s1 = fma(nb, d, s1);
+    s2 += (double)p.z + nb * d * d;
+  }
+  __shared__ double red[3][NT];
+  red[0][threadIdx.x] = n; red[1][threadIdx.x] = s1; red[2][threadIdx.x] = s2;
   __syncthreads();
-  if (g == 0 && ch < c) {
-    n = 0; mean = 0; m2 = 0;
-    for (int k = 0; k < 32; ++k) chan_add(n, mean, m2, red[k][lc][0], red[k][lc][1], red[k][lc][2]);
+  for (int h = NT / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] += red[1][threadIdx.x + h];
+      red[2][threadIdx.x] += red[2][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    n = red[0][0]; s1 = red[1][0]; s2 = red[2][0];
+    const double mean = n > 0 ? K + s1 / n : 0.0;
+    double m2 = n > 0 ? s2 - s1 * (s1 / n) : 0.0;
+    if (m2 < 0) m2 = 0;
     const double var = n > 0 ? m2 / n : 0.0;
     const double inv = 1.0 / sqrt(var + (double)eps);
     smean[ch] = (float)mean;
@@ -232,22 +238,26 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
                                                    const float* mean, const float* inv,
                                                    const float* gamma, float* dgamma,
                                                    float* dbeta, float* coef) {
-  const int lc = threadIdx.x & 7, g = threadIdx.x >> 3;
-  const int ch = blockIdx.x * 8 + lc;
+  const int ch = blockIdx.x;  // one workgroup per channel, fixed-order tree reduction
   double s = 0.0, q = 0.0;
-  if (ch < c) {
-    for (int b = g; b < nrb; b += 32) {
-      s += part[((long)b * c + ch) * 2];
-      q += part[((long)b * c + ch) * 2 + 1];
-    }
+  for (int b = threadIdx.x; b < nrb; b += NT) {
+    s += part[((long)b * c + ch) * 2];
+    q += part[((long)b * c + ch) * 2 + 1];
   }
-  __shared__ double red[32][8][2];
-  red[g][lc][0] = s;
-  red[g][lc][1] = q;
+  __shared__ double red[2][NT];
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
   __syncthreads();
-  if (g == 0 && ch < c) {
-    s = 0.0; q = 0.0;
-    for (int k = 0; k < 32; ++k) { s += red[k][lc][0]; q += red[k][lc][1]; }
+  for (int h = NT / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] += red[1][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    s = red[0][0];
+    q = red[1][0];
     const double iv = inv[ch];
     const double dbt = s;
     const double dgm = q * iv;  // sum dzh * xhat
@@ -327,7 +337,7 @@ TMR_API int tmr_bn_finalize(const void* partials, int nparts, int c, const float
                             float momentum, float eps, float* save_mean, float* save_invstd,
                             float* scale, float* shift, hipStream_t stream) {
   TMR_CHECK_ARG(nparts > 0 && c > 0, "tmr_bn_finalize: empty partials");
-  hipLaunchKernelGGL(bn_finalize_k, dim3(cdiv(c, 8)), dim3(NT), 0, stream, (const float4*)partials,
+  hipLaunchKernelGGL(bn_finalize_k, dim3(c), dim3(NT), 0, stream, (const float4*)partials,
                      nparts, c, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd, scale, shift);
   TMR_CHECK_LAUNCH("bn_finalize");
@@ -393,7 +403,7 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
   else
     hipLaunchKernelGGL((bn_bwd_partial<0>), pg, dim3(NT), 0, stream, dzw, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
   TMR_CHECK_LAUNCH("bn_bwd_partial");
-  hipLaunchKernelGGL(bn_bwd_final, dim3(cdiv(c, 8)), dim3(NT), 0, stream, part, p.nrb, rows, c,
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");
   long n4 = (long)rows * c / 4;

@@ -530,7 +530,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
   }
   // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
-  // then M2 about it; combined across tiles by tmr_bn_finalize (Chan, double, fixed order).
+  // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
   if (MODE == MODE_FWD && a.stats != nullptr) {
     float* red = smem;  // main loop ended with a barrier: LDS is free
     const int nrows = min(BM, a.M - m0);
