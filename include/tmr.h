@@ -60,6 +60,14 @@ typedef struct tmr_conv_desc {
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
 int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
                    const float* bias, float* y, float beta, hipStream_t stream);
+/* Inference conv + BatchNorm(running stats) [+ residual] [+ ReLU] in one launch (eval-mode
+ * Bottleneck units: LFB construction, Training TMRNet/train_only_non-local_pretrained.py:570-590,
+ * and the eval scripts): y = [relu](fmaf(conv(x, w_krsc), scale[k], shift[k]) + residual),
+ * the same arithmetic as tmr_conv2d_fwd followed by tmr_bn_apply, without the y round trip.
+ * scale/shift from tmr_bn_eval_params; residual (NHWC like y) may be NULL, must not alias y. */
+int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                         const float* scale, const float* shift, const float* residual, float* y,
+                         int relu, hipStream_t stream);
 /* Forward conv whose epilogue also emits BatchNorm batch-statistic partials of y:
  * stats = float4 [tmr_conv2d_fwd_stats_parts(d)][k] of (count, mean, M2, 0) per output-row
  * tile, consumed by tmr_bn_finalize (fuses the separate statistics pass of nn.BatchNorm2d). */
@@ -247,7 +255,8 @@ int tmr_timeconv_max5_bwd(const float* dy, const uint8_t* code, float* d1, float
 /* ---------------- LSTM cell (head.hip) -------------------------------------
  * nn.LSTM(2048,512) gates in PyTorch order i,f,g,o (train_only_non-local_pretrained.py:215,
  * :230-231).  gx: x W_ih^T + b_ih + b_hh for step t (row stride ldgx); ghh: h_{t-1} W_hh^T
- * (NULL at t=0); c_prev NULL at t=0.  act saves (i,f,g,o) activations [b][4h]. */
+ * (NULL at t=0); c_prev NULL at t=0.  act saves (i,f,g,o) activations [b][4h] for the
+ * backward (NULL: inference, nothing saved). */
 int tmr_lstm_cell_fwd(const float* gx, int ldgx, const float* ghh, const float* c_prev,
                       float* h_out, int ldh, float* c_out, float* act, int b, int hdim,
                       hipStream_t stream);

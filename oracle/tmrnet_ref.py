@@ -28,6 +28,9 @@ reference checkout, ``code/``):
 * ``crop_normalize_ref`` -- crop at a per-clip offset + ToTensor + Normalize
                          (``train_only_non-local_pretrained.py:101-126``, ``:335-341``)
 * ``train_step_ref``  -- the step at ``train_only_non-local_pretrained.py:698-725``
+* ``LFBModelRef`` / ``build_lfb_ref`` -- ``resnet_lstm_LFB`` (:243-270) and the LFB
+                         construction loop (:534-607): eval mode, centre crop (:360-366),
+                         clips in valid-start order, last hidden state per clip, float64 bank
 * ``emulate_bf16_convs`` -- the bf16 configs (BASELINE.json configs[3], [4]) have no reference
                          implementation (the reference is fp32 only): this restates the
                          build's TMR_MATH_BF16 contract on torch ops -- every trunk conv with
@@ -36,6 +39,7 @@ reference checkout, ``code/``):
 """
 import math
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -369,6 +373,45 @@ class MemoryBankRef(nn.Module):
         y = y.contiguous().view(-1, 512)
         y = y * mask if mask is not None else self.dropout(y)
         return self.fc(y)
+
+
+class LFBModelRef(nn.Module):
+    """resnet_lstm_LFB (train_only_non-local_pretrained.py:243-270)."""
+
+    def __init__(self, seq_len=10):
+        super().__init__()
+        self.seq_len = seq_len
+        self.share = resnet50_share()
+        self.lstm = nn.LSTM(2048, 512, batch_first=True)
+        init.xavier_normal_(self.lstm.all_weights[0][0])
+        init.xavier_normal_(self.lstm.all_weights[0][1])
+
+    def forward(self, x):
+        T = self.seq_len
+        x = self.share(x.reshape(-1, 3, 224, 224)).reshape(-1, T, 2048)
+        y, _ = self.lstm(x)
+        return y.contiguous().view(-1, 512)[T - 1::T]
+
+
+def build_lfb_ref(model, frames_u8, lengths, batch_clips=4):
+    """The LFB construction loop of train_only_non-local_pretrained.py:547-607: SeqSampler over
+    train_idx_LFB (each valid start + its T-1 successors, :491-494), test transform = centre crop
+    (crop_type 1, :360-366), model in eval mode under no_grad, outputs appended row by row with
+    np.concatenate onto a float64 (0, 512) array (:574-581).  frames_u8: (N,250,250,3) uint8."""
+    T = model.seq_len
+    model.eval()
+    valid = get_useful_start_idx(T, lengths)
+    off = int(round((frames_u8.shape[1] - 224) / 2.0))
+    bank = np.zeros(shape=(0, 512))
+    with torch.no_grad():
+        for b0 in range(0, len(valid), batch_clips):
+            starts = valid[b0:b0 + batch_clips]
+            idx = [s + j for s in starts for j in range(T)]
+            x = crop_normalize_ref(frames_u8[idx], [(off, off)] * len(starts), T)
+            out = model(x.view(-1, T, 3, 224, 224))
+            for j in range(len(out)):
+                bank = np.concatenate((bank, out.data.cpu()[j].numpy().reshape(1, 512)), axis=0)
+    return bank, valid
 
 
 # --------------------------------------------------------------------------

@@ -291,3 +291,37 @@ def test_conv_frame_chunks(dev, case):
         outs.append(ops.bn_finalize(st_, np_, torch.ones(c, device=dev), torch.zeros(c, device=dev),
                                     torch.zeros(c, device=dev), torch.ones(c, device=dev), 0.1, 1e-5))
     assert rel_err(outs[1][0], outs[0][0]) < 1e-5 and rel_err(outs[1][1], outs[0][1]) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 256, 1, 1, 0, True, True),
+                                  (3, 14, 14, 128, 128, 3, 2, 1, False, True),
+                                  (2, 9, 9, 256, 64, 1, 1, 0, False, False),
+                                  (1, 28, 28, 3, 64, 7, 2, 3, False, True)])
+def test_conv_fused_eval_bn(dev, case):
+    """tmr_conv2d_fwd_fused (eval BN + residual + ReLU in the epilogue) is bit-identical to
+    tmr_conv2d_fwd followed by tmr_bn_apply (the same fmaf/add/max sequence)."""
+    n, h, w, cin, cout, r, st, pad, res, relu = case
+    g = torch.Generator().manual_seed(7)
+    cs = 4 if cin == 3 else cin
+    x = torch.zeros(n, h, w, cs)
+    x[..., :cin] = torch.randn(n, h, w, cin, generator=g)
+    wt = torch.randn(cout, cin, r, r, generator=g) / np.sqrt(cin * r * r)
+    x = x.to(dev)
+    wk = ops.weight_to_krsc(wt.to(dev), cpad=cs)
+    scale = (torch.rand(cout, generator=g) + 0.5).to(dev)
+    shift = torch.randn(cout, generator=g).to(dev)
+    y = ops.conv_fwd(x, wk, st, pad, c_real=cin)
+    resid = torch.randn(y.shape, generator=g).to(dev) if res else None
+    z_ref = ops.bn_apply(y, scale, shift, resid, relu)
+    z = ops.conv_fwd_fused(x, wk, st, pad, scale, shift, resid, relu, c_real=cin)
+    torch.cuda.synchronize()
+    assert torch.equal(z, z_ref)
+    # and against float64 torch: conv -> affine -> (+res) -> relu
+    xd = x[..., :cin].permute(0, 3, 1, 2).double().cpu()
+    yd = F.conv2d(xd, wt.double(), stride=st, padding=pad).permute(0, 2, 3, 1)
+    zd = yd * scale.double().cpu() + shift.double().cpu()
+    if res:
+        zd = zd + resid.double().cpu()
+    if relu:
+        zd = zd.clamp_min(0)
+    assert rel_err(z, zd) < 1e-5

@@ -33,6 +33,7 @@ SIGNATURES = {
     "tmr_abi_version": [],
     "tmr_last_error": [],
     "tmr_conv2d_fwd": [DP, P, P, P, P, F, P],
+    "tmr_conv2d_fwd_fused": [DP, P, P, P, P, P, P, I, P],
     "tmr_conv2d_fwd_stats_parts": [DP],
     "tmr_conv2d_fwd_bnstats": [DP, P, P, P, P, SZ, P],
     "tmr_conv2d_dgrad": [DP, P, P, P, F, P],

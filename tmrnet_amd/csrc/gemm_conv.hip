@@ -63,6 +63,11 @@ struct GemmArgs {
   long slab;
   // FWD: optional per-(m-tile, column) BatchNorm partials (n, mean, M2, 0)
   float4* stats;
+  // FWD inference epilogue: C = [relu](fmaf(acc, scale, bias) + res), res laid out like C
+  // (eval-mode BatchNorm, the residual add and ReLU of a Bottleneck fused into the conv)
+  const float* scale;
+  const float* res;
+  int relu;
   // byte extents of A and B (buffer-descriptor range checks)
   uint32_t Abytes, Bbytes;
   int prec;  // TMR_MATH_F32 / TMR_MATH_BF16
@@ -600,7 +605,14 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = col0 + 32 * j;
-        if (col < a.N) Cb[ro + col] = acc[i][j][r] + bvals[j];
+        if (col >= a.N) continue;
+        float v = acc[i][j][r] + bvals[j];
+        if (MODE == MODE_FWD) {
+          if (a.scale) v = fmaf(acc[i][j][r], a.scale[col], bvals[j]);
+          if (a.res) v += a.res[ro + col];
+          if (a.relu) v = fmaxf(v, 0.f);
+        }
+        Cb[ro + col] = v;
       }
     }
 }
@@ -806,6 +818,28 @@ TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* 
     bool al;
     int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, bias, y + f0 * y_frame(d), beta, a, al);
     if (!rc) rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                                 const float* scale, const float* shift, const float* residual,
+                                 float* y, int relu, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_fwd_fused: null descriptor");
+  TMR_CHECK_ARG(scale && shift, "tmr_conv2d_fwd_fused: null BatchNorm scale/shift");
+  TMR_CHECK_ARG(!residual || residual != y, "tmr_conv2d_fwd_fused: residual must not alias y");
+  const int fc = frames_per_launch(d);
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    GemmArgs a;
+    bool al;
+    int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, shift, y + f0 * y_frame(d), 0.f, a, al);
+    if (rc) return rc;
+    a.scale = scale;
+    a.res = residual ? residual + f0 * y_frame(d) : nullptr;
+    a.relu = relu;
+    rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
     if (rc) return rc;
   }
   return 0;

@@ -34,8 +34,10 @@ __global__ void lstm_cell_fwd_k(const float* __restrict__ gx, int ldgx,
   const float cn = fg * cprev + ig * gg;
   c[i] = cn;
   h[(long)bb * ldh + j] = og * tanhf(cn);
-  float* a = act + (long)bb * 4 * hd;
-  a[j] = ig; a[hd + j] = fg; a[2 * hd + j] = gg; a[3 * hd + j] = og;
+  if (act) {
+    float* a = act + (long)bb * 4 * hd;
+    a[j] = ig; a[hd + j] = fg; a[2 * hd + j] = gg; a[3 * hd + j] = og;
+  }
 }
 
 __global__ void lstm_cell_bwd_k(const float* __restrict__ dho, int lddh,

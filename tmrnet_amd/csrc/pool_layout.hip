@@ -220,6 +220,7 @@ TMR_API int tmr_weight_oihw_to_krsc(const float* w, float* wk, int k, int c, int
   return 0;
 }
 
+
 TMR_API int tmr_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, int cpad,
                              hipStream_t stream) {
   TMR_CHECK_ARG(cpad >= c, "tmr_nchw_to_nhwc: cpad < c");

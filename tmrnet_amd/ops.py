@@ -100,6 +100,30 @@ def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None,
     return out
 
 
+def conv_fwd_fused(x, w_krsc, stride, pad, scale, shift, residual=None, relu=True, c_real=None,
+                   pad_w=None, math="fp32"):
+    """Inference conv + BN(running stats) [+ residual] [+ ReLU] in one launch:
+    [relu](conv(x, w_krsc) * scale + shift + residual) -> (N,Ho,Wo,K)."""
+    _req(x, "x"); _req(w_krsc, "w"); _req(scale, "scale"); _req(shift, "shift")
+    n, h, w, c = x.shape
+    k, r, s, c2 = w_krsc.shape
+    assert c == c2, (x.shape, w_krsc.shape)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
+    out = _empty((n, d.ho, d.wo, k), x)
+    if residual is not None:
+        _req(residual, "residual")
+        if residual.shape != out.shape:
+            raise RuntimeError("conv_fwd_fused: residual %s != output %s"
+                               % (tuple(residual.shape), tuple(out.shape)))
+    ysz = n * d.ho * d.wo * k
+    with _prof("conv_fwd" + _SUFFIX[math], 2.0 * ysz * r * s * (c_real or c),
+               (n, h, w, c, k, r, stride),
+               4 * (n * h * w * c + k * r * s * c + ysz * (2 if residual is not None else 1))):
+        call("tmr_conv2d_fwd_fused", ctypes.byref(d), x, w_krsc, scale, shift, residual, out,
+             int(relu), stream_ptr())
+    return out
+
+
 def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32"):
     """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts)."""
     _req(x, "x"); _req(w_krsc, "w")
@@ -441,8 +465,9 @@ def nl_attn_bwd(lt, rows, u, p, dctx, B, L, scale, want_dlt):
     return ut, dlt
 
 
-def lstm_cell_fwd(gx_t, ghh, c_prev, h_t, c_t, act_t):
-    """gx_t (B,4H) row-strided view, h_t (B,H) row-strided view of y[:, t]."""
+def lstm_cell_fwd(gx_t, ghh, c_prev, h_t, c_t, act_t=None):
+    """gx_t (B,4H) row-strided view, h_t (B,H) row-strided view of y[:, t]; act_t None =
+    inference (activations not saved)."""
     B, H = c_t.shape
     call("tmr_lstm_cell_fwd", gx_t, gx_t.stride(0), ghh, c_prev, h_t, h_t.stride(0), c_t, act_t,
          B, H, stream_ptr())

@@ -73,10 +73,12 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
             bn.running_var, _bn_momentum(bn), bn.eps)
         bn.num_batches_tracked.add_(1)
     else:
-        y = ops.conv_fwd(x, wk, stride, pad, c_real=c, math=math)
-        mean = inv = None
+        # eval: running-stat BN, residual and ReLU in the conv epilogue (one launch, no y pass;
+        # same arithmetic as conv_fwd + bn_apply)
         scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                                           bn.running_var, bn.eps)
+        return ops.conv_fwd_fused(x, wk, stride, pad, scale, shift, residual, relu, c_real=c,
+                                  math=math)
     z = ops.bn_apply(y, scale, shift, residual, relu)
     if recs is not None:
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
