@@ -193,6 +193,11 @@ int tmr_dropout_mask(float* mask, long n, float p, uint64_t seed, uint64_t offse
  * preds = argmax (torch.max tie rule: first). weight may be NULL. */
 int tmr_ce_sum(const float* logits, const int64_t* labels, const float* weight, int b, int k,
                float gscale, float* loss, float* dlogits, int64_t* preds, hipStream_t stream);
+/* Eval head: probs = nn.Softmax(dim=1)(logits), (pmax, preds) = torch.max(probs, 1)
+ * (eval/python/test_singlenet_phase_non-local_pretrained_2fc_copy_mutiConv6_3.py:470-473).
+ * Any output pointer may be NULL. */
+int tmr_softmax_max(const float* logits, int b, int k, float* probs, float* pmax, int64_t* preds,
+                    hipStream_t stream);
 /* torch.optim.SGD step (momentum, dampening, weight_decay, nesterov), :725 */
 int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr, float momentum,
                  float dampening, float weight_decay, int nesterov, int first_step,

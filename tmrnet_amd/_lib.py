@@ -66,6 +66,7 @@ SIGNATURES = {
     "tmr_avgpool2d_bwd": [P, P, I, I, I, I, I, I, I, I, I, I, P],
     "tmr_col_sum": [P, I, I, I, P, F, P],
     "tmr_dropout_mask": [P, L, F, U64, U64, P],
+    "tmr_softmax_max": [P, I, I, P, P, P, P],
     "tmr_ce_sum": [P, P, P, I, I, F, P, P, P, P],
     "tmr_sgd_step": [P, P, P, L, F, F, F, F, I, I, P],
     "tmr_lfb_index": [P, I, P, I, I, P, P],

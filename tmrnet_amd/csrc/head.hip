@@ -333,6 +333,28 @@ __global__ void ce_sum_k(const float* __restrict__ x, const int64_t* __restrict_
   }
 }
 
+// nn.Softmax over classes + torch.max(probs, 1) (eval scripts, e.g.
+// eval/python/test_singlenet_phase_non-local_pretrained_2fc_copy_mutiConv6_3.py:470-473):
+// one thread per clip row; argmax = first maximal logit (softmax is monotone, so the max
+// probability is at the max logit; the same tie rule as ce_sum_k).
+__global__ void softmax_max_k(const float* __restrict__ x, int b, int k, float* __restrict__ probs,
+                              float* __restrict__ pmax, int64_t* __restrict__ preds) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b) return;
+  const float* xr = x + (long)i * k;
+  float mx = xr[0];
+  int am = 0;
+  for (int j = 1; j < k; ++j)
+    if (xr[j] > mx) { mx = xr[j]; am = j; }
+  float s = 0.f;
+  for (int j = 0; j < k; ++j) s += expf(xr[j] - mx);
+  const float inv = 1.0f / s;
+  if (probs)
+    for (int j = 0; j < k; ++j) probs[(long)i * k + j] = expf(xr[j] - mx) * inv;
+  if (pmax) pmax[i] = inv;   // exp(0) / s
+  if (preds) preds[i] = am;
+}
+
 // ------------------------------------------------------------ column sums
 __global__ void col_sum_k(const float* __restrict__ x, int rows, int cols, int ld,
                           float* __restrict__ out, float beta) {
@@ -471,6 +493,16 @@ TMR_API int tmr_ce_sum(const float* logits, const int64_t* labels, const float* 
   hipLaunchKernelGGL(ce_sum_k, dim3(1), dim3(256), b * sizeof(float), stream, logits, labels,
                      weight, b, k, gscale, loss, dlogits, preds);
   TMR_CHECK_LAUNCH("ce_sum");
+  return 0;
+}
+
+TMR_API int tmr_softmax_max(const float* logits, int b, int k, float* probs, float* pmax,
+                            int64_t* preds, hipStream_t stream) {
+  TMR_CHECK_ARG(b >= 0 && k >= 1, "tmr_softmax_max: bad shape b=%d k=%d", b, k);
+  if (b == 0) return 0;
+  hipLaunchKernelGGL(softmax_max_k, dim3(cdiv(b, 256)), dim3(256), 0, stream, logits, b, k, probs,
+                     pmax, preds);
+  TMR_CHECK_LAUNCH("softmax_max");
   return 0;
 }
 

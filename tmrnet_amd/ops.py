@@ -385,6 +385,17 @@ def ce_sum(logits, labels, weight=None, gscale=1.0, want_grad=True):
     return loss, dl, preds
 
 
+def softmax_max(logits):
+    """(probs, max prob, argmax) of nn.Softmax(dim=1) + torch.max(., 1) over (B, K) logits."""
+    _req(logits, "logits")
+    b, k = logits.shape
+    probs = _empty((b, k), logits)
+    pmax = _empty((b,), logits)
+    preds = torch.empty((b,), dtype=torch.int64, device=logits.device)
+    call("tmr_softmax_max", logits, b, k, probs, pmax, preds, stream_ptr())
+    return probs, pmax, preds
+
+
 def sgd_step(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step):
     call("tmr_sgd_step", p, g, buf, p.numel(), float(lr), float(momentum), float(dampening),
          float(weight_decay), int(nesterov), int(first_step), stream_ptr())
