@@ -189,6 +189,8 @@ def main():
         cpu = cpu_baseline(args)
 
     if rank == 0:
+        print("sgd table uploads: %d over %d steps" % (opt.table_uploads, args.warmup + args.steps),
+              file=sys.stderr)
         line = {
             "metric": ("train frames/sec, TMRNet ResNet50 seq=%d LFB=%d" % (T, L)
                        if args.model == "resnet50" else

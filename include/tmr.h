@@ -202,6 +202,22 @@ int tmr_softmax_max(const float* logits, int b, int k, float* probs, float* pmax
 int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr, float momentum,
                  float dampening, float weight_decay, int nesterov, int first_step,
                  hipStream_t stream);
+/* Multi-tensor SGD: every (param, grad, momentum buffer) of every param group in ONE launch
+ * (optimizer.step() of :725 over the groups of :646-655).  table: DEVICE array of ntensors
+ * entries; entry t covers workgroups [block_begin_t, block_begin_{t+1}), i.e. block_begin is the
+ * prefix sum of ceil(n / tmr_sgd_chunk()) and nblocks the total. */
+typedef struct tmr_sgd_tensor {
+  float* p;
+  const float* g;
+  float* buf;           /* NULL when momentum == 0 */
+  int64_t n;
+  int64_t block_begin;
+  float lr, momentum, dampening, weight_decay;
+  int32_t nesterov, first_step;
+} tmr_sgd_tensor;
+int64_t tmr_sgd_chunk(void);
+int tmr_sgd_step_multi(const tmr_sgd_tensor* table, int ntensors, int64_t nblocks,
+                       hipStream_t stream);
 /* LFB row table of get_long_feature (train_only_non-local_pretrained.py:293-311):
  * rows[b][k] = index of the first valid start >= max(start_b - k - 1, 0) in the sorted
  * valid-start list (== the reference's dict walk, incl. own-row fallback and

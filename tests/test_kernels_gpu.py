@@ -325,3 +325,39 @@ def test_conv_fused_eval_bn(dev, case):
     if relu:
         zd = zd.clamp_min(0)
     assert rel_err(z, zd) < 1e-5
+
+
+def test_sgd_optimizer_multi_tensor_matches_torch(dev):
+    """tmrnet_amd.SGD (one tmr_sgd_step_multi launch per step) vs torch.optim.SGD over three
+    steps: groups with different lr / momentum / dampening / nesterov / weight decay, tensors
+    straddling the 8192-element chunk, a parameter without grad, an lr change mid-run."""
+    import tmrnet_amd
+    g = torch.Generator().manual_seed(0)
+    shapes = [(3,), (8192,), (8193,), (70, 300), (1,), (5, 7)]
+    base = [torch.randn(s, generator=g) for s in shapes]
+    ours = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    ref = [torch.nn.Parameter(b.clone().double()) for b in base]
+
+    def groups(ps):
+        return [{"params": ps[0:2]},
+                {"params": ps[2:4], "lr": 0.05, "nesterov": True, "momentum": 0.8,
+                 "dampening": 0.0},
+                {"params": ps[4:5], "momentum": 0.0},
+                {"params": ps[5:6], "dampening": 0.3, "weight_decay": 0.0}]
+    o1 = tmrnet_amd.SGD(groups(ours), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    o2 = torch.optim.SGD(groups(ref), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    for step in range(3):
+        if step == 2:
+            for a, b in zip(o1.param_groups, o2.param_groups):
+                a["lr"] *= 0.1; b["lr"] *= 0.1
+        for i, (a, b) in enumerate(zip(ours, ref)):
+            if i == 4 and step == 1:
+                a.grad = None; b.grad = None        # no grad this step: untouched
+                continue
+            gr = torch.randn(a.shape, generator=g)
+            a.grad = gr.to(dev) if i != 3 else gr.t().contiguous().t().to(dev)
+            b.grad = gr.double()
+        o1.step(); o2.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ours, ref):
+        assert rel_err(a, b) < 1e-6

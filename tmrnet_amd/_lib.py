@@ -68,6 +68,8 @@ SIGNATURES = {
     "tmr_dropout_mask": [P, L, F, U64, U64, P],
     "tmr_softmax_max": [P, I, I, P, P, P, P],
     "tmr_ce_sum": [P, P, P, I, I, F, P, P, P, P],
+    "tmr_sgd_chunk": [],
+    "tmr_sgd_step_multi": [P, I, ctypes.c_int64, P],
     "tmr_sgd_step": [P, P, P, L, F, F, F, F, I, I, P],
     "tmr_lfb_index": [P, I, P, I, I, P, P],
     "tmr_lfb_gather": [P, P, P, L, I, P],
@@ -88,6 +90,7 @@ _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,
     "tmr_conv2d_wgrad_ws_bytes": SZ,
     "tmr_bn_ws_bytes": SZ,
+    "tmr_sgd_chunk": ctypes.c_int64,
 }
 
 _lib = None

@@ -382,6 +382,33 @@ __global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, float*
   }
 }
 
+// Multi-tensor SGD: one launch for every parameter of every group.  Workgroup b handles
+// SGD_CHUNK elements of the tensor whose [block_begin, next block_begin) range holds b (binary
+// search over the small table, read through the scalar cache).
+constexpr int SGD_CHUNK = 8192;
+__global__ __launch_bounds__(256) void sgd_multi_k(const tmr_sgd_tensor* __restrict__ tab, int nt) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].block_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const tmr_sgd_tensor t = tab[lo];
+  const long base = (b - t.block_begin) * SGD_CHUNK;
+  const long end = base + SGD_CHUNK < t.n ? base + SGD_CHUNK : t.n;
+  for (long i = base + threadIdx.x; i < end; i += 256) {
+    const float pv = t.p[i];
+    float d = t.g[i];
+    if (t.weight_decay != 0.f) d = d + t.weight_decay * pv;
+    if (t.momentum != 0.f) {
+      const float bv = t.first_step ? d : t.momentum * t.buf[i] + (1.f - t.dampening) * d;
+      t.buf[i] = bv;
+      d = t.nesterov ? d + t.momentum * bv : bv;
+    }
+    t.p[i] = pv - t.lr * d;
+  }
+}
+
 int blocks_for(long n, int bs) {
   long b = (n + bs - 1) / bs;
   if (b > 8192) b = 8192;
@@ -523,6 +550,18 @@ TMR_API int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr,
   hipLaunchKernelGGL(sgd_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, p, g, buf, n, lr,
                      momentum, dampening, weight_decay, nesterov, first_step);
   TMR_CHECK_LAUNCH("sgd_step");
+  return 0;
+}
+
+TMR_API int64_t tmr_sgd_chunk(void) { return SGD_CHUNK; }
+
+TMR_API int tmr_sgd_step_multi(const tmr_sgd_tensor* table, int ntensors, int64_t nblocks,
+                               hipStream_t stream) {
+  if (ntensors == 0 || nblocks == 0) return 0;
+  TMR_CHECK_ARG(table && ntensors > 0 && nblocks > 0 && nblocks < (1L << 31),
+                "tmr_sgd_step_multi: bad table (%d tensors, %ld blocks)", ntensors, (long)nblocks);
+  hipLaunchKernelGGL(sgd_multi_k, dim3((unsigned)nblocks), dim3(256), 0, stream, table, ntensors);
+  TMR_CHECK_LAUNCH("sgd_step_multi");
   return 0;
 }
 

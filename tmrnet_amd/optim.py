@@ -1,11 +1,23 @@
 """SGD with the semantics of torch.optim.SGD (momentum, dampening, weight_decay, nesterov, per-group
-lr), stepping each parameter with the fused tmr_sgd_step kernel.  Mirrors the reference's
-optimizer wiring (train_only_non-local_pretrained.py:636-667: momentum 0.9, wd 5e-4, groups
-share/lstm at lr/10 and nl_block/fc at lr).  Being a torch.optim.Optimizer, the reference's
-lr schedulers (StepLR, ReduceLROnPlateau) attach unchanged."""
+lr).  Mirrors the reference's optimizer wiring (train_only_non-local_pretrained.py:636-667:
+momentum 0.9, wd 5e-4, groups share/lstm at lr/10 and nl_block/fc at lr).  Being a
+torch.optim.Optimizer, the reference's lr schedulers (StepLR, ReduceLROnPlateau) attach unchanged.
+
+One step is ONE kernel launch over every parameter of every group (tmr_sgd_step_multi): the
+per-tensor table (pointers, sizes, group hyper-parameters) is built on the host and uploaded only
+when it changes (gradient addresses move between steps), through pinned memory and an async
+copy on the step's stream, so a step never blocks the host.
+"""
+import numpy as np
 import torch
 
-from . import ops
+from ._lib import call, query, stream_ptr
+
+_ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("buf", "<u8"), ("n", "<i8"),
+                   ("block_begin", "<i8"), ("lr", "<f4"), ("momentum", "<f4"),
+                   ("dampening", "<f4"), ("weight_decay", "<f4"), ("nesterov", "<i4"),
+                   ("first_step", "<i4")])
+assert _ENTRY.itemsize == 64   # sizeof(tmr_sgd_tensor), include/tmr.h
 
 
 class SGD(torch.optim.Optimizer):
@@ -16,6 +28,10 @@ class SGD(torch.optim.Optimizer):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening,
                         weight_decay=weight_decay, nesterov=nesterov)
         super().__init__(params, defaults)
+        self._table_key = None
+        self._table_dev = None
+        self._keep = None
+        self.table_uploads = 0
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -23,23 +39,50 @@ class SGD(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        entries, keep, dev = [], [], None
+        chunk = None
         for group in self.param_groups:
             mom = group["momentum"]
             for p in group["params"]:
                 if p.grad is None:
                     continue
+                if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
+                    raise RuntimeError("SGD: parameters must be contiguous fp32 GPU tensors")
+                if dev is None:
+                    dev = p.device
+                    chunk = int(query("tmr_sgd_chunk"))
+                elif p.device != dev:
+                    raise RuntimeError("SGD: all parameters must be on one device")
                 g = p.grad
                 if not g.is_contiguous():
                     g = g.contiguous()
+                keep.append(g)
                 state = self.state[p]
-                first = False
+                first = 0
                 buf = None
                 if mom != 0:
                     buf = state.get("momentum_buffer")
                     if buf is None:
                         buf = torch.empty_like(p)
                         state["momentum_buffer"] = buf
-                        first = True
-                ops.sgd_step(p, g, buf, group["lr"], mom, group["dampening"],
-                             group["weight_decay"], group["nesterov"], first)
+                        first = 1
+                entries.append((p.data_ptr(), g.data_ptr(), buf.data_ptr() if buf is not None else 0,
+                                p.numel(), 0, group["lr"], mom, group["dampening"],
+                                group["weight_decay"], int(group["nesterov"]), first))
+        entries = [e for e in entries if e[3] > 0]
+        if not entries:
+            return loss
+        tab = np.array(entries, dtype=_ENTRY)
+        nblk = (tab["n"] + chunk - 1) // chunk
+        tab["block_begin"] = np.concatenate([[0], np.cumsum(nblk)[:-1]])
+        key = tab.tobytes()
+        if key != self._table_key or self._table_dev is None or self._table_dev.device != dev:
+            # pinned staging from torch's host caching allocator + async copy on this stream:
+            # no host sync, and the block is not reused before the copy has run
+            host = torch.frombuffer(bytearray(key), dtype=torch.uint8).pin_memory()
+            self._table_dev = host.to(dev, non_blocking=True)
+            self._table_key = key
+            self.table_uploads += 1
+        self._keep = keep        # contiguous grad copies stay alive until the next step
+        call("tmr_sgd_step_multi", self._table_dev, len(entries), int(nblk.sum()), stream_ptr(dev))
         return loss
