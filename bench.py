@@ -1,6 +1,8 @@
 """Benchmark: TMRNet train step (ResNet50 + LSTM + NLBlock, seq_len=10, LFB=40) on MI355X.
 
-One step = crop+normalize of B clips x T synthetic 250x250x3 uint8 frames resident in HBM ->
+One step = the reference's default training transform (use_flip=1: per-clip RandomCrop, ColorJitter,
+flip, RandomRotation, ToTensor, Normalize -- bit-exact to PIL, on the device; --augment crop keeps
+only crop+normalize) of B clips x T synthetic 250x250x3 uint8 frames resident in HBM ->
 LFB row table (reference rule, on device) -> TMRNet forward (rows read from the resident bank)
 -> CE(sum) -> backward -> [RCCL all-reduce SUM of grads when N>1] -> fused SGD step.
 This is the per-step work of train_only_non-local_pretrained.py:698-725 (BASELINE.json configs[1],
@@ -44,6 +46,10 @@ def parse():
     ap.add_argument("--conv-table", action="store_true", help="per-launch conv table on stderr")
     ap.add_argument("--cpu-clips", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--augment", choices=["reference", "crop"], default="reference",
+                    help="reference = the scripts' default train transform (use_flip=1, "
+                         "train_only_non-local_pretrained.py:342-350) on the device; crop = "
+                         "RandomCrop + Normalize only")
     ap.add_argument("--model", choices=["resnet50", "resnest50"], default="resnet50",
                     help="resnest50 = C4 model (ResNeSt50 + TimeConv head, fp32 here); the "
                          "metric line is defined on resnet50")
@@ -107,10 +113,15 @@ def main():
     reducer = GradAllReduce(model, dist) if dist is not None else None
     frames, bank, vs_d, offs, starts, labels = synth_inputs(args, rank, dev)
     B, T, L = args.clips, args.seq, args.lfb
+    from tmrnet_amd.augment import ClipAugment
+    aug = ClipAugment(seq_len=T, use_flip=1) if args.augment == "reference" else None
 
     def step(i):
         opt.zero_grad(set_to_none=True)
-        x4 = ops.crop_normalize(frames[i % len(frames)], offs[i], T)
+        if aug is not None:
+            x4 = aug(frames[i % len(frames)])
+        else:
+            x4 = ops.crop_normalize(frames[i % len(frames)], offs[i], T)
         rows = ops.lfb_index(vs_d, starts[i], L)
         out = model(x4, LFBRows(bank, rows))
         loss = crit(out, labels[i])
@@ -204,7 +215,9 @@ def main():
                                  if args.model == "resnet50" else
                                  "resnet_lstm (train_non-local_mutiConv_resnest)"),
                        "global_batch": B * world, "clips_per_gpu": B, "seq_len": T, "lfb_len": L,
-                       "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
+                       "frames_per_step": B * T * world, "parallelism": "dp%d" % world,
+                       "input_transform": ("reference train transform (use_flip=1) on device"
+                                           if aug is not None else "crop+normalize")},
             "loss_last": loss_v,
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -260,7 +273,10 @@ def cpu_baseline(args):
     labels = torch.randint(0, 7, (B,), generator=g)
 
     def one():
-        x = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
+        if args.augment == "reference":
+            x = ref.augment_ref(frames.numpy(), range(B * T), T).view(B, T, 3, 224, 224)
+        else:
+            x = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
         ref.train_step_ref(m, opt, x, lt, labels)
 
     one()  # warm-up
@@ -277,9 +293,10 @@ def cpu_baseline(args):
         pass
     return {"value": round(B * T * args.cpu_steps / el, 3), "unit": "frames/s", "cores": threads,
             "kind": "port", "cpu": model_name,
-            "sample": "oracle TMRNetRef fp32 train step (crop+norm, fwd, CE-sum, bwd, SGD), "
+            "sample": "oracle TMRNetRef fp32 train step (%s, fwd, CE-sum, bwd, SGD), "
                       "%d clips x %d frames, L=%d, %d timed steps after 1 warm-up"
-                      % (B, T, L, args.cpu_steps)}
+                      % ("PIL train transform" if args.augment == "reference" else "crop+norm",
+                         B, T, L, args.cpu_steps)}
 
 
 if __name__ == "__main__":

@@ -108,6 +108,28 @@ int tmr_crop_normalize(const uint8_t* frames, const int32_t* offsets, float* out
                        int win, int seq_len, int crop, float m0, float m1, float m2, float s0,
                        float s1, float s2, hipStream_t stream);
 
+/* ---------------- training augmentation (augment.hip) ----------------------
+ * The reference's default per-clip training transform (use_flip = 1,
+ * Training TMRNet/train_only_non-local_pretrained.py:342-350; classes :101-177):
+ * RandomCrop -> ColorJitter -> RandomHorizontalFlip -> RandomRotation -> ToTensor -> Normalize,
+ * bit-exact to PIL (ImageEnhance blends, L conversion, RGB<->HSV, Image.rotate NEAREST).
+ * One tmr_clip_aug per FRAME (device memory), filled on the host by the reference's seeding
+ * rule (tmrnet_amd/augment.py). */
+typedef struct tmr_clip_aug {
+  int32_t x1, y1;       /* crop offset in the input frame */
+  int32_t flip;         /* horizontal flip (after the jitter) */
+  int32_t rotate;       /* 1: PIL affine_fixed nearest rotation with a[] (16.16 fixed point) */
+  int32_t a[6];         /* a0, a1, a2 (x origin), a3, a4, a5 (y origin) */
+  int32_t jitter;       /* 1: brightness, contrast, saturation, hue */
+  int32_t hue_shift;    /* uint8 shift added to the PIL HSV hue (mod 256) */
+  float brightness, contrast, saturation;
+  int32_t reserved;
+} tmr_clip_aug;
+/* frames uint8 [f][hin][win][3]; lmean int32 [f] workspace; out fp32 NHWC [f][crop][crop][4] */
+int tmr_clip_augment(const uint8_t* frames, const tmr_clip_aug* params, int32_t* lmean, float* out,
+                     int f, int hin, int win, int crop, float m0, float m1, float m2, float s0,
+                     float s1, float s2, hipStream_t stream);
+
 /* ---------------- batch norm + ReLU + residual (bn.hip) ---------------------
  * Replaces nn.BatchNorm2d (train mode, batch statistics, eps, momentum) + ReLU +
  * the bottleneck residual add of torchvision resnet50.  ws: double workspace of

@@ -28,6 +28,12 @@ reference checkout, ``code/``):
 * ``crop_normalize_ref`` -- crop at a per-clip offset + ToTensor + Normalize
                          (``train_only_non-local_pretrained.py:101-126``, ``:335-341``)
 * ``train_step_ref``  -- the step at ``train_only_non-local_pretrained.py:698-725``
+* ``augment_ref``     -- the training transform classes RandomCrop / ColorJitter /
+                         RandomHorizontalFlip / RandomRotation (train_only_non-local_pretrained.py
+                         :101-177, composed :334-350) on PIL, with torchvision's thin F_pil
+                         wrappers (adjust_brightness/contrast/saturation = ImageEnhance, adjust_hue
+                         = HSV round trip, rotate = Image.rotate NEAREST fill 0) restated inline
+                         (torchvision is not installed; PIL is)
 * ``LFBModelRef`` / ``build_lfb_ref`` -- ``resnet_lstm_LFB`` (:243-270) and the LFB
                          construction loop (:534-607): eval mode, centre crop (:360-366),
                          clips in valid-start order, last hidden state per clip, float64 bank
@@ -457,6 +463,57 @@ def crop_normalize_ref(frames_u8, offsets, seq_len):
         x1, y1 = (int(v) for v in offsets[f // seq_len])
         crop = frames_u8[f, y1:y1 + 224, x1:x1 + 224, :].permute(2, 0, 1).float() / 255.0
         out[f] = (crop - mean) / std
+    return out
+
+
+def _adjust_hue_pil(img, hue_factor):
+    """torchvision (0.15) functional_pil.adjust_hue."""
+    from PIL import Image
+    h, s, v = img.convert("HSV").split()
+    np_h = np.array(h, dtype=np.uint8)
+    np_h = (np_h.astype(np.int64) + (int(math.trunc(hue_factor * 255)) & 255)) & 255  # uint8 wrap
+    h = Image.fromarray(np_h.astype(np.uint8), "L")
+    return Image.merge("HSV", (h, s, v)).convert("RGB")
+
+
+def augment_ref(frames_u8, counts, seq_len, use_flip=1, crop=224):
+    """Reference training transform per frame (PIL), then ToTensor + Normalize -> (F,3,crop,crop).
+    frames_u8: numpy/torch uint8 (F, H, W, 3); counts: the transforms' call counter per frame."""
+    import random
+    from PIL import Image, ImageEnhance
+    frames_u8 = np.asarray(frames_u8)
+    mean = torch.tensor(MEAN).view(3, 1, 1)
+    std = torch.tensor(STD).view(3, 1, 1)
+    out = torch.empty(len(frames_u8), 3, crop, crop)
+    rnd = random.Random()
+    for i, (fr, count) in enumerate(zip(frames_u8, counts)):
+        img = Image.fromarray(fr)
+        seed = int(count) // seq_len
+        w, h = img.size
+        if not (w == crop and h == crop):                                   # RandomCrop :110-126
+            rnd.seed(seed)
+            x1 = rnd.randint(0, w - crop)
+            y1 = rnd.randint(0, h - crop)
+            img = img.crop((x1, y1, x1 + crop, y1 + crop))
+        if use_flip == 1:                                                   # ColorJitter :162-177
+            rnd.seed(seed)
+            bf = rnd.uniform(1 - 0.1, 1 + 0.1)
+            cf = rnd.uniform(1 - 0.1, 1 + 0.1)
+            sf = rnd.uniform(1 - 0.1, 1 + 0.1)
+            hf = rnd.uniform(-0.05, 0.05)
+            img = ImageEnhance.Brightness(img).enhance(bf)
+            img = ImageEnhance.Contrast(img).enhance(cf)
+            img = ImageEnhance.Color(img).enhance(sf)
+            img = _adjust_hue_pil(img, hf)
+        rnd.seed(seed)                                                      # flip :133-141
+        if rnd.random() < 0.5:
+            img = img.transpose(Image.FLIP_LEFT_RIGHT)
+        if use_flip == 1:                                                   # rotation :147-153
+            rnd.seed(seed)
+            angle = rnd.randint(-5, 5)
+            img = img.rotate(angle, Image.NEAREST, expand=False, center=None, fillcolor=(0, 0, 0))
+        t = torch.from_numpy(np.array(img, copy=True)).permute(2, 0, 1).float().div(255)
+        out[i] = (t - mean) / std
     return out
 
 

@@ -45,6 +45,7 @@ SIGNATURES = {
     "tmr_weight_oihw_to_krsc": [P, P, I, I, I, I, I, P],
     "tmr_nchw_to_nhwc": [P, P, I, I, I, I, I, P],
     "tmr_nhwc_to_nchw": [P, P, I, I, I, I, I, P],
+    "tmr_clip_augment": [P, P, P, P, I, I, I, I, F, F, F, F, F, F, P],
     "tmr_crop_normalize": [P, P, P, I, I, I, I, I, F, F, F, F, F, F, P],
     "tmr_bn_ws_bytes": [I, I],
     "tmr_bn_fwd_stats": [P, I, I, P, P, P, P, F, F, P, P, P, P, P, SZ, P],
