@@ -77,6 +77,18 @@ int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const float* 
 /* dx[n,h,w,c] = beta*dx + conv_transpose(dy, w_krsc) */
 int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
                      float beta, hipStream_t stream);
+/* dgrad whose epilogue also runs the first pass of the backward of the BatchNorm(+ReLU) that
+ * produced this conv's input (the previous unit of the Bottleneck chain): dx receives the
+ * ReLU-masked gradient (mask 1: z > 0, 2: y*scale+shift > 0, 0: none) -- i.e. the BN output
+ * gradient, and for a residual unit the identity branch's gradient -- and parts the per-tile
+ * column sums (sum g, sum g*(y - mean)) as float2 [tmr_conv2d_dgrad_bnbwd_parts(d)][c], finished
+ * by tmr_bn_bwd_parts.  Removes the separate statistics pass over (dz, y[, z]) of tmr_bn_bwd.
+ * dx, y, z dense NHWC (x_ld == c). */
+int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d);
+int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
+                           float beta, const float* y, const float* z, const float* scale,
+                           const float* shift, const float* mean, int mask, void* parts,
+                           size_t parts_bytes, hipStream_t stream);
 size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d);
 /* dw_oihw[k, c_real, r, s] = beta*dw + sum_m dy[m,k] * im2col(x)[m,(r,s,c)] */
 int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float* dy, float* dw_oihw,
@@ -159,6 +171,12 @@ int tmr_bn_apply(const float* y, const float* scale, const float* shift, const f
  * saves one full read of z).  z/scale/shift unused when relu == 0.  dres may alias dz: the
  * first pass then overwrites dz with the masked gradient (the residual branch's gradient, in
  * place) and the second pass reads it back without re-reading the mask source. */
+/* BatchNorm backward from the fused-dgrad partials: g = the already masked output gradient;
+ * dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); ws >= 3*c floats. */
+int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, int nparts,
+                     const float* save_mean, const float* save_invstd, const float* gamma,
+                     float* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
+                     size_t ws_bytes, hipStream_t stream);
 int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* scale,
                const float* shift, const float* save_mean, const float* save_invstd,
                const float* gamma, float* dy, float* dres, float* dgamma, float* dbeta, int rows,

@@ -361,3 +361,69 @@ def test_sgd_optimizer_multi_tensor_matches_torch(dev):
     torch.cuda.synchronize()
     for a, b in zip(ours, ref):
         assert rel_err(a, b) < 1e-6
+
+
+@pytest.mark.parametrize("case", [
+    # n, h, w, cin(dx channels), cout(dy channels), r, stride, pad, mask, beta
+    (3, 14, 14, 64, 256, 1, 1, 0, 2, 0.0),     # conv3 dgrad -> conv2's BN (mask from y)
+    (2, 14, 14, 128, 128, 3, 2, 1, 2, 0.0),    # strided 3x3: four parity-class launches
+    (3, 12, 12, 256, 64, 1, 1, 0, 1, 1.0),     # conv1 dgrad += identity grad -> prev block (z)
+    (2, 14, 14, 256, 512, 1, 2, 0, 1, 1.0),    # strided 1x1 downsample: tap-less classes
+    (2, 9, 9, 64, 64, 3, 1, 1, 0, 0.0),        # no ReLU
+])
+def test_conv_dgrad_fused_bn_backward(dev, case):
+    """conv_dgrad_bnbwd + bn_bwd_parts == conv_dgrad followed by bn_bwd (the separate passes):
+    the masked dx bit-exactly, dy / dgamma / dbeta to fp32 summation-order tolerance."""
+    n, h, w, cin, cout, r, st, pad, mask, beta = case
+    g = torch.Generator().manual_seed(11)
+    ho = (h + 2 * pad - r) // st + 1
+    wo = (w + 2 * pad - r) // st + 1
+    dy = torch.randn(n, ho, wo, cout, generator=g).to(dev)
+    wt = (torch.randn(cout, cin, r, r, generator=g) / np.sqrt(cout * r * r)).to(dev)
+    wk = ops.weight_to_krsc(wt)
+    y = torch.randn(n, h, w, cin, generator=g).to(dev)
+    mean = y.view(-1, cin).mean(0)
+    inv = 1.0 / (y.view(-1, cin).var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = (torch.rand(cin, generator=g) + 0.5).to(dev)
+    scale = gamma * inv
+    shift = (torch.randn(cin, generator=g) * 0.1).to(dev) - mean * scale
+    res = torch.randn(n, h, w, cin, generator=g).to(dev)
+    z = torch.relu(y * scale + shift + res) if mask == 1 else None
+    old = torch.randn(n, h, w, cin, generator=g).to(dev)
+    # separate passes
+    dz = ops.conv_dgrad(dy, wk, (h, w), st, pad, out=old.clone(), beta=beta)
+    dy_ref, dres_ref, dg_ref, db_ref = ops.bn_bwd(dz, y, z, mean, inv, gamma, mask != 0,
+                                                  want_dres=True, scale=scale, shift=shift)
+    # fused
+    dzf, parts, npart = ops.conv_dgrad_bnbwd(dy, wk, (h, w), st, pad, y, mean, mask, z=z,
+                                              scale=scale, shift=shift, out=old.clone(), beta=beta)
+    dyf, dgf, dbf = ops.bn_bwd_parts(dzf, y, parts, npart, mean, inv, gamma)
+    torch.cuda.synchronize()
+    assert torch.equal(dzf, dres_ref)          # the masked BN-output gradient
+    assert rel_err(dyf, dy_ref) < 1e-5
+    assert rel_err(dgf, dg_ref) < 1e-5 and rel_err(dbf, db_ref) < 1e-5
+
+
+def test_conv_dgrad_fused_bn_backward_frame_chunks(dev):
+    """Partials stay in launch order across frame chunks (max_frames) and parity classes."""
+    g = torch.Generator().manual_seed(12)
+    n, h, w, cin, cout = 5, 14, 14, 128, 128
+    dy = torch.randn(n, 7, 7, cout, generator=g).to(dev)
+    wk = ops.weight_to_krsc((torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(dev))
+    y = torch.randn(n, h, w, cin, generator=g).to(dev)
+    mean = y.view(-1, cin).mean(0)
+    inv = 1.0 / (y.view(-1, cin).var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = torch.ones(cin, device=dev)
+    sc, sh = gamma * inv, -mean * inv
+    a = ops.conv_dgrad_bnbwd(dy, wk, (h, w), 2, 1, y, mean, 2, scale=sc, shift=sh)
+    old = ops.MAX_FRAMES
+    try:
+        ops.MAX_FRAMES = 2
+        b = ops.conv_dgrad_bnbwd(dy, wk, (h, w), 2, 1, y, mean, 2, scale=sc, shift=sh)
+    finally:
+        ops.MAX_FRAMES = old
+    ya = ops.bn_bwd_parts(a[0], y, a[1], a[2], mean, inv, gamma)[0]
+    yb = ops.bn_bwd_parts(b[0], y, b[1], b[2], mean, inv, gamma)[0]
+    torch.cuda.synchronize()
+    assert b[2] > a[2]
+    assert torch.equal(a[0], b[0]) and rel_err(yb, ya) < 1e-6

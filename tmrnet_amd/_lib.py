@@ -37,6 +37,8 @@ SIGNATURES = {
     "tmr_conv2d_fwd_stats_parts": [DP],
     "tmr_conv2d_fwd_bnstats": [DP, P, P, P, P, SZ, P],
     "tmr_conv2d_dgrad": [DP, P, P, P, F, P],
+    "tmr_conv2d_dgrad_bnbwd_parts": [DP],
+    "tmr_conv2d_dgrad_bnbwd": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, P],
     "tmr_conv2d_wgrad_ws_bytes": [DP],
     "tmr_conv2d_wgrad": [DP, P, P, P, I, F, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
@@ -52,6 +54,7 @@ SIGNATURES = {
     "tmr_bn_finalize": [P, I, I, P, P, P, P, F, F, P, P, P, P, P],
     "tmr_bn_eval_params": [P, P, P, P, F, I, P, P, P],
     "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
+    "tmr_bn_bwd_parts": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_maxpool2d_fwd": [P, P, P, I, I, I, I, I, I, P],
     "tmr_maxpool2d_bwd": [P, P, P, I, I, I, I, I, I, P],

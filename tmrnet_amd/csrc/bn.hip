@@ -275,6 +275,47 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
   }
 }
 
+// bn_bwd_final over float2 (sum g, sum g*(y-mean)) partials emitted by a fused dgrad epilogue
+__global__ __launch_bounds__(NT) void bn_bwd_final_f2(const float2* __restrict__ part, int nrb,
+                                                      int rows, int c, const float* mean,
+                                                      const float* inv, const float* gamma,
+                                                      float* dgamma, float* dbeta, float* coef) {
+  const int ch = blockIdx.x;
+  double s = 0.0, q = 0.0;
+  for (int b = threadIdx.x; b < nrb; b += NT) {
+    const float2 p = part[(long)b * c + ch];
+    s += p.x;
+    q += p.y;
+  }
+  __shared__ double red[2][NT];
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  for (int h = NT / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] += red[1][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    s = red[0][0];
+    q = red[1][0];
+    const double iv = inv[ch];
+    const double dgm = q * iv;
+    if (dgamma) dgamma[ch] = (float)dgm;
+    if (dbeta) dbeta[ch] = (float)s;
+    const double n = (double)rows;
+    const double gm = gamma ? gamma[ch] : 1.0;
+    const double A = gm * iv;
+    const double B = -gm * iv * iv * (dgm / n);
+    const double C = -A * (s / n) - B * (double)mean[ch];
+    coef[ch] = (float)A;
+    coef[c + ch] = (float)B;
+    coef[2 * c + ch] = (float)C;
+  }
+}
+
 template <int MASK, bool DRES>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const float* __restrict__ y,
                                                    const float* __restrict__ z,
@@ -418,6 +459,24 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
     if (mask == 1) TMR_BN_APPLY(1, false); else if (mask == 2) TMR_BN_APPLY(2, false); else TMR_BN_APPLY(0, false);
   }
 #undef TMR_BN_APPLY
+  TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, int nparts,
+                             const float* save_mean, const float* save_invstd, const float* gamma,
+                             float* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
+                             size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows > 0 && nparts > 0,
+                "tmr_bn_bwd_parts: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
+  TMR_CHECK_ARG(ws && ws_bytes >= (size_t)3 * c * sizeof(float), "tmr_bn_bwd_parts: workspace too small");
+  float* coef = (float*)ws;
+  hipLaunchKernelGGL(bn_bwd_final_f2, dim3(c), dim3(NT), 0, stream, (const float2*)parts, nparts,
+                     rows, c, save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final_f2");
+  const long n4 = (long)rows * c / 4;
+  hipLaunchKernelGGL((bn_bwd_apply<0, false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
+                     nullptr, nullptr, nullptr, coef, dy, nullptr, n4, c / 4);
   TMR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }

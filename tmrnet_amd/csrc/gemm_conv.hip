@@ -68,6 +68,16 @@ struct GemmArgs {
   const float* scale;
   const float* res;
   int relu;
+  // DGRAD epilogue fused with the backward of the BatchNorm(+ReLU) whose output gradient this
+  // dgrad produces: C = relu-mask(C) (mask 1: bn_z > 0, 2: fmaf(bn_y, bn_sc, bn_sh) > 0) and
+  // per-(m-tile, column) partials (sum g, sum g * (bn_y - bn_mean)) -> bn_part (float2)
+  const float* bn_y;
+  const float* bn_z;
+  const float* bn_sc;
+  const float* bn_sh;
+  const float* bn_mean;
+  float2* bn_part;
+  int bn_mask;
   // byte extents of A and B (buffer-descriptor range checks)
   uint32_t Abytes, Bbytes;
   int prec;  // TMR_MATH_F32 / TMR_MATH_BF16
@@ -527,6 +537,67 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         }
       }
   }
+  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums
+  if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
+    float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = col0 + 32 * j;
+      const bool okc = col < a.N;
+      mu[j] = okc ? a.bn_mean[col] : 0.f;
+      bsc[j] = (okc && a.bn_mask == 2) ? a.bn_sc[col] : 0.f;
+      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : 0.f;
+      cs[j] = 0.f;
+      cq[j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long ro = row_off(i, r);
+        if (ro < 0) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = col0 + 32 * j;
+          if (col >= a.N) continue;
+          float v = acc[i][j][r];
+          const float yv = a.bn_y[ro + col];
+          bool keep = true;
+          if (a.bn_mask == 1) keep = a.bn_z[ro + col] > 0.f;
+          else if (a.bn_mask == 2) keep = fmaf(yv, bsc[j], bsh[j]) > 0.f;
+          v = keep ? v : 0.f;
+          Cb[ro + col] = v;
+          cs[j] += v;
+          cq[j] = fmaf(v, yv - mu[j], cq[j]);
+        }
+      }
+    float* red = smem;  // [WM][BN][2]; the main loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+      if (hh == 0) {
+        const int c = wn * (BN / WN) + 32 * j + l31;
+        red[(wm * BN + c) * 2] = cs[j];
+        red[(wm * BN + c) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * (BN / WN) + 32 * j + l31;
+        float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          t0 += red[(w * BN + c) * 2];
+          t1 += red[(w * BN + c) * 2 + 1];
+        }
+        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+      }
+    }
+    return;
+  }
   // (2) bias + stores
   float bvals[TN];
 #pragma unroll
@@ -878,8 +949,18 @@ TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const
   return 0;
 }
 
+// Fused BatchNorm-backward epilogue state of one dgrad call (nullptr: plain dgrad).  part
+// advances over the launches; count_only tallies the partial rows without launching.
+struct BnBwdFuse {
+  const float *y, *z, *sc, *sh, *mean;
+  int mask;
+  float2* part;
+  long nparts;
+  bool count_only;
+};
+
 static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
-                           float* dx, float beta, hipStream_t stream) {
+                           float* dx, float beta, hipStream_t stream, BnBwdFuse* fz = nullptr) {
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
   const int lk = ilog2_exact(d->k);
   TMR_CHECK_ARG(lk >= 2, "tmr_conv2d_dgrad: output channels %d must be a power of two >= 4", d->k);
@@ -918,13 +999,70 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
       } else {
         a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
       }
-      if (a.K == 0 && beta == 1.f) continue;  // nothing to add
+      // nothing to add -- unless the fused BN backward must still see (mask, sum) these pixels
+      if (a.K == 0 && beta == 1.f && !fz) continue;
+      if (fz) {
+        const long nmt = cdiv(a.M, kCfgs[pick_cfg(a.M, a.N, a.K, MODE_DGRAD)].bm);
+        if (fz->count_only) { fz->nparts += nmt; continue; }
+        a.bn_y = fz->y; a.bn_z = fz->z; a.bn_sc = fz->sc; a.bn_sh = fz->sh; a.bn_mean = fz->mean;
+        a.bn_mask = fz->mask;
+        a.bn_part = fz->part;
+        fz->part += nmt * a.N;
+        fz->nparts += nmt;
+      }
       bool al = aligned16(dy) && aligned16(w_krsc) && aligned16(dx) && a.lds % 4 == 0;
       int rc = launch_gemm<MODE_DGRAD>(a, al, 1, stream);
       if (rc) return rc;
     }
   }
   return 0;
+}
+
+static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
+                           float beta, BnBwdFuse* fz, hipStream_t stream) {
+  const int fc = frames_per_launch(d);
+  const long px_frame = (long)d->h * d->w * d->c;   // dense dx / y / z (checked by the caller)
+  float2* part0 = fz->part;
+  for (int f0 = 0; f0 < d->n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+    BnBwdFuse fc_ = *fz;
+    fc_.y = fz->y ? fz->y + f0 * px_frame : nullptr;
+    fc_.z = fz->z ? fz->z + f0 * px_frame : nullptr;
+    fc_.nparts = 0;
+    int rc = conv_dgrad_impl(&c, dy ? dy + f0 * y_frame(d) : nullptr, w_krsc,
+                             dx ? dx + f0 * x_frame(d) : nullptr, beta, stream, &fc_);
+    if (rc) return rc;
+    fz->part = fc_.part;
+    fz->nparts += fc_.nparts;
+  }
+  fz->part = part0;
+  return 0;
+}
+
+TMR_API int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d) {
+  if (!d) return -1;
+  BnBwdFuse fz{};
+  fz.count_only = true;
+  if (dgrad_bnbwd_run(d, nullptr, nullptr, nullptr, 1.f, &fz, nullptr)) return -1;
+  return (int)fz.nparts;
+}
+
+TMR_API int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                                   float* dx, float beta, const float* y, const float* z,
+                                   const float* scale, const float* shift, const float* mean,
+                                   int mask, void* parts, size_t parts_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd: null descriptor");
+  TMR_CHECK_ARG(xld_of(d) == d->c, "tmr_conv2d_dgrad_bnbwd: dx must be dense (x_ld == c)");
+  TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
+  TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift),
+                "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1) or scale/shift (2)", mask);
+  const int np = tmr_conv2d_dgrad_bnbwd_parts(d);
+  TMR_CHECK_ARG(np >= 0 && parts_bytes >= (size_t)np * d->c * sizeof(float2),
+                "tmr_conv2d_dgrad_bnbwd: parts buffer too small");
+  BnBwdFuse fz{};
+  fz.y = y; fz.z = z; fz.sc = scale; fz.sh = shift; fz.mean = mean; fz.mask = mask;
+  fz.part = (float2*)parts;
+  return dgrad_bnbwd_run(d, dy, w_krsc, dx, beta, &fz, stream);
 }
 
 TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc,

@@ -169,6 +169,46 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
     return out
 
 
+def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scale=None,
+                     shift=None, out=None, beta=0.0, math="fp32"):
+    """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
+    y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts)."""
+    _req(w_krsc, "w"); _req(y, "y"); _req(mean, "mean")
+    n, ho, wo, k = dy.shape
+    k2, r, s, c = w_krsc.shape
+    h, w = in_hw
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math)
+    assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
+    if out is None:
+        out = _empty((n, h, w, c), dy)
+    if tuple(y.shape) != tuple(out.shape) or (z is not None and tuple(z.shape) != tuple(out.shape)):
+        raise RuntimeError("conv_dgrad_bnbwd: y/z must have dx's shape %s" % (tuple(out.shape),))
+    d.x_ld = _nhwc_ld(out, "dx")
+    d.y_ld = _nhwc_ld(dy, "dy")
+    nparts = query("tmr_conv2d_dgrad_bnbwd_parts", ctypes.byref(d))
+    if nparts < 0:
+        raise RuntimeError("tmr_conv2d_dgrad_bnbwd_parts failed")
+    parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
+    with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
+               4 * (n * ho * wo * k + k * r * s * c + n * h * w * c * (3 if beta else 2)
+                    + (n * h * w * c if z is not None else 0))):
+        call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z, scale,
+             shift, mean, int(mask), parts, ctypes.c_size_t(parts.numel() * 4), stream_ptr())
+    return out, parts, nparts
+
+
+def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma):
+    """BN backward from conv_dgrad_bnbwd partials: g already masked -> (dy, dgamma, dbeta)."""
+    c = y.shape[-1]
+    rows = y.numel() // c
+    dy = torch.empty_like(y)
+    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
+    ws = torch.empty((3 * c,), dtype=f32, device=y.device)
+    call("tmr_bn_bwd_parts", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta, rows,
+         c, ws, ctypes.c_size_t(ws.numel() * 4), stream_ptr())
+    return dy, dgamma, dbeta
+
+
 def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None,
                math="fp32"):
     """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW (x/dy may be channel slices)."""

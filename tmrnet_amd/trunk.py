@@ -15,6 +15,8 @@ BN semantics follow nn.BatchNorm2d in train mode: batch mean / biased variance
 for normalisation, running stats updated with momentum and the unbiased
 variance, num_batches_tracked += 1; eval mode uses running stats.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -90,26 +92,46 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
 
 
 def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
-                 dres_inplace=False):
-    """BN backward (ReLU mask from the saved z, or recomputed from y when there was no
-    residual), wgrad, dgrad (optionally accumulated into dx_out).  dres_inplace: the
-    pre-activation gradient (the identity branch's) overwrites dz and is returned as dres."""
+                 dres_inplace=False, parts=None, fuse_prev=None):
+    """BN backward, wgrad, dgrad (optionally accumulated into dx_out) of one conv+BN unit.
+
+    parts: dz was produced by a fused dgrad (conv_dgrad_bnbwd): it is already ReLU-masked and
+    `parts` holds its BN-backward partial sums.  Otherwise the ReLU mask comes from the saved z,
+    or is recomputed from y when there was no residual.  dres_inplace: the pre-activation
+    gradient (the identity branch's) overwrites dz and is returned as dres.
+    fuse_prev: the unit whose BN output gradient this unit's dgrad produces -- its mask and
+    partial sums are then computed in the dgrad epilogue; returned as the third value."""
     conv, bn = rec["conv"], rec["bn"]
-    dy, dres, dg, db = ops.bn_bwd(dz, rec["y"], rec["z"], rec["mean"], rec["inv"],
-                                  bn.weight.detach(), rec["relu"], want_dres=want_dres,
-                                  dres_out=dz if dres_inplace else None,
-                                  scale=rec["scale"], shift=rec["shift"])
+    if parts is not None:
+        dy, dg, db = ops.bn_bwd_parts(dz, rec["y"], parts[0], parts[1], rec["mean"], rec["inv"],
+                                      bn.weight.detach())
+        dres = dz if want_dres else None
+    else:
+        dy, dres, dg, db = ops.bn_bwd(dz, rec["y"], rec["z"], rec["mean"], rec["inv"],
+                                      bn.weight.detach(), rec["relu"], want_dres=want_dres,
+                                      dres_out=dz if dres_inplace else None,
+                                      scale=rec["scale"], shift=rec["shift"])
     grads[bn.weight] = dg
     grads[bn.bias] = db
     x = rec["x"]
     k, c, r, s = conv.weight.shape
     grads[conv.weight] = ops.conv_wgrad(x, dy, r, s, rec["stride"], rec["pad"],
                                         c_real=rec["c_real"], math=rec["math"])
-    dx = None
+    dx, fused = None, None
     if need_dx:
-        dx = ops.conv_dgrad(dy, rec["wk"], (x.shape[1], x.shape[2]), rec["stride"], rec["pad"],
-                            out=dx_out, beta=dx_beta, math=rec["math"])
-    return dx, dres
+        hw = (x.shape[1], x.shape[2])
+        if fuse_prev is not None:
+            p = fuse_prev
+            mask = (1 if p["z"] is not None else 2) if p["relu"] else 0
+            dx, pp, npp = ops.conv_dgrad_bnbwd(dy, rec["wk"], hw, rec["stride"], rec["pad"],
+                                               p["y"], p["mean"], mask, z=p["z"],
+                                               scale=p["scale"], shift=p["shift"], out=dx_out,
+                                               beta=dx_beta, math=rec["math"])
+            fused = (pp, npp)
+        else:
+            dx = ops.conv_dgrad(dy, rec["wk"], hw, rec["stride"], rec["pad"], out=dx_out,
+                                beta=dx_beta, math=rec["math"])
+    return dx, dres, fused
 
 
 class TrunkFn(torch.autograd.Function):
@@ -159,21 +181,28 @@ class TrunkFn(torch.autograd.Function):
         grads = {}
         g = ops.avgpool_bwd(dfeat.contiguous(), ctx.last_hw)   # grad at the last block output
         blocks = ctx.blocks
+        fuse = os.environ.get("TMR_FUSE_BN_BWD", "1") != "0"
+        pending = None     # BN-backward partials of g when the dgrad that produced it was fused
         while blocks:
             blk, brec = blocks.pop()
             has_ds = blk.downsample is not None
             r1, r2 = brec[0], brec[1]
             rd = brec[2] if has_ds else None
             r3 = brec[-1]
+            # the previous block's last unit: its BN output gradient is this block's dx
+            prev3 = blocks[-1][1][-1] if (blocks and fuse) else None
             # g (owned here) becomes the masked pre-ReLU gradient = the identity-branch grad
-            dz2, dres = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True)
-            dz1, _ = _conv_bn_bwd(r2, dz2, grads)
+            dz2, dres, fz2 = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True,
+                                          parts=pending, fuse_prev=r2 if fuse else None)
+            dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1 if fuse else None)
             del dz2
             if has_ds:
-                dx, _ = _conv_bn_bwd(r1, dz1, grads)
-                _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0)
+                dx, _, _ = _conv_bn_bwd(r1, dz1, grads, parts=fz1)
+                _, _, pending = _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0,
+                                             fuse_prev=prev3)
             else:
-                dx, _ = _conv_bn_bwd(r1, dz1, grads, dx_out=dres, dx_beta=1.0)
+                dx, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dres, dx_beta=1.0,
+                                              fuse_prev=prev3)
             del dz1, brec, dres
             g = dx
         dh = g
