@@ -57,7 +57,7 @@ struct GemmArgs {
   // output
   int ldc;
   float beta;
-  int oH, oW, osy, osx, oyc, oxc;  // DGRAD output-pixel map (osy==0: rows contiguous)
+  int oH, oW, osy, osx, oyc, oxc;  // DGRAD output-pixel map of the row grid (n, y, x)
   // WGRAD split-K
   int kchunk;
   long slab;
@@ -78,8 +78,9 @@ struct GemmArgs {
   const float* bn_mean;
   float2* bn_part;
   int bn_mask;
-  // byte extents of A and B (buffer-descriptor range checks)
-  uint32_t Abytes, Bbytes;
+  // byte extents of A, B and C (buffer-descriptor range checks; C's also bounds the tensors
+  // laid out like C: res, bn_y, bn_z; WGRAD: one split slab)
+  uint32_t Abytes, Bbytes, Cbytes;
   int prec;  // TMR_MATH_F32 / TMR_MATH_BF16
 };
 
@@ -506,70 +507,105 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   }
 
   // ---- epilogue ----
+  // Branch-free: every access to C (and to the tensors laid out like C) goes through a buffer
+  // descriptor over C's extent; rows outside M and columns outside N get an out-of-range offset
+  // (loads return 0, stores are dropped).  Rows are handled in chunks of ER accumulator
+  // registers so each chunk's loads are issued back to back before any is consumed.
   float* Cb = a.C;
   if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
+  const __amdgpu_buffer_rsrc_t rC = make_rsrc(Cb, a.Cbytes);
   const int col0 = n0 + wn * (BN / WN) + l31;
-  // output row offset for accumulator register r of row-tile i (-1: outside M)
-  auto row_off = [&](int i, int r) -> long {
+  constexpr int ER = TN >= 4 ? 4 : 16 / (2 * TN);   // rows per chunk: 16 / 8 / 4 (TN = 1 / 2 / 4)
+  uint32_t cob[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    cob[j] = col0 + 32 * j < a.N ? (uint32_t)(col0 + 32 * j) * 4u : OOB;
+  // byte offset of accumulator row (i, r) in C; OOB outside M
+  auto row_off = [&](int i, int r) -> uint32_t {
     const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-    if (row >= a.M) return -1;
-    if (MODE == MODE_DGRAD && a.osy != 0) {
-      uint32_t n = fdiv((uint32_t)row, a.dHW);
-      uint32_t rem = row - n * a.dHW.d;
-      uint32_t y = fdiv(rem, a.dW);
-      uint32_t x = rem - y * a.dW.d;
-      long pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
-      return pix * a.ldc;
+    uint32_t pix = (uint32_t)row;
+    if (MODE == MODE_DGRAD) {   // output-pixel map of the parity class (identity when st == 1)
+      const uint32_t n = fdiv((uint32_t)row, a.dHW);
+      const uint32_t rem = row - n * a.dHW.d;
+      const uint32_t y = fdiv(rem, a.dW);
+      const uint32_t x = rem - y * a.dW.d;
+      pix = ((n * a.oH + y * a.osy + a.oyc) * a.oW + x * a.osx + a.oxc);
     }
-    return (long)row * a.ldc;
+    return row < a.M ? pix * (uint32_t)a.ldc * 4u : OOB;
   };
-  // (1) all reads of the old output first (beta), so they are issued back to back
+  // rob OOB + a column offset stays >= 2^31 (no wrap): still out of range
+  auto eoff = [&](uint32_t rob, int j) -> uint32_t { return cob[j] == OOB ? OOB : rob + cob[j]; };
+  auto st1 = [&](float v, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rC, off, 0, 0);
+  };
+  // (1) beta: acc += beta * C_old
   if (a.beta != 0.f) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long ro = row_off(i, r);
+      for (int r0 = 0; r0 < 16; r0 += ER) {
+        float old[ER][TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = col0 + 32 * j;
-          if (ro >= 0 && col < a.N) acc[i][j][r] += a.beta * Cb[ro + col];
+        for (int r = 0; r < ER; ++r) {
+          const uint32_t ro = row_off(i, r0 + r);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) old[r][j] = bld1(rC, eoff(ro, j));
         }
+#pragma unroll
+        for (int r = 0; r < ER; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j][r0 + r] += a.beta * old[r][j];
+        __builtin_amdgcn_sched_barrier(0);   // keep each chunk's loads in its own live range
       }
   }
-  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums
+  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums.  Rows /
+  // columns outside the output hold acc == 0 (their operand loads returned zeros) and read
+  // bn_y == 0, so they add nothing to either sum.
   if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
+    const __amdgpu_buffer_rsrc_t rY = make_rsrc(a.bn_y, a.Cbytes);
+    const __amdgpu_buffer_rsrc_t rZ = make_rsrc(a.bn_mask == 1 ? a.bn_z : a.bn_y, a.Cbytes);
+    const uint32_t zoob = a.bn_mask == 1 ? 0u : OOB;   // z is read only for mask 1
     float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = col0 + 32 * j;
       const bool okc = col < a.N;
       mu[j] = okc ? a.bn_mean[col] : 0.f;
+      // keep test t = z + fmaf(y, bsc, bsh) > 0, branch-free over the mask modes:
+      // 1: z (bsc = bsh = 0); 2: y*scale+shift (z loads are out of range -> 0); 0: 1 > 0
       bsc[j] = (okc && a.bn_mask == 2) ? a.bn_sc[col] : 0.f;
-      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : 0.f;
+      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : (a.bn_mask == 0 ? 1.f : 0.f);
       cs[j] = 0.f;
       cq[j] = 0.f;
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long ro = row_off(i, r);
-        if (ro < 0) continue;
+      for (int r0 = 0; r0 < 16; r0 += ER) {
+        uint32_t off[ER][TN];
+        float yv[ER][TN], zv[ER][TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = col0 + 32 * j;
-          if (col >= a.N) continue;
-          float v = acc[i][j][r];
-          const float yv = a.bn_y[ro + col];
-          bool keep = true;
-          if (a.bn_mask == 1) keep = a.bn_z[ro + col] > 0.f;
-          else if (a.bn_mask == 2) keep = fmaf(yv, bsc[j], bsh[j]) > 0.f;
-          v = keep ? v : 0.f;
-          Cb[ro + col] = v;
-          cs[j] += v;
-          cq[j] = fmaf(v, yv - mu[j], cq[j]);
+        for (int r = 0; r < ER; ++r) {
+          const uint32_t ro = row_off(i, r0 + r);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            off[r][j] = eoff(ro, j);
+            yv[r][j] = bld1(rY, off[r][j]);
+            zv[r][j] = bld1(rZ, zoob | off[r][j]);
+          }
         }
+#pragma unroll
+        for (int r = 0; r < ER; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float v = acc[i][j][r0 + r];
+            const bool keep = zv[r][j] + fmaf(yv[r][j], bsc[j], bsh[j]) > 0.f;
+            v = keep ? v : 0.f;
+            st1(v, off[r][j]);
+            cs[j] += v;
+            cq[j] = fmaf(v, yv[r][j] - mu[j], cq[j]);
+          }
+        __builtin_amdgcn_sched_barrier(0);
       }
     float* red = smem;  // [WM][BN][2]; the main loop ended with a barrier
 #pragma unroll
@@ -598,7 +634,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
     }
     return;
   }
-  // (2) bias + stores
+  // (2) bias
   float bvals[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -667,12 +703,15 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
       }
     }
   }
+  // (3) stores (FWD inference epilogue: scale, residual, ReLU).  Plain stores under branches:
+  // nothing waits on them.
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const long ro = row_off(i, r);
-      if (ro < 0) continue;
+      const uint32_t ro = row_off(i, r);
+      if (ro == OOB) continue;
+      const long re = ro >> 2;   // element index of the row start
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = col0 + 32 * j;
@@ -680,10 +719,10 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         float v = acc[i][j][r] + bvals[j];
         if (MODE == MODE_FWD) {
           if (a.scale) v = fmaf(acc[i][j][r], a.scale[col], bvals[j]);
-          if (a.res) v += a.res[ro + col];
+          if (a.res) v += a.res[re + col];
           if (a.relu) v = fmaxf(v, 0.f);
         }
-        Cb[ro + col] = v;
+        Cb[re + col] = v;
       }
     }
 }
@@ -758,7 +797,7 @@ int pick_cfg(long M, long N, long K, int mode) {
 
 template <int MODE>
 int launch_gemm(const GemmArgs& a, bool al, int splits, hipStream_t st) {
-  TMR_CHECK_ARG(a.Abytes < 0x80000000u && a.Bbytes < 0x80000000u,
+  TMR_CHECK_ARG(a.Abytes < 0x80000000u && a.Bbytes < 0x80000000u && a.Cbytes < 0x80000000u,
                 "gemm: operand larger than 2 GiB (split the batch)");
   // WGRAD resolves taps per column (fixed per thread); FWD/DGRAD per k-tile when uniform
   // (a k-tile of BK must not straddle two taps: channels per tap >= BK)
@@ -848,6 +887,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.Abytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
   a.prec = d->math;
   a.Bbytes = clamp_bytes((long)d->k * a.K);
+  a.Cbytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldc, d->k));
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
 }
@@ -994,11 +1034,8 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
       a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.lds, d->k));
       a.prec = d->math;
       a.Bbytes = clamp_bytes((long)d->k * d->r * d->s * d->c);
-      if (st == 1) {
-        a.osy = 0;
-      } else {
-        a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
-      }
+      a.Cbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.ldc, d->c));
+      a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
       // nothing to add -- unless the fused BN backward must still see (mask, sum) these pixels
       if (a.K == 0 && beta == 1.f && !fz) continue;
       if (fz) {
@@ -1152,6 +1189,7 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldb, d->k));
   a.prec = d->math;
   a.Bbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
+  a.Cbytes = clamp_bytes(slab);
   bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0) && a.lds % 4 == 0 && a.ldb % 4 == 0;
   int rc = launch_gemm<MODE_WGRAD>(a, al, sp, stream);
   if (rc) return rc;
@@ -1179,6 +1217,7 @@ TMR_API int tmr_gemm_nt(int M, int N, int K, const float* A, int lda, const floa
   a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta;
   a.Abytes = clamp_bytes(M > 0 ? (long)(M - 1) * lda + K : 0);
   a.Bbytes = clamp_bytes(N > 0 ? (long)(N - 1) * ldb + K : 0);
+  a.Cbytes = clamp_bytes(M > 0 ? (long)(M - 1) * ldc + N : 0);
   bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && K % 4 == 0;
   return launch_gemm<MODE_FWD>(a, al, 1, stream);
 }
@@ -1195,9 +1234,11 @@ TMR_API int tmr_gemm_nn(int M, int N, int K, const float* A, int lda, const floa
   a.wr0 = 0; a.ws0 = 0; a.wst = 1; a.wS = 1;
   set_grid(a, M, 1, 1);
   a.Hs = 1; a.Ws = 1; a.sy = 1; a.sx = 1;
-  a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta; a.osy = 0;
+  a.lds = lda; a.ldb = ldb; a.ldc = ldc; a.beta = beta;
+  a.oH = 1; a.oW = 1; a.osy = 1; a.osx = 1; a.oyc = 0; a.oxc = 0;   // identity row map
   a.Abytes = clamp_bytes(M > 0 ? (long)(M - 1) * lda + K : 0);
   a.Bbytes = clamp_bytes(K > 0 ? (long)(K - 1) * ldb + N : 0);
+  a.Cbytes = clamp_bytes(M > 0 ? (long)(M - 1) * ldc + N : 0);
   bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && K % 4 == 0 &&
             N % 4 == 0;
   return launch_gemm<MODE_DGRAD>(a, al, 1, stream);
@@ -1218,6 +1259,7 @@ TMR_API int tmr_gemm_tn(int M, int N, int K, const float* A, int lda, const floa
   a.kchunk = K > 0 ? K : 1; a.slab = 0;
   a.Abytes = clamp_bytes(K > 0 ? (long)(K - 1) * lda + M : 0);
   a.Bbytes = clamp_bytes(K > 0 ? (long)(K - 1) * ldb + N : 0);
+  a.Cbytes = clamp_bytes(M > 0 ? (long)(M - 1) * ldc + N : 0);
   bool al = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && M % 4 == 0 &&
             N % 4 == 0;
   return launch_gemm<MODE_WGRAD>(a, al, 1, stream);
