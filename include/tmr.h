@@ -165,6 +165,13 @@ int tmr_bn_eval_params(const float* gamma, const float* beta, const float* runni
 /* z = act(y*scale + shift (+ residual)), act = ReLU if relu */
 int tmr_bn_apply(const float* y, const float* scale, const float* shift, const float* residual,
                  float* z, int rows, int c, int relu, hipStream_t stream);
+/* z = act(y*scale + shift + (yr*rscale + rshift)): Bottleneck bn3 + downsample-branch BN
+ * (torchvision Bottleneck.forward: out = bn3(conv3) + downsample(x); relu) with the branch's BN
+ * applied on the fly -- identical to tmr_bn_apply(yr, rscale, rshift, NULL, r, 0) followed by
+ * tmr_bn_apply(y, scale, shift, r, z, relu), without materialising r. */
+int tmr_bn_apply2(const float* y, const float* scale, const float* shift, const float* yr,
+                  const float* rscale, const float* rshift, float* z, int rows, int c, int relu,
+                  hipStream_t stream);
 /* backward of z = act(bn(y) (+res)): dy, optional dres (= grad at the pre-activation),
  * dgamma, dbeta.  ReLU mask: z > 0 from the saved output z when z != NULL, otherwise
  * y*scale+shift > 0 recomputed from the forward's scale/shift (valid without a residual;
@@ -188,6 +195,12 @@ int tmr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int n, int h, i
                       int ho, int wo, hipStream_t stream);
 int tmr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int n, int h, int w,
                       int c, int ho, int wo, hipStream_t stream);
+/* share.bn1 -> share.relu -> share.maxpool (:205-207) in one pass: x is the stem conv's pre-BN
+ * output, relu(x*scale + shift) is applied per loaded element (same result and argmax as
+ * tmr_bn_apply + tmr_maxpool2d_fwd; the stem's 112x112x64 BN output is never written). */
+int tmr_maxpool2d_fwd_bn(const float* x, const float* scale, const float* shift, float* y,
+                         uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
+                         hipStream_t stream);
 /* AdaptiveAvgPool2d(1) of share.avgpool (:214): x [n][hw][c] -> y [n][c] */
 int tmr_avgpool_fwd(const float* x, float* y, int n, int hw, int c, hipStream_t stream);
 int tmr_avgpool_bwd(const float* dy, float* dx, int n, int hw, int c, hipStream_t stream);

@@ -427,3 +427,24 @@ def test_conv_dgrad_fused_bn_backward_frame_chunks(dev):
     torch.cuda.synchronize()
     assert b[2] > a[2]
     assert torch.equal(a[0], b[0]) and rel_err(yb, ya) < 1e-6
+
+
+def test_bn_apply_fused_consumers(dev):
+    """The two BN applications folded into their consumers are bit-identical to the unfused
+    sequence: bn_apply2 (Bottleneck bn3 + downsample-branch BN + ReLU, torchvision
+    Bottleneck.forward) and maxpool_fwd_bn (share.bn1 -> relu -> maxpool, :205-207)."""
+    g = torch.Generator().manual_seed(11)
+    rows, c = 3 * 14 * 14, 256
+    y = torch.randn(rows, c, generator=g).to(dev)
+    yr = torch.randn(rows, c, generator=g).to(dev)
+    sc, sh = torch.randn(c, generator=g).to(dev), torch.randn(c, generator=g).to(dev)
+    rs, rf = torch.randn(c, generator=g).to(dev), torch.randn(c, generator=g).to(dev)
+    for relu in (True, False):
+        r = ops.bn_apply(yr, rs, rf, None, False)
+        ref = ops.bn_apply(y, sc, sh, r, relu)
+        assert torch.equal(ops.bn_apply2(y, sc, sh, yr, rs, rf, relu), ref)
+    x = torch.randn(2, 37, 29, 64, generator=g).to(dev)        # odd sizes: padded windows
+    s0, t0 = torch.randn(64, generator=g).to(dev), torch.randn(64, generator=g).to(dev)
+    p_ref, am_ref = ops.maxpool_fwd(ops.bn_apply(x.view(-1, 64), s0, t0, None, True).view_as(x))
+    p, am = ops.maxpool_fwd_bn(x, s0, t0)
+    assert torch.equal(p, p_ref) and torch.equal(am, am_ref)

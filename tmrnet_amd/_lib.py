@@ -54,9 +54,11 @@ SIGNATURES = {
     "tmr_bn_finalize": [P, I, I, P, P, P, P, F, F, P, P, P, P, P],
     "tmr_bn_eval_params": [P, P, P, P, F, I, P, P, P],
     "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
+    "tmr_bn_apply2": [P, P, P, P, P, P, P, I, I, I, P],
     "tmr_bn_bwd_parts": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_maxpool2d_fwd": [P, P, P, I, I, I, I, I, I, P],
+    "tmr_maxpool2d_fwd_bn": [P, P, P, P, P, I, I, I, I, I, I, P],
     "tmr_maxpool2d_bwd": [P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd": [P, P, I, I, I, P],
     "tmr_avgpool_bwd": [P, P, I, I, I, P],

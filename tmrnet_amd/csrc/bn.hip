@@ -171,6 +171,35 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, co
   }
 }
 
+// z = act(y*scale + shift + (yr*rscale + rshift)): the Bottleneck's BN3 + residual + ReLU with the
+// downsample branch's BatchNorm applied on the fly (its output is never materialised).  Same
+// fmaf/add/max sequence as bn_apply of the branch followed by bn_apply with that residual.
+template <bool RELU>
+__global__ __launch_bounds__(NT) void bn_apply2_k(const float* __restrict__ y, const float* __restrict__ scale,
+                                                  const float* __restrict__ shift,
+                                                  const float* __restrict__ yr,
+                                                  const float* __restrict__ rscale,
+                                                  const float* __restrict__ rshift,
+                                                  float* __restrict__ z, long n4, int c4) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    const int cc = (int)(i % c4) * 4;
+    float4 v = reinterpret_cast<const float4*>(y)[i];
+    const float4 r = reinterpret_cast<const float4*>(yr)[i];
+    const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
+    const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
+    const float4 rs = *reinterpret_cast<const float4*>(rscale + cc);
+    const float4 rf = *reinterpret_cast<const float4*>(rshift + cc);
+    v.x = fmaf(v.x, sc.x, sf.x) + fmaf(r.x, rs.x, rf.x);
+    v.y = fmaf(v.y, sc.y, sf.y) + fmaf(r.y, rs.y, rf.y);
+    v.z = fmaf(v.z, sc.z, sf.z) + fmaf(r.z, rs.z, rf.z);
+    v.w = fmaf(v.w, sc.w, sf.w) + fmaf(r.w, rs.w, rf.w);
+    if (RELU) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    reinterpret_cast<float4*>(z)[i] = v;
+  }
+}
+
 // ReLU mask of the backward: MASK 0 = none, 1 = saved output z > 0, 2 = recomputed
 // fmaf(y, scale, shift) > 0 (bit-identical to the forward's z > 0 when there is no residual,
 // and saves reading z)
@@ -409,6 +438,23 @@ TMR_API int tmr_bn_apply(const float* y, const float* scale, const float* shift,
     else hipLaunchKernelGGL((bn_apply_k<false, false>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
   }
   TMR_CHECK_LAUNCH("bn_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply2(const float* y, const float* scale, const float* shift, const float* yr,
+                          const float* rscale, const float* rshift, float* z, int rows, int c,
+                          int relu, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_bn_apply2: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(y && scale && shift && yr && rscale && rshift && z, "tmr_bn_apply2: null operand");
+  TMR_CHECK_ARG(yr != z, "tmr_bn_apply2: the branch input must not alias z");
+  const long n4 = (long)rows * c / 4;
+  if (relu)
+    hipLaunchKernelGGL((bn_apply2_k<true>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale, shift,
+                       yr, rscale, rshift, z, n4, c / 4);
+  else
+    hipLaunchKernelGGL((bn_apply2_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale, shift,
+                       yr, rscale, rshift, z, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply2");
   return 0;
 }
 

@@ -17,9 +17,14 @@ int ew_blocks(long n) {
   return (int)(b > 0 ? b : 1);
 }
 
+// BN: the input is the stem conv's pre-BN output; relu(x*scale + shift) is applied per loaded
+// element (the stem's BN+ReLU output is never materialised; same fmaf/max as bn_apply).
+template <bool BN>
 __global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x, float* __restrict__ y,
                                                     uchar4* __restrict__ am, int n, int h, int w,
-                                                    int c4, int ho, int wo) {
+                                                    int c4, int ho, int wo,
+                                                    const float* __restrict__ scale,
+                                                    const float* __restrict__ shift) {
   const long total = (long)n * ho * wo * c4;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
     const int cq = (int)(i % c4);
@@ -30,13 +35,24 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x,
     const int nn = (int)(p / ho);
     float4 best = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     uchar4 bi = make_uchar4(0, 0, 0, 0);
+    float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sf = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (BN) {
+      sc = reinterpret_cast<const float4*>(scale)[cq];
+      sf = reinterpret_cast<const float4*>(shift)[cq];
+    }
     for (int dy = 0; dy < 3; ++dy) {
       const int iy = oy * 2 - 1 + dy;
       if (iy < 0 || iy >= h) continue;
       for (int dx = 0; dx < 3; ++dx) {
         const int ix = ox * 2 - 1 + dx;
         if (ix < 0 || ix >= w) continue;
-        const float4 v = reinterpret_cast<const float4*>(x)[(((long)nn * h + iy) * w + ix) * c4 + cq];
+        float4 v = reinterpret_cast<const float4*>(x)[(((long)nn * h + iy) * w + ix) * c4 + cq];
+        if (BN) {
+          v.x = fmaxf(fmaf(v.x, sc.x, sf.x), 0.f);
+          v.y = fmaxf(fmaf(v.y, sc.y, sf.y), 0.f);
+          v.z = fmaxf(fmaf(v.z, sc.z, sf.z), 0.f);
+          v.w = fmaxf(fmaf(v.w, sc.w, sf.w), 0.f);
+        }
         const unsigned char id = (unsigned char)(dy * 3 + dx);
         // first maximum in scan order wins (PyTorch: val > max || isnan(val))
         if (v.x > best.x || isnan(v.x)) { best.x = v.x; bi.x = id; }
@@ -179,9 +195,21 @@ TMR_API int tmr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int n, 
                               int c, int ho, int wo, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd: channels %d must be a multiple of 4", c);
   const long total = (long)n * ho * wo * (c / 4);
-  hipLaunchKernelGGL(maxpool_fwd_k, dim3(ew_blocks(total)), dim3(NT), 0, stream, x, y,
-                     (uchar4*)argmax, n, h, w, c / 4, ho, wo);
+  hipLaunchKernelGGL(maxpool_fwd_k<false>, dim3(ew_blocks(total)), dim3(NT), 0, stream, x, y,
+                     (uchar4*)argmax, n, h, w, c / 4, ho, wo, nullptr, nullptr);
   TMR_CHECK_LAUNCH("maxpool_fwd");
+  return 0;
+}
+
+TMR_API int tmr_maxpool2d_fwd_bn(const float* x, const float* scale, const float* shift, float* y,
+                                 uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
+                                 hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd_bn: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(scale && shift, "tmr_maxpool2d_fwd_bn: null BatchNorm scale/shift");
+  const long total = (long)n * ho * wo * (c / 4);
+  hipLaunchKernelGGL(maxpool_fwd_k<true>, dim3(ew_blocks(total)), dim3(NT), 0, stream, x, y,
+                     (uchar4*)argmax, n, h, w, c / 4, ho, wo, scale, shift);
+  TMR_CHECK_LAUNCH("maxpool_fwd_bn");
   return 0;
 }
 

@@ -356,6 +356,19 @@ def bn_apply(y, scale, shift, residual=None, relu=True, out=None):
     return out
 
 
+def bn_apply2(y, scale, shift, yr, rscale, rshift, relu=True, out=None):
+    """act(y*scale + shift + (yr*rscale + rshift)): BN3 + the downsample branch's BN + ReLU."""
+    c = y.shape[-1]
+    rows = y.numel() // c
+    if yr.shape != y.shape:
+        raise RuntimeError("bn_apply2: branch shape %s != %s" % (tuple(yr.shape), tuple(y.shape)))
+    if out is None:
+        out = torch.empty_like(y)
+    call("tmr_bn_apply2", y, scale, shift, yr, rscale, rshift, out, rows, c, int(relu),
+         stream_ptr())
+    return out
+
+
 def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None, scale=None,
            shift=None):
     """ReLU mask from the saved output z, or (z=None) recomputed from y with the forward's
@@ -381,6 +394,17 @@ def maxpool_fwd(x):
     y = _empty((n, ho, wo, c), x)
     am = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
     call("tmr_maxpool2d_fwd", x, y, am, n, h, w, c, ho, wo, stream_ptr())
+    return y, am
+
+
+def maxpool_fwd_bn(x, scale, shift):
+    """MaxPool2d(3,2,1)(relu(x*scale + shift)) with the BN+ReLU applied on load."""
+    n, h, w, c = x.shape
+    ho = (h + 2 - 3) // 2 + 1
+    wo = (w + 2 - 3) // 2 + 1
+    y = _empty((n, ho, wo, c), x)
+    am = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
+    call("tmr_maxpool2d_fwd_bn", x, scale, shift, y, am, n, h, w, c, ho, wo, stream_ptr())
     return y, am
 
 

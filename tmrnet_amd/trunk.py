@@ -58,8 +58,13 @@ def _bn_momentum(bn):
     return bn.momentum
 
 
-def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32"):
-    """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z."""
+def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
+             defer=False, branch=None):
+    """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z.
+
+    Train mode only: ``defer`` returns (y, scale, shift) instead of applying the BN -- the
+    consumer applies it on load (the downsample branch inside its block's BN3 pass, the stem
+    inside the maxpool); ``branch`` = such a deferred (y, scale, shift) used as the residual."""
     w = conv.weight
     k, c, r, s = w.shape
     cs = x.shape[3]
@@ -81,14 +86,20 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
                                           bn.running_var, bn.eps)
         return ops.conv_fwd_fused(x, wk, stride, pad, scale, shift, residual, relu, c_real=c,
                                   math=math)
-    z = ops.bn_apply(y, scale, shift, residual, relu)
+    if defer:
+        z = None
+    elif branch is not None:
+        z = ops.bn_apply2(y, scale, shift, branch[0], branch[1], branch[2], relu)
+    else:
+        z = ops.bn_apply(y, scale, shift, residual, relu)
     if recs is not None:
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
-        recs.append({"x": x, "wk": wk, "y": y, "z": z if residual is not None else None,
+        has_res = residual is not None or branch is not None
+        recs.append({"x": x, "wk": wk, "y": y, "z": z if has_res else None,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
                      "c_real": c, "math": math})
-    return z
+    return (y, scale, shift) if defer else z
 
 
 def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
@@ -144,9 +155,17 @@ class TrunkFn(torch.autograd.Function):
         recs = [] if keep else None
         conv1, bn1, layers = share.trunk_parts()
         mt = share.precision
-        z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt)
-        p, am = ops.maxpool_fwd(z)
-        stem_hw = (z.shape[1], z.shape[2])
+        if training:
+            # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
+            # mask from y, so the stem's BN output is never needed)
+            y0, sc0, sh0 = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
+                                    defer=True)
+            p, am = ops.maxpool_fwd_bn(y0, sc0, sh0)
+            stem_hw = (y0.shape[1], y0.shape[2])
+        else:
+            z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt)
+            p, am = ops.maxpool_fwd(z)
+            stem_hw = (z.shape[1], z.shape[2])
         h = p
         blocks = []
         for layer in layers:
@@ -156,12 +175,17 @@ class TrunkFn(torch.autograd.Function):
                 z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec,
                               math=mt)
                 if blk.downsample is not None:
+                    # train: the branch's BN is applied inside the BN3 pass (bn_apply2)
                     idn = _conv_bn(h, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
-                                   training, recs=brec, math=mt)
+                                   training, recs=brec, math=mt, defer=training)
                 else:
                     idn = h
-                h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, residual=idn,
-                             recs=brec, math=mt)
+                if isinstance(idn, tuple):
+                    h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, branch=idn,
+                                 recs=brec, math=mt)
+                else:
+                    h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, residual=idn,
+                                 recs=brec, math=mt)
                 blocks.append((blk, brec))
         feat = ops.avgpool_fwd(h)
         ctx.keep = keep
