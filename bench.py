@@ -88,12 +88,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    dev = torch.device("cuda", local)
+    # rehearsal knobs (a multi-rank run on a one-GPU box): TMR_BENCH_DEVICE pins every rank to
+    # one device, TMR_BENCH_DIST_BACKEND=gloo replaces RCCL (which needs one GPU per rank)
+    dev = torch.device("cuda", int(os.environ.get("TMR_BENCH_DEVICE", local)))
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("TMR_BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import tmrnet_amd
     from tmrnet_amd import ops, LFBRows
