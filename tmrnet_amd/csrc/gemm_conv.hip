@@ -34,7 +34,9 @@ enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 #define TMR_GEMM_WAVES 3
 #endif
 #if TMR_GEMM_WAVES > 0
-#define TMR_GEMM_LB __launch_bounds__(64 * WM * WN, TMR_GEMM_WAVES)
+// f32 8-wave workgroups (256x128, 128x256, BK 16) are held to 128 VGPRs: two workgroups per CU, so one
+// workgroup's epilogue stores overlap the other's main loop (short-reduction GEMMs)
+#define TMR_GEMM_LB __launch_bounds__(64 * WM * WN, (WM * WN == 8 && PREC == 0 && BK == 16 ? 4 : TMR_GEMM_WAVES))
 #else
 #define TMR_GEMM_LB __launch_bounds__(64 * WM * WN)
 #endif
@@ -987,7 +989,7 @@ int pick_cfg(long M, long N, long K, int mode) {
     if (M <= 64 && N >= 512) return 3;
     if (M >= 256 && N >= 128) return 4;
   }
-  if (mode == MODE_FWD && N <= 128 && K >= 576 && M >= 4096) return 3;
+  if (mode == MODE_FWD && N <= 64 && K >= 576 && M >= 4096) return 3;
   if (M >= 256 && N >= 256) return 6;   // 256x256, 16 waves (measured best, convbench)
   if (M >= 256 && N >= 128) return 4;   // 256x128, 8 waves
   if (N <= 64 && M >= 256) return 1;
