@@ -158,6 +158,13 @@ int tmr_bn_finalize(const void* partials, int nparts, int c, const float* gamma,
                     float* running_mean, float* running_var, float momentum, float eps,
                     float* save_mean, float* save_invstd, float* scale, float* shift,
                     hipStream_t stream);
+/* tmr_bn_finalize with a two-level reduction (channel-group x row-slab blocks, then one thread
+ * per channel adding the slabs in order; deterministic): ws >= tmr_bn_parts_ws_bytes(nparts, c) */
+size_t tmr_bn_parts_ws_bytes(int nparts, int c);
+int tmr_bn_finalize_ws(const void* partials, int nparts, int c, const float* gamma,
+                       const float* beta, float* running_mean, float* running_var, float momentum,
+                       float eps, float* save_mean, float* save_invstd, float* scale, float* shift,
+                       void* ws, size_t ws_bytes, hipStream_t stream);
 /* eval mode: scale/shift from running stats */
 int tmr_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, int c, float* scale, float* shift,
@@ -179,7 +186,7 @@ int tmr_bn_apply2(const float* y, const float* scale, const float* shift, const 
  * first pass then overwrites dz with the masked gradient (the residual branch's gradient, in
  * place) and the second pass reads it back without re-reading the mask source. */
 /* BatchNorm backward from the fused-dgrad partials: g = the already masked output gradient;
- * dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); ws >= 3*c floats. */
+ * dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); ws >= tmr_bn_parts_ws_bytes(nparts, c). */
 int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, int nparts,
                      const float* save_mean, const float* save_invstd, const float* gamma,
                      float* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,

@@ -52,6 +52,8 @@ SIGNATURES = {
     "tmr_bn_ws_bytes": [I, I],
     "tmr_bn_fwd_stats": [P, I, I, P, P, P, P, F, F, P, P, P, P, P, SZ, P],
     "tmr_bn_finalize": [P, I, I, P, P, P, P, F, F, P, P, P, P, P],
+    "tmr_bn_finalize_ws": [P, I, I, P, P, P, P, F, F, P, P, P, P, P, SZ, P],
+    "tmr_bn_parts_ws_bytes": [I, I],
     "tmr_bn_eval_params": [P, P, P, P, F, I, P, P, P],
     "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2": [P, P, P, P, P, P, P, I, I, I, P],
@@ -96,6 +98,7 @@ _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,
     "tmr_conv2d_wgrad_ws_bytes": SZ,
     "tmr_bn_ws_bytes": SZ,
+    "tmr_bn_parts_ws_bytes": SZ,
     "tmr_sgd_chunk": ctypes.c_int64,
 }
 

@@ -304,47 +304,6 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
   }
 }
 
-// bn_bwd_final over float2 (sum g, sum g*(y-mean)) partials emitted by a fused dgrad epilogue
-__global__ __launch_bounds__(NT) void bn_bwd_final_f2(const float2* __restrict__ part, int nrb,
-                                                      int rows, int c, const float* mean,
-                                                      const float* inv, const float* gamma,
-                                                      float* dgamma, float* dbeta, float* coef) {
-  const int ch = blockIdx.x;
-  double s = 0.0, q = 0.0;
-  for (int b = threadIdx.x; b < nrb; b += NT) {
-    const float2 p = part[(long)b * c + ch];
-    s += p.x;
-    q += p.y;
-  }
-  __shared__ double red[2][NT];
-  red[0][threadIdx.x] = s;
-  red[1][threadIdx.x] = q;
-  __syncthreads();
-  for (int h = NT / 2; h > 0; h >>= 1) {
-    if (threadIdx.x < h) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + h];
-      red[1][threadIdx.x] += red[1][threadIdx.x + h];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    s = red[0][0];
-    q = red[1][0];
-    const double iv = inv[ch];
-    const double dgm = q * iv;
-    if (dgamma) dgamma[ch] = (float)dgm;
-    if (dbeta) dbeta[ch] = (float)s;
-    const double n = (double)rows;
-    const double gm = gamma ? gamma[ch] : 1.0;
-    const double A = gm * iv;
-    const double B = -gm * iv * iv * (dgm / n);
-    const double C = -A * (s / n) - B * (double)mean[ch];
-    coef[ch] = (float)A;
-    coef[c + ch] = (float)B;
-    coef[2 * c + ch] = (float)C;
-  }
-}
-
 template <int MASK, bool DRES>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const float* __restrict__ y,
                                                    const float* __restrict__ z,
@@ -372,6 +331,164 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
     o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
     reinterpret_cast<float4*>(dy)[i] = o;
   }
+}
+
+// ---- per-channel reductions of the GEMM-epilogue partials, two levels ----------------------
+// The conv epilogues leave one partial row per m-tile ([nparts][c]; up to ~31k rows for the
+// 64x64-tile dgrads of layer1).  Level 1: a (channel-group x row-slab) grid, 64 channels x 4
+// row phases per block, coalesced 1-KB rows, double accumulators -> slab sums in ws.  Level 2:
+// one block per channel group, 4 slab phases per channel combined in a fixed order
+// (deterministic), then the BN math.
+constexpr int SLAB_CH = 64;
+
+struct SlabPlan {
+  int groups, nslabs, rows;
+};
+
+SlabPlan slab_plan(int nparts, int c) {
+  SlabPlan p;
+  p.groups = cdiv(c, SLAB_CH);
+  int target = 512 / p.groups;
+  if (target < 1) target = 1;
+  int r = cdiv(nparts, 32);
+  if (r > target) r = target;
+  if (r < 1) r = 1;
+  p.rows = cdiv(nparts, r);
+  p.nslabs = cdiv(nparts, p.rows);
+  return p;
+}
+
+size_t slab_ws_bytes(int nparts, int c) {
+  const SlabPlan p = slab_plan(nparts, c);
+  return (size_t)p.nslabs * 3 * c * sizeof(double);
+}
+
+// KIND 0: float4 (count, mean, M2, -) partials -> (N, S1, S2) about K = the first partial's mean
+// KIND 1: float2 (sum g, sum g*(y-mean)) partials -> (S, Q, -)
+template <int KIND>
+__global__ __launch_bounds__(256) void parts_slab_k(const void* __restrict__ part, int nparts, int c,
+                                                    int rows, double* __restrict__ ws) {
+  const int ch = blockIdx.x * SLAB_CH + (threadIdx.x & (SLAB_CH - 1));
+  const int ph = threadIdx.x / SLAB_CH;
+  const int b0 = blockIdx.y * rows;
+  const int b1 = min(nparts, b0 + rows);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  if (ch < c) {
+    if (KIND == 0) {
+      const float4* p = (const float4*)part;
+      const double K = p[ch].y;
+      for (int b = b0 + ph; b < b1; b += 4) {
+        const float4 v = p[(long)b * c + ch];
+        const double nb = v.x, d = (double)v.y - K;
+        a0 += nb;
+        a1 = fma(nb, d, a1);
+        a2 += (double)v.z + nb * d * d;
+      }
+    } else {
+      const float2* p = (const float2*)part;
+      for (int b = b0 + ph; b < b1; b += 4) {
+        const float2 v = p[(long)b * c + ch];
+        a0 += v.x;
+        a1 += v.y;
+      }
+    }
+  }
+  __shared__ double red[3][256];
+  red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2;
+  __syncthreads();
+  if (ph == 0 && ch < c) {
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      t0 += red[0][q * SLAB_CH + threadIdx.x];
+      t1 += red[1][q * SLAB_CH + threadIdx.x];
+      t2 += red[2][q * SLAB_CH + threadIdx.x];
+    }
+    double* w = ws + (long)blockIdx.y * 3 * c;
+    w[ch] = t0; w[c + ch] = t1; w[2 * c + ch] = t2;
+  }
+}
+
+// sum of the slab partials of channel group blockIdx.x: SLAB_PH slab phases per channel (a
+// 64 x SLAB_PH block), combined in phase order; true on the one thread per channel holding the totals
+constexpr int SLAB_PH = 16;
+template <int NV>
+__device__ __forceinline__ bool slab_sum(const double* __restrict__ ws, int nslabs, int c, int& ch,
+                                         double (&t)[3]) {
+  ch = blockIdx.x * SLAB_CH + (threadIdx.x & (SLAB_CH - 1));
+  const int ph = threadIdx.x / SLAB_CH;
+  double a[3] = {0.0, 0.0, 0.0};
+  if (ch < c)
+    for (int r = ph; r < nslabs; r += SLAB_PH) {
+      const double* w = ws + (long)r * 3 * c;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) a[j] += w[j * c + ch];
+    }
+  __shared__ double red[3][SLAB_CH * SLAB_PH];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) red[j][threadIdx.x] = a[j];
+  __syncthreads();
+  if (ph != 0 || ch >= c) return false;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    t[j] = 0.0;
+#pragma unroll
+    for (int q = 0; q < SLAB_PH; ++q) t[j] += red[j][q * SLAB_CH + threadIdx.x];
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(SLAB_CH * SLAB_PH) void finalize_slabs_k(const double* __restrict__ ws, int nslabs,
+                                                        const float4* __restrict__ part, int c,
+                                                        const float* gamma, const float* beta,
+                                                        float* rmean, float* rvar, float momentum,
+                                                        float eps, float* smean, float* sinv,
+                                                        float* scale, float* shift) {
+  int ch;
+  double t[3];
+  if (!slab_sum<3>(ws, nslabs, c, ch, t)) return;
+  const double n = t[0], s1 = t[1], s2 = t[2];
+  const double K = part[ch].y;
+  const double mean = n > 0 ? K + s1 / n : 0.0;
+  double m2 = n > 0 ? s2 - s1 * (s1 / n) : 0.0;
+  if (m2 < 0) m2 = 0;
+  const double var = n > 0 ? m2 / n : 0.0;
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  smean[ch] = (float)mean;
+  sinv[ch] = (float)inv;
+  const double gm = gamma ? gamma[ch] : 1.0;
+  const double bt = beta ? beta[ch] : 0.0;
+  scale[ch] = (float)(gm * inv);
+  shift[ch] = (float)(bt - mean * gm * inv);
+  if (rmean) {
+    const double unb = n > 1 ? m2 / (n - 1.0) : var;
+    rmean[ch] = (float)((1.0 - momentum) * rmean[ch] + momentum * mean);
+    rvar[ch] = (float)((1.0 - momentum) * rvar[ch] + momentum * unb);
+  }
+}
+
+__global__ __launch_bounds__(SLAB_CH * SLAB_PH) void bwd_final_slabs_k(const double* __restrict__ ws, int nslabs,
+                                                         int rows, int c, const float* mean,
+                                                         const float* inv, const float* gamma,
+                                                         float* dgamma, float* dbeta, float* coef) {
+  int ch;
+  double t[3];
+  if (!slab_sum<2>(ws, nslabs, c, ch, t)) return;
+  const double s = t[0], q = t[1];
+  const double iv = inv[ch];
+  const double dbt = s;
+  const double dgm = q * iv;  // sum dzh * xhat
+  if (dgamma) dgamma[ch] = (float)dgm;
+  if (dbeta) dbeta[ch] = (float)dbt;
+  const double n = (double)rows;
+  const double gm = gamma ? gamma[ch] : 1.0;
+  const double A = gm * iv;
+  const double mdz = dbt / n, mdx = dgm / n;
+  const double B = -gm * iv * iv * mdx;
+  const double C = -A * mdz - B * (double)mean[ch];
+  coef[ch] = (float)A;
+  coef[c + ch] = (float)B;
+  coef[2 * c + ch] = (float)C;
 }
 
 int ew_blocks(long n4) {
@@ -411,6 +528,29 @@ TMR_API int tmr_bn_finalize(const void* partials, int nparts, int c, const float
                      nparts, c, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd, scale, shift);
   TMR_CHECK_LAUNCH("bn_finalize");
+  return 0;
+}
+
+TMR_API size_t tmr_bn_parts_ws_bytes(int nparts, int c) {
+  return nparts > 0 && c > 0 ? slab_ws_bytes(nparts, c) + (size_t)3 * c * sizeof(float) + 64 : 0;
+}
+
+TMR_API int tmr_bn_finalize_ws(const void* partials, int nparts, int c, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var,
+                               float momentum, float eps, float* save_mean, float* save_invstd,
+                               float* scale, float* shift, void* ws, size_t ws_bytes,
+                               hipStream_t stream) {
+  TMR_CHECK_ARG(nparts > 0 && c > 0, "tmr_bn_finalize_ws: empty partials");
+  TMR_CHECK_ARG(ws && ws_bytes >= slab_ws_bytes(nparts, c), "tmr_bn_finalize_ws: workspace too small");
+  const SlabPlan p = slab_plan(nparts, c);
+  hipLaunchKernelGGL(parts_slab_k<0>, dim3(p.groups, p.nslabs), dim3(256), 0, stream, partials,
+                     nparts, c, p.rows, (double*)ws);
+  TMR_CHECK_LAUNCH("bn_parts_slab");
+  hipLaunchKernelGGL(finalize_slabs_k, dim3(p.groups), dim3(SLAB_CH * SLAB_PH), 0, stream,
+                     (const double*)ws, p.nslabs, (const float4*)partials, c, gamma, beta,
+                     running_mean, running_var, momentum, eps, save_mean, save_invstd, scale,
+                     shift);
+  TMR_CHECK_LAUNCH("bn_finalize_slabs");
   return 0;
 }
 
@@ -515,11 +655,18 @@ TMR_API int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, 
                              size_t ws_bytes, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows > 0 && nparts > 0,
                 "tmr_bn_bwd_parts: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
-  TMR_CHECK_ARG(ws && ws_bytes >= (size_t)3 * c * sizeof(float), "tmr_bn_bwd_parts: workspace too small");
-  float* coef = (float*)ws;
-  hipLaunchKernelGGL(bn_bwd_final_f2, dim3(c), dim3(NT), 0, stream, (const float2*)parts, nparts,
-                     rows, c, save_mean, save_invstd, gamma, dgamma, dbeta, coef);
-  TMR_CHECK_LAUNCH("bn_bwd_final_f2");
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_bn_parts_ws_bytes(nparts, c),
+                "tmr_bn_bwd_parts: workspace too small (need tmr_bn_parts_ws_bytes)");
+  const SlabPlan sp = slab_plan(nparts, c);
+  double* slabs = (double*)ws;
+  float* coef = (float*)((char*)ws + slab_ws_bytes(nparts, c));
+  hipLaunchKernelGGL(parts_slab_k<1>, dim3(sp.groups, sp.nslabs), dim3(256), 0, stream, parts,
+                     nparts, c, sp.rows, slabs);
+  TMR_CHECK_LAUNCH("bn_parts_slab");
+  hipLaunchKernelGGL(bwd_final_slabs_k, dim3(sp.groups), dim3(SLAB_CH * SLAB_PH), 0, stream,
+                     (const double*)slabs, sp.nslabs, rows, c, save_mean, save_invstd, gamma,
+                     dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
   const long n4 = (long)rows * c / 4;
   hipLaunchKernelGGL((bn_bwd_apply<0, false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
                      nullptr, nullptr, nullptr, coef, dy, nullptr, n4, c / 4);

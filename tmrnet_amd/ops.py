@@ -146,8 +146,11 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
     c = stats.shape[1]
     mean = _empty((c,), stats); inv = _empty((c,), stats)
     scale = _empty((c,), stats); shift = _empty((c,), stats)
-    call("tmr_bn_finalize", stats, nparts, c, gamma, beta, running_mean, running_var,
-         float(momentum), float(eps), mean, inv, scale, shift, stream_ptr())
+    nb = query("tmr_bn_parts_ws_bytes", int(nparts), c)
+    ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=stats.device)
+    call("tmr_bn_finalize_ws", stats, nparts, c, gamma, beta, running_mean, running_var,
+         float(momentum), float(eps), mean, inv, scale, shift, ws, ctypes.c_size_t(ws.numel() * 8),
+         stream_ptr())
     return mean, inv, scale, shift
 
 
@@ -203,9 +206,10 @@ def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma):
     rows = y.numel() // c
     dy = torch.empty_like(y)
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)
-    ws = torch.empty((3 * c,), dtype=f32, device=y.device)
+    nb = query("tmr_bn_parts_ws_bytes", int(nparts), c)
+    ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=y.device)
     call("tmr_bn_bwd_parts", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta, rows,
-         c, ws, ctypes.c_size_t(ws.numel() * 4), stream_ptr())
+         c, ws, ctypes.c_size_t(ws.numel() * 8), stream_ptr())
     return dy, dgamma, dbeta
 
 
