@@ -185,6 +185,16 @@ int tmr_bn_apply2(const float* y, const float* scale, const float* shift, const 
  * saves one full read of z).  z/scale/shift unused when relu == 0.  dres may alias dz: the
  * first pass then overwrites dz with the masked gradient (the residual branch's gradient, in
  * place) and the second pass reads it back without re-reading the mask source. */
+/* share.bn1 -> relu -> maxpool backward (:205-207) without materialising the maxpool's input
+ * gradient: dz is gathered from the pooled gradient dyp (n,ho,wo,c) and argmax, masked by
+ * y*scale+shift > 0 (y = the stem conv's pre-BN output (n,h,w,c)); then the BatchNorm backward
+ * of tmr_bn_bwd.  ws >= tmr_bn_ws_bytes(n*h*w, c).  Same result as tmr_maxpool2d_bwd followed by
+ * tmr_bn_bwd(relu=1, z=NULL). */
+int tmr_bn_bwd_maxpool(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho, int wo,
+                       const float* y, const float* scale, const float* shift,
+                       const float* save_mean, const float* save_invstd, const float* gamma,
+                       float* dy, float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                       hipStream_t stream);
 /* BatchNorm backward from the fused-dgrad partials: g = the already masked output gradient;
  * dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); ws >= tmr_bn_parts_ws_bytes(nparts, c). */
 int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, int nparts,

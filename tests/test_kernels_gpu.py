@@ -448,3 +448,24 @@ def test_bn_apply_fused_consumers(dev):
     p_ref, am_ref = ops.maxpool_fwd(ops.bn_apply(x.view(-1, 64), s0, t0, None, True).view_as(x))
     p, am = ops.maxpool_fwd_bn(x, s0, t0)
     assert torch.equal(p, p_ref) and torch.equal(am, am_ref)
+
+
+def test_stem_bwd_maxpool_fused(dev):
+    """bn_bwd_maxpool (share.maxpool -> relu -> bn1 backward in two passes over y, dz gathered)
+    against maxpool_bwd followed by bn_bwd with the mask recomputed from y: same arithmetic per
+    element, partial sums in a different row order -> equal to fp32 rounding."""
+    g = torch.Generator().manual_seed(12)
+    n, h, w, c = 3, 37, 29, 64
+    y = torch.randn(n, h, w, c, generator=g).to(dev)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
+    beta = torch.randn(c, generator=g).to(dev)
+    rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
+    mean, inv, scale, shift = ops.bn_fwd_train(y.view(-1, c), gamma, beta, rm, rv, 0.1, 1e-5)
+    p, am = ops.maxpool_fwd_bn(y, scale, shift)
+    dp = torch.randn(p.shape, generator=g).to(dev)
+    dz = ops.maxpool_bwd(dp, am, (h, w))
+    dy_ref, _, dg_ref, db_ref = ops.bn_bwd(dz.view(-1, c), y.view(-1, c), None, mean, inv, gamma,
+                                           True, scale=scale, shift=shift)
+    dy, dg, db = ops.bn_bwd_maxpool(dp, am, y, scale, shift, mean, inv, gamma)
+    assert rel_err(dy.view(-1, c), dy_ref) < 1e-5
+    assert rel_err(dg, dg_ref) < 1e-5 and rel_err(db, db_ref) < 1e-5

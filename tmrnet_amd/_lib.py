@@ -58,6 +58,7 @@ SIGNATURES = {
     "tmr_bn_apply": [P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2": [P, P, P, P, P, P, P, I, I, I, P],
     "tmr_bn_bwd_parts": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_bwd_maxpool": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
     "tmr_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_maxpool2d_fwd": [P, P, P, I, I, I, I, I, I, P],
     "tmr_maxpool2d_fwd_bn": [P, P, P, P, P, I, I, I, I, I, I, P],

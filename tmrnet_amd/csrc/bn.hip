@@ -491,6 +491,89 @@ __global__ __launch_bounds__(SLAB_CH * SLAB_PH) void bwd_final_slabs_k(const dou
   coef[2 * c + ch] = (float)C;
 }
 
+// share.maxpool -> share.relu -> share.bn1 backward in two passes (the stem: pre-BN output y
+// (rows = n*h*w pixels), ReLU mask recomputed from y*scale+shift, dz gathered from the pooled
+// gradient -- neither dz nor the maxpool's input gradient is ever written)
+struct PoolGeo {
+  const float* dyp;
+  const uchar4* am;
+  FastDiv dHW, dW;
+  int ho, wo;
+};
+
+__device__ __forceinline__ float4 stem_dz(const PoolGeo& pg, uint32_t r, int cq, int c4) {
+  const uint32_t nn = fdiv(r, pg.dHW);
+  const uint32_t rem = r - nn * pg.dHW.d;
+  const uint32_t iy = fdiv(rem, pg.dW);
+  const uint32_t ix = rem - iy * pg.dW.d;
+  return maxpool_grad4(pg.dyp, pg.am, (int)nn, (int)iy, (int)ix, cq, c4, pg.ho, pg.wo);
+}
+
+__global__ __launch_bounds__(NT) void stem_bwd_partial(const PoolGeo pg, const float* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ mean, int rows,
+                                                       int c, int rpb, int cthreads,
+                                                       double* __restrict__ part) {
+  const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
+  const int rthreads = NT / cthreads;
+  const int ch = (blockIdx.y * cthreads + tc) * 4;
+  const float4 mu = *reinterpret_cast<const float4*>(mean + ch);
+  const float4 sc = *reinterpret_cast<const float4*>(scale + ch);
+  const float4 sf = *reinterpret_cast<const float4*>(shift + ch);
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  for (int r = r0 + tr; r < r1; r += rthreads) {
+    const float4 v = *reinterpret_cast<const float4*>(y + (long)r * c + ch);
+    const float4 g = relu_mask4(stem_dz(pg, (uint32_t)r, ch / 4, c / 4), affine4(v, sc, sf));
+    s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
+    q.x = fmaf(g.x, v.x - mu.x, q.x); q.y = fmaf(g.y, v.y - mu.y, q.y);
+    q.z = fmaf(g.z, v.z - mu.z, q.z); q.w = fmaf(g.w, v.w - mu.w, q.w);
+  }
+  __shared__ double red[NT][8];
+  red[threadIdx.x][0] = s.x; red[threadIdx.x][1] = s.y; red[threadIdx.x][2] = s.z;
+  red[threadIdx.x][3] = s.w; red[threadIdx.x][4] = q.x; red[threadIdx.x][5] = q.y;
+  red[threadIdx.x][6] = q.z; red[threadIdx.x][7] = q.w;
+  __syncthreads();
+  if (tr == 0) {
+    double acc[8];
+    for (int e = 0; e < 8; ++e) acc[e] = 0.0;
+    for (int k = 0; k < rthreads; ++k)
+      for (int e = 0; e < 8; ++e) acc[e] += red[k * cthreads + tc][e];
+    double* o = part + ((long)blockIdx.x * c + ch) * 2;
+    for (int e = 0; e < 4; ++e) {
+      o[2 * e] = acc[e];
+      o[2 * e + 1] = acc[4 + e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const float* __restrict__ y,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift,
+                                                     const float* __restrict__ coef,
+                                                     float* __restrict__ dy, long n4, int c4) {
+  const int c = c4 * 4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    const int cq = (int)(i % c4);
+    const int cc = cq * 4;
+    const float4 v = reinterpret_cast<const float4*>(y)[i];
+    const float4 g = relu_mask4(stem_dz(pg, (uint32_t)(i / c4), cq, c4),
+                                affine4(v, *reinterpret_cast<const float4*>(scale + cc),
+                                        *reinterpret_cast<const float4*>(shift + cc)));
+    const float4 A = *reinterpret_cast<const float4*>(coef + cc);
+    const float4 B = *reinterpret_cast<const float4*>(coef + c + cc);
+    const float4 C = *reinterpret_cast<const float4*>(coef + 2 * c + cc);
+    float4 o;
+    o.x = fmaf(A.x, g.x, fmaf(B.x, v.x, C.x));
+    o.y = fmaf(A.y, g.y, fmaf(B.y, v.y, C.y));
+    o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
+    o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
+    reinterpret_cast<float4*>(dy)[i] = o;
+  }
+}
+
 int ew_blocks(long n4) {
   long b = (n4 + NT - 1) / NT;
   if (b > 2048 * 4) b = 2048 * 4;
@@ -646,6 +729,39 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
   }
 #undef TMR_BN_APPLY
   TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_maxpool(const float* dyp, const uint8_t* argmax, int n, int h, int w,
+                               int ho, int wo, const float* y, const float* scale,
+                               const float* shift, const float* save_mean,
+                               const float* save_invstd, const float* gamma, float* dy,
+                               float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                               hipStream_t stream) {
+  const long rows_l = (long)n * h * w;
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows_l > 0 && rows_l < 0x7fffffffL,
+                "tmr_bn_bwd_maxpool: bad shape n=%d h=%d w=%d c=%d", n, h, w, c);
+  TMR_CHECK_ARG(ho == (h + 2 - 3) / 2 + 1 && wo == (w + 2 - 3) / 2 + 1,
+                "tmr_bn_bwd_maxpool: pooled %dx%d is not MaxPool2d(3,2,1) of %dx%d", ho, wo, h, w);
+  const int rows = (int)rows_l;
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd_maxpool: workspace too small");
+  PoolGeo pg;
+  pg.dyp = dyp; pg.am = (const uchar4*)argmax;
+  pg.dHW = make_fastdiv((uint32_t)(h * w)); pg.dW = make_fastdiv((uint32_t)w);
+  pg.ho = ho; pg.wo = wo;
+  Plan p = make_plan(rows, c);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
+  hipLaunchKernelGGL(stem_bwd_partial, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg, y, scale,
+                     shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("stem_bwd_partial");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  const long n4 = rows_l * c / 4;
+  hipLaunchKernelGGL(stem_bwd_apply, dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg, y, scale, shift,
+                     coef, dy, n4, c / 4);
+  TMR_CHECK_LAUNCH("stem_bwd_apply");
   return 0;
 }
 

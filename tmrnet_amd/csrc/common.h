@@ -65,3 +65,27 @@ __device__ __forceinline__ float warp_max(float v) {
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Gradient reaching input pixel (nn, iy, ix), channel quad cq, through MaxPool2d(3, 2, 1): the
+// gather form of its backward (each input pixel sits in at most 2x2 windows; a window passes its
+// gradient to the input its argmax -- the first maximum in scan order, 0..8 -- points at).
+__device__ __forceinline__ float4 maxpool_grad4(const float* __restrict__ dy,
+                                                const uchar4* __restrict__ am, int nn, int iy,
+                                                int ix, int cq, int c4, int ho, int wo) {
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int oy0 = iy / 2, oy1 = min((iy + 1) / 2, ho - 1);
+  const int ox0 = ix / 2, ox1 = min((ix + 1) / 2, wo - 1);
+  for (int oy = oy0; oy <= oy1; ++oy) {
+    for (int ox = ox0; ox <= ox1; ++ox) {
+      const long o = (((long)nn * ho + oy) * wo + ox) * c4 + cq;
+      const unsigned char id = (unsigned char)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
+      const uchar4 a = am[o];
+      const float4 d = reinterpret_cast<const float4*>(dy)[o];
+      if (a.x == id) g.x += d.x;
+      if (a.y == id) g.y += d.y;
+      if (a.z == id) g.z += d.z;
+      if (a.w == id) g.w += d.w;
+    }
+  }
+  return g;
+}

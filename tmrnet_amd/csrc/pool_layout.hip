@@ -77,21 +77,7 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_k(const float* __restrict__ dy
     p /= w;
     const int iy = (int)(p % h);
     const int nn = (int)(p / h);
-    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int oy0 = iy / 2, oy1 = min((iy + 1) / 2, ho - 1);
-    const int ox0 = ix / 2, ox1 = min((ix + 1) / 2, wo - 1);
-    for (int oy = oy0; oy <= oy1; ++oy) {
-      for (int ox = ox0; ox <= ox1; ++ox) {
-        const long o = (((long)nn * ho + oy) * wo + ox) * c4 + cq;
-        const unsigned char id = (unsigned char)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
-        const uchar4 a = am[o];
-        const float4 d = reinterpret_cast<const float4*>(dy)[o];
-        if (a.x == id) g.x += d.x;
-        if (a.y == id) g.y += d.y;
-        if (a.z == id) g.z += d.z;
-        if (a.w == id) g.w += d.w;
-      }
-    }
+    const float4 g = maxpool_grad4(dy, am, nn, iy, ix, cq, c4, ho, wo);
     reinterpret_cast<float4*>(dx)[i] = g;
   }
 }

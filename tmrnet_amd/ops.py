@@ -200,6 +200,19 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     return out, parts, nparts
 
 
+def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma):
+    """Stem backward: maxpool(3,2,1) backward + ReLU mask (from y) + BN backward in two passes
+    over y; the maxpool's input gradient is never written.  -> (dy, dgamma, dbeta)."""
+    n, h, w, c = y.shape
+    _, ho, wo, _ = dyp.shape
+    ws, nb = _bn_ws(n * h * w, c, y.device)
+    dy = torch.empty_like(y)
+    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
+    call("tmr_bn_bwd_maxpool", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma, dy,
+         dgamma, dbeta, c, ws, ctypes.c_size_t(nb), stream_ptr())
+    return dy, dgamma, dbeta
+
+
 def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma):
     """BN backward from conv_dgrad_bnbwd partials: g already masked -> (dy, dgamma, dbeta)."""
     c = y.shape[-1]

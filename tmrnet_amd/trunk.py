@@ -103,7 +103,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
 
 
 def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
-                 dres_inplace=False, parts=None, fuse_prev=None):
+                 dres_inplace=False, parts=None, fuse_prev=None, pool=None):
     """BN backward, wgrad, dgrad (optionally accumulated into dx_out) of one conv+BN unit.
 
     parts: dz was produced by a fused dgrad (conv_dgrad_bnbwd): it is already ReLU-masked and
@@ -111,9 +111,16 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     or is recomputed from y when there was no residual.  dres_inplace: the pre-activation
     gradient (the identity branch's) overwrites dz and is returned as dres.
     fuse_prev: the unit whose BN output gradient this unit's dgrad produces -- its mask and
-    partial sums are then computed in the dgrad epilogue; returned as the third value."""
+    partial sums are then computed in the dgrad epilogue; returned as the third value.
+    pool: (pooled gradient, argmax) of the maxpool that consumed this unit's output (the stem);
+    dz is then gathered from it inside the BN backward."""
     conv, bn = rec["conv"], rec["bn"]
-    if parts is not None:
+    if pool is not None:
+        # the stem: maxpool backward + ReLU mask + BN backward without writing dz
+        dy, dg, db = ops.bn_bwd_maxpool(pool[0], pool[1], rec["y"], rec["scale"], rec["shift"],
+                                        rec["mean"], rec["inv"], bn.weight.detach())
+        dres = None
+    elif parts is not None:
         dy, dg, db = ops.bn_bwd_parts(dz, rec["y"], parts[0], parts[1], rec["mean"], rec["inv"],
                                       bn.weight.detach())
         dres = dz if want_dres else None
@@ -231,8 +238,7 @@ class TrunkFn(torch.autograd.Function):
             g = dx
         dh = g
         am, stem_hw = ctx.pool
-        dz = ops.maxpool_bwd(dh, am, stem_hw)
-        _conv_bn_bwd(ctx.stem[0], dz, grads, need_dx=False)
+        _conv_bn_bwd(ctx.stem[0], None, grads, need_dx=False, pool=(dh, am))
         out = [grads.get(p) for p in ctx.params]
         ctx.blocks = ctx.stem = None
         return (None, None, None) + tuple(out)
