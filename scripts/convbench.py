@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--stats", action="store_true",
+                    help="forward with the fused BatchNorm-statistics epilogue (as the train step)")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
@@ -57,7 +59,8 @@ def main():
         for kind in kinds:
             if kind == "dgrad" and cin == 3:
                 continue
-            fn = {"fwd": lambda: ops.conv_fwd(x, wk, st, pad, out=y),
+            fn = {"fwd": (lambda: ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin)) if args.stats
+                  else (lambda: ops.conv_fwd(x, wk, st, pad, out=y)),
                   "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x,
                                                   beta=args.dgrad_beta),
                   "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin)}[kind]
