@@ -1,0 +1,31 @@
+"""The data-parallel train step end to end on the GPU: bench.py at world size 2, both ranks on
+cuda:0 with the gloo backend (RCCL needs one GPU per rank; the 8-GPU RCCL run is the driver's).
+Exercises rank-0 weight broadcast, the bucketed gradient SUM (tmrnet_amd.ddp.GradAllReduce), the
+barrier/max-over-ranks timing and the rank-0 JSON line (train_only_non-local_pretrained.py:628,
+DataParallel -> one process per GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_one_gpu():
+    env = dict(os.environ, TMR_BENCH_DEVICE="0", TMR_BENCH_DIST_BACKEND="gloo",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29547", "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--clips", "2", "--no-cpu-baseline", "--no-roofline"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]      # rank 0 prints exactly one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4
+    assert d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert d["loss_last"] == d["loss_last"]       # finite
