@@ -930,6 +930,23 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   }
 }
 
+// sum over the split slabs in split order, loads issued 8 at a time (the adds stay in order, so
+// the result is bit-identical to a plain loop; only the load latency is overlapped)
+__device__ __forceinline__ float split_sum(const float* __restrict__ slabs, int nsplit, long slab,
+                                           long src) {
+  float s = 0.f;
+  int p = 0;
+  for (; p + 8 <= nsplit; p += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slabs[(p + u) * slab + src];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; p < nsplit; ++p) s += slabs[p * slab + src];
+  return s;
+}
+
 // WGRAD split reduction: dW[co][tap][c] (KRSC with c < creal) summed over splits in
 // split order, written to OIHW (co, c, r, s) of the real weight.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit, long slab,
@@ -944,9 +961,34 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int nsplit,
     int c = (int)(t2 % creal);
     int co = (int)(t2 / creal);
     long src = ((long)co * ntaps + tap) * Cpad + c;
-    float s = 0.f;
-    for (int p = 0; p < nsplit; ++p) s += slabs[p * slab + src];
+    const float s = split_sum(slabs, nsplit, slab, src);
     out[o] = beta != 0.f ? s + beta * out[o] : s;
+  }
+}
+
+// The same reduction for multi-tap weights: one block per (co, 64-channel group) sums the splits
+// with reads along c (coalesced), transposes (tap, c) -> (c, tap) through LDS and writes OIHW rows
+// contiguously.  Per element the split order is the same as wgrad_reduce_kernel's.
+__global__ __launch_bounds__(256) void wgrad_reduce_taps_kernel(const float* __restrict__ slabs,
+                                                                int nsplit, long slab,
+                                                                float* __restrict__ out, int ntaps,
+                                                                int Cpad, int creal, float beta) {
+  __shared__ float tile[49 * 64];   // ntaps <= 49 (7x7), checked on the host
+  const int co = blockIdx.x;
+  const int c0 = blockIdx.y * 64;
+  const int nc = min(64, creal - c0);
+  for (int idx = threadIdx.x; idx < ntaps * 64; idx += 256) {
+    const int tap = idx >> 6, cl = idx & 63;
+    float sum = 0.f;
+    if (cl < nc) sum = split_sum(slabs, nsplit, slab, ((long)co * ntaps + tap) * Cpad + c0 + cl);
+    tile[tap * 64 + cl] = sum;
+  }
+  __syncthreads();
+  float* o = out + ((long)co * creal + c0) * ntaps;
+  for (int idx = threadIdx.x; idx < nc * ntaps; idx += 256) {
+    const int cl = idx / ntaps, tap = idx - cl * ntaps;
+    const float v = tile[tap * 64 + cl];
+    o[idx] = beta != 0.f ? v + beta * o[idx] : v;
   }
 }
 
@@ -1396,11 +1438,18 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0) && a.lds % 4 == 0 && a.ldb % 4 == 0;
   int rc = launch_gemm<MODE_WGRAD>(a, al, sp, stream);
   if (rc) return rc;
-  long total = (long)d->k * d->r * d->s * c_real;
+  const int ntaps = d->r * d->s;
+  if (ntaps > 1 && ntaps <= 49) {
+    hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, cdiv(c_real, 64)), dim3(256), 0,
+                       stream, ws, sp, slab, dw_oihw, ntaps, d->c, c_real, beta);
+    TMR_CHECK_LAUNCH("wgrad_reduce_taps_kernel");
+    return 0;
+  }
+  long total = (long)d->k * ntaps * c_real;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, ws, sp, slab,
-                     dw_oihw, d->k, d->r * d->s, d->c, c_real, beta);
+                     dw_oihw, d->k, ntaps, d->c, c_real, beta);
   TMR_CHECK_LAUNCH("wgrad_reduce_kernel");
   return 0;
 }
