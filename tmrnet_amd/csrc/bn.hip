@@ -509,42 +509,58 @@ __device__ __forceinline__ float4 stem_dz(const PoolGeo& pg, uint32_t r, int cq,
   return maxpool_grad4(pg.dyp, pg.am, (int)nn, (int)iy, (int)ix, cq, c4, pg.ho, pg.wo);
 }
 
-__global__ __launch_bounds__(NT) void stem_bwd_partial(const PoolGeo pg, const float* __restrict__ y,
-                                                       const float* __restrict__ scale,
-                                                       const float* __restrict__ shift,
-                                                       const float* __restrict__ mean, int rows,
-                                                       int c, int rpb, int cthreads,
-                                                       double* __restrict__ part) {
+// Partial sums from the pooled side: every pooled output passes its gradient to exactly one
+// input pixel per channel (its argmax), so sum g and sum g*(y - mean) over the input pixels equal
+// the sums over pooled outputs of dyp * mask(y[argmax]) and that times (y[argmax] - mean): one
+// read of the pooled gradient and argmax plus one y element per channel, no gather of windows.
+__global__ __launch_bounds__(NT) void stem_bwd_partial_pooled(
+    const PoolGeo pg, int h, int w, const float* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, int prows, int c, int rpb,
+    int cthreads, FastDiv dPHW, FastDiv dPW, double* __restrict__ part) {
   const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
   const int rthreads = NT / cthreads;
   const int ch = (blockIdx.y * cthreads + tc) * 4;
-  const float4 mu = *reinterpret_cast<const float4*>(mean + ch);
-  const float4 sc = *reinterpret_cast<const float4*>(scale + ch);
-  const float4 sf = *reinterpret_cast<const float4*>(shift + ch);
+  const float mu[4] = {mean[ch], mean[ch + 1], mean[ch + 2], mean[ch + 3]};
+  const float sc[4] = {scale[ch], scale[ch + 1], scale[ch + 2], scale[ch + 3]};
+  const float sf[4] = {shift[ch], shift[ch + 1], shift[ch + 2], shift[ch + 3]};
+  const int c4 = c / 4;
   const int r0 = blockIdx.x * rpb;
-  const int r1 = min(rows, r0 + rpb);
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  const int r1 = min(prows, r0 + rpb);
+  float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
   for (int r = r0 + tr; r < r1; r += rthreads) {
-    const float4 v = *reinterpret_cast<const float4*>(y + (long)r * c + ch);
-    const float4 g = relu_mask4(stem_dz(pg, (uint32_t)r, ch / 4, c / 4), affine4(v, sc, sf));
-    s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
-    q.x = fmaf(g.x, v.x - mu.x, q.x); q.y = fmaf(g.y, v.y - mu.y, q.y);
-    q.z = fmaf(g.z, v.z - mu.z, q.z); q.w = fmaf(g.w, v.w - mu.w, q.w);
+    const uint32_t nn = fdiv((uint32_t)r, dPHW);
+    const uint32_t rem = r - nn * dPHW.d;
+    const uint32_t oy = fdiv(rem, dPW);
+    const uint32_t ox = rem - oy * dPW.d;
+    const long o = (long)r * c4 + ch / 4;
+    const uchar4 a = pg.am[o];
+    const float4 d = reinterpret_cast<const float4*>(pg.dyp)[o];
+    const unsigned char ids[4] = {a.x, a.y, a.z, a.w};
+    const float ds[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int iy = (int)oy * 2 - 1 + ids[e] / 3, ix = (int)ox * 2 - 1 + ids[e] % 3;
+      const float v = y[(((long)nn * h + iy) * w + ix) * c + ch + e];
+      const float g = fmaf(v, sc[e], sf[e]) > 0.f ? ds[e] : 0.f;
+      s[e] += g;
+      q[e] = fmaf(g, v - mu[e], q[e]);
+    }
   }
   __shared__ double red[NT][8];
-  red[threadIdx.x][0] = s.x; red[threadIdx.x][1] = s.y; red[threadIdx.x][2] = s.z;
-  red[threadIdx.x][3] = s.w; red[threadIdx.x][4] = q.x; red[threadIdx.x][5] = q.y;
-  red[threadIdx.x][6] = q.z; red[threadIdx.x][7] = q.w;
+  for (int e = 0; e < 4; ++e) {
+    red[threadIdx.x][e] = s[e];
+    red[threadIdx.x][4 + e] = q[e];
+  }
   __syncthreads();
   if (tr == 0) {
     double acc[8];
     for (int e = 0; e < 8; ++e) acc[e] = 0.0;
     for (int k = 0; k < rthreads; ++k)
       for (int e = 0; e < 8; ++e) acc[e] += red[k * cthreads + tc][e];
-    double* o = part + ((long)blockIdx.x * c + ch) * 2;
+    double* op = part + ((long)blockIdx.x * c + ch) * 2;
     for (int e = 0; e < 4; ++e) {
-      o[2 * e] = acc[e];
-      o[2 * e + 1] = acc[4 + e];
+      op[2 * e] = acc[e];
+      op[2 * e + 1] = acc[4 + e];
     }
   }
 }
@@ -749,12 +765,15 @@ TMR_API int tmr_bn_bwd_maxpool(const float* dyp, const uint8_t* argmax, int n, i
   pg.dyp = dyp; pg.am = (const uchar4*)argmax;
   pg.dHW = make_fastdiv((uint32_t)(h * w)); pg.dW = make_fastdiv((uint32_t)w);
   pg.ho = ho; pg.wo = wo;
-  Plan p = make_plan(rows, c);
+  // partials over the pooled rows (fewer than the input rows: the workspace of `rows` suffices)
+  const int prows = n * ho * wo;
+  Plan p = make_plan(prows, c);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
-  hipLaunchKernelGGL(stem_bwd_partial, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg, y, scale,
-                     shift, save_mean, rows, c, p.rpb, p.cthreads, part);
-  TMR_CHECK_LAUNCH("stem_bwd_partial");
+  hipLaunchKernelGGL(stem_bwd_partial_pooled, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg, h, w,
+                     y, scale, shift, save_mean, prows, c, p.rpb, p.cthreads,
+                     make_fastdiv((uint32_t)(ho * wo)), make_fastdiv((uint32_t)wo), part);
+  TMR_CHECK_LAUNCH("stem_bwd_partial_pooled");
   hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");

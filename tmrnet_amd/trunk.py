@@ -59,7 +59,7 @@ def _bn_momentum(bn):
 
 
 def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
-             defer=False, branch=None):
+             defer=False, branch=None, nbt=None):
     """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z.
 
     Train mode only: ``defer`` returns (y, scale, shift) instead of applying the BN -- the
@@ -78,7 +78,11 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         mean, inv, scale, shift = ops.bn_finalize(
             stats, nparts, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
             bn.running_var, _bn_momentum(bn), bn.eps)
-        bn.num_batches_tracked.add_(1)
+        # num_batches_tracked += 1; the trunk batches these into one launch (nbt list)
+        if nbt is None:
+            bn.num_batches_tracked.add_(1)
+        else:
+            nbt.append(bn.num_batches_tracked)
     else:
         # eval: running-stat BN, residual and ReLU in the conv epilogue (one launch, no y pass;
         # same arithmetic as conv_fwd + bn_apply)
@@ -160,17 +164,18 @@ class TrunkFn(torch.autograd.Function):
         training = share.training
         keep = keep and training
         recs = [] if keep else None
+        nbt = []   # BatchNorm num_batches_tracked counters, incremented together at the end
         conv1, bn1, layers = share.trunk_parts()
         mt = share.precision
         if training:
             # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
             # mask from y, so the stem's BN output is never needed)
             y0, sc0, sh0 = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
-                                    defer=True)
+                                    defer=True, nbt=nbt)
             p, am = ops.maxpool_fwd_bn(y0, sc0, sh0)
             stem_hw = (y0.shape[1], y0.shape[2])
         else:
-            z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt)
+            z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt, nbt=nbt)
             p, am = ops.maxpool_fwd(z)
             stem_hw = (z.shape[1], z.shape[2])
         h = p
@@ -178,23 +183,26 @@ class TrunkFn(torch.autograd.Function):
         for layer in layers:
             for blk in layer:
                 brec = [] if keep else None
-                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt)
+                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt,
+                              nbt=nbt)
                 z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec,
-                              math=mt)
+                              math=mt, nbt=nbt)
                 if blk.downsample is not None:
                     # train: the branch's BN is applied inside the BN3 pass (bn_apply2)
                     idn = _conv_bn(h, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
-                                   training, recs=brec, math=mt, defer=training)
+                                   training, recs=brec, math=mt, defer=training, nbt=nbt)
                 else:
                     idn = h
                 if isinstance(idn, tuple):
                     h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, branch=idn,
-                                 recs=brec, math=mt)
+                                 recs=brec, math=mt, nbt=nbt)
                 else:
                     h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, residual=idn,
-                                 recs=brec, math=mt)
+                                 recs=brec, math=mt, nbt=nbt)
                 blocks.append((blk, brec))
         feat = ops.avgpool_fwd(h)
+        if nbt:
+            torch._foreach_add_(nbt, 1)
         ctx.keep = keep
         if keep:
             ctx.share = share
