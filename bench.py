@@ -246,8 +246,8 @@ def workload_name(args):
 def load_traffic(model):
     """HBM bytes of the conv kernels per step from the committed rocprofv3 PMC passes of this
     workload (scripts/pmc.sh -> scripts/pmc_summary.py -> profiles/<round>/pmc_traffic_<model>.json:
-    FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE of gemm_kernel + wgrad_reduce_kernel
-    launches, per train step).  None when no PMC pass has been committed."""
+    FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE of gemm_kernel and the split-K
+    reductions (wgrad_reduce_kernel, wgrad_reduce_taps_kernel), per train step).  None when no PMC pass has been committed."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_%s.json" % model)))
     if not files:
@@ -257,7 +257,8 @@ def load_traffic(model):
     fams = d.get("families", {})
     if "gemm_kernel" not in fams:
         return None
-    per_step = sum(fams[k]["hbm_bytes_per_step"] for k in ("gemm_kernel", "wgrad_reduce_kernel")
+    per_step = sum(fams[k]["hbm_bytes_per_step"]
+                   for k in ("gemm_kernel", "wgrad_reduce_kernel", "wgrad_reduce_taps_kernel")
                    if k in fams)
     return {"hbm_bytes_per_step": per_step, "source": os.path.relpath(files[-1], ROOT)}
 
