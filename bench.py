@@ -36,8 +36,8 @@ GFLOP_PER_FRAME = {"resnet50": 24.33, "resnest50": 32.3}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--clips", type=int, default=64, help="clips per rank (reference batch)")
     ap.add_argument("--seq", type=int, default=10)
     ap.add_argument("--lfb", type=int, default=40)
