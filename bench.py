@@ -117,6 +117,8 @@ def main():
                          weight_decay=5e-4)
     crit = tmrnet_amd.CrossEntropyLoss(size_average=False)
     reducer = GradAllReduce(model, dist) if dist is not None else None
+    if reducer is not None and os.environ.get("TMR_DDP_OVERLAP", "1") != "0":
+        model.share.grad_ready = reducer.grads_ready   # trunk grads exchanged during the backward
     frames, bank, vs_d, offs, starts, labels = synth_inputs(args, rank, dev)
     B, T, L = args.clips, args.seq, args.lfb
     from tmrnet_amd.augment import ClipAugment

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, early=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -28,6 +28,9 @@ def _worker(rank, world, port, q):
     red = GradAllReduce(m, dist, bucket_bytes=4 * 1024)
     for i, p in enumerate(m.parameters()):
         p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
+    if early:   # the trunk's per-block launch during the backward (TrunkFn.backward)
+        ps = list(m.parameters())
+        red.grads_ready([(p, p.grad.clone()) for p in ps[2:]])
     red.all_reduce_sum()
     # numpy copies: torch tensors would travel as shared-memory fds that vanish with the child
     out = [p.grad.numpy().copy() for p in m.parameters()]
@@ -36,12 +39,16 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_grad_all_reduce_sum_world2():
+import pytest
+
+
+@pytest.mark.parametrize("early", [False, True])
+def test_grad_all_reduce_sum_world2(early):
     world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, early)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

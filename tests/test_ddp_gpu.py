@@ -29,3 +29,19 @@ def test_bench_two_ranks_one_gpu():
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4
     assert d["config"]["parallelism"] == "dp2" and d["value"] > 0
     assert d["loss_last"] == d["loss_last"]       # finite
+
+
+def test_overlap_matches_post_backward():
+    """Trunk grads launched per block during the backward sum to the same values as the
+    all-after-backward buckets (a block handed over too early, or skipped, would differ ~2x)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29548", "tests/_ddp_overlap_worker.py"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("OVERLAP_REL_DIFF")]
+    assert len(line) == 1, p.stdout[-2000:]
+    f = line[0].split()
+    worst, n, early_off, early_on = float(f[1]), int(f[2]), int(f[3]), int(f[4])
+    assert early_off == 0 and early_on == 16, line[0]    # one launch per bottleneck block
+    assert n > 100 and worst < 1e-5, line[0]

@@ -222,6 +222,7 @@ class TrunkFn(torch.autograd.Function):
         blocks = ctx.blocks
         fuse = os.environ.get("TMR_FUSE_BN_BWD", "1") != "0"
         pending = None     # BN-backward partials of g when the dgrad that produced it was fused
+        ready = getattr(ctx.share, "grad_ready", None)   # ddp.GradAllReduce.grads_ready, or None
         while blocks:
             blk, brec = blocks.pop()
             has_ds = blk.downsample is not None
@@ -244,6 +245,8 @@ class TrunkFn(torch.autograd.Function):
                                               fuse_prev=prev3)
             del dz1, brec, dres
             g = dx
+            if ready is not None:   # this block's parameter grads are final: start their exchange
+                ready([(p, grads[p]) for p in blk.parameters() if p in grads])
         dh = g
         am, stem_hw = ctx.pool
         _conv_bn_bwd(ctx.stem[0], None, grads, need_dx=False, pool=(dh, am))
