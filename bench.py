@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -45,7 +46,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--conv-table", action="store_true", help="per-launch conv table on stderr")
     ap.add_argument("--cpu-clips", type=int, default=4)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--augment", choices=["reference", "crop"], default="reference",
                     help="reference = the scripts' default train transform (use_flip=1, "
                          "train_only_non-local_pretrained.py:342-350) on the device; crop = "
@@ -59,11 +61,26 @@ def parse():
     return ap.parse_args()
 
 
-def synth_inputs(args, rank, dev, nvar=2):
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run as a
+    child process (this process has not touched the GPU) and exit with its status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def synth_inputs(args, rank, world, dev, nvar=2):
     B, T, L = args.clips, args.seq, args.lfb
     # LFB geometry of SURVEY.md §8d: 40 videos x 2500 frames
     lengths = [2500] * 40
     from tmrnet_amd.lfb import valid_starts
+    from tmrnet_amd.sampler import ClipSampler
     vs = valid_starts(T, lengths)
     g1 = torch.Generator().manual_seed(1)
     frames = [torch.randint(0, 256, (B * T, 250, 250, 3), generator=g1, dtype=torch.uint8).to(dev)
@@ -74,8 +91,15 @@ def synth_inputs(args, rank, dev, nvar=2):
     steps = args.warmup + args.steps + 2
     g2 = torch.Generator().manual_seed(2 + 1000 * rank)
     offs = torch.randint(0, 27, (steps, B, 2), generator=g2, dtype=torch.int32).to(dev)
-    rng = np.random.default_rng(4 + rank)
-    starts = torch.from_numpy(rng.choice(np.array(vs), size=(steps, B))).to(torch.int64).to(dev)
+    # rank-disjoint clips: one shuffled start list shared by all ranks (seed 4), global batch i
+    # split into per-rank chunks as DataParallel scatters it (tmrnet_amd.sampler.ClipSampler)
+    sampler = ClipSampler(vs, B, rank, world, seed=4)
+    if steps > sampler.steps_per_epoch():
+        raise SystemExit("bench: %d steps exceed one epoch of %d global batches"
+                         % (steps, sampler.steps_per_epoch()))
+    perm = sampler.permutation(0)
+    starts = torch.from_numpy(np.stack([sampler.batch(i, perm=perm) for i in range(steps)]))
+    starts = starts.to(torch.int64).to(dev)
     g5 = torch.Generator().manual_seed(5 + 1000 * rank)
     labels = torch.randint(0, 7, (steps, B), generator=g5).to(dev)
     return frames, bank, vs_d, offs, starts, labels
@@ -83,11 +107,15 @@ def synth_inputs(args, rank, dev, nvar=2):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if args.gpus != world:
+        print("bench: --gpus %d but WORLD_SIZE %d (launch with --nproc-per-node equal to --gpus)"
+              % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
     # rehearsal knobs (a multi-rank run on a one-GPU box): TMR_BENCH_DEVICE pins every rank to
     # one device, TMR_BENCH_DIST_BACKEND=gloo replaces RCCL (which needs one GPU per rank)
     dev = torch.device("cuda", int(os.environ.get("TMR_BENCH_DEVICE", local)))
@@ -104,7 +132,7 @@ def main():
     import tmrnet_amd
     from tmrnet_amd import ops, LFBRows
     from tmrnet_amd.ddp import GradAllReduce
-    from oracle.tmrnet_ref import sgd_param_groups
+    from tmrnet_amd.optim import sgd_param_groups
 
     torch.manual_seed(0)
     if args.model == "resnet50":
@@ -116,10 +144,10 @@ def main():
     opt = tmrnet_amd.SGD(sgd_param_groups(model, lr), lr=lr / 10, momentum=0.9,
                          weight_decay=5e-4)
     crit = tmrnet_amd.CrossEntropyLoss(size_average=False)
-    reducer = GradAllReduce(model, dist) if dist is not None else None
-    if reducer is not None and os.environ.get("TMR_DDP_OVERLAP", "1") != "0":
-        model.share.grad_ready = reducer.grads_ready   # trunk grads exchanged during the backward
-    frames, bank, vs_d, offs, starts, labels = synth_inputs(args, rank, dev)
+    # trunk grads are exchanged block by block during the backward unless TMR_DDP_OVERLAP=0
+    reducer = (GradAllReduce(model, dist, overlap=os.environ.get("TMR_DDP_OVERLAP", "1") != "0")
+               if dist is not None else None)
+    frames, bank, vs_d, offs, starts, labels = synth_inputs(args, rank, world, dev)
     B, T, L = args.clips, args.seq, args.lfb
     from tmrnet_amd.augment import ClipAugment
     aug = ClipAugment(seq_len=T, use_flip=1) if args.augment == "reference" else None
@@ -203,6 +231,17 @@ def main():
                 "step_mfma_frac": round(fps / world * GFLOP_PER_FRAME.get(args.model, 0.0) * 1e9 /
                                         (peak * 1e12), 4)}
 
+    # whole-step HBM fraction: SURVEY.md §8d's activation-traffic model
+    # (4 touches x 32.0 M activation elements per frame x dtype bytes) and the measured PMC bytes
+    # of every kernel of a step (committed profile of this workload), both over the step time
+    act_bytes = 4 * 32.0e6 * (4 if args.precision == "fp32" else 2)
+    hbm = {"model_bytes_per_frame": act_bytes,
+           "model_frac": round(fps / world * act_bytes / (HBM_PEAK_GBS * 1e9), 4),
+           "pmc_bytes_per_step": traffic["all_kernels_bytes_per_step"] if traffic else None,
+           "pmc_frac": (round(traffic["all_kernels_bytes_per_step"] / (ms * 1e-3)
+                              / (HBM_PEAK_GBS * 1e9), 4) if traffic else None),
+           "peak_gbs": HBM_PEAK_GBS}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -228,6 +267,7 @@ def main():
                                            if aug is not None else "crop+normalize")},
             "loss_last": loss_v,
             "roofline": roof,
+            "hbm": hbm,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -262,37 +302,72 @@ def load_traffic(model):
     per_step = sum(fams[k]["hbm_bytes_per_step"]
                    for k in ("gemm_kernel", "wgrad_reduce_kernel", "wgrad_reduce_taps_kernel")
                    if k in fams)
-    return {"hbm_bytes_per_step": per_step, "source": os.path.relpath(files[-1], ROOT)}
+    return {"hbm_bytes_per_step": per_step,
+            "all_kernels_bytes_per_step": sum(f["hbm_bytes_per_step"] for f in fams.values()),
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline.  BASELINE.md §4 asks for os.cpu_count(); on the GPU box
+    that reports the whole host (many times the job's CPU share), so the share is taken from
+    OMP_NUM_THREADS (set to it there) or the affinity mask; os.cpu_count() is reported beside."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline(args):
-    """The CPU oracle (pure-torch restatement of the reference step) on the host cores."""
+    """The CPU oracle (pure-torch restatement of the reference step) on the host cores:
+    BASELINE.md §4 -- C1 (memory-bank model, 4 clips x 10) and the C2 model at 4 clips x 10,
+    L=40, fp32, 2 warm-up + 5 timed steps each."""
     from oracle import tmrnet_ref as ref
-    threads = min(16, os.cpu_count() or 1)
+    from tmrnet_amd.optim import sgd_param_groups
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     B, T, L = args.cpu_clips, args.seq, args.lfb
-    torch.manual_seed(0)
-    m = ref.TMRNetRef(seq_len=T, time_conv=(args.model == "resnest50"),
-                      backbone=args.model).train()
-    opt = torch.optim.SGD(ref.sgd_param_groups(m, 5e-7), lr=5e-8, momentum=0.9, weight_decay=5e-4)
     g = torch.Generator().manual_seed(1)
     frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8)
     off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32)
     lt = torch.rand(B, L, 512, generator=g) * 2 - 1
     labels = torch.randint(0, 7, (B,), generator=g)
+    labels_f = torch.randint(0, 7, (B * T,), generator=g)
 
-    def one():
+    def inputs():
         if args.augment == "reference":
-            x = ref.augment_ref(frames.numpy(), range(B * T), T).view(B, T, 3, 224, 224)
-        else:
-            x = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
-        ref.train_step_ref(m, opt, x, lt, labels)
+            return ref.augment_ref(frames.numpy(), range(B * T), T).view(B, T, 3, 224, 224)
+        return ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
 
-    one()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        one()
-    el = time.perf_counter() - t0
+    def run(model, one):
+        opt = torch.optim.SGD(sgd_param_groups(model, 5e-7), lr=5e-8, momentum=0.9,
+                              weight_decay=5e-4)
+        for _ in range(args.cpu_warmup):
+            one(model, opt)
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            one(model, opt)
+        return B * T * args.cpu_steps / (time.perf_counter() - t0)
+
+    def step_c2(m, opt):   # train_only_non-local_pretrained.py:698-725
+        ref.train_step_ref(m, opt, inputs(), lt, labels)
+
+    def step_c1(m, opt):   # train_singlenet_phase_1fc.py:545-566: CE on outputs[T-1::T]
+        opt.zero_grad()
+        out = m(inputs())[T - 1::T]
+        loss = ref.ce_sum_ref(out, labels_f[T - 1::T])
+        loss.backward()
+        opt.step()
+
+    torch.manual_seed(0)
+    c2 = run(ref.TMRNetRef(seq_len=T, time_conv=(args.model == "resnest50"),
+                           backbone=args.model).train(), step_c2)
+    c1 = None
+    if args.model == "resnet50":
+        torch.manual_seed(0)
+        c1 = run(ref.MemoryBankRef(seq_len=T).train(), step_c1)
     model_name = platform.processor() or "unknown"
     try:
         for l in subprocess.check_output(["lscpu"], text=True).splitlines():
@@ -300,12 +375,14 @@ def cpu_baseline(args):
                 model_name = l.split(":", 1)[1].strip()
     except Exception:
         pass
-    return {"value": round(B * T * args.cpu_steps / el, 3), "unit": "frames/s", "cores": threads,
-            "kind": "port", "cpu": model_name,
-            "sample": "oracle TMRNetRef fp32 train step (%s, fwd, CE-sum, bwd, SGD), "
-                      "%d clips x %d frames, L=%d, %d timed steps after 1 warm-up"
+    return {"value": round(c2, 3), "unit": "frames/s", "cores": threads,
+            "os_cpu_count": os.cpu_count(), "kind": "port", "cpu": model_name,
+            "c1_memory_bank_frames_per_s": round(c1, 3) if c1 is not None else None,
+            "sample": "oracle fp32 train steps on the host (%s, fwd, CE-sum, bwd, SGD): value = C2 "
+                      "model (TMRNetRef) at %d clips x %d frames, L=%d; c1 = memory-bank model "
+                      "(MemoryBankRef) at %d x %d; %d timed steps after %d warm-up each"
                       % ("PIL train transform" if args.augment == "reference" else "crop+norm",
-                         B, T, L, args.cpu_steps)}
+                         B, T, L, B, T, args.cpu_steps, args.cpu_warmup)}
 
 
 if __name__ == "__main__":

@@ -32,6 +32,8 @@ extern "C" {
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
+/* Empty the calling thread's error message (size queries report failure through it). */
+void tmr_clear_error(void);
 
 /* ---------------- convolution / GEMM (gemm_conv.hip) ----------------------
  * Replaces torchvision resnet50's nn.Conv2d fwd/bwd (cuDNN), reached from

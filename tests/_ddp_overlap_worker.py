@@ -20,11 +20,12 @@ def main():
     import tmrnet_amd
     from tmrnet_amd import ops
     from tmrnet_amd.ddp import GradAllReduce
+    from tmrnet_amd.trunk import set_grad_ready
 
     B, T, L = 2, 3, 5
     torch.manual_seed(0)
     m = tmrnet_amd.resnet_lstm(seq_len=T).to(dev).train()
-    red = GradAllReduce(m, dist)
+    red = GradAllReduce(m, dist, overlap=False)
     g = torch.Generator().manual_seed(10 + rank)
     frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
     off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)
@@ -37,7 +38,7 @@ def main():
     launched = []
 
     def grads(overlap):
-        m.share.grad_ready = red.grads_ready if overlap else None
+        set_grad_ready(m.share, red.grads_ready if overlap else None)
         for p in m.parameters():
             p.grad = None
         loss = crit(m(ops.crop_normalize(frames, off, T), lt), labels)

@@ -47,3 +47,28 @@ def test_code_object_targets_gfx950(built):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
     for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
         assert other not in blob
+
+
+def test_argument_errors_raise_with_message(built):
+    """Bad arguments come back as a non-zero status + tmr_last_error() text, raised by the
+    binding as RuntimeError (include/tmr.h contract; checked before any device work)."""
+    import ctypes
+    from tmrnet_amd import _lib
+    with pytest.raises(RuntimeError, match="null descriptor"):
+        _lib.call("tmr_conv2d_fwd", None, None, None, None, None, 0.0, None)
+    d = _lib.ConvDesc(2, 8, 8, 3, 16, 3, 3, 1, 1, 8, 8, 1, 0, 0, 0, 0)   # c=3: not a power of 2
+    with pytest.raises(RuntimeError, match="power of two"):
+        _lib.call("tmr_conv2d_fwd", ctypes.byref(d), None, None, None, None, 0.0, None)
+    d.c, d.math = 4, 7
+    with pytest.raises(RuntimeError, match="bad math mode"):
+        _lib.call("tmr_conv2d_fwd", ctypes.byref(d), None, None, None, None, 0.0, None)
+    with pytest.raises(RuntimeError, match="tmr_bn_ws_bytes"):
+        _lib.query("tmr_bn_ws_bytes", 0, 64)
+    with pytest.raises(RuntimeError, match="tmr_bn_parts_ws_bytes"):
+        _lib.query("tmr_bn_parts_ws_bytes", -1, 64)
+    with pytest.raises(RuntimeError, match="stats_parts"):
+        _lib.query("tmr_conv2d_fwd_stats_parts", None)
+    with pytest.raises(RuntimeError, match="wgrad_ws_bytes"):
+        _lib.query("tmr_conv2d_wgrad_ws_bytes", None)
+    # a good query after a failure is not poisoned by the old message
+    assert _lib.query("tmr_bn_ws_bytes", 1024, 64) > 0

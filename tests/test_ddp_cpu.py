@@ -65,3 +65,52 @@ def test_grad_all_reduce_sum_world2(early):
         assert (g == res[1][0][i]).all()
     for w0, w1 in zip(res[0][1], res[1][1]):
         assert (w0 == w1).all()
+
+
+def _accum_worker(rank, world, port, q):
+    """Two backwards before all_reduce_sum; the early per-block launch of the first must not
+    replace the accumulated gradient (ddp.py overwrote it with micro-batch 2 only)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tmrnet_amd.ddp import GradAllReduce
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(30, 20), torch.nn.Linear(20, 7),
+                            torch.nn.Linear(7, 3))
+    unused = m[2]
+    red = GradAllReduce(m, dist, bucket_bytes=1024, overlap=False)
+    ps = list(m.parameters())[:4]
+    for mb in range(2):          # micro-batches: what TrunkFn.backward + autograd would do
+        local = [torch.full_like(p, float((rank + 1) * (mb + 1) * (i + 1)))
+                 for i, p in enumerate(ps)]
+        red.grads_ready([(p, g) for p, g in zip(ps[2:], local[2:])])
+        for p, g in zip(ps, local):
+            p.grad = g.clone() if p.grad is None else p.grad + g
+    # unused[2]: grad None on both ranks (stays None); weight of layer 3 present on rank 1 only
+    if rank == 1:
+        unused.weight.grad = torch.full_like(unused.weight, 5.0)
+    red.all_reduce_sum()
+    out = [None if p.grad is None else p.grad.numpy().copy() for p in m.parameters()]
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_grad_accumulation_and_none_grads_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        g = res[r]
+        for i in range(4):
+            # sum over ranks (1, 2) of micro-batches (1, 2): (1+2) * (1+2) * (i+1)
+            assert (g[i] == 9.0 * (i + 1)).all(), (r, i, g[i].ravel()[:3])
+        assert (g[4] == 5.0).all()          # present on one rank: the sum, not None
+        assert g[5] is None                 # None everywhere stays None (SGD skips it)

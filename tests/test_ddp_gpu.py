@@ -5,6 +5,7 @@ barrier/max-over-ranks timing and the rank-0 JSON line (train_only_non-local_pre
 DataParallel -> one process per GPU)."""
 import json
 import os
+import socket
 import subprocess
 import sys
 
@@ -15,11 +16,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def test_bench_two_ranks_one_gpu():
+    # plain `bench.py --gpus 2`: bench.py launches its own two ranks (the driver's 1->8 run may
+    # call it without a launcher); rehearsal knobs put both ranks on cuda:0 over gloo
     env = dict(os.environ, TMR_BENCH_DEVICE="0", TMR_BENCH_DIST_BACKEND="gloo",
                HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29547", "bench.py", "--gpus", "2",
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--clips", "2", "--no-cpu-baseline", "--no-roofline"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -36,7 +47,8 @@ def test_overlap_matches_post_backward():
     all-after-backward buckets (a block handed over too early, or skipped, would differ ~2x)."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29548", "tests/_ddp_overlap_worker.py"]
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "tests/_ddp_overlap_worker.py"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [l for l in p.stdout.splitlines() if l.startswith("OVERLAP_REL_DIFF")]

@@ -32,6 +32,7 @@ DP = ctypes.POINTER(ConvDesc)
 SIGNATURES = {
     "tmr_abi_version": [],
     "tmr_last_error": [],
+    "tmr_clear_error": [],
     "tmr_conv2d_fwd": [DP, P, P, P, P, F, P],
     "tmr_conv2d_fwd_fused": [DP, P, P, P, P, P, P, I, P],
     "tmr_conv2d_fwd_stats_parts": [DP],
@@ -97,6 +98,7 @@ SIGNATURES = {
 }
 _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,
+    "tmr_clear_error": None,
     "tmr_conv2d_wgrad_ws_bytes": SZ,
     "tmr_bn_ws_bytes": SZ,
     "tmr_bn_parts_ws_bytes": SZ,
@@ -146,5 +148,13 @@ def call(name, *args):
 
 
 def query(name, *args):
-    fn = getattr(lib(), name)
-    return fn(*[_conv(a) for a in args])
+    """Size / count queries (workspace bytes, partial-row counts).  Integer queries report a
+    bad argument as a negative value; size queries as 0 with tmr_last_error set -- both raise."""
+    h = lib()
+    h.tmr_clear_error()
+    fn = getattr(h, name)
+    v = fn(*[_conv(a) for a in args])
+    err = h.tmr_last_error()
+    if (_RESTYPES.get(name, ctypes.c_int) is ctypes.c_int and v < 0) or err:
+        raise RuntimeError("%s failed (%d): %s" % (name, v, (err or b"").decode()))
+    return v

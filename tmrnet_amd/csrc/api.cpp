@@ -15,4 +15,5 @@ void tmr_set_error(const char* fmt, ...) {
 }
 
 TMR_API const char* tmr_last_error(void) { return g_err; }
+TMR_API void tmr_clear_error(void) { g_err[0] = 0; }
 TMR_API int tmr_abi_version(void) { return TMR_ABI_VERSION; }

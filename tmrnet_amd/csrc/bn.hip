@@ -598,7 +598,13 @@ int ew_blocks(long n4) {
 
 }  // namespace
 
-TMR_API size_t tmr_bn_ws_bytes(int rows, int c) { return ws_need(rows, c); }
+TMR_API size_t tmr_bn_ws_bytes(int rows, int c) {
+  if (rows <= 0 || c < 4 || c % 4) {
+    tmr_set_error("tmr_bn_ws_bytes: bad size (rows %d, channels %d)", rows, c);
+    return 0;
+  }
+  return ws_need(rows, c);
+}
 
 TMR_API int tmr_bn_fwd_stats(const float* y, int rows, int c, const float* gamma,
                              const float* beta, float* running_mean, float* running_var,
@@ -631,7 +637,11 @@ TMR_API int tmr_bn_finalize(const void* partials, int nparts, int c, const float
 }
 
 TMR_API size_t tmr_bn_parts_ws_bytes(int nparts, int c) {
-  return nparts > 0 && c > 0 ? slab_ws_bytes(nparts, c) + (size_t)3 * c * sizeof(float) + 64 : 0;
+  if (nparts <= 0 || c <= 0) {
+    tmr_set_error("tmr_bn_parts_ws_bytes: bad size (parts %d, channels %d)", nparts, c);
+    return 0;
+  }
+  return slab_ws_bytes(nparts, c) + (size_t)3 * c * sizeof(float) + 64;
 }
 
 TMR_API int tmr_bn_finalize_ws(const void* partials, int nparts, int c, const float* gamma,

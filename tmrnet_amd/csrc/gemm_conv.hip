@@ -1202,6 +1202,10 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
 }
 
 TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
+  if (!d || d->n <= 0) {
+    tmr_set_error("tmr_conv2d_fwd_stats_parts: null or empty descriptor");
+    return -1;
+  }
   const int fc = frames_per_launch(d);
   int parts = 0;
   for (int f0 = 0; f0 < d->n; f0 += fc) {
@@ -1322,7 +1326,10 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
 }
 
 TMR_API int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d) {
-  if (!d) return -1;
+  if (!d || d->n <= 0) {
+    tmr_set_error("tmr_conv2d_dgrad_bnbwd_parts: null or empty descriptor");
+    return -1;
+  }
   BnBwdFuse fz{};
   fz.count_only = true;
   if (dgrad_bnbwd_run(d, nullptr, nullptr, nullptr, 1.f, &fz, nullptr)) return -1;
@@ -1382,6 +1389,10 @@ static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* sl
 }
 
 TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
+  if (!d || d->n <= 0 || d->k <= 0 || d->c <= 0 || d->r <= 0 || d->s <= 0) {
+    tmr_set_error("tmr_conv2d_wgrad_ws_bytes: null or empty descriptor");
+    return 0;
+  }
   int sp, kc;
   long slab;
   const tmr_conv_desc c = chunk_desc(d, frames_per_launch(d));   // the largest chunk

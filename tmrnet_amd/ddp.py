@@ -5,14 +5,29 @@ every clip's gradient onto cuda:0 because the loss is CrossEntropyLoss(reduction
 global batch, so the exchange here is a SUM (DDP's default would average).  BN statistics stay
 per rank, as DP's per-replica BN does.  Gradients are packed into ~25 MB buckets (few, large
 collectives suit the per-link-bound xGMI ring) and reduced with the "nccl" (= RCCL) backend.
-The trunk's gradients are launched block by block from inside its backward (grads_ready), so
-their exchange overlaps the remaining backward; the rest go in buckets after the backward.
+
+Overlap: with ``overlap=True`` the reducer registers itself with the model's trunk
+(``trunk.set_grad_ready``), which hands over each bottleneck block's final gradients from inside
+its backward, deepest block first; their all-reduce then runs while the rest of the backward
+does.  The hook is kept in a weak side table, not on the module, so ``copy.deepcopy(model)`` and
+``torch.save(model)`` are unaffected.
+
+Semantics kept from torch.optim + DataParallel:
+* gradient accumulation (several backwards before ``all_reduce_sum``): an early launch is used
+  only when it is exact -- the parameter had no gradient before this backward and no second
+  backward touched it since; otherwise the accumulated ``p.grad`` goes through the buckets;
+* ``p.grad is None`` stays None when it is None on every rank (torch.optim.SGD then skips the
+  parameter); a presence flag per parameter rides in the same bucket, so no extra collective.
 """
 import torch
 
+_flatten = torch._utils._flatten_dense_tensors
+_unflatten = torch._utils._unflatten_dense_tensors
+
 
 class GradAllReduce:
-    def __init__(self, model, dist, bucket_bytes=25 * 1024 * 1024, broadcast_init=True):
+    def __init__(self, model, dist, bucket_bytes=25 * 1024 * 1024, broadcast_init=True,
+                 overlap=True):
         self.dist = dist
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.buckets = []
@@ -31,41 +46,82 @@ class GradAllReduce:
                     dist.broadcast(p, 0)
                 for b in model.buffers():
                     dist.broadcast(b, 0)
+        self.early = []         # (params, flat, handle) launched during the backward
+        self.early_ids = set()  # params whose reduced gradient an early launch will deliver
+        self.stale_ids = set()  # early-launched params touched again by a later backward
+        self.overlap = bool(overlap) and self._multi()
+        share = getattr(model, "share", None)
+        if self.overlap and share is not None:
+            from .trunk import set_grad_ready
+            set_grad_ready(share, self.grads_ready)
 
-        self.early = []         # (params, grads, flat, handle) launched during the backward
-        self.early_ids = set()
+    def _multi(self):
+        return self.dist is not None and self.dist.get_world_size() > 1
 
     def grads_ready(self, pairs):
         """Launch the SUM of some final gradients while the backward is still running.
 
-        `pairs` = [(param, grad)] whose grads no later backward work touches (the trunk calls this
-        once per bottleneck block, deepest first, TrunkFn.backward).  The grads are packed into a
-        fresh buffer on the compute stream, so autograd may still steal or clone them into
-        `p.grad`; all_reduce_sum() waits and copies the reduced values into `p.grad`."""
-        if self.dist is None or self.dist.get_world_size() == 1 or not pairs:
+        `pairs` = [(param, grad)]: this backward's gradient of each param, final for this
+        backward (the trunk calls this once per bottleneck block, TrunkFn.backward).  The grads
+        are packed into a fresh buffer on the compute stream, so autograd may still steal them
+        into `p.grad`; all_reduce_sum() waits and installs the reduced values.  Every rank runs
+        the same sequence of backwards, so the launch decisions below agree across ranks."""
+        if not self._multi() or not pairs:
             return
         params = [p for p, _ in pairs]
-        grads = [g for _, g in pairs]
-        flat = torch._utils._flatten_dense_tensors(grads)
-        self.early.append((params, grads, flat, self.dist.all_reduce(flat, async_op=True)))
-        self.early_ids.update(id(p) for p in params)
+        ids = [id(p) for p in params]
+        # a second backward before all_reduce_sum: the earlier launch holds one micro-batch only
+        if any(i in self.early_ids for i in ids):
+            self.stale_ids.update(i for i in ids if i in self.early_ids)
+            return
+        # accumulating into an existing gradient: the launch would miss the earlier part
+        if any(p.grad is not None for p in params):
+            return
+        flat = _flatten([g for _, g in pairs])
+        self.early.append((params, flat, self.dist.all_reduce(flat, async_op=True)))
+        self.early_ids.update(ids)
+
+    def reset(self):
+        """Drop (after waiting for) early launches of a backward that is not being reduced."""
+        for _, _, h in self.early:
+            h.wait()
+        self.early, self.early_ids, self.stale_ids = [], set(), set()
 
     def all_reduce_sum(self):
-        if self.dist is None or self.dist.get_world_size() == 1:
+        if not self._multi():
             return
-        handles, early, done = [], self.early, self.early_ids
-        self.early, self.early_ids = [], set()
+        early, stale = self.early, self.stale_ids
+        done = self.early_ids - stale
+        self.early, self.early_ids, self.stale_ids = [], set(), set()
+        handles = []
         for bucket in self.buckets:
             bucket = [p for p in bucket if id(p) not in done]
             if not bucket:
                 continue
             grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
-            flat = torch._utils._flatten_dense_tensors(grads)
-            handles.append((bucket, grads, flat, self.dist.all_reduce(flat, async_op=True)))
-        for bucket, grads, flat, h in early + handles:
+            local = [p.grad is not None for p in bucket]
+            if all(local):   # the common case: no host round trip
+                present = torch.ones(len(bucket), dtype=grads[0].dtype, device=grads[0].device)
+            else:
+                present = torch.tensor([float(v) for v in local],
+                                       dtype=grads[0].dtype).to(grads[0].device)
+            flat = _flatten(grads + [present])
+            handles.append((bucket, grads + [present], flat, all(local),
+                            self.dist.all_reduce(flat, async_op=True)))
+        for params, flat, h in early:
             h.wait()
-            for p, g in zip(bucket, torch._utils._unflatten_dense_tensors(flat, grads)):
-                if p.grad is None:
+            for p, g in zip(params, _unflatten(flat, params)):
+                if id(p) not in stale:          # stale ones were reduced again from p.grad
+                    p.grad = g
+        for bucket, like, flat, all_local, h in handles:
+            h.wait()
+            outs = _unflatten(flat, like)
+            # every local grad present -> every sum >= 1; read the flags only otherwise
+            present = [1.0] * len(bucket) if all_local else outs[-1].tolist()
+            for p, g, n in zip(bucket, outs[:-1], present):
+                if n == 0:
+                    p.grad = None                   # no rank produced a gradient
+                elif p.grad is None:
                     p.grad = g
                 else:
                     p.grad.copy_(g)

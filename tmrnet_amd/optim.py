@@ -86,3 +86,27 @@ class SGD(torch.optim.Optimizer):
         self._keep = keep        # contiguous grad copies stay alive until the next step
         call("tmr_sgd_step_multi", self._table_dev, len(entries), int(nblk.sum()), stream_ptr(dev))
         return loss
+
+
+def sgd_param_groups(model, lr):
+    """Parameter groups of the reference's multi_optim=1 optimizer: `share` and `lstm` at the
+    optimizer's default lr (the scripts pass lr/10), every later module at `lr`.
+
+    train_only_non-local_pretrained.py:646-655 (share, lstm, nl_block, fc_h_c, fc_c);
+    train_non-local_mutiConv_resnet.py:797-804 and the resnest twin add `time_conv` at `lr`
+    between lstm and nl_block.  The memory-bank model (`fc` head,
+    Training memory bank model/train_singlenet_phase_1fc.py:498-501) puts lstm and fc at `lr`.
+    Use as ``SGD(sgd_param_groups(model, lr), lr=lr / 10, ...)``.
+    """
+    if hasattr(model, "fc") and not hasattr(model, "nl_block"):
+        # memory-bank model, train_singlenet_phase_1fc.py:498-501: only `share` at lr/10
+        return [{"params": list(model.share.parameters())},
+                {"params": list(model.lstm.parameters()), "lr": lr},
+                {"params": list(model.fc.parameters()), "lr": lr}]
+    groups = [{"params": list(model.share.parameters())},
+              {"params": list(model.lstm.parameters())}]
+    if getattr(model, "time_conv", None) is not None:
+        groups.append({"params": list(model.time_conv.parameters()), "lr": lr})
+    for name in ("nl_block", "fc_h_c", "fc_c"):
+        groups.append({"params": list(getattr(model, name).parameters()), "lr": lr})
+    return groups

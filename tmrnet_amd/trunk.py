@@ -16,6 +16,7 @@ for normalisation, running stats updated with momentum and the unbiased
 variance, num_batches_tracked += 1; eval mode uses running stats.
 """
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -52,6 +53,23 @@ def _make_layer(inplanes, planes, blocks, stride):
 
 
 # --------------------------------------------------------------------- engine
+# share module -> callable(pairs) told each block's final gradients during the backward
+# (ddp.GradAllReduce registers itself here).  A weak side table rather than a module attribute,
+# so deepcopy / torch.save of the model never see the reducer or its process group.
+_GRAD_READY = weakref.WeakKeyDictionary()
+
+
+def set_grad_ready(share, fn):
+    """Register (fn) or clear (None) the per-block gradient hook of a trunk module."""
+    if fn is None:
+        _GRAD_READY.pop(share, None)
+    else:
+        _GRAD_READY[share] = fn
+
+
+def get_grad_ready(share):
+    return _GRAD_READY.get(share, getattr(share, "grad_ready", None))
+
 def _bn_momentum(bn):
     if bn.momentum is None:
         raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative average) is not supported")
@@ -222,7 +240,7 @@ class TrunkFn(torch.autograd.Function):
         blocks = ctx.blocks
         fuse = os.environ.get("TMR_FUSE_BN_BWD", "1") != "0"
         pending = None     # BN-backward partials of g when the dgrad that produced it was fused
-        ready = getattr(ctx.share, "grad_ready", None)   # ddp.GradAllReduce.grads_ready, or None
+        ready = get_grad_ready(ctx.share)   # ddp.GradAllReduce.grads_ready, or None
         while blocks:
             blk, brec = blocks.pop()
             has_ds = blk.downsample is not None
