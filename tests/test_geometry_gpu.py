@@ -1,0 +1,231 @@
+"""Parity at the benchmarked geometry (BASELINE.json configs C2 and C5), not only at B=2, T=3.
+
+* C2 geometry, oracle-checked: T=10, L=40, B=2 (20 frames per BN batch), train mode with the
+  dropout masks injected on both sides -- logits within 1e-4 and identical argmax, then every
+  parameter gradient against a float64 run of the oracle.
+* C5 geometry at bf16, oracle-checked: T=30, L=300, LFB rows served from a resident bank, B=1.
+* The full C2 step (64 clips x 10 frames, L=40, bank rows), property-checked: the oracle cannot
+  run 640 frames in seconds, so the checks are size-independent identities of the step.
+
+Gradient criterion: tests/test_model_parity_gpu._assert_vs_fp64 -- scale-free against the fp32
+CPU oracle's own distance from float64, no absolute floor (measured here: the head/LSTM/NL
+gradients agree to ~1e-5, the stem's to 1.5-2.2e-2 for the fp32 oracle itself, 20 frames per BN
+batch; HIP/oracle aggregate error ratio 1.16-1.21).  The bf16 test adds an explicit allowance per
+head ReLU flip, counted exactly.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import tmrnet_amd
+from tmrnet_amd import ops, LFBRows
+from oracle import tmrnet_ref as ref
+from tests.test_model_parity_gpu import (_assert_vs_fp64, _double_copy, _inputs, l2_err,
+                                         GRAD_RATIO)
+
+pytestmark = pytest.mark.gpu
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+
+
+def _record(name, data):
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, "geometry_%s.json" % name), "w") as f:
+        json.dump(data, f, indent=1)
+
+
+def _check_grads(ours, r32, r64, what, slack=0.0):
+    """tests/test_model_parity_gpu._assert_vs_fp64 (GRAD_RATIO / AGG_RATIO), plus a record of
+    every parameter's errors."""
+    _record(what, {"rows": [(n, l2_err(t, r64[n]), l2_err(r32[n], r64[n]))
+                            for n, t in ours.items()]})
+    _assert_vs_fp64(ours, r32, r64, what, slack=slack)
+
+
+def _masks(B, seed):
+    g = torch.Generator().manual_seed(seed)
+    return {"nl": (torch.rand(B, 512, generator=g) >= 0.2).float() / 0.8,
+            "head": (torch.rand(B, 512, generator=g) >= 0.5).float() / 0.5}
+
+
+def _bank_rows(B, L, T, seed, nvid=3, vlen=None):
+    """A small resident bank with the reference's row rule (get_long_feature, :293-311)."""
+    vlen = vlen or (L + 2 * T)
+    lengths = [vlen] * nvid
+    vs = ref.get_useful_start_idx(T, lengths)
+    g = torch.Generator().manual_seed(seed)
+    bank = torch.rand(len(vs), 512, generator=g) * 2 - 1
+    pick = torch.randint(0, len(vs), (B,), generator=g)
+    starts = torch.tensor([vs[i] for i in pick.tolist()], dtype=torch.int64)
+    rows = torch.from_numpy(np.asarray(ref.lfb_index_table(starts.numpy(), vs, L), dtype=np.int64))
+    return bank, vs, starts, rows
+
+
+def test_c2_geometry_step_parity(dev):
+    """T=10, L=40, B=2: logits, loss, gradients and running statistics vs the oracle."""
+    B, T, L = 2, 10, 40
+    torch.manual_seed(11)
+    m = tmrnet_amd.resnet_lstm(seq_len=T).to(dev).train()
+    r = ref.TMRNetRef(seq_len=T).train()
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    r64 = _double_copy(r, None, B, T, L)
+    frames, off, _, labels = _inputs(B, T, L, seed=12)
+    bank, vs, starts, rows = _bank_rows(B, L, T, 13)
+    lt = bank[rows.view(-1)].view(B, L, 512)
+    masks = _masks(B, 14)
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    rows_d = ops.lfb_index(torch.tensor(vs, dtype=torch.int64, device=dev), starts.to(dev), L)
+    assert torch.equal(rows_d.cpu().long(), rows)
+    out = m(x4, LFBRows(bank.to(dev), rows_d))
+    x_ref = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
+    out_r = r(x_ref, lt, masks=masks)
+    out64 = r64(x_ref.double(), lt.double(), masks={k: v.double() for k, v in masks.items()})
+    err = (out.detach().cpu() - out_r.detach()).abs().max().item()
+    assert err < 1e-4, err
+    assert torch.equal(out.detach().cpu().argmax(1), out_r.argmax(1))
+    crit = tmrnet_amd.CrossEntropyLoss(size_average=False)
+    loss = crit(out, labels.to(dev))
+    loss_r = ref.ce_sum_ref(out_r, labels)
+    assert abs(loss.item() - loss_r.item()) <= 1e-5 * max(1.0, abs(loss_r.item()))
+    loss.backward()
+    loss_r.backward()
+    ref.ce_sum_ref(out64, labels).backward()
+    g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
+    _check_grads(g(m), g(r), g(r64), "c2_grads")
+    rb = dict(r.named_buffers())
+    for name, b in m.named_buffers():
+        if b.dtype.is_floating_point:
+            assert l2_err(b, rb[name]) < 1e-5, name
+        else:
+            assert torch.equal(b.cpu(), rb[name]), name
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_c5_geometry_step(dev, prec):
+    """T=30, L=300 (C5), LFB rows from a resident bank, B=1 (30 frames); C5 runs bf16 conv
+    operands, the fp32 run of the same geometry is held to the strict bound."""
+    B, T, L = 1, 30, 300
+    torch.manual_seed(21)
+    m = tmrnet_amd.resnet_lstm(seq_len=T, precision=prec).to(dev).train()
+    r = ref.TMRNetRef(seq_len=T, precision=prec).train()
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    r64 = _double_copy(r, None, B, T, L)
+    frames, off, _, labels = _inputs(B, T, L, seed=22)
+    bank, vs, starts, rows = _bank_rows(B, L, T, 23, nvid=2, vlen=2 * L)
+    lt = bank[rows.view(-1)].view(B, L, 512)
+    masks = _masks(B, 24)
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+    out = m(x4, LFBRows(bank.to(dev), rows.to(torch.int32).to(dev)))
+    x_ref = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
+    out_r = r(x_ref, lt, masks=masks)
+    out64 = r64(x_ref.double(), lt.double(), masks={k: v.double() for k, v in masks.items()})
+    e_hip = (out.detach().cpu().double() - out64.detach()).abs().max().item()
+    e_cpu = (out_r.detach().double() - out64.detach()).abs().max().item()
+    _record("c5_%s_logits" % prec, {"e_hip": e_hip, "e_cpu": e_cpu})
+    # bf16 rounding flips (fp32 summation order decides a tie-near rounding now and then) set the
+    # scale; the bound is the same scale-free one as the gradients'
+    assert e_hip <= GRAD_RATIO * e_cpu + 1e-5, (e_hip, e_cpu)
+    top2 = out64.detach().topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 2 * max(e_hip, e_cpu)
+    assert torch.equal(out.detach().cpu().argmax(1)[sure], out64.detach().argmax(1)[sure])
+    tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels.to(dev)).backward()
+    ref.ce_sum_ref(out_r, labels).backward()
+    ref.ce_sum_ref(out64, labels).backward()
+    g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
+    # Head ReLU flips.  With bf16 operands both fp32 implementations sit ~2e-2 from float64 on
+    # the logits (chaotic rounding flips through 30-frame batch-stat BN), so a pre-ReLU head unit
+    # h_j within that distance of 0 can take the other sign: its whole gradient da_j is then kept
+    # or dropped.  fc_h_c.bias.grad IS dh, so a zero-pattern mismatch against float64 (dropout
+    # zeros are shared) counts the flips exactly.  One flip among 512 units measured 0.15
+    # relative-L2 on every gradient downstream of it (fc_h_c, NLBlock, LSTM; the fp32 run of the
+    # same geometry has none and meets the strict bound).  Each counted flip buys 0.2 slack.
+    dh, dh64 = m.fc_h_c.bias.grad.cpu(), r64.fc_h_c.bias.grad
+    flips = int(((dh == 0) != (dh64 == 0)).sum())
+    assert flips <= (2 if prec == "bf16" else 0), flips
+    _check_grads(g(m), g(r), g(r64), "c5_%s_grads" % prec, slack=0.2 * flips)
+
+
+def _stem_stats64(x4, w, chans):
+    """float64 batch mean / unbiased variance of the stem conv output (7x7/2, pad 3) for a few
+    output channels, by im2col in frame chunks (share.conv1 -> share.bn1, :204-205)."""
+    F_ = x4.shape[0]
+    w64 = w[chans].double()                                   # (c, 3, 7, 7)
+    s1 = torch.zeros(len(chans), dtype=torch.float64)
+    s2 = torch.zeros(len(chans), dtype=torch.float64)
+    n = 0
+    for f0 in range(0, F_, 32):
+        xb = x4[f0:f0 + 32, :, :, :3].permute(0, 3, 1, 2).double()
+        y = torch.nn.functional.conv2d(xb, w64, stride=2, padding=3)   # (f, c, 112, 112)
+        s1 += y.sum(dim=(0, 2, 3))
+        n += y.shape[0] * y.shape[2] * y.shape[3]
+    mean = s1 / n
+    for f0 in range(0, F_, 32):
+        xb = x4[f0:f0 + 32, :, :, :3].permute(0, 3, 1, 2).double()
+        y = torch.nn.functional.conv2d(xb, w64, stride=2, padding=3)
+        s2 += ((y - mean[None, :, None, None]) ** 2).sum(dim=(0, 2, 3))
+    return mean, s2 / (n - 1)
+
+
+def test_c2_full_step_properties(dev):
+    """The benchmarked C2 step itself: 64 clips x 10 frames, L=40, rows from a bank of §8d's
+    geometry (40 videos x 2500 frames), the reference train transform on the device."""
+    from tmrnet_amd.augment import ClipAugment
+    from tmrnet_amd.lfb import valid_starts
+    from tmrnet_amd.sampler import ClipSampler
+    B, T, L = 64, 10, 40
+    torch.manual_seed(0)
+    m = tmrnet_amd.resnet_lstm(seq_len=T).to(dev).train()
+    w_stem = m.share.conv1.weight.detach().cpu().clone()
+    vs = valid_starts(T, [2500] * 40)
+    g = torch.Generator().manual_seed(3)
+    bank = (torch.rand(len(vs), 512, generator=g) * 2 - 1).to(dev)
+    starts = torch.from_numpy(ClipSampler(vs, B, seed=4).batch(0)).to(dev)
+    rows = ops.lfb_index(torch.tensor(vs, dtype=torch.int64, device=dev), starts, L)
+    # the device row table against the reference rule on the host
+    exp = ref.lfb_index_table(starts.cpu().numpy(), vs, L)
+    assert np.array_equal(rows.cpu().numpy(), np.asarray(exp))
+    g1 = torch.Generator().manual_seed(1)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g1, dtype=torch.uint8).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=torch.Generator().manual_seed(5)).to(dev)
+    x4 = ClipAugment(seq_len=T, use_flip=1)(frames)
+    masks = _masks(B, 6)
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    out = m(x4, LFBRows(bank, rows))
+    # (1) stem BatchNorm running statistics (momentum 0.1 from mean 0 / var 1) against float64
+    chans = [0, 17, 42, 63]
+    rm = m.share.bn1.running_mean.detach().cpu().double()[chans]
+    rv = m.share.bn1.running_var.detach().cpu().double()[chans]
+    mean64, var64 = _stem_stats64(x4.cpu(), w_stem, chans)
+    assert ((rm - 0.1 * mean64).abs() <= 1e-5 * (0.1 * mean64).abs().max() + 1e-7).all(), (rm, mean64)
+    assert ((rv - (0.9 + 0.1 * var64)).abs() <= 1e-5 * rv.abs()).all(), (rv, var64)
+    # (2) CE-sum equals float64 CE recomputed from the GPU logits; (3) its gradient reaches fc_c
+    # as sum_b (softmax_b - onehot_b) (the bias gradient, exact up to fp32 rounding)
+    loss = tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels)
+    o64 = out.detach().cpu().double()
+    lab = labels.cpu()
+    ce64 = (torch.logsumexp(o64, 1) - o64[torch.arange(B), lab]).sum().item()
+    assert abs(loss.item() - ce64) <= 1e-5 * abs(ce64)
+    loss.backward()
+    p64 = torch.softmax(o64, 1)
+    p64[torch.arange(B), lab] -= 1
+    db = m.fc_c.bias.grad.detach().cpu().double()
+    assert (db - p64.sum(0)).abs().max().item() <= 1e-5
+    bad = [n for n, p in m.named_parameters() if p.grad is None or not torch.isfinite(p.grad).all()]
+    assert not bad, bad
+    # every trunk parameter receives a non-trivial gradient
+    zero = [n for n, p in m.named_parameters() if n.startswith("share") and
+            p.grad.abs().max().item() == 0]
+    assert not zero, zero
+    # (4) rows served from the resident bank == the dense gather (:293-313) through the model
+    m.eval()
+    with torch.no_grad():
+        o_rows = m(x4, LFBRows(bank, rows))
+        o_dense = m(x4, ops.lfb_gather(bank, rows))
+    assert torch.equal(o_rows, o_dense)

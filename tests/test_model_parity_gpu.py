@@ -137,7 +137,7 @@ def test_tmrnet_step_parity(dev, train):
                 masks={k: v.double() for k, v in masks.items()})
     ref.ce_sum_ref(out64, labels).backward()
     g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
-    _assert_vs_fp64(g(m), g(r), g(m64), 2e-3, "grad")
+    _assert_vs_fp64(g(m), g(r), g(m64), "grad")
     # running statistics after one train-mode forward
     rb = dict(r.named_buffers())
     for name, b in m.named_buffers():
@@ -155,16 +155,46 @@ def l2_err(a, b, scale=None):
     return ((a - b).norm() / ((b.norm() if scale is None else scale) + 1e-30)).item()
 
 
-def _assert_vs_fp64(ours, ref32, ref64, floor, what, scales=None):
-    """HIP result no further (relative L2) from the float64 oracle than 3x the fp32 CPU oracle
-    is, or `floor`.  At random init with a handful of frames per BN batch the trunk gradients
-    are ill-conditioned: the fp32 CPU oracle itself is ~2% (L2) away from float64 there, so a
-    fixed tight tolerance against the fp32 oracle would test rounding noise, not correctness."""
+GRAD_RATIO = 4.0      # per parameter: e_hip <= GRAD_RATIO * e_cpu + 1e-5 (+ slack)
+AGG_RATIO = 1.5       # all parameters: sqrt(sum e_hip^2 / sum e_cpu^2) <= AGG_RATIO
+
+
+def _assert_vs_fp64(ours, ref32, ref64, what, scales=None, slack=0.0, record=None):
+    """HIP result vs the float64 oracle, scaled by the fp32 CPU oracle's own distance from it.
+
+    At random init the trunk gradients are ill-conditioned in fp32 whatever the BN batch: each
+    Bottleneck's BatchNorm backward (a projection with cancellation) multiplies the relative
+    error, so the fp32 CPU oracle is ~1e-5 from float64 at the head but 1-2e-2 at the stem
+    (measured at B=2, T=3 and at the benchmarked B=2, T=10, tests/test_geometry_gpu.py).  A
+    fixed tolerance would test fp32 rounding noise at the stem or be loose at the head, so the
+    bound is scale-free and has no absolute floor: taken together the HIP gradients may be no
+    further from float64 than AGG_RATIO x the fp32 oracle (measured 1.16-1.21), and no single
+    parameter further than GRAD_RATIO x (+1e-5 relative; a per-parameter ratio is a ratio of two
+    noisy errors, and the CPU oracle accumulates BN reductions in double where the kernels use
+    fp32 tiles: measured worst 1.3-3.6).  `slack` adds an explicit allowance (bf16 head ReLU
+    flips, tests/test_geometry_gpu.py)."""
+    import inspect
+    import json
     scales = scales or {}
+    rows, bad = [], []
     for name, t in ours.items():
         e_hip = l2_err(t, ref64[name], scales.get(name))
         e_cpu = l2_err(ref32[name], ref64[name], scales.get(name))
-        assert e_hip < max(floor, 3 * e_cpu), (what, name, e_hip, e_cpu)
+        rows.append((name, e_hip, e_cpu))
+        if not e_hip <= GRAD_RATIO * e_cpu + 1e-5 + slack:
+            bad.append((name, e_hip, e_cpu))
+    # a parameter whose exact gradient is 0 (nl_block.linear2.bias: the q.b2 score term is
+    # constant over the LFB rows and cancels in the softmax) has no relative error
+    agg_rows = [r for r in rows if not r[0].endswith("linear2.bias") or r[0] in scales]
+    agg = (sum(h * h for _, h, _ in agg_rows) / max(sum(c * c for _, _, c in agg_rows), 1e-300)) ** 0.5
+    rec = {"test": record or inspect.stack()[1].function, "what": what, "slack": slack,
+           "max_ratio": max(h / max(c, 1e-12) for _, h, c in agg_rows), "agg_ratio": agg}
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out, exist_ok=True)     # scratch record of the measured ratios
+    with open(os.path.join(out, "grad_ratios.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
+    assert not bad, (what, bad[:5])
+    assert agg <= AGG_RATIO, (what, agg)
 
 
 def test_sgd_step_after_backward_parity(dev):
@@ -199,7 +229,7 @@ def test_sgd_step_after_backward_parity(dev):
     # compare the parameter UPDATES (p - p0) against the float64 trajectory
     upd = lambda named: {n: p.detach().cpu().double() - p0[n] for n, p in named}
     _assert_vs_fp64(upd(m.named_parameters()), upd(r.named_parameters()),
-                    upd(r64.named_parameters()), 2e-3, "update")
+                    upd(r64.named_parameters()), "update")
 
 
 def test_memory_bank_model_parity(dev):
@@ -226,7 +256,7 @@ def test_memory_bank_model_parity(dev):
     out64 = r64(x_ref.double(), mask=mask.double())
     ref.ce_sum_ref(out64[T - 1::T], labels).backward()
     g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
-    _assert_vs_fp64(g(m), g(r), g(r64), 2e-3, "grad")
+    _assert_vs_fp64(g(m), g(r), g(r64), "grad")
 
 
 def test_timeconv_golden(dev):
