@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 1
+#define TMR_ABI_VERSION 2
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
@@ -320,21 +320,98 @@ int tmr_mask_relu_bwd(const float* da, const float* a, const float* mask, float*
 int tmr_mul(const float* a, const float* b, const float* scalar, float* out, long n,
             hipStream_t stream);
 
-/* ---------------- NLBlock attention core (head.hip) -------------------------
+/* ---------------- NLBlock attention core (nlblock.hip) ----------------------
  * NLBlock_MutiConv6_3.py:28-34 in GEMV form.  With q = linear1(St) and
  * u = W2^T q, the reference scores q.(W2 Lt_l + b2) equal Lt_l.u + q.b2; the
  * q.b2 term is constant over l and cancels in the softmax, so
  *   p_l = softmax_l(scale * Lt_l . u),  ctx = sum_l p_l Lt_l,
  * and SLL = linear3 applied to ctx (sum_l p_l = 1).  Lt rows come either from a
  * dense (B,L,D) tensor (rows == NULL) or straight from the resident LFB bank via
- * the row table (lt = bank, rows = tmr_lfb_index output). */
+ * the row table (lt = bank, rows = tmr_lfb_index output).  Each clip's L rows are
+ * split over 32-row workgroups (one read of Lt per pass) and combined in a fixed
+ * order.  d = 256, 512 or 1024; ws >= tmr_nl_attn_ws_bytes(b, l, d). */
+size_t tmr_nl_attn_ws_bytes(int b, int l, int d);
 int tmr_nl_attn_fwd(const float* lt, const int32_t* rows, const float* u, float* p, float* ctx,
-                    int b, int l, int d, float scale, hipStream_t stream);
+                    int b, int l, int d, float scale, void* ws, size_t ws_bytes,
+                    hipStream_t stream);
 /* given dctx: dp_l = dctx.Lt_l; ds_l = scale*p_l*(dp_l - sum_k p_k dp_k);
  * ut = sum_l ds_l Lt_l (= dL/du); dlt (optional, dense Lt only) = p_l*dctx + ds_l*u */
 int tmr_nl_attn_bwd(const float* lt, const int32_t* rows, const float* u, const float* p,
                     const float* dctx, float* ut, float* dlt, int b, int l, int d, float scale,
-                    hipStream_t stream);
+                    void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* ---------------- module-level entry points (nlblock.hip, lstm.hip) ---------
+ * The reference's module ops as single C calls, for callers without Python.
+ * "saved" buffers carry what the forward keeps for the backward (caller-owned, opaque, sized by
+ * the *_saved_bytes query); "ws" is scratch (*_ws_bytes).  Weights/grads in the reference's
+ * torch layouts (nn.Linear (out, in), nn.Conv1d (out, in, k), nn.LSTM (4H, I) / (4H, H)). */
+
+/* nn.Linear (train_only_non-local_pretrained.py:216-217, NLBlock_MutiConv6_3.py:13-16):
+ * y = x W^T + b (bias may be NULL); backward dx = dy W, dw = beta*dw + dy^T x,
+ * db = beta*db + colsum(dy); dx / dw / db may each be NULL. */
+int tmr_linear_fwd(const float* x, int rows, int in, int out, const float* w, const float* bias,
+                   float* y, hipStream_t stream);
+int tmr_linear_bwd(const float* dy, const float* x, int rows, int in, int out, const float* w,
+                   float* dx, float* dw, float* db, float beta, hipStream_t stream);
+
+/* NLBlock(512) forward/backward (NLBlock_MutiConv6_3.py:10-40; called at
+ * train_only_non-local_pretrained.py:235).  St (b,512), Lt dense (b,l,512) or bank rows
+ * (lt = bank, rows = (b,l) int32), mask = the Dropout(0.2) mask already scaled by 1/0.8 (NULL in
+ * eval).  out = St + dropout(linear4(relu(LN(linear3(attn(St, Lt)))))).  The backward writes
+ * dSt, every parameter gradient (dL/db2 = 0 exactly: q.b2 cancels in the softmax) and, for a
+ * dense Lt only, dLt (may be NULL). */
+typedef struct tmr_nlblock_weights {
+  const float *w1, *b1, *w2, *b2, *w3, *b3, *ln_w, *ln_b, *w4, *b4;
+} tmr_nlblock_weights;
+typedef struct tmr_nlblock_grads {
+  float *w1, *b1, *w2, *b2, *w3, *b3, *ln_w, *ln_b, *w4, *b4;
+} tmr_nlblock_grads;
+size_t tmr_nlblock_saved_bytes(int b, int l);
+size_t tmr_nlblock_ws_bytes(int b, int l);
+int tmr_nlblock_fwd(const tmr_nlblock_weights* w, const float* st, const float* lt,
+                    const int32_t* rows, int b, int l, const float* mask, float* out, void* saved,
+                    size_t saved_bytes, void* ws, size_t ws_bytes, hipStream_t stream);
+int tmr_nlblock_bwd(const tmr_nlblock_weights* w, const float* dout, const float* st,
+                    const float* lt, const int32_t* rows, int b, int l, const float* mask,
+                    const void* saved, size_t saved_bytes, float* dst, float* dlt,
+                    const tmr_nlblock_grads* g, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* TimeConv forward / weight gradient (NLBlock_MutiConv6_3.py:43-79, any L; called at
+ * train_non-local_mutiConv_resnet.py:246): x (b,l,512) -> max(x, conv3, conv5, conv7,
+ * maxpool2(pad_left0 x)); weights Conv1d (512,512,k) + bias for k = 3, 5, 7.  The backward writes
+ * the six parameter gradients and, when dx != NULL, dL/dx (the reference never needs it: the LFB
+ * is constant). */
+size_t tmr_timeconv_saved_bytes(int b, int l);
+size_t tmr_timeconv_ws_bytes(int b, int l);
+int tmr_timeconv_fwd(const float* x, int b, int l, const float* w3, const float* b3,
+                     const float* w5, const float* b5, const float* w7, const float* b7,
+                     float* out, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
+                     hipStream_t stream);
+int tmr_timeconv_wgrad(const float* dy, const float* x, int b, int l, const float* w3,
+                       const float* w5, const float* w7, const void* saved, size_t saved_bytes,
+                       float* dx, float* dw3, float* db3, float* dw5, float* db5, float* dw7,
+                       float* db7, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* nn.LSTM(i, h, batch_first=True) forward / BPTT (train_only_non-local_pretrained.py:215,
+ * :230-231; gates i,f,g,o).  x (b,t,i) -> y (b,t,h); hn, cn (b,h) may be NULL; saved NULL =
+ * inference.  Forward: x W_ih^T + b_ih + b_hh for all b*t frames in one GEMM, then the t-step
+ * recurrence (gate GEMM h W_hh^T + sigma/tanh + cell update) in ONE persistent cooperative
+ * launch (h = 512; per-step launches otherwise, or when the grid would not be resident).  The
+ * backward likewise runs BPTT in one launch, then dW_ih, dW_hh, dx (may be NULL) as GEMMs and
+ * db_ih = db_hh = colsum(dgates).  dy = dL/dy for every step (zeros where unused). */
+size_t tmr_lstm_saved_bytes(int b, int t, int h);
+size_t tmr_lstm_ws_bytes(int b, int t, int i, int h);
+int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float* w_ih,
+                 const float* w_hh, const float* b_ih, const float* b_hh, float* y, float* hn,
+                 float* cn, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
+                 hipStream_t stream);
+int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, int h, const float* w_ih,
+                 const float* w_hh, const float* y, const void* saved, size_t saved_bytes,
+                 float* dx, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, void* ws,
+                 size_t ws_bytes, hipStream_t stream);
+/* timeout word of the last persistent LSTM launch on ws (0 = every grid barrier completed);
+ * synchronises the stream */
+int tmr_lstm_sync_status(const void* ws, unsigned* timeout_out, hipStream_t stream);
 
 /* TimeConv (NLBlock_MutiConv6_3.py:43-79, generalised in L): the three Conv1d branches run
  * on tmr_conv2d_* (L as H, W=1); these kernels take the elementwise max of
@@ -345,7 +422,7 @@ int tmr_timeconv_max5_fwd(const float* x, const float* y1, const float* y2, cons
 int tmr_timeconv_max5_bwd(const float* dy, const uint8_t* code, float* d1, float* d2, float* d3,
                           float* dx, int b, int l, int c, hipStream_t stream);
 
-/* ---------------- LSTM cell (head.hip) -------------------------------------
+/* ---------------- LSTM cell (head.hip; the per-step path of tmr_lstm_fwd/bwd) --
  * nn.LSTM(2048,512) gates in PyTorch order i,f,g,o (train_only_non-local_pretrained.py:215,
  * :230-231).  gx: x W_ih^T + b_ih + b_hh for step t (row stride ldgx); ghh: h_{t-1} W_hh^T
  * (NULL at t=0); c_prev NULL at t=0.  act saves (i,f,g,o) activations [b][4h] for the

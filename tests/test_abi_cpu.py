@@ -38,7 +38,7 @@ def test_python_binding_covers_header(built):
 def test_library_loads_and_reports_version(built):
     from tmrnet_amd import _lib
     h = _lib.lib()
-    assert h.tmr_abi_version() == 1
+    assert h.tmr_abi_version() == 2
     assert isinstance(h.tmr_last_error(), bytes)
 
 
@@ -70,5 +70,26 @@ def test_argument_errors_raise_with_message(built):
         _lib.query("tmr_conv2d_fwd_stats_parts", None)
     with pytest.raises(RuntimeError, match="wgrad_ws_bytes"):
         _lib.query("tmr_conv2d_wgrad_ws_bytes", None)
+    # module-level entry points: size queries and null operands fail before any device work
+    for q, args in (("tmr_lstm_ws_bytes", (4, 10, 2048, 0)), ("tmr_lstm_saved_bytes", (-1, 10, 512)),
+                    ("tmr_nlblock_ws_bytes", (4, 0)), ("tmr_nlblock_saved_bytes", (-2, 40)),
+                    ("tmr_timeconv_ws_bytes", (4, 0)), ("tmr_nl_attn_ws_bytes", (4, 40, 300))):
+        with pytest.raises(RuntimeError, match=q):
+            _lib.query(q, *args)
+    with pytest.raises(RuntimeError, match="tmr_lstm_fwd: bad sizes"):
+        _lib.call("tmr_lstm_fwd", None, 2, 3, 0, 512, *([None] * 7), None, 0, None, 0, None)
+    with pytest.raises(RuntimeError, match="tmr_lstm_fwd: null operand"):
+        _lib.call("tmr_lstm_fwd", None, 2, 3, 64, 512, *([None] * 7), None, 0, None, 0, None)
+    with pytest.raises(RuntimeError, match="tmr_nlblock_fwd: null operand"):
+        _lib.call("tmr_nlblock_fwd", None, None, None, None, 2, 40, None, None, None, 0, None, 0,
+                  None)
+    with pytest.raises(RuntimeError, match="tmr_timeconv_wgrad: null operand"):
+        _lib.call("tmr_timeconv_wgrad", *([None] * 2), 2, 30, *([None] * 4), 0, *([None] * 8), 0,
+                  None)
+    with pytest.raises(RuntimeError, match="tmr_linear_fwd: bad sizes"):
+        _lib.call("tmr_linear_fwd", None, 4, 0, 8, None, None, None, None)
+    with pytest.raises(RuntimeError, match="feature dim"):
+        _lib.call("tmr_nl_attn_fwd", None, None, None, None, None, 2, 40, 300, 1.0, None, 0, None)
     # a good query after a failure is not poisoned by the old message
     assert _lib.query("tmr_bn_ws_bytes", 1024, 64) > 0
+    assert _lib.query("tmr_lstm_ws_bytes", 64, 10, 2048, 512) > 0

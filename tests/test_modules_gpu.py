@@ -1,0 +1,134 @@
+"""Module-level C entry points (include/tmr.h: tmr_lstm_*, tmr_nlblock_*, tmr_timeconv_*,
+tmr_linear_*) against float64 torch, and their two execution paths.
+
+* tmr_lstm_fwd/bwd: the persistent one-launch recurrence (hidden 512; grid 64 x ceil(B/16)
+  workgroups behind a grid barrier) and the per-step path it falls back to (TMR_LSTM_PERSIST=0,
+  other hidden sizes, or a grid the cooperative launch refuses: B > 64 at one workgroup per CU)
+  -- both against nn.LSTM in float64 (train_only_non-local_pretrained.py:215, :230-231), and the
+  barrier's timeout word must read 0.
+* tmr_nl_attn split over 32-row chunks at the C5 shape (B=64, L=300, bank rows) against float64.
+* tmr_linear_fwd/bwd against float64 nn.Linear.
+"""
+import os
+
+import pytest
+import torch
+
+from tmrnet_amd import ops
+from tmrnet_amd.lstm import LSTM
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def _lstm_case(dev, B, T, I, H, seed):
+    torch.manual_seed(seed)
+    ref = torch.nn.LSTM(I, H, batch_first=True).double()
+    m = LSTM(I, H).to(dev)
+    m.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = torch.randn(B, T, I, dtype=torch.float64)
+    dy = torch.randn(B, T, H, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    yr, (hr, cr) = ref(xr)
+    yr.backward(dy)
+    xd = x.float().to(dev).requires_grad_(True)
+    y, (hn, cn) = m(xd)
+    y.backward(dy.float().to(dev))
+    torch.cuda.synchronize()
+    assert rel(y, yr) < 5e-6
+    assert rel(hn, hr) < 5e-6 and rel(cn, cr) < 5e-6
+    assert rel(xd.grad, xr.grad) < 2e-5
+    for (n1, p1), (n2, p2) in zip(m.named_parameters(), ref.named_parameters()):
+        assert n1 == n2
+        assert rel(p1.grad, p2.grad) < 2e-5, n1
+
+
+@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("B,T", [(64, 10), (5, 30), (1, 1), (100, 3)])
+def test_lstm_entry_points(dev, monkeypatch, persist, B, T):
+    """Hidden 512 as in the reference; B=64 x T=10 is C2's clip batch (4 workgroup rows of 16
+    clips, the persistent grid fills 256 CUs), B=100 needs 7 rows (448 > 256 workgroups): the
+    cooperative launch refuses it and the per-step path runs."""
+    monkeypatch.setenv("TMR_LSTM_PERSIST", persist)
+    _lstm_case(dev, B, T, 256, 512, seed=B * 100 + T)
+
+
+def test_lstm_persistent_barrier_status(dev):
+    """The timeout word of the grid barrier stays 0 over a full C2-shaped forward + backward, and
+    the persistent and per-step paths agree to fp32 summation order."""
+    torch.manual_seed(3)
+    B, T, I, H = 64, 10, 2048, 512
+    x = torch.randn(B, T, I, device=dev)
+    w_ih = torch.randn(4 * H, I, device=dev) * (2.0 / (I + 4 * H)) ** 0.5
+    w_hh = torch.randn(4 * H, H, device=dev) * (2.0 / (H + 4 * H)) ** 0.5
+    b_ih = torch.rand(4 * H, device=dev) * 0.08 - 0.04
+    b_hh = torch.rand(4 * H, device=dev) * 0.08 - 0.04
+    os.environ["TMR_LSTM_PERSIST"] = "1"
+    try:
+        y1, h1, c1, saved1, ws1 = ops.lstm_fwd(x, w_ih, w_hh, b_ih, b_hh)
+        assert ops.lstm_sync_status(ws1) == 0
+        dy = torch.randn_like(y1)
+        g1 = ops.lstm_bwd(dy, x, w_ih, w_hh, y1, saved1)
+        assert ops.lstm_sync_status(g1[-1]) == 0
+        os.environ["TMR_LSTM_PERSIST"] = "0"
+        y0, h0, c0, saved0, _ = ops.lstm_fwd(x, w_ih, w_hh, b_ih, b_hh)
+        g0 = ops.lstm_bwd(dy, x, w_ih, w_hh, y0, saved0)
+    finally:
+        os.environ.pop("TMR_LSTM_PERSIST", None)
+    assert rel(y1, y0) < 1e-5 and rel(c1, c0) < 1e-5
+    for a, b in zip(g1[:5], g0[:5]):
+        assert rel(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("B,L,rows", [(64, 300, True), (3, 40, False), (2, 1, False),
+                                      (4, 33, True)])
+def test_nl_attn_split(dev, B, L, rows):
+    """Chunked attention core (32-row chunks + ordered combine) vs float64, incl. a ragged last
+    chunk (L=33), L=1 and C5's B=64, L=300 read from a bank through the row table."""
+    g = torch.Generator().manual_seed(B * 1000 + L)
+    D = 512
+    u = torch.randn(B, D, generator=g, dtype=torch.float64)
+    dctx = torch.randn(B, D, generator=g, dtype=torch.float64)
+    if rows:
+        bank = torch.rand(5 * L + 7, D, generator=g, dtype=torch.float64) * 2 - 1
+        idx = torch.randint(0, bank.shape[0], (B, L), generator=g)
+        lt64 = bank[idx]
+        lt_d, rows_d = bank.float().to(dev), idx.to(torch.int32).to(dev)
+    else:
+        lt64 = torch.rand(B, L, D, generator=g, dtype=torch.float64) * 2 - 1
+        lt_d, rows_d = lt64.float().to(dev), None
+    scale = (1.0 / 512) ** 0.5
+    s = torch.einsum("bld,bd->bl", lt64, u) * scale
+    p64 = torch.softmax(s, 1)
+    ctx64 = torch.einsum("bl,bld->bd", p64, lt64)
+    dp = torch.einsum("bld,bd->bl", lt64, dctx)
+    ds = scale * p64 * (dp - (p64 * dp).sum(1, keepdim=True))
+    ut64 = torch.einsum("bl,bld->bd", ds, lt64)
+    dlt64 = p64[:, :, None] * dctx[:, None, :] + ds[:, :, None] * u[:, None, :]
+    p, ctx = ops.nl_attn_fwd(lt_d, rows_d, u.float().to(dev), B, L, scale)
+    assert rel(p, p64) < 1e-5 and rel(ctx, ctx64) < 1e-5
+    ut, dlt = ops.nl_attn_bwd(lt_d, rows_d, u.float().to(dev), p, dctx.float().to(dev), B, L,
+                              scale, rows_d is None)
+    assert rel(ut, ut64) < 2e-5
+    if rows_d is None:
+        assert rel(dlt, dlt64) < 2e-5
+
+
+def test_linear_entry_points(dev):
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(37, 1024, generator=g, dtype=torch.float64)
+    lin = torch.nn.Linear(1024, 7).double()
+    dy = torch.randn(37, 7, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    lin(xr).backward(dy)
+    w, b = lin.weight.detach().float().to(dev), lin.bias.detach().float().to(dev)
+    y = ops.linear_fwd(x.float().to(dev), w, b)
+    assert rel(y, lin(x)) < 2e-6
+    dx, dw, db = ops.linear_bwd(dy.float().to(dev), x.float().to(dev), w)
+    assert rel(dx, xr.grad) < 2e-6
+    assert rel(dw, lin.weight.grad) < 2e-6 and rel(db, lin.bias.grad) < 2e-6

@@ -28,6 +28,13 @@ class ConvDesc(ctypes.Structure):
 
 DP = ctypes.POINTER(ConvDesc)
 
+_NL_FIELDS = ("w1", "b1", "w2", "b2", "w3", "b3", "ln_w", "ln_b", "w4", "b4")
+
+
+class NLBlockPtrs(ctypes.Structure):
+    """tmr_nlblock_weights / tmr_nlblock_grads: ten device pointers in NLBlock parameter order."""
+    _fields_ = [(n, ctypes.c_void_p) for n in _NL_FIELDS]
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "tmr_abi_version": [],
@@ -89,8 +96,24 @@ SIGNATURES = {
     "tmr_mask_relu_fwd": [P, P, P, L, P],
     "tmr_mask_relu_bwd": [P, P, P, P, L, P],
     "tmr_mul": [P, P, P, P, L, P],
-    "tmr_nl_attn_fwd": [P, P, P, P, P, I, I, I, F, P],
-    "tmr_nl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, F, P],
+    "tmr_nl_attn_ws_bytes": [I, I, I],
+    "tmr_nl_attn_fwd": [P, P, P, P, P, I, I, I, F, P, SZ, P],
+    "tmr_nl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, F, P, SZ, P],
+    "tmr_linear_fwd": [P, I, I, I, P, P, P, P],
+    "tmr_linear_bwd": [P, P, I, I, I, P, P, P, P, F, P],
+    "tmr_nlblock_saved_bytes": [I, I],
+    "tmr_nlblock_ws_bytes": [I, I],
+    "tmr_nlblock_fwd": [P, P, P, P, I, I, P, P, P, SZ, P, SZ, P],
+    "tmr_nlblock_bwd": [P, P, P, P, P, I, I, P, P, SZ, P, P, P, P, SZ, P],
+    "tmr_timeconv_saved_bytes": [I, I],
+    "tmr_timeconv_ws_bytes": [I, I],
+    "tmr_timeconv_fwd": [P, I, I, P, P, P, P, P, P, P, P, SZ, P, SZ, P],
+    "tmr_timeconv_wgrad": [P, P, I, I, P, P, P, P, SZ, P, P, P, P, P, P, P, P, SZ, P],
+    "tmr_lstm_saved_bytes": [I, I, I],
+    "tmr_lstm_ws_bytes": [I, I, I, I],
+    "tmr_lstm_fwd": [P, I, I, I, I, P, P, P, P, P, P, P, P, SZ, P, SZ, P],
+    "tmr_lstm_bwd": [P, P, I, I, I, I, P, P, P, P, SZ, P, P, P, P, P, P, SZ, P],
+    "tmr_lstm_sync_status": [P, ctypes.POINTER(ctypes.c_uint), P],
     "tmr_timeconv_max5_fwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_timeconv_max5_bwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],
@@ -103,6 +126,13 @@ _RESTYPES = {
     "tmr_bn_ws_bytes": SZ,
     "tmr_bn_parts_ws_bytes": SZ,
     "tmr_sgd_chunk": ctypes.c_int64,
+    "tmr_nl_attn_ws_bytes": SZ,
+    "tmr_nlblock_saved_bytes": SZ,
+    "tmr_nlblock_ws_bytes": SZ,
+    "tmr_timeconv_saved_bytes": SZ,
+    "tmr_timeconv_ws_bytes": SZ,
+    "tmr_lstm_saved_bytes": SZ,
+    "tmr_lstm_ws_bytes": SZ,
 }
 
 _lib = None

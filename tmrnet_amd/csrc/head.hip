@@ -1,5 +1,5 @@
-// Clip-level kernels after the frame encoder: LSTM cell, NLBlock attention core,
-// LayerNorm+ReLU, LFB index/gather, dropout, cross-entropy, bias grads, SGD.
+// Clip-level kernels after the frame encoder: LSTM cell (per-step path), LayerNorm+ReLU,
+// LFB index/gather, dropout, cross-entropy, bias grads, SGD.  (NLBlock attention: nlblock.hip.)
 //
 // Reference (paths under code/):
 //   LSTM            nn.LSTM(2048,512) -- Training TMRNet/train_only_non-local_pretrained.py:215,:230-233
@@ -63,116 +63,6 @@ __global__ void lstm_cell_bwd_k(const float* __restrict__ dho, int lddh,
   d[2 * hd + j] = dc * ig * (1.f - gg * gg);
   d[3 * hd + j] = dor * og * (1.f - og);
   dcp[i] = dc * fg;
-}
-
-// ------------------------------------------------------ NLBlock attention core
-// one workgroup per clip; wave-per-row dot products, LDS softmax over L
-__global__ __launch_bounds__(NT) void nl_attn_fwd_k(const float* __restrict__ lt,
-                                                    const int32_t* __restrict__ rows,
-                                                    const float* __restrict__ u,
-                                                    float* __restrict__ p, float* __restrict__ ctx,
-                                                    int L, int D, float scale) {
-  extern __shared__ float sm[];  // [L]
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* ub = u + (long)b * D;
-  for (int l = wave; l < L; l += NT / 64) {
-    const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
-    const float* row = lt + r * D;
-    float s = 0.f;
-    for (int c = lane * 4; c < D; c += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(row + c);
-      const float4 w = *reinterpret_cast<const float4*>(ub + c);
-      s = fmaf(v.x, w.x, s); s = fmaf(v.y, w.y, s); s = fmaf(v.z, w.z, s); s = fmaf(v.w, w.w, s);
-    }
-    s = warp_sum(s);
-    if (lane == 0) sm[l] = s * scale;
-  }
-  __syncthreads();
-  // softmax over L (every wave computes the same max/sum; L is small)
-  float mx = -INFINITY;
-  for (int l = lane; l < L; l += 64) mx = fmaxf(mx, sm[l]);
-  mx = warp_max(mx);
-  float den = 0.f;
-  for (int l = lane; l < L; l += 64) den += expf(sm[l] - mx);
-  den = warp_sum(den);
-  __syncthreads();
-  const float inv = 1.0f / den;
-  // every wave has finished reading the scores (barrier above): overwrite in place
-  for (int l = threadIdx.x; l < L; l += NT) {
-    const float e = expf(sm[l] - mx) * inv;
-    p[(long)b * L + l] = e;
-    sm[l] = e;
-  }
-  __syncthreads();
-  for (int c = threadIdx.x * 2; c < D; c += NT * 2) {
-    float a0 = 0.f, a1 = 0.f;
-    for (int l = 0; l < L; ++l) {
-      const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
-      const float2 v = *reinterpret_cast<const float2*>(lt + r * D + c);
-      a0 = fmaf(sm[l], v.x, a0);
-      a1 = fmaf(sm[l], v.y, a1);
-    }
-    ctx[(long)b * D + c] = a0;
-    ctx[(long)b * D + c + 1] = a1;
-  }
-}
-
-__global__ __launch_bounds__(NT) void nl_attn_bwd_k(const float* __restrict__ lt,
-                                                    const int32_t* __restrict__ rows,
-                                                    const float* __restrict__ u,
-                                                    const float* __restrict__ p,
-                                                    const float* __restrict__ dctx,
-                                                    float* __restrict__ ut,
-                                                    float* __restrict__ dlt, int L, int D,
-                                                    float scale) {
-  extern __shared__ float sm[];  // [2L]: dp, ds
-  float* dps = sm;
-  float* dss = sm + L;
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* gb = dctx + (long)b * D;
-  for (int l = wave; l < L; l += NT / 64) {
-    const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
-    const float* row = lt + r * D;
-    float s = 0.f;
-    for (int c = lane * 4; c < D; c += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(row + c);
-      const float4 w = *reinterpret_cast<const float4*>(gb + c);
-      s = fmaf(v.x, w.x, s); s = fmaf(v.y, w.y, s); s = fmaf(v.z, w.z, s); s = fmaf(v.w, w.w, s);
-    }
-    s = warp_sum(s);
-    if (lane == 0) dps[l] = s;
-  }
-  __syncthreads();
-  float t = 0.f;
-  for (int l = lane; l < L; l += 64) t = fmaf(p[(long)b * L + l], dps[l], t);
-  t = warp_sum(t);
-  __syncthreads();
-  for (int l = threadIdx.x; l < L; l += NT) {
-    const float pl = p[(long)b * L + l];
-    dss[l] = scale * pl * (dps[l] - t);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x * 2; c < D; c += NT * 2) {
-    float a0 = 0.f, a1 = 0.f;
-    const float g0 = gb[c], g1 = gb[c + 1];
-    const float u0 = u[(long)b * D + c], u1 = u[(long)b * D + c + 1];
-    for (int l = 0; l < L; ++l) {
-      const long r = rows ? (long)rows[(long)b * L + l] : (long)b * L + l;
-      const float2 v = *reinterpret_cast<const float2*>(lt + r * D + c);
-      a0 = fmaf(dss[l], v.x, a0);
-      a1 = fmaf(dss[l], v.y, a1);
-      if (dlt) {
-        const float pl = p[(long)b * L + l];
-        float* o = dlt + ((long)b * L + l) * D + c;
-        o[0] = fmaf(pl, g0, dss[l] * u0);
-        o[1] = fmaf(pl, g1, dss[l] * u1);
-      }
-    }
-    ut[(long)b * D + c] = a0;
-    ut[(long)b * D + c + 1] = a1;
-  }
 }
 
 // ------------------------------------------------------------ LayerNorm+ReLU
@@ -433,29 +323,6 @@ TMR_API int tmr_lstm_cell_bwd(const float* dh_out, int lddh, const float* dh_rec
   hipLaunchKernelGGL(lstm_cell_bwd_k, dim3(cdiv((long)b * hdim, NT)), dim3(NT), 0, stream, dh_out,
                      lddh, dh_rec, dc_next, act, c, c_prev, dgates, lddg, dc_prev, b, hdim);
   TMR_CHECK_LAUNCH("lstm_cell_bwd");
-  return 0;
-}
-
-TMR_API int tmr_nl_attn_fwd(const float* lt, const int32_t* rows, const float* u, float* p,
-                            float* ctx, int b, int l, int d, float scale, hipStream_t stream) {
-  TMR_CHECK_ARG(d % 256 == 0, "tmr_nl_attn_fwd: feature dim %d must be a multiple of 256", d);
-  TMR_CHECK_ARG(l >= 1 && l <= 16384, "tmr_nl_attn_fwd: bad L %d", l);
-  if (b == 0) return 0;
-  hipLaunchKernelGGL(nl_attn_fwd_k, dim3(b), dim3(NT), l * sizeof(float), stream, lt, rows, u, p,
-                     ctx, l, d, scale);
-  TMR_CHECK_LAUNCH("nl_attn_fwd");
-  return 0;
-}
-
-TMR_API int tmr_nl_attn_bwd(const float* lt, const int32_t* rows, const float* u, const float* p,
-                            const float* dctx, float* ut, float* dlt, int b, int l, int d,
-                            float scale, hipStream_t stream) {
-  TMR_CHECK_ARG(d % 256 == 0, "tmr_nl_attn_bwd: feature dim %d must be a multiple of 256", d);
-  TMR_CHECK_ARG(!(dlt && rows), "tmr_nl_attn_bwd: dLt only for a dense Lt");
-  if (b == 0) return 0;
-  hipLaunchKernelGGL(nl_attn_bwd_k, dim3(b), dim3(NT), 2 * l * sizeof(float), stream, lt, rows, u,
-                     p, dctx, ut, dlt, l, d, scale);
-  TMR_CHECK_LAUNCH("nl_attn_bwd");
   return 0;
 }
 

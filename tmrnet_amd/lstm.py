@@ -6,10 +6,11 @@ bias_ih_l0, bias_hh_l0; gate order i,f,g,o), so `lstm.*` state_dict keys load
 unchanged, and `all_weights` is provided for the reference's
 ``init.xavier_normal_(self.lstm.all_weights[0][0])`` (:221-222).
 
-Forward: one MFMA GEMM for the input projection of all B*T frames
-(x W_ih^T + b_ih + b_hh), then per step a GEMM h_{t-1} W_hh^T and a fused
-gate/cell kernel.  Backward: per-step fused gate backward + the recurrent dgrad
-GEMM, then one GEMM each for dW_ih, dW_hh and dX over all steps.
+Forward (tmr_lstm_fwd): one MFMA GEMM for the input projection of all B*T frames
+(x W_ih^T + b_ih + b_hh), then the whole T-step recurrence -- gate GEMM h_{t-1} W_hh^T,
+sigma/tanh, cell update -- in one persistent launch (csrc/lstm.hip).  Backward
+(tmr_lstm_bwd): BPTT in one persistent launch, then one GEMM each for dW_ih, dW_hh and dX
+over all steps.
 """
 import math
 
@@ -20,60 +21,29 @@ from . import ops
 
 
 class LSTMFn(torch.autograd.Function):
+    """tmr_lstm_fwd / tmr_lstm_bwd: one C call each way (the recurrence is one persistent launch,
+    include/tmr.h)."""
+
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh):
-        B, T, I = x.shape
-        H = w_hh.shape[1]
-        x2 = x.contiguous().view(B * T, I)
-        bias = ops.residual_mask(b_ih.detach().contiguous(), b_hh.detach().contiguous(), None)
-        gx = ops.gemm_nt(x2, w_ih.detach(), bias=bias).view(B, T, 4 * H)   # x W_ih^T + b
-        y = torch.empty((B, T, H), dtype=x.dtype, device=x.device)
-        cs = torch.empty((T, B, H), dtype=x.dtype, device=x.device)
-        acts = torch.empty((T, B, 4 * H), dtype=x.dtype, device=x.device)
-        ghh = torch.empty((B, 4 * H), dtype=x.dtype, device=x.device)
-        whh = w_hh.detach()
-        for t in range(T):
-            if t > 0:
-                ops.gemm_nt(y[:, t - 1, :], whh, out=ghh)                  # h_{t-1} W_hh^T
-            ops.lstm_cell_fwd(gx[:, t, :], ghh if t > 0 else None,
-                              cs[t - 1] if t > 0 else None, y[:, t, :], cs[t], acts[t])
-        ctx.save_for_backward(x2, w_ih, w_hh, y, cs, acts)
-        ctx.dims = (B, T, I, H)
-        hn = y[:, T - 1, :].unsqueeze(0).contiguous()
-        cn = cs[T - 1].unsqueeze(0).contiguous()
+        x = x.contiguous()
+        wi, wh = w_ih.detach().contiguous(), w_hh.detach().contiguous()
+        train = torch.is_grad_enabled() or any(ctx.needs_input_grad)
+        y, hn, cn, saved, _ = ops.lstm_fwd(x, wi, wh, b_ih.detach().contiguous(),
+                                           b_hh.detach().contiguous(), train=train)
+        if saved is not None:
+            ctx.save_for_backward(x, wi, wh, y, saved)
+        hn, cn = hn.unsqueeze(0), cn.unsqueeze(0)
         ctx.mark_non_differentiable(hn, cn)
         return y, hn, cn
 
     @staticmethod
     def backward(ctx, dy, dhn, dcn):
-        x2, w_ih, w_hh, y, cs, acts = ctx.saved_tensors
-        B, T, I, H = ctx.dims
+        x, wi, wh, y, saved = ctx.saved_tensors
         dy = dy.contiguous() if dy is not None else torch.zeros_like(y)
-        dg = torch.empty((B, T, 4 * H), dtype=y.dtype, device=y.device)
-        whh = w_hh.detach()
-        dcp = [torch.empty((B, H), dtype=y.dtype, device=y.device) for _ in range(2)]
-        dh_buf = torch.empty((B, H), dtype=y.dtype, device=y.device)
-        dh_rec = None
-        dc_next = None
-        for t in range(T - 1, -1, -1):
-            ops.lstm_cell_bwd(dy[:, t, :], dh_rec, dc_next, acts[t], cs[t],
-                              cs[t - 1] if t > 0 else None, dg[:, t, :], dcp[t & 1])
-            dc_next = dcp[t & 1]
-            if t > 0:
-                ops.gemm_nn(dg[:, t, :], whh, out=dh_buf)                 # dgates_t W_hh
-                dh_rec = dh_buf
-        # h_{t-1} for every (b,t), zero at t=0
-        hprev = torch.zeros((B, T, H), dtype=y.dtype, device=y.device)
-        if T > 1:
-            hprev[:, 1:, :].copy_(y[:, :-1, :])
-        dg2 = dg.view(B * T, 4 * H)
-        dw_ih = ops.gemm_tn(dg2, x2)                                      # (4H, I)
-        dw_hh = ops.gemm_tn(dg2, hprev.view(B * T, H))                    # (4H, H)
-        db = ops.col_sum(dg2, B * T, 4 * H, 4 * H)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = ops.gemm_nn(dg2, w_ih.detach()).view(B, T, I)
-        return dx, dw_ih, dw_hh, db, ops.mul(db)
+        dx, dw_ih, dw_hh, db_ih, db_hh, _ = ops.lstm_bwd(dy, x, wi, wh, y, saved,
+                                                         want_dx=ctx.needs_input_grad[0])
+        return dx, dw_ih, dw_hh, db_ih, db_hh
 
 
 class LSTM(nn.Module):

@@ -55,49 +55,29 @@ class _DropoutRNG:
 
 
 class NLBlockFn(torch.autograd.Function):
+    """One autograd node over tmr_nlblock_fwd / tmr_nlblock_bwd (the whole block is one C call
+    each way; include/tmr.h)."""
+
     @staticmethod
     def forward(ctx, St, lt, rows, mask, L, w1, b1, w2, b2, w3, b3, g, bt, w4, b4):
-        B = St.shape[0]
         St = St.contiguous()
-        scale = (1.0 / 512) ** 0.5
-        q = ops.gemm_nt(St, w1.detach(), bias=b1.detach())                 # linear1
-        u = ops.gemm_nn(q, w2.detach())                                    # W2^T q
-        p, c = ops.nl_attn_fwd(lt, rows, u, B, L, scale)                   # softmax, ctx
-        sll = ops.gemm_nt(c, w3.detach(), bias=b3.detach())                # linear3 (sum p = 1)
-        a, mu, rs = ops.layernorm_relu_fwd(sll, g.detach().reshape(-1).contiguous(),
-                                           bt.detach().reshape(-1).contiguous(), 1e-5)
-        z = ops.gemm_nt(a, w4.detach(), bias=b4.detach())                  # linear4
-        out = ops.residual_mask(St, z, mask)                               # dropout + residual
-        ctx.save_for_backward(St, lt, rows, mask, q, u, p, c, sll, a, mu, rs,
-                              w1, w2, w3, g, w4)
-        ctx.dims = (B, L)
+        weights = [t.detach().contiguous().reshape(-1) if t.dim() == 2 and t.shape[0] == 1
+                   else t.detach().contiguous() for t in (w1, b1, w2, b2, w3, b3, g, bt, w4, b4)]
+        out, saved = ops.nlblock_fwd(St, lt, rows, L, mask, weights)
+        ctx.save_for_backward(St, lt, rows, mask, saved, *weights)
+        ctx.L = L
         ctx.lt_grad = ctx.needs_input_grad[1] and rows is None
+        ctx.g_shape = g.shape
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (St, lt, rows, mask, q, u, p, c, sll, a, mu, rs, w1, w2, w3, g, w4) = ctx.saved_tensors
-        B, L = ctx.dims
-        dout = dout.contiguous()
-        scale = (1.0 / 512) ** 0.5
-        dz = ops.mul(dout, mask) if mask is not None else dout
-        dw4 = ops.gemm_tn(dz, a)
-        db4 = ops.col_sum(dz, B, 512, 512)
-        da = ops.gemm_nn(dz, w4.detach())
-        dsll, dg, dbt = ops.layernorm_relu_bwd(da, sll, a, g.detach().reshape(-1).contiguous(),
-                                               mu, rs)
-        dw3 = ops.gemm_tn(dsll, c)
-        db3 = ops.col_sum(dsll, B, 512, 512)
-        dc = ops.gemm_nn(dsll, w3.detach())
-        ut, dlt = ops.nl_attn_bwd(lt, rows, u, p, dc, B, L, scale, ctx.lt_grad)
-        dq = ops.gemm_nt(ut, w2.detach())                                  # W2 ut
-        dw2 = ops.gemm_tn(q, ut)                                           # q ut^T
-        db2 = torch.zeros_like(db3)  # sum_l dscore_l == 0: q.b2 cancels in the softmax
-        dw1 = ops.gemm_tn(dq, St)
-        db1 = ops.col_sum(dq, B, 512, 512)
-        dSt = ops.gemm_nn(dq, w1.detach(), out=ops.mul(dout), beta=1.0)   # dout + W1^T dq
+        St, lt, rows, mask, saved, *weights = ctx.saved_tensors
+        dSt, dlt, gr = ops.nlblock_bwd(dout.contiguous(), St, lt, rows, ctx.L, mask, saved,
+                                       weights, ctx.lt_grad)
+        dw1, db1, dw2, db2, dw3, db3, dg, dbt, dw4, db4 = gr
         return (dSt, dlt, None, None, None, dw1, db1, dw2, db2, dw3, db3,
-                dg.view_as(g), dbt.view_as(g), dw4, db4)
+                dg.view(ctx.g_shape), dbt.view(ctx.g_shape), dw4, db4)
 
 
 class NLBlock(nn.Module):

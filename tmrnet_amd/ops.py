@@ -541,11 +541,18 @@ def mul(a, b=None, scalar=None, out=None):
     return out
 
 
+def _ws(nbytes, like):
+    """Scratch / saved buffer for the module-level entry points (torch's caching allocator)."""
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=like.device)
+
+
 def nl_attn_fwd(lt, rows, u, B, L, scale):
     d = u.shape[1]
     p = _empty((B, L), u)
     ctx = _empty((B, d), u)
-    call("tmr_nl_attn_fwd", lt, rows, u, p, ctx, B, L, d, float(scale), stream_ptr())
+    ws = _ws(query("tmr_nl_attn_ws_bytes", B, L, d), u)
+    call("tmr_nl_attn_fwd", lt, rows, u, p, ctx, B, L, d, float(scale), ws, ws.numel(),
+         stream_ptr())
     return p, ctx
 
 
@@ -553,8 +560,135 @@ def nl_attn_bwd(lt, rows, u, p, dctx, B, L, scale, want_dlt):
     d = u.shape[1]
     ut = _empty((B, d), u)
     dlt = _empty((B, L, d), u) if want_dlt else None
-    call("tmr_nl_attn_bwd", lt, rows, u, p, dctx, ut, dlt, B, L, d, float(scale), stream_ptr())
+    ws = _ws(query("tmr_nl_attn_ws_bytes", B, L, d), u)
+    call("tmr_nl_attn_bwd", lt, rows, u, p, dctx, ut, dlt, B, L, d, float(scale), ws, ws.numel(),
+         stream_ptr())
     return ut, dlt
+
+
+# ------------------------------------------------------- module-level entry points
+def _nl_ptrs(ts):
+    from ._lib import NLBlockPtrs
+    for t in ts:
+        _req(t, "NLBlock parameter")
+    return NLBlockPtrs(*[t.data_ptr() for t in ts])
+
+
+def nlblock_fwd(st, lt, rows, L, mask, weights):
+    """tmr_nlblock_fwd: weights = (w1, b1, w2, b2, w3, b3, ln_w, ln_b, w4, b4) (detached,
+    contiguous).  Returns (out, saved)."""
+    B = st.shape[0]
+    _req(st, "St")
+    _req(lt, "Lt")
+    if rows is not None:
+        _req(rows, "rows", torch.int32)
+    out = _empty((B, 512), st)
+    saved = _ws(query("tmr_nlblock_saved_bytes", B, L), st)
+    ws = _ws(query("tmr_nlblock_ws_bytes", B, L), st)
+    w = _nl_ptrs(weights)
+    call("tmr_nlblock_fwd", ctypes.byref(w), st, lt, rows, B, L, mask, out, saved, saved.numel(),
+         ws, ws.numel(), stream_ptr())
+    return out, saved
+
+
+def nlblock_bwd(dout, st, lt, rows, L, mask, saved, weights, want_dlt):
+    """tmr_nlblock_bwd -> (dSt, dLt or None, [grads in weight order])."""
+    B = st.shape[0]
+    _req(dout, "dout")
+    dst = _empty((B, 512), st)
+    dlt = _empty((B, L, 512), st) if want_dlt else None
+    grads = [torch.empty_like(t) for t in weights]
+    ws = _ws(query("tmr_nlblock_ws_bytes", B, L), st)
+    w = _nl_ptrs(weights)
+    g = _nl_ptrs(grads)
+    call("tmr_nlblock_bwd", ctypes.byref(w), dout, st, lt, rows, B, L, mask, saved, saved.numel(),
+         dst, dlt, ctypes.byref(g), ws, ws.numel(), stream_ptr())
+    return dst, dlt, grads
+
+
+def timeconv_fwd(x, w3, b3, w5, b5, w7, b7):
+    """tmr_timeconv_fwd: x (B,L,512) -> (out, saved max-branch codes)."""
+    _req(x, "x")
+    B, L, _ = x.shape
+    out = torch.empty_like(x)
+    saved = _ws(query("tmr_timeconv_saved_bytes", B, L), x)
+    ws = _ws(query("tmr_timeconv_ws_bytes", B, L), x)
+    for t in (w3, b3, w5, b5, w7, b7):
+        _req(t, "TimeConv parameter")
+    call("tmr_timeconv_fwd", x, B, L, w3, b3, w5, b5, w7, b7, out, saved, saved.numel(), ws,
+         ws.numel(), stream_ptr())
+    return out, saved
+
+
+def timeconv_wgrad(dy, x, saved, w3, w5, w7, want_dx):
+    """tmr_timeconv_wgrad -> (dx or None, dw3, db3, dw5, db5, dw7, db7)."""
+    _req(dy, "dy")
+    B, L, C = x.shape
+    dx = torch.empty_like(x) if want_dx else None
+    g = [torch.empty_like(w) for w in (w3, w5, w7)]
+    bg = [_empty((C,), x) for _ in range(3)]
+    ws = _ws(query("tmr_timeconv_ws_bytes", B, L), x)
+    call("tmr_timeconv_wgrad", dy, x, B, L, w3, w5, w7, saved, saved.numel(), dx, g[0], bg[0],
+         g[1], bg[1], g[2], bg[2], ws, ws.numel(), stream_ptr())
+    return dx, g[0], bg[0], g[1], bg[1], g[2], bg[2]
+
+
+def lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, train=True):
+    """tmr_lstm_fwd: x (B,T,I) -> (y (B,T,H), h_n (B,H), c_n (B,H), saved or None, ws)."""
+    _req(x, "x")
+    for t in (w_ih, w_hh, b_ih, b_hh):
+        _req(t, "LSTM parameter")
+    B, T, I = x.shape
+    H = w_hh.shape[1]
+    y = _empty((B, T, H), x)
+    hn = _empty((B, H), x)
+    cn = _empty((B, H), x)
+    saved = _ws(query("tmr_lstm_saved_bytes", B, T, H), x) if train else None
+    ws = _ws(query("tmr_lstm_ws_bytes", B, T, I, H), x)
+    call("tmr_lstm_fwd", x, B, T, I, H, w_ih, w_hh, b_ih, b_hh, y, hn, cn, saved,
+         saved.numel() if saved is not None else 0, ws, ws.numel(), stream_ptr())
+    return y, hn, cn, saved, ws
+
+
+def lstm_bwd(dy, x, w_ih, w_hh, y, saved, want_dx=True):
+    """tmr_lstm_bwd -> (dx or None, dw_ih, dw_hh, db_ih, db_hh, ws)."""
+    _req(dy, "dy")
+    B, T, I = x.shape
+    H = w_hh.shape[1]
+    dx = torch.empty_like(x) if want_dx else None
+    dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+    db_ih, db_hh = _empty((4 * H,), x), _empty((4 * H,), x)
+    ws = _ws(query("tmr_lstm_ws_bytes", B, T, I, H), x)
+    call("tmr_lstm_bwd", dy, x, B, T, I, H, w_ih, w_hh, y, saved, saved.numel(), dx, dw_ih, dw_hh,
+         db_ih, db_hh, ws, ws.numel(), stream_ptr())
+    return dx, dw_ih, dw_hh, db_ih, db_hh, ws
+
+
+def lstm_sync_status(ws):
+    """Timeout word of the last persistent LSTM launch on `ws` (0 = all grid barriers done)."""
+    v = ctypes.c_uint(0)
+    call("tmr_lstm_sync_status", ws, ctypes.byref(v), stream_ptr())
+    return v.value
+
+
+def linear_fwd(x, w, b=None):
+    _req(x, "x"); _req(w, "w")
+    rows, i = x.shape
+    o = w.shape[0]
+    y = _empty((rows, o), x)
+    call("tmr_linear_fwd", x, rows, i, o, w, b, y, stream_ptr())
+    return y
+
+
+def linear_bwd(dy, x, w, want_dx=True, want_db=True):
+    _req(dy, "dy")
+    rows, i = x.shape
+    o = w.shape[0]
+    dx = _empty((rows, i), x) if want_dx else None
+    dw = torch.empty_like(w)
+    db = _empty((o,), x) if want_db else None
+    call("tmr_linear_bwd", dy, x, rows, i, o, w, dx, dw, db, 0.0, stream_ptr())
+    return dx, dw, db
 
 
 def lstm_cell_fwd(gx_t, ghh, c_prev, h_t, c_t, act_t=None):
