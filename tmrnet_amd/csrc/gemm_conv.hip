@@ -1020,12 +1020,7 @@ int env_int(const char* name, int dflt) {
 // (profiles/r1/convbench_cfgs.txt).  Short reductions (K <= 576: the 1x1 dgrads that accumulate
 // into the residual gradient, the 3x3 ones at 64 channels) are epilogue/latency bound and run
 // best as 64x64 tiles at high occupancy; wgrad prefers 256x128 to 256x256.
-int pick_cfg(long M, long N, long K, int mode) {
-  static const int forced = env_int("TMR_GEMM_CFG", -1);  // experiments only
-  if (forced >= 0 && forced < kNumCfgs) {
-    const TileCfg c = kCfgs[forced];
-    if (M >= c.bm && N >= c.bn) return forced;
-  }
+int pick_cfg_shape(long M, long N, long K, int mode) {
   if (mode == MODE_DGRAD && K <= 576 && M >= 4096) return 3;
   if (mode == MODE_WGRAD) {
     if (M <= 64 && N >= 512) return 3;
@@ -1038,6 +1033,33 @@ int pick_cfg(long M, long N, long K, int mode) {
   if (M <= 64 && N >= 256) return 2;
   if (M <= 64 || N <= 64) return 3;
   return 0;
+}
+
+long cfg_tiles(long M, long N, int c) {
+  return ((M + kCfgs[c].bm - 1) / kCfgs[c].bm) * ((N + kCfgs[c].bn - 1) / kCfgs[c].bn);
+}
+
+int pick_cfg(long M, long N, long K, int mode) {
+  static const int forced = env_int("TMR_GEMM_CFG", -1);  // experiments only
+  if (forced >= 0 && forced < kNumCfgs) {
+    const TileCfg c = kCfgs[forced];
+    if (M >= c.bm && N >= c.bn) return forced;
+  }
+  int cfg = pick_cfg_shape(M, N, K, mode);
+  // Plain GEMMs with few output rows (the LSTM input projection and its dgrad: M = B*T = 640,
+  // N = K = 2048) leave most of the 256 CUs idle on the big tiles: step down through 256x128,
+  // 128x128 and 64x64 until the grid has >= 256 workgroups.  (The conv views have M >= F*49 rows
+  // and never get here; WGRAD splits its reduction over blockIdx.y instead.)
+  if (mode != MODE_WGRAD && cfg_tiles(M, N, cfg) < 128) {
+    const long area = (long)kCfgs[cfg].bm * kCfgs[cfg].bn;
+    for (const int c2 : {4, 0, 3}) {
+      if ((long)kCfgs[c2].bm * kCfgs[c2].bn >= area || cfg_tiles(M, N, c2) <= cfg_tiles(M, N, cfg))
+        continue;
+      cfg = c2;
+      if (cfg_tiles(M, N, cfg) >= 256) break;
+    }
+  }
+  return cfg;
 }
 
 template <int MODE>

@@ -246,13 +246,33 @@ __global__ void softmax_max_k(const float* __restrict__ x, int b, int k, float* 
 }
 
 // ------------------------------------------------------------ column sums
-__global__ void col_sum_k(const float* __restrict__ x, int rows, int cols, int ld,
-                          float* __restrict__ out, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// 16 columns x 16 row lanes per block: lane q sums rows q, q+16, ... (8 loads in flight), the 16
+// lane sums are added in lane order (deterministic)
+__global__ __launch_bounds__(256) void col_sum_k(const float* __restrict__ x, int rows, int cols,
+                                                 int ld, float* __restrict__ out, float beta) {
+  __shared__ float part[16][17];
+  const int cl = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += x[(long)r * ld + c];
-  out[c] = beta != 0.f ? s + beta * out[c] : s;
+  if (c < cols) {
+    int r = q;
+    for (; r + 16 * 7 < rows; r += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x[(long)(r + 16 * u) * ld + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < rows; r += 16) s += x[(long)r * ld + c];
+  }
+  part[q][cl] = s;
+  __syncthreads();
+  if (q == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][cl];
+    out[c] = beta != 0.f ? t + beta * out[c] : t;
+  }
 }
 
 // --------------------------------------------------------------------- SGD
@@ -403,7 +423,7 @@ TMR_API int tmr_softmax_max(const float* logits, int b, int k, float* probs, flo
 TMR_API int tmr_col_sum(const float* x, int rows, int cols, int ld, float* out, float beta,
                         hipStream_t stream) {
   if (cols == 0) return 0;
-  hipLaunchKernelGGL(col_sum_k, dim3(cdiv(cols, 256)), dim3(256), 0, stream, x, rows, cols, ld, out,
+  hipLaunchKernelGGL(col_sum_k, dim3(cdiv(cols, 16)), dim3(256), 0, stream, x, rows, cols, ld, out,
                      beta);
   TMR_CHECK_LAUNCH("col_sum");
   return 0;

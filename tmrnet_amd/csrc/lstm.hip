@@ -8,11 +8,11 @@
 //             one GEMM each for dW_ih, dW_hh, dx and a column sum for the biases.
 //
 // Persistent geometry (hidden size 512): workgroup (jx, by) owns hidden units 8*jx..8*jx+7 -- the
-// 32 rows of W_hh (forward) / 32 columns of W_hh^T (backward) that feed them stay in LDS for all
-// steps -- and clips 16*by..16*by+15; 64 x ceil(b/16) workgroups, one per CU.  Consecutive steps
-// hand h_t (forward) / dgates_t (backward) between workgroups through HBM behind a grid barrier:
-// one monotonic counter, agent-scope release before the arrival and agent-scope acquire after
-// the wait (every spin bounded; a give-up sets the timeout word).  The launch is cooperative, so
+// 32 rows of W_hh (forward) / 8 columns of W_hh (backward) that feed them stay on the CU for all
+// steps, in registers -- and clips 16*by..16*by+15; 64 x ceil(b/16) workgroups, one per CU.  Consecutive steps
+// hand h_t (forward) / dgates_t (backward) between workgroups behind a grid barrier: write-through
+// (sc1) stores, one monotonic counter, sc1 loads (every spin bounded; a give-up sets the timeout
+// word).  The launch is cooperative, so
 // a grid that is not fully resident is refused at launch instead of deadlocking; it then falls
 // back to the per-step path (one gate GEMM + one cell kernel per step).
 #include "common.h"
@@ -24,33 +24,44 @@ constexpr int LH = 512;        // hidden size served by the persistent kernels
 constexpr int HU = 8;          // hidden units per workgroup
 constexpr int NGC = 4 * HU;    // gate columns per workgroup
 constexpr int BBC = 16;        // clips per workgroup
-constexpr int WLD = LH + 4;    // LDS row stride of the forward W_hh slice
-constexpr int CH = 512;        // backward: gate-gradient columns staged per chunk
-constexpr int TLD = 4 * LH + 4;  // LDS row stride of the backward W_hh^T slice
-constexpr int DLD = CH + 4;
-constexpr unsigned SPIN_LIMIT = 1u << 23;   // x s_sleep(2): ~0.5 s, then give up
+constexpr unsigned SPIN_LIMIT = 1u << 24;   // x s_sleep(1): ~0.5 s, then give up
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// Grid barrier number `target` / nwg.  sync[0] = arrival counter, sync[1] = timeout word; both
-// zeroed by the host before every launch.  Returns false after a give-up (then every workgroup
-// leaves its loop: the results are garbage and the timeout word says so).
+// Hand-off between steps (MI355X_MICROARCH.md, visibility: the counter row of the sc1 table).
+// The handed-off bytes (h_t forward, dgates_t backward) are stored write-through (sc1) and every
+// load of them in the kernel is an sc1 load, so no release / acquire fence is needed: each
+// storing wave drains its stores, the workgroup barrier joins them, ONE lane adds to the counter
+// and polls it (sc1 loads, bounded), the workgroup barrier releases the other waves.
+// sync[0] = arrival counter, sync[1] = timeout word; both zeroed by the host before every
+// launch.  Returns false after a give-up (every workgroup then leaves its loop: the results are
+// garbage and the timeout word says so).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store sc1
+}
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);   // aux 16 = sc1
+  return __builtin_bit_cast(float4, v);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
 __device__ bool grid_barrier(unsigned* sync, unsigned target) {
   gu32* cnt = (gu32*)sync;
   gu32* tmo = (gu32*)(sync + 1);
   __shared__ int ok_s;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its own stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its own sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     unsigned spins = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
       if (++spins > SPIN_LIMIT ||
           __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
         __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -58,8 +69,7 @@ __device__ bool grid_barrier(unsigned* sync, unsigned target) {
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only
     ok_s = ok;
   }
   __syncthreads();
@@ -68,91 +78,121 @@ __device__ bool grid_barrier(unsigned* sync, unsigned target) {
 
 // ---------------------------------------------------------------- forward recurrence
 // gx (b,t,4H): x W_ih^T + b_ih + b_hh.  Writes y (b,t,H) = h_t, and when given: cs (t,b,H) cell
-// states, acts (t,b,4H) gate activations (i,f,g,o) for the backward, cn (b,H).
+// states, acts (t,b,4H) gate activations (i,f,g,o) for the backward, hn / cn (b,H).
+// Thread (kg = tid / 32, c = tid % 32) keeps W_hh[row(c)][64 kg .. 64 kg + 63] in registers for
+// all steps (the slice never leaves the CU); h_{t-1} of the 16 clips is staged in LDS with one
+// batch of loads per thread; the 8 k-group partial dot products are added in a fixed order.
 __global__ __launch_bounds__(256) void lstm_rec_fwd_k(const float* __restrict__ gx,
                                                       const float* __restrict__ whh,
                                                       float* __restrict__ y, float* __restrict__ cs,
                                                       float* __restrict__ acts,
+                                                      float* __restrict__ hn,
                                                       float* __restrict__ cn, int B, int T,
                                                       unsigned* sync) {
-  __shared__ __attribute__((aligned(16))) float wsl[NGC * WLD];   // W_hh rows of this slice
-  __shared__ __attribute__((aligned(16))) float hs[BBC * WLD];    // h_{t-1} of this clip group
-  __shared__ float gs[BBC][NGC + 1];                               // gate pre-activations
+  constexpr int KG = 64;                 // k per register slice
+  constexpr int HLD = LH + 4 * (LH / KG);  // padded h row: +4 floats per 64 (bank spread)
+  __shared__ __attribute__((aligned(16))) float hs[BBC * HLD];
+  __shared__ float red[BBC][NGC][LH / KG + 1];   // partial dot products per k-group
+  __shared__ float gs[BBC][NGC + 1];              // gate pre-activations
   const int tid = threadIdx.x;
   const int j0 = blockIdx.x * HU;
   const int b0 = blockIdx.y * BBC;
   const int nwg = gridDim.x * gridDim.y;
-  // gate column c of this slice: gate q = c / HU, unit u = c % HU -> W_hh row q*H + j0 + u
-  for (int idx = tid; idx < NGC * (LH / 4); idx += 256) {
-    const int c = idx / (LH / 4), k4 = idx % (LH / 4);
-    const int row = (c / HU) * LH + j0 + (c % HU);
-    *reinterpret_cast<float4*>(&wsl[c * WLD + 4 * k4]) =
-        *reinterpret_cast<const float4*>(&whh[(long)row * LH + 4 * k4]);
+  const int c = tid & (NGC - 1), kg = tid / NGC;            // 32 columns x 8 k-groups
+  const int wrow = (c / HU) * LH + j0 + (c % HU);           // W_hh row of gate column c
+  float wreg[KG];
+#pragma unroll
+  for (int i = 0; i < KG; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(&whh[(long)wrow * LH + kg * KG + i]);
+    wreg[i] = v.x; wreg[i + 1] = v.y; wreg[i + 2] = v.z; wreg[i + 3] = v.w;
   }
-  // dot-product role: clip tb, gate columns 2*tc, 2*tc+1
-  const int tb = tid >> 4, tc = tid & 15;
-  const int gb = b0 + tb;
-  const int c0 = 2 * tc, c1 = 2 * tc + 1;
-  const int gcol0 = (c0 / HU) * LH + j0 + (c0 % HU);
-  const int gcol1 = (c1 / HU) * LH + j0 + (c1 % HU);
   // cell role (tid < 128): clip cb, unit cu; the cell state lives in a register for all steps
   const int cb = tid / HU, cu = tid % HU;
   const int cgb = b0 + cb, cj = j0 + cu;
   const bool cell = tid < BBC * HU && cgb < B;
   float creg = 0.f;
-  __syncthreads();
+  const __amdgpu_buffer_rsrc_t ry = rsrc(y, (uint32_t)((long)B * T * LH * 4));
   for (int t = 0; t < T; ++t) {
+    // this step's input projections, issued before the h_{t-1} hand-off loads
+    float gxv[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int o = tid + 256 * e;
+      const int bl = o / NGC, cc = o % NGC;
+      gxv[e] = b0 + bl < B
+                   ? gx[((long)(b0 + bl) * T + t) * (4 * LH) + (cc / HU) * LH + j0 + (cc % HU)]
+                   : 0.f;
+    }
     if (t > 0) {
-      for (int idx = tid; idx < BBC * (LH / 4); idx += 256) {
+      constexpr int NL = BBC * (LH / 4) / 256;   // float4 loads per thread (8)
+      float4 v[NL];
+#pragma unroll
+      for (int q = 0; q < NL; ++q) {
+        const int idx = tid + 256 * q;
         const int bl = idx / (LH / 4), k4 = idx % (LH / 4);
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (b0 + bl < B)
-          v = *reinterpret_cast<const float4*>(&y[((long)(b0 + bl) * T + (t - 1)) * LH + 4 * k4]);
-        *reinterpret_cast<float4*>(&hs[bl * WLD + 4 * k4]) = v;
+        const uint32_t off = (uint32_t)((((long)(b0 + bl) * T + (t - 1)) * LH + 4 * k4) * 4);
+        v[q] = ld_sc1(ry, b0 + bl < B ? off : 0x80000000u);   // out of range -> 0
+      }
+#pragma unroll
+      for (int q = 0; q < NL; ++q) {
+        const int idx = tid + 256 * q;
+        const int bl = idx / (LH / 4), k = 4 * (idx % (LH / 4));
+        *reinterpret_cast<float4*>(&hs[bl * HLD + k + 4 * (k / KG)]) = v[q];
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int bl = 0; bl < BBC; ++bl) {
+        const float* hr = &hs[bl * HLD + kg * (KG + 4)];
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < KG; i += 4) {
+          const float4 h4 = *reinterpret_cast<const float4*>(hr + i);
+          a = fmaf(h4.x, wreg[i], a); a = fmaf(h4.y, wreg[i + 1], a);
+          a = fmaf(h4.z, wreg[i + 2], a); a = fmaf(h4.w, wreg[i + 3], a);
+        }
+        red[bl][c][kg] = a;
       }
       __syncthreads();
     }
-    float a0 = 0.f, a1 = 0.f;
-    if (t > 0) {
-      const float* hrow = &hs[tb * WLD];
-      const float* w0 = &wsl[c0 * WLD];
-      const float* w1 = &wsl[c1 * WLD];
-#pragma unroll 8
-      for (int k = 0; k < LH; k += 4) {
-        const float4 h4 = *reinterpret_cast<const float4*>(hrow + k);
-        const float4 x0 = *reinterpret_cast<const float4*>(w0 + k);
-        const float4 x1 = *reinterpret_cast<const float4*>(w1 + k);
-        a0 = fmaf(h4.x, x0.x, a0); a0 = fmaf(h4.y, x0.y, a0);
-        a0 = fmaf(h4.z, x0.z, a0); a0 = fmaf(h4.w, x0.w, a0);
-        a1 = fmaf(h4.x, x1.x, a1); a1 = fmaf(h4.y, x1.y, a1);
-        a1 = fmaf(h4.z, x1.z, a1); a1 = fmaf(h4.w, x1.w, a1);
+    // gate pre-activations: thread -> (clip, 2 columns), k-groups added in order
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int o = tid + 256 * e;
+      const int bl = o / NGC, cc = o % NGC;
+      float a = 0.f;
+      if (t > 0) {
+#pragma unroll
+        for (int g = 0; g < LH / KG; ++g) a += red[bl][cc][g];
       }
-    }
-    if (gb < B) {
-      const float* g = gx + ((long)gb * T + t) * (4 * LH);
-      gs[tb][c0] = g[gcol0] + a0;
-      gs[tb][c1] = g[gcol1] + a1;
+      gs[bl][cc] = gxv[e] + a;
     }
     __syncthreads();
     if (cell) {
       const float ig = sigm(gs[cb][cu]), fg = sigm(gs[cb][HU + cu]);
       const float gg = tanhf(gs[cb][2 * HU + cu]), og = sigm(gs[cb][3 * HU + cu]);
       creg = fg * creg + ig * gg;
-      y[((long)cgb * T + t) * LH + cj] = og * tanhf(creg);
+      const float h = og * tanhf(creg);
+      st_sc1(&y[((long)cgb * T + t) * LH + cj], h);   // handed to every workgroup
       if (cs) cs[((long)t * B + cgb) * LH + cj] = creg;
       if (acts) {
         float* a = acts + ((long)t * B + cgb) * (4 * LH);
         a[cj] = ig; a[LH + cj] = fg; a[2 * LH + cj] = gg; a[3 * LH + cj] = og;
       }
+      if (t + 1 == T) {
+        if (hn) hn[(long)cgb * LH + cj] = h;
+        if (cn) cn[(long)cgb * LH + cj] = creg;
+      }
     }
     if (t + 1 < T && !grid_barrier(sync, (unsigned)((t + 1) * nwg))) return;
   }
-  if (cell && cn) cn[(long)cgb * LH + cj] = creg;
 }
 
 // ---------------------------------------------------------------- backward recurrence
 // dy (b,t,H): dL/dh_t from the output sequence.  Writes dg (b,t,4H) = dL/d(gate pre-activations)
 // and hprev (b,t,H) = h_{t-1} (0 at t = 0), the operand of dW_hh.
+// Thread (g = tid / 8, u = tid % 8) keeps W_hh[64 g .. 64 g + 63][j0 + u] in registers; the whole
+// dg_{t+1} row block of the 16 clips (16 x 2048) is staged in LDS with one batch of loads per
+// thread; the 32 partial sums per (clip, unit) are added in a fixed order.
 __global__ __launch_bounds__(256) void lstm_rec_bwd_k(const float* __restrict__ dy,
                                                       const float* __restrict__ whh,
                                                       const float* __restrict__ y,
@@ -161,67 +201,86 @@ __global__ __launch_bounds__(256) void lstm_rec_bwd_k(const float* __restrict__ 
                                                       float* __restrict__ dg,
                                                       float* __restrict__ hprev, int B, int T,
                                                       unsigned* sync) {
-  __shared__ __attribute__((aligned(16))) float wt[HU * TLD];     // W_hh[:, j0 + u] as rows u
-  __shared__ __attribute__((aligned(16))) float ds[BBC * DLD];    // one chunk of dg_{t+1}
-  __shared__ float part[BBC * HU][2];
+  constexpr int G4 = 4 * LH;               // gate columns (2048)
+  constexpr int KG = 64;                   // gate columns per register slice
+  constexpr int NG = G4 / KG;              // 32 slices
+  constexpr int DLDP = G4 + 4 * NG;        // padded dg row (+4 floats per 64: bank spread)
+  __shared__ __attribute__((aligned(16))) float ds[BBC * DLDP];
+  __shared__ float red[BBC * HU][NG + 1];
   const int tid = threadIdx.x;
   const int j0 = blockIdx.x * HU;
   const int b0 = blockIdx.y * BBC;
   const int nwg = gridDim.x * gridDim.y;
-  for (int idx = tid; idx < 4 * LH * HU; idx += 256) {
-    const int c = idx / HU, u = idx % HU;
-    wt[u * TLD + c] = whh[(long)c * LH + j0 + u];
-  }
-  // dot role: clip db, unit du, half dh of each staged chunk
-  const int dhalf = tid & 1, du = (tid >> 1) & (HU - 1), db = tid >> 4;
+  const int u = tid % HU, g = tid / HU;
+  float wreg[KG];
+#pragma unroll
+  for (int i = 0; i < KG; ++i) wreg[i] = whh[(long)(g * KG + i) * LH + j0 + u];
   // cell role (tid < 128)
   const int cb = tid / HU, cu = tid % HU;
   const int cgb = b0 + cb, cj = j0 + cu;
   const bool cell = tid < BBC * HU && cgb < B;
   float dc = 0.f;
-  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rdg = rsrc(dg, (uint32_t)((long)B * T * G4 * 4));
   for (int t = T - 1; t >= 0; --t) {
-    float acc = 0.f;
-    if (t + 1 < T) {
-      for (int cc0 = 0; cc0 < 4 * LH; cc0 += CH) {
-        for (int idx = tid; idx < BBC * (CH / 4); idx += 256) {
-          const int bl = idx / (CH / 4), k4 = idx % (CH / 4);
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (b0 + bl < B)
-            v = *reinterpret_cast<const float4*>(
-                &dg[((long)(b0 + bl) * T + (t + 1)) * (4 * LH) + cc0 + 4 * k4]);
-          *reinterpret_cast<float4*>(&ds[bl * DLD + 4 * k4]) = v;
-        }
-        __syncthreads();
-        const float* drow = &ds[db * DLD + dhalf * (CH / 2)];
-        const float* wrow = &wt[du * TLD + cc0 + dhalf * (CH / 2)];
-#pragma unroll 8
-        for (int k = 0; k < CH / 2; k += 4) {
-          const float4 d4 = *reinterpret_cast<const float4*>(drow + k);
-          const float4 w4 = *reinterpret_cast<const float4*>(wrow + k);
-          acc = fmaf(d4.x, w4.x, acc); acc = fmaf(d4.y, w4.y, acc);
-          acc = fmaf(d4.z, w4.z, acc); acc = fmaf(d4.w, w4.w, acc);
-        }
-        __syncthreads();
+    // this step's cell operands (written by the forward launch), issued before the hand-off loads
+    float dyv = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cv = 0.f, cp = 0.f, hp = 0.f;
+    if (cell) {
+      dyv = dy[((long)cgb * T + t) * LH + cj];
+      const float* a = acts + ((long)t * B + cgb) * G4;
+      ig = a[cj]; fg = a[LH + cj]; gg = a[2 * LH + cj]; og = a[3 * LH + cj];
+      cv = cs[((long)t * B + cgb) * LH + cj];
+      if (t > 0) {
+        cp = cs[((long)(t - 1) * B + cgb) * LH + cj];
+        hp = y[((long)cgb * T + (t - 1)) * LH + cj];
       }
     }
-    part[db * HU + du][dhalf] = acc;
-    __syncthreads();
+    if (t + 1 < T) {
+      constexpr int NL = BBC * (G4 / 4) / 256;   // float4 loads per thread (32)
+      float4 v[NL];
+#pragma unroll
+      for (int q = 0; q < NL; ++q) {
+        const int idx = tid + 256 * q;
+        const int bl = idx / (G4 / 4), k4 = idx % (G4 / 4);
+        const uint32_t off = (uint32_t)((((long)(b0 + bl) * T + (t + 1)) * G4 + 4 * k4) * 4);
+        v[q] = ld_sc1(rdg, b0 + bl < B ? off : 0x80000000u);
+      }
+#pragma unroll
+      for (int q = 0; q < NL; ++q) {
+        const int idx = tid + 256 * q;
+        const int bl = idx / (G4 / 4), k = 4 * (idx % (G4 / 4));
+        *reinterpret_cast<float4*>(&ds[bl * DLDP + k + 4 * (k / KG)]) = v[q];
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int bl = 0; bl < BBC; ++bl) {
+        const float* dr = &ds[bl * DLDP + g * (KG + 4)];
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < KG; i += 4) {
+          const float4 d4 = *reinterpret_cast<const float4*>(dr + i);
+          a = fmaf(d4.x, wreg[i], a); a = fmaf(d4.y, wreg[i + 1], a);
+          a = fmaf(d4.z, wreg[i + 2], a); a = fmaf(d4.w, wreg[i + 3], a);
+        }
+        red[bl * HU + u][g] = a;
+      }
+      __syncthreads();
+    }
     if (cell) {
-      float dh = dy[((long)cgb * T + t) * LH + cj] + (part[tid][0] + part[tid][1]);
-      const float* a = acts + ((long)t * B + cgb) * (4 * LH);
-      const float ig = a[cj], fg = a[LH + cj], gg = a[2 * LH + cj], og = a[3 * LH + cj];
-      const float c = cs[((long)t * B + cgb) * LH + cj];
-      const float cp = t > 0 ? cs[((long)(t - 1) * B + cgb) * LH + cj] : 0.f;
-      const float tc = tanhf(c);
+      float rec = 0.f;
+      if (t + 1 < T) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q) rec += red[tid][q];
+      }
+      const float dh = dyv + rec;
+      const float tc = tanhf(cv);
       const float dct = dh * og * (1.f - tc * tc) + dc;
-      float* d = dg + ((long)cgb * T + t) * (4 * LH);
-      d[cj] = dct * gg * ig * (1.f - ig);
-      d[LH + cj] = dct * cp * fg * (1.f - fg);
-      d[2 * LH + cj] = dct * ig * (1.f - gg * gg);
-      d[3 * LH + cj] = dh * tc * og * (1.f - og);
+      float* d = dg + ((long)cgb * T + t) * G4;
+      st_sc1(&d[cj], dct * gg * ig * (1.f - ig));            // handed to every workgroup
+      st_sc1(&d[LH + cj], dct * cp * fg * (1.f - fg));
+      st_sc1(&d[2 * LH + cj], dct * ig * (1.f - gg * gg));
+      st_sc1(&d[3 * LH + cj], dh * tc * og * (1.f - og));
       dc = dct * fg;
-      hprev[((long)cgb * T + t) * LH + cj] = t > 0 ? y[((long)cgb * T + (t - 1)) * LH + cj] : 0.f;
+      hprev[((long)cgb * T + t) * LH + cj] = hp;
     }
     if (t > 0 && !grid_barrier(sync, (unsigned)((T - t) * nwg))) return;
   }
@@ -294,7 +353,10 @@ TMR_API size_t tmr_lstm_ws_bytes(int b, int t, int i, int h) {
   return lstm_ws(b, t, i, h).total;
 }
 
-static bool lstm_persistent_shape(int b, int h) { return h == LH && b > 0; }
+// 32-bit buffer offsets in the persistent kernels' hand-off loads
+static bool lstm_persistent_shape(int b, int t, int h) {
+  return h == LH && b > 0 && (long)b * t * 4 * h * 4 < 0x80000000L;
+}
 
 TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float* w_ih,
                          const float* w_hh, const float* b_ih, const float* b_hh, float* y,
@@ -323,7 +385,7 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
   TMR_CHECK_LAUNCH("lstm bias");
   int rc = tmr_gemm_nt(b * t, 4 * h, i, x, i, w_ih, i, bias, gx, 4 * h, 0.f, stream);
   if (rc) return rc;
-  if (persist_allowed() && lstm_persistent_shape(b, h)) {
+  if (persist_allowed() && lstm_persistent_shape(b, t, h)) {
     unsigned* sync = (unsigned*)(w + L.sync);
     if (hipMemsetAsync(sync, 0, 16, stream) != hipSuccess) {
       tmr_set_error("tmr_lstm_fwd: memset failed");
@@ -331,20 +393,11 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
     }
     dim3 grid(LH / HU, cdiv(b, BBC));
     const float* gxc = gx;
-    void* args[] = {(void*)&gxc, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&cn,
-                    (void*)&b, (void*)&t, (void*)&sync};
+    void* args[] = {(void*)&gxc, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&hn,
+                    (void*)&cn, (void*)&b, (void*)&t, (void*)&sync};
     hipError_t e = hipLaunchCooperativeKernel((const void*)lstm_rec_fwd_k, grid, dim3(256), args,
                                               0, stream);
-    if (e == hipSuccess) {
-      if (hn) {
-        // h_n = y[:, t-1, :]
-        TMR_CHECK_ARG(hipMemcpy2DAsync(hn, (size_t)h * 4, y + (size_t)(t - 1) * h,
-                                       (size_t)t * h * 4, (size_t)h * 4, b,
-                                       hipMemcpyDeviceToDevice, stream) == hipSuccess,
-                      "tmr_lstm_fwd: h_n copy failed");
-      }
-      return 0;
-    }
+    if (e == hipSuccess) return 0;
     (void)hipGetLastError();   // not resident (cooperative check): per-step path below
   }
   // per-step path: gate GEMM + fused cell kernel per step
@@ -403,7 +456,7 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
     return 0;
   }
   bool done = false;
-  if (persist_allowed() && lstm_persistent_shape(b, h)) {
+  if (persist_allowed() && lstm_persistent_shape(b, t, h)) {
     unsigned* sync = (unsigned*)(w + L.sync);
     if (hipMemsetAsync(sync, 0, 16, stream) != hipSuccess) {
       tmr_set_error("tmr_lstm_bwd: memset failed");
