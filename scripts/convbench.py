@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--stats", action="store_true",
                     help="forward with the fused BatchNorm-statistics epilogue (as the train step)")
+    ap.add_argument("--pro", action="store_true",
+                    help="operand prologues as the folded train step uses them: BN+ReLU on the X "
+                         "operand (fwd, wgrad) and the BN backward on dY (dgrad, wgrad), every "
+                         "conv but the stem")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
@@ -56,14 +60,20 @@ def main():
         wk = torch.randn(cout, r, r, cs, device=dev)
         y = ops.conv_fwd(x, wk, st, pad)
         dy = torch.randn_like(y)
+        xpro = dpro = None
+        if args.pro and cin != 3:
+            xpro = (torch.rand(cs, device=dev) + 0.5, torch.randn(cs, device=dev) * 0.1)
+            dpro = (torch.randn_like(y), torch.randn(3, cout, device=dev))
         for kind in kinds:
             if kind == "dgrad" and cin == 3:
                 continue
-            fn = {"fwd": (lambda: ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin)) if args.stats
+            fn = {"fwd": (lambda: ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin, xpro=xpro))
+                  if (args.stats or xpro is not None)
                   else (lambda: ops.conv_fwd(x, wk, st, pad, out=y)),
                   "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x,
-                                                  beta=args.dgrad_beta),
-                  "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin)}[kind]
+                                                  beta=args.dgrad_beta, dpro=dpro),
+                  "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin, xpro=xpro,
+                                                  dpro=dpro)}[kind]
             fn()
             torch.cuda.synchronize()
             e0 = torch.cuda.Event(enable_timing=True)

@@ -469,3 +469,40 @@ def test_stem_bwd_maxpool_fused(dev):
     dy, dg, db = ops.bn_bwd_maxpool(dp, am, y, scale, shift, mean, inv, gamma)
     assert rel_err(dy.view(-1, c), dy_ref) < 1e-5
     assert rel_err(dg, dg_ref) < 1e-5 and rel_err(db, db_ref) < 1e-5
+
+
+def test_bn_fold_bit_identical(dev):
+    """Train step with the BatchNorm folded into the conv loaders (tmr_conv_prologue: BN+ReLU of
+    units 1-2 on the X operand, the BN backward on every dY operand) against the explicit passes
+    (tmr_bn_apply / tmr_bn_bwd_parts / tmr_bn_bwd): same operand values by construction, same
+    GEMM arithmetic -> logits, every gradient and the running statistics bit-identical."""
+    import tmrnet_amd
+    from tmrnet_amd import trunk
+    B, T, L = 2, 5, 7
+    g = torch.Generator().manual_seed(3)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)
+    lt = (torch.rand(B, L, 512, generator=g) * 2 - 1).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=g).to(dev)
+    res = {}
+    saved = trunk.FOLD_BN
+    try:
+        for fold in (True, False):
+            trunk.FOLD_BN = fold
+            torch.manual_seed(0)
+            m = tmrnet_amd.resnet_lstm(seq_len=T).to(dev).train()
+            m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+            m.forced_head_mask = torch.ones(B, 512, device=dev)
+            x4 = ops.crop_normalize(frames, off, T)
+            out = m(x4, lt)
+            tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels).backward()
+            torch.cuda.synchronize()
+            res[fold] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                         {n: b.clone() for n, b in m.named_buffers()})
+    finally:
+        trunk.FOLD_BN = saved
+    assert torch.equal(res[True][0], res[False][0])
+    for n in res[True][1]:
+        assert torch.equal(res[True][1][n], res[False][1][n]), n
+    for n in res[True][2]:
+        assert torch.equal(res[True][2][n], res[False][2][n]), n

@@ -28,6 +28,14 @@ class ConvDesc(ctypes.Structure):
 
 DP = ctypes.POINTER(ConvDesc)
 
+
+class ConvPrologue(ctypes.Structure):
+    """tmr_conv_prologue: BN(+ReLU) of the X operand / BN backward of the dY operand on load."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("x_scale", "x_shift", "dy_y", "dy_coef")]
+
+
+PP = ctypes.POINTER(ConvPrologue)
+
 _NL_FIELDS = ("w1", "b1", "w2", "b2", "w3", "b3", "ln_w", "ln_b", "w4", "b4")
 
 
@@ -49,6 +57,12 @@ SIGNATURES = {
     "tmr_conv2d_dgrad_bnbwd": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, P],
     "tmr_conv2d_wgrad_ws_bytes": [DP],
     "tmr_conv2d_wgrad": [DP, P, P, P, I, F, P, SZ, P],
+    "tmr_conv2d_fwd_bnstats_pro": [DP, P, P, P, P, SZ, PP, P],
+    "tmr_conv2d_dgrad_pro": [DP, P, P, P, F, PP, P],
+    "tmr_conv2d_dgrad_bnbwd_pro": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, PP, P],
+    "tmr_conv2d_wgrad_pro": [DP, P, P, P, I, F, P, SZ, PP, P],
+    "tmr_bn_bwd_coefs": [P, I, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
     "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],
     "tmr_gemm_tn": [I, I, I, P, I, P, I, P, I, F, P],

@@ -818,3 +818,58 @@ TMR_API int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, 
   TMR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }
+
+// ---- BatchNorm backward as per-channel coefficients (the apply folded into the consumer GEMMs) --
+// dy = fmaf(A[c], g, fmaf(B[c], y, C[c])) -- the arithmetic of bn_bwd_apply -- is evaluated by
+// the dgrad / wgrad operand loaders (tmr_conv_prologue.dy_coef = coef [3][c]), so dy is never
+// written.
+
+TMR_API int tmr_bn_bwd_coefs(const void* parts, int nparts, const float* save_mean,
+                             const float* save_invstd, const float* gamma, float* coef,
+                             float* dgamma, float* dbeta, int rows, int c, void* ws,
+                             size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows > 0 && nparts > 0,
+                "tmr_bn_bwd_coefs: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
+  TMR_CHECK_ARG(parts && save_mean && save_invstd && coef, "tmr_bn_bwd_coefs: null operand");
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_bn_parts_ws_bytes(nparts, c),
+                "tmr_bn_bwd_coefs: workspace too small (need tmr_bn_parts_ws_bytes)");
+  const SlabPlan sp = slab_plan(nparts, c);
+  double* slabs = (double*)ws;
+  hipLaunchKernelGGL(parts_slab_k<1>, dim3(sp.groups, sp.nslabs), dim3(256), 0, stream, parts,
+                     nparts, c, sp.rows, slabs);
+  TMR_CHECK_LAUNCH("bn_parts_slab");
+  hipLaunchKernelGGL(bwd_final_slabs_k, dim3(sp.groups), dim3(SLAB_CH * SLAB_PH), 0, stream,
+                     (const double*)slabs, sp.nslabs, rows, c, save_mean, save_invstd, gamma,
+                     dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, const float* scale,
+                                   const float* shift, const float* save_mean,
+                                   const float* save_invstd, const float* gamma, float* coef,
+                                   float* dgamma, float* dbeta, int rows, int c, int relu,
+                                   void* ws, size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4, "tmr_bn_bwd_coefs_dense: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(rows > 0, "tmr_bn_bwd_coefs_dense: empty input");
+  TMR_CHECK_ARG(g && y && save_mean && save_invstd && coef, "tmr_bn_bwd_coefs_dense: null operand");
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd_coefs_dense: workspace too small");
+  TMR_CHECK_ARG(!relu || z || (scale && shift),
+                "tmr_bn_bwd_coefs_dense: relu backward needs the saved output z or the forward scale/shift");
+  Plan p = make_plan(rows, c);
+  double* part = (double*)ws;
+  const dim3 pg(p.nrb, p.cblocks);
+  // the ReLU mask is applied to g in place (the masked gradient is the consumers' dY operand
+  // and, for a residual unit, the identity branch's gradient)
+  if (relu && z)
+    hipLaunchKernelGGL((bn_bwd_partial<1, true>), pg, dim3(NT), 0, stream, g, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_partial<2, true>), pg, dim3(NT), 0, stream, g, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial<0>), pg, dim3(NT), 0, stream, g, y, z, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_bwd_partial");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  return 0;
+}

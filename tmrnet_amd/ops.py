@@ -7,7 +7,7 @@ anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 """
 import torch
 
-from ._lib import call, query, stream_ptr, ConvDesc
+from ._lib import call, query, stream_ptr, ConvDesc, ConvPrologue
 import ctypes
 
 f32 = torch.float32
@@ -124,8 +124,22 @@ def conv_fwd_fused(x, w_krsc, stride, pad, scale, shift, residual=None, relu=Tru
     return out
 
 
-def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32"):
-    """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts)."""
+def _prologue(xpro=None, dpro=None):
+    """tmr_conv_prologue from (scale, shift) of the X operand's producer BN+ReLU and/or (y, coef)
+    of this conv's BN backward; None when neither is given."""
+    if xpro is None and dpro is None:
+        return None
+    p = ConvPrologue()
+    if xpro is not None:
+        p.x_scale, p.x_shift = _req(xpro[0], "x_scale").data_ptr(), _req(xpro[1], "x_shift").data_ptr()
+    if dpro is not None:
+        p.dy_y, p.dy_coef = _req(dpro[0], "dy_y").data_ptr(), _req(dpro[1], "dy_coef").data_ptr()
+    return p
+
+
+def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32", xpro=None):
+    """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts).
+    xpro = (scale, shift): x is a pre-BN tensor read as relu(x*scale + shift) (0 at padding)."""
     _req(x, "x"); _req(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
@@ -137,8 +151,13 @@ def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32
     with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
                (n, h, w, c, k, r, stride),
                4 * (n * h * w * c + k * r * s * c + n * d.ho * d.wo * k) + stats.numel() * 4):
-        call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
-             ctypes.c_size_t(stats.numel() * 4), stream_ptr())
+        pro = _prologue(xpro)
+        if pro is None:
+            call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
+                 ctypes.c_size_t(stats.numel() * 4), stream_ptr())
+        else:
+            call("tmr_conv2d_fwd_bnstats_pro", ctypes.byref(d), x, w_krsc, out, stats,
+                 ctypes.c_size_t(stats.numel() * 4), ctypes.byref(pro), stream_ptr())
     return out, stats, nparts
 
 
@@ -154,8 +173,11 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
     return mean, inv, scale, shift
 
 
-def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, math="fp32"):
-    """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices)."""
+def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, math="fp32",
+               dpro=None):
+    """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices).
+    dpro = (y, coef): dy is the masked BN-output gradient g, read as the BN backward
+    A*g + B*y + C (tmr_bn_bwd_coefs)."""
     _req(w_krsc, "w")
     n, ho, wo, k = dy.shape
     k2, r, s, c = w_krsc.shape
@@ -167,13 +189,19 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
-               4 * (n * ho * wo * k + k * r * s * c + n * h * w * c * (2 if beta else 1))):
-        call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
+               4 * (n * ho * wo * k * (2 if dpro is not None else 1) + k * r * s * c
+                    + n * h * w * c * (2 if beta else 1))):
+        pro = _prologue(None, dpro)
+        if pro is None:
+            call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
+        else:
+            call("tmr_conv2d_dgrad_pro", ctypes.byref(d), dy, w_krsc, out, float(beta),
+                 ctypes.byref(pro), stream_ptr())
     return out
 
 
 def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scale=None,
-                     shift=None, out=None, beta=0.0, math="fp32"):
+                     shift=None, out=None, beta=0.0, math="fp32", dpro=None):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts)."""
     _req(w_krsc, "w"); _req(y, "y"); _req(mean, "mean")
@@ -193,10 +221,17 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
         raise RuntimeError("tmr_conv2d_dgrad_bnbwd_parts failed")
     parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
-               4 * (n * ho * wo * k + k * r * s * c + n * h * w * c * (3 if beta else 2)
-                    + (n * h * w * c if z is not None else 0))):
-        call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z, scale,
-             shift, mean, int(mask), parts, ctypes.c_size_t(parts.numel() * 4), stream_ptr())
+               4 * (n * ho * wo * k * (2 if dpro is not None else 1) + k * r * s * c
+                    + n * h * w * c * (3 if beta else 2) + (n * h * w * c if z is not None else 0))):
+        pro = _prologue(None, dpro)
+        if pro is None:
+            call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z,
+                 scale, shift, mean, int(mask), parts, ctypes.c_size_t(parts.numel() * 4),
+                 stream_ptr())
+        else:
+            call("tmr_conv2d_dgrad_bnbwd_pro", ctypes.byref(d), dy, w_krsc, out, float(beta), y,
+                 z, scale, shift, mean, int(mask), parts, ctypes.c_size_t(parts.numel() * 4),
+                 ctypes.byref(pro), stream_ptr())
     return out, parts, nparts
 
 
@@ -213,6 +248,34 @@ def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma):
     return dy, dgamma, dbeta
 
 
+def bn_bwd_coefs(parts, nparts, mean, inv, gamma, rows):
+    """BN backward coefficients from conv_dgrad_bnbwd partials -> (coef [3][c], dgamma, dbeta);
+    the consumers apply dy = A*g + B*y + C on load (dpro=(y, coef))."""
+    c = mean.shape[0]
+    coef = _empty((3, c), mean)
+    dgamma = _empty((c,), mean); dbeta = _empty((c,), mean)
+    nb = query("tmr_bn_parts_ws_bytes", int(nparts), c)
+    ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=mean.device)
+    call("tmr_bn_bwd_coefs", parts, int(nparts), mean, inv, gamma, coef, dgamma, dbeta, int(rows),
+         c, ws, ctypes.c_size_t(ws.numel() * 8), stream_ptr())
+    return coef, dgamma, dbeta
+
+
+def bn_bwd_coefs_dense(g, y, z, scale, shift, mean, inv, gamma, relu):
+    """BN backward coefficients from the output gradient g itself (one reduction pass over g and
+    y); with relu, g is masked IN PLACE (z > 0, or y*scale+shift > 0 when z is None).
+    -> (coef [3][c], dgamma, dbeta)."""
+    c = y.shape[-1]
+    rows = y.numel() // c
+    _req(g, "g"); _req(y, "y")
+    coef = _empty((3, c), y)
+    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
+    ws, nb = _bn_ws(rows, c, y.device)
+    call("tmr_bn_bwd_coefs_dense", g, y, z, scale, shift, mean, inv, gamma, coef, dgamma, dbeta,
+         rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
+    return coef, dgamma, dbeta
+
+
 def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma):
     """BN backward from conv_dgrad_bnbwd partials: g already masked -> (dy, dgamma, dbeta)."""
     c = y.shape[-1]
@@ -227,8 +290,10 @@ def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma):
 
 
 def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None,
-               math="fp32"):
-    """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW (x/dy may be channel slices)."""
+               math="fp32", xpro=None, dpro=None):
+    """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW (x/dy may be channel slices).
+    xpro = (scale, shift): x read as relu(x*scale + shift); dpro = (y, coef): dy read as the BN
+    backward A*dy + B*y + C."""
     n, h, w, c = x.shape
     k = dy.shape[3]
     c_real = c if c_real is None else c_real
@@ -242,9 +307,15 @@ def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=
     ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
     with _prof("conv_wgrad" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * c_real,
                (n, h, w, c, k, r, stride),
-               4 * (n * h * w * c + n * d.ho * d.wo * k + k * r * s * c_real)):
-        call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,
-             ctypes.c_size_t(ws.numel() * 4), stream_ptr())
+               4 * (n * h * w * c + n * d.ho * d.wo * k * (2 if dpro is not None else 1)
+                    + k * r * s * c_real)):
+        pro = _prologue(xpro, dpro)
+        if pro is None:
+            call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,
+                 ctypes.c_size_t(ws.numel() * 4), stream_ptr())
+        else:
+            call("tmr_conv2d_wgrad_pro", ctypes.byref(d), x, dy, out, int(c_real), float(beta),
+                 ws, ctypes.c_size_t(ws.numel() * 4), ctypes.byref(pro), stream_ptr())
     return out
 
 

@@ -76,13 +76,30 @@ def _bn_momentum(bn):
     return bn.momentum
 
 
+# Train-mode BatchNorm folding (TMR_FOLD_BN=1; off by default): the BN+ReLU outputs of each
+# Bottleneck's first two units are never written -- the next conv reads the pre-BN y through an
+# X-operand prologue (tmr_conv_prologue) in its forward and wgrad loaders -- and no BatchNorm
+# backward writes dy: the conv's dgrad and wgrad read the masked gradient g and y through a
+# dY-operand prologue with per-channel coefficients.  Bit-identical to the explicit passes
+# (tests/test_kernels_gpu.py::test_bn_fold_bit_identical), but measured slower on MI355X: the
+# prologue costs the MFMA-bound fp32 GEMMs more (wgrad +21 ms, dgrad +12 ms, fwd +6 ms per step,
+# profiles/r2/convbench_fold/) than the HBM-bound passes it removes (~17 ms) -- C2 210 vs 181
+# ms/step.  Kept for the bf16 path and for A/B measurements.
+FOLD_BN = os.environ.get("TMR_FOLD_BN", "0") == "1"
+
+
 def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
              defer=False, branch=None, nbt=None):
     """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z.
 
     Train mode only: ``defer`` returns (y, scale, shift) instead of applying the BN -- the
     consumer applies it on load (the downsample branch inside its block's BN3 pass, the stem
-    inside the maxpool); ``branch`` = such a deferred (y, scale, shift) used as the residual."""
+    inside the maxpool, with FOLD_BN the next conv's loaders); ``branch`` = such a deferred
+    (y, scale, shift) used as the residual; ``x`` may itself be a deferred (y, scale, shift) of a
+    ReLU unit, read through the conv's X-operand prologue."""
+    xpro = None
+    if isinstance(x, tuple):
+        x, xpro = x[0], (x[1], x[2])
     w = conv.weight
     k, c, r, s = w.shape
     cs = x.shape[3]
@@ -92,7 +109,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs)
     if training:
         # batch statistics come out of the conv epilogue (no separate pass over y)
-        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c, math=math)
+        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c, math=math,
+                                                xpro=xpro)
         mean, inv, scale, shift = ops.bn_finalize(
             stats, nparts, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
             bn.running_var, _bn_momentum(bn), bn.eps)
@@ -102,6 +120,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         else:
             nbt.append(bn.num_batches_tracked)
     else:
+        if xpro is not None:
+            raise RuntimeError("deferred BatchNorm inputs exist in train mode only")
         # eval: running-stat BN, residual and ReLU in the conv epilogue (one launch, no y pass;
         # same arithmetic as conv_fwd + bn_apply)
         scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
@@ -117,7 +137,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     if recs is not None:
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
         has_res = residual is not None or branch is not None
-        recs.append({"x": x, "wk": wk, "y": y, "z": z if has_res else None,
+        recs.append({"x": x, "xpro": xpro, "wk": wk, "y": y, "z": z if has_res else None,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
                      "c_real": c, "math": math})
@@ -137,11 +157,25 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     pool: (pooled gradient, argmax) of the maxpool that consumed this unit's output (the stem);
     dz is then gathered from it inside the BN backward."""
     conv, bn = rec["conv"], rec["bn"]
+    dpro = None    # (y, coef): dy = A*g + B*y + C evaluated by the consumer convs' loaders
     if pool is not None:
         # the stem: maxpool backward + ReLU mask + BN backward without writing dz
         dy, dg, db = ops.bn_bwd_maxpool(pool[0], pool[1], rec["y"], rec["scale"], rec["shift"],
                                         rec["mean"], rec["inv"], bn.weight.detach())
         dres = None
+    elif FOLD_BN:
+        rows = rec["y"].numel() // rec["y"].shape[-1]
+        if parts is not None:   # dz already masked by the producing dgrad's epilogue
+            coef, dg, db = ops.bn_bwd_coefs(parts[0], parts[1], rec["mean"], rec["inv"],
+                                            bn.weight.detach(), rows)
+        else:                   # one reduction pass; the ReLU mask is applied to dz in place
+            if want_dres and not dres_inplace:
+                raise RuntimeError("folded BN backward: the identity gradient is dz itself")
+            coef, dg, db = ops.bn_bwd_coefs_dense(dz, rec["y"], rec["z"], rec["scale"],
+                                                  rec["shift"], rec["mean"], rec["inv"],
+                                                  bn.weight.detach(), rec["relu"])
+        dy, dpro = dz, (rec["y"], coef)
+        dres = dz if want_dres else None
     elif parts is not None:
         dy, dg, db = ops.bn_bwd_parts(dz, rec["y"], parts[0], parts[1], rec["mean"], rec["inv"],
                                       bn.weight.detach())
@@ -156,7 +190,8 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     x = rec["x"]
     k, c, r, s = conv.weight.shape
     grads[conv.weight] = ops.conv_wgrad(x, dy, r, s, rec["stride"], rec["pad"],
-                                        c_real=rec["c_real"], math=rec["math"])
+                                        c_real=rec["c_real"], math=rec["math"],
+                                        xpro=rec.get("xpro"), dpro=dpro)
     dx, fused = None, None
     if need_dx:
         hw = (x.shape[1], x.shape[2])
@@ -166,11 +201,11 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
             dx, pp, npp = ops.conv_dgrad_bnbwd(dy, rec["wk"], hw, rec["stride"], rec["pad"],
                                                p["y"], p["mean"], mask, z=p["z"],
                                                scale=p["scale"], shift=p["shift"], out=dx_out,
-                                               beta=dx_beta, math=rec["math"])
+                                               beta=dx_beta, math=rec["math"], dpro=dpro)
             fused = (pp, npp)
         else:
             dx = ops.conv_dgrad(dy, rec["wk"], hw, rec["stride"], rec["pad"], out=dx_out,
-                                beta=dx_beta, math=rec["math"])
+                                beta=dx_beta, math=rec["math"], dpro=dpro)
     return dx, dres, fused
 
 
@@ -201,10 +236,11 @@ class TrunkFn(torch.autograd.Function):
         for layer in layers:
             for blk in layer:
                 brec = [] if keep else None
+                fold = training and FOLD_BN
                 z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt,
-                              nbt=nbt)
+                              nbt=nbt, defer=fold)
                 z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec,
-                              math=mt, nbt=nbt)
+                              math=mt, nbt=nbt, defer=fold)
                 if blk.downsample is not None:
                     # train: the branch's BN is applied inside the BN3 pass (bn_apply2)
                     idn = _conv_bn(h, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
