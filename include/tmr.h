@@ -55,9 +55,18 @@ typedef struct tmr_conv_desc {
   int max_frames;         /* frames per kernel launch, 0 = automatic.  Operands of one launch
                              must stay < 2 GiB (32-bit buffer offsets): larger batches run as
                              consecutive frame chunks (wgrad accumulates them in order) */
+  int io;                 /* TMR_MATH_BF16 only: operands stored as bf16 (2-byte elements) --
+                             TMR_IO_X_BF16 the input x (fwd A, wgrad B), TMR_IO_W_BF16 the KRSC
+                             weights (fwd / dgrad B), TMR_IO_DY_BF16 the output gradient dy (dgrad
+                             / wgrad A).  Exact: the bf16 math rounds those operands to bf16 (RNE)
+                             anyway, so a tensor consumed only as a conv operand may be stored
+                             rounded.  Outputs (y, dx, dw) stay fp32. */
 } tmr_conv_desc;
 #define TMR_MATH_F32 0
 #define TMR_MATH_BF16 1
+#define TMR_IO_X_BF16 1
+#define TMR_IO_W_BF16 2
+#define TMR_IO_DY_BF16 4
 
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
 int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
@@ -253,6 +262,28 @@ int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* sca
                const float* shift, const float* save_mean, const float* save_invstd,
                const float* gamma, float* dy, float* dres, float* dgamma, float* dbeta, int rows,
                int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* bf16-output forms (out_bf16 = 1: the output tensor holds bf16, RNE -- the rounding the bf16
+ * conv loaders apply; for tensors consumed only as bf16-math conv operands, TMR_IO_*_BF16):
+ * z of a non-residual BN+ReLU (tmr_bn_apply), dy of the BatchNorm backward (tmr_bn_bwd_parts,
+ * tmr_bn_bwd, tmr_bn_bwd_maxpool; dres, dgamma, dbeta stay fp32), KRSC weights. */
+int tmr_bn_apply_x(const float* y, const float* scale, const float* shift, const float* residual,
+                   void* z, int rows, int c, int relu, int out_bf16, hipStream_t stream);
+int tmr_bn_bwd_parts_x(const float* g, const float* y, const void* parts, int nparts,
+                       const float* save_mean, const float* save_invstd, const float* gamma,
+                       void* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
+                       size_t ws_bytes, int out_bf16, hipStream_t stream);
+int tmr_bn_bwd_x(const float* dz, const float* y, const float* z, const float* scale,
+                 const float* shift, const float* save_mean, const float* save_invstd,
+                 const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta, int rows,
+                 int c, int relu, void* ws, size_t ws_bytes, int out_bf16, hipStream_t stream);
+int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho,
+                         int wo, const float* y, const float* scale, const float* shift,
+                         const float* save_mean, const float* save_invstd, const float* gamma,
+                         void* dy, float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                         int out_bf16, hipStream_t stream);
+int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, int r, int s, int cpad,
+                              int out_bf16, hipStream_t stream);
 
 /* ---------------- pooling (pool_layout.hip) --------------------------------------- */
 /* MaxPool2d(3,2,1) of share.maxpool (train_only_non-local_pretrained.py:207), NHWC */

@@ -45,6 +45,8 @@ def main():
                     help="operand prologues as the folded train step uses them: BN+ReLU on the X "
                          "operand (fwd, wgrad) and the BN backward on dY (dgrad, wgrad), every "
                          "conv but the stem")
+    ap.add_argument("--math", choices=["fp32", "bf16"], default="fp32",
+                    help="conv operand precision (bf16 = the C4/C5 configs)")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
@@ -67,13 +69,15 @@ def main():
         for kind in kinds:
             if kind == "dgrad" and cin == 3:
                 continue
-            fn = {"fwd": (lambda: ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin, xpro=xpro))
+            mt = args.math
+            fn = {"fwd": (lambda: ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin, xpro=xpro,
+                                                       math=mt))
                   if (args.stats or xpro is not None)
-                  else (lambda: ops.conv_fwd(x, wk, st, pad, out=y)),
+                  else (lambda: ops.conv_fwd(x, wk, st, pad, out=y, math=mt)),
                   "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x,
-                                                  beta=args.dgrad_beta, dpro=dpro),
+                                                  beta=args.dgrad_beta, dpro=dpro, math=mt),
                   "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin, xpro=xpro,
-                                                  dpro=dpro)}[kind]
+                                                  dpro=dpro, math=mt)}[kind]
             fn()
             torch.cuda.synchronize()
             e0 = torch.cuda.Event(enable_timing=True)

@@ -170,3 +170,88 @@ def test_conv_bf16_all_resnet50_shapes(dev):
         w16 = ops.conv_wgrad(xd, dy, r, r, st, pad, c_real=cin, math="bf16")
         w32 = ops.conv_wgrad(xd, dy, r, r, st, pad, c_real=cin)
         assert rel_err(w16, w32) < 5e-6, ("wgrad", shp)
+
+
+@pytest.mark.parametrize("backbone,time_conv", [("resnet50", False)])
+def test_bf16_storage_bit_identical(dev, backbone, time_conv):
+    """bf16 storage of the conv-operand-only tensors (KRSC weights, non-residual BN+ReLU outputs,
+    BatchNorm-backward outputs; tmr_conv_desc.io) against fp32 storage of the same bf16-math
+    step: the convs round those operands to bf16 (RNE) either way, so the logits, every
+    gradient and the running statistics are bit-identical."""
+    from tmrnet_amd import trunk
+    B, T, L = 2, 5, 7
+    frames, off, lt, labels = _inputs(B, T, L, seed=51)
+    res = {}
+    saved = trunk.BF16_STORE
+    try:
+        for store in (True, False):
+            trunk.BF16_STORE = store
+            torch.manual_seed(52)
+            m = tmrnet_amd.resnet_lstm(seq_len=T, time_conv=time_conv, backbone=backbone,
+                                       precision="bf16").to(dev).train()
+            m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+            m.forced_head_mask = torch.ones(B, 512, device=dev)
+            x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+            out = m(x4, lt.to(dev))
+            tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels.to(dev)).backward()
+            torch.cuda.synchronize()
+            res[store] = (out.detach().clone(),
+                          {n: p.grad.clone() for n, p in m.named_parameters()},
+                          {n: b.clone() for n, b in m.named_buffers()})
+            if store:   # eval mode (fused conv epilogue) with bf16 weights
+                m.eval()
+                with torch.no_grad():
+                    res["eval16"] = m(x4, lt.to(dev)).clone()
+            else:
+                m.eval()
+                with torch.no_grad():
+                    res["eval32"] = m(x4, lt.to(dev)).clone()
+    finally:
+        trunk.BF16_STORE = saved
+    assert torch.equal(res[True][0], res[False][0])
+    for n in res[True][1]:
+        assert torch.equal(res[True][1][n], res[False][1][n]), n
+    for n in res[True][2]:
+        assert torch.equal(res[True][2][n], res[False][2][n]), n
+    assert torch.equal(res["eval16"], res["eval32"])
+
+
+def test_bf16_storage_conv_kernels(dev):
+    """Each bf16-stored operand combination (tmr_conv_desc.io) against the same conv with the
+    operands stored fp32 (already bf16-representable): bit-identical (same rounding, same
+    arithmetic), on every distinct ResNet-50 shape at 2 frames, incl. the stem and strided 1x1 /
+    3x3 convs (dgrad parity classes) and frame-chunked launches."""
+    from scripts.convbench import resnet50_convs
+    g = torch.Generator().manual_seed(61)
+    saved = ops.MAX_FRAMES
+    try:
+        for mf in (0, 1):
+            ops.MAX_FRAMES = mf
+            for shp in sorted(set(resnet50_convs(2))):
+                n, h, w, cin, cout, r, st, pad = shp
+                cs = 4 if cin == 3 else cin
+                x = _r(torch.randn(n, h, w, cs, generator=g))
+                if cin == 3:
+                    x[..., 3] = 0
+                wt = torch.randn(cout, cin, r, r, generator=g) / (cin * r * r) ** 0.5
+                xd, wd = x.to(dev), wt.to(dev)
+                w32 = ops.weight_to_krsc(wd, cpad=cs)
+                w16 = ops.weight_to_krsc(wd, cpad=cs, bf16=True)
+                assert torch.equal(w16.float(), _r(w32.cpu()).to(dev)), shp
+                x16 = xd.to(torch.bfloat16)
+                xin = xd if cin == 3 else x16     # the stem input stays fp32 (VAR 1 gather)
+                y32, _, _ = ops.conv_fwd_bnstats(xd, w32, st, pad, c_real=cin, math="bf16")
+                y16, _, _ = ops.conv_fwd_bnstats(xin, w16, st, pad, c_real=cin, math="bf16")
+                assert torch.equal(y16, y32), ("fwd", shp, mf)
+                dy = _r(torch.randn(y32.shape, generator=g)).to(dev)
+                dy16 = dy.to(torch.bfloat16)
+                if cin != 3:
+                    d32 = ops.conv_dgrad(dy, w32, (h, w), st, pad, math="bf16")
+                    d16 = ops.conv_dgrad(dy16, w16, (h, w), st, pad, math="bf16")
+                    assert torch.equal(d16, d32), ("dgrad", shp, mf)
+                for xa in ((xd, x16) if cin != 3 else (xd,)):
+                    g32 = ops.conv_wgrad(xd, dy, r, r, st, pad, c_real=cin, math="bf16")
+                    g16 = ops.conv_wgrad(xa, dy16, r, r, st, pad, c_real=cin, math="bf16")
+                    assert torch.equal(g16, g32), ("wgrad", shp, mf, xa.dtype)
+    finally:
+        ops.MAX_FRAMES = saved

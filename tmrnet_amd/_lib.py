@@ -23,7 +23,7 @@ SZ = ctypes.c_size_t
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "pad_w",
-                 "x_ld", "y_ld", "math", "max_frames")]
+                 "x_ld", "y_ld", "math", "max_frames", "io")]
 
 
 DP = ctypes.POINTER(ConvDesc)
@@ -62,6 +62,11 @@ SIGNATURES = {
     "tmr_conv2d_dgrad_bnbwd_pro": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, PP, P],
     "tmr_conv2d_wgrad_pro": [DP, P, P, P, I, F, P, SZ, PP, P],
     "tmr_bn_bwd_coefs": [P, I, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_apply_x": [P, P, P, P, P, I, I, I, I, P],
+    "tmr_bn_bwd_parts_x": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, I, P],
+    "tmr_bn_bwd_x": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, I, P],
+    "tmr_bn_bwd_maxpool_x": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, I, P],
+    "tmr_weight_oihw_to_krsc_x": [P, P, I, I, I, I, I, I, P],
     "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
     "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],

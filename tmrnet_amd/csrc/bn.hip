@@ -146,10 +146,21 @@ __global__ void bn_eval_params_k(const float* gamma, const float* beta, const fl
   shift[ch] = b - rm[ch] * g * inv;
 }
 
-template <bool RES, bool RELU>
+// 4 values to 4 consecutive elements of an fp32 or bf16 (RNE, the conv loaders' rounding) tensor
+__device__ __forceinline__ void st4(float* p, long i4, float4 v) {
+  reinterpret_cast<float4*>(p)[i4] = v;
+}
+__device__ __forceinline__ void st4(__bf16* p, long i4, float4 v) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t a = {(__bf16)v.x, (__bf16)v.y}, b = {(__bf16)v.z, (__bf16)v.w};
+  reinterpret_cast<uint2*>(p)[i4] =
+      make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+}
+
+template <bool RES, bool RELU, typename TZ = float>
 __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift,
-                                                 const float* __restrict__ res, float* __restrict__ z,
+                                                 const float* __restrict__ res, TZ* __restrict__ z,
                                                  long n4, int c4) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cc = (int)(i % c4) * 4;
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, co
     if (RELU) {
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
     }
-    reinterpret_cast<float4*>(z)[i] = v;
+    st4(z, i, v);
   }
 }
 
@@ -304,12 +315,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
   }
 }
 
-template <int MASK, bool DRES>
+template <int MASK, bool DRES, typename TD = float>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const float* __restrict__ y,
                                                    const float* __restrict__ z,
                                                    const float* __restrict__ scale,
                                                    const float* __restrict__ shift,
-                                                   const float* __restrict__ coef, float* __restrict__ dy,
+                                                   const float* __restrict__ coef, TD* __restrict__ dy,
                                                    float* __restrict__ dres, long n4, int c4) {
   const int c = c4 * 4;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
@@ -329,7 +340,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
     o.y = fmaf(A.y, g.y, fmaf(B.y, v.y, C.y));
     o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
     o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
-    reinterpret_cast<float4*>(dy)[i] = o;
+    st4(dy, i, o);
   }
 }
 
@@ -565,11 +576,12 @@ __global__ __launch_bounds__(NT) void stem_bwd_partial_pooled(
   }
 }
 
+template <typename TD>
 __global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const float* __restrict__ y,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift,
                                                      const float* __restrict__ coef,
-                                                     float* __restrict__ dy, long n4, int c4) {
+                                                     TD* __restrict__ dy, long n4, int c4) {
   const int c = c4 * 4;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cq = (int)(i % c4);
@@ -586,7 +598,7 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const flo
     o.y = fmaf(A.y, g.y, fmaf(B.y, v.y, C.y));
     o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
     o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
-    reinterpret_cast<float4*>(dy)[i] = o;
+    st4(dy, i, o);
   }
 }
 
@@ -675,10 +687,24 @@ TMR_API int tmr_bn_eval_params(const float* gamma, const float* beta, const floa
 TMR_API int tmr_bn_apply(const float* y, const float* scale, const float* shift,
                          const float* residual, float* z, int rows, int c, int relu,
                          hipStream_t stream) {
+  return tmr_bn_apply_x(y, scale, shift, residual, z, rows, c, relu, 0, stream);
+}
+
+TMR_API int tmr_bn_apply_x(const float* y, const float* scale, const float* shift,
+                           const float* residual, void* zv, int rows, int c, int relu,
+                           int out_bf16, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_bn_apply: channels %d must be a multiple of 4", c);
   long n4 = (long)rows * c / 4;
   int nb = ew_blocks(n4);
   int c4 = c / 4;
+  if (out_bf16) {
+    TMR_CHECK_ARG(!residual, "tmr_bn_apply_x: a bf16 output is for conv-operand-only tensors (no residual)");
+    if (relu) hipLaunchKernelGGL((bn_apply_k<false, true, __bf16>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, (__bf16*)zv, n4, c4);
+    else hipLaunchKernelGGL((bn_apply_k<false, false, __bf16>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, (__bf16*)zv, n4, c4);
+    TMR_CHECK_LAUNCH("bn_apply");
+    return 0;
+  }
+  float* z = (float*)zv;
   if (residual) {
     if (relu) hipLaunchKernelGGL((bn_apply_k<true, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
     else hipLaunchKernelGGL((bn_apply_k<true, false>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4);
@@ -711,6 +737,15 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
                        const float* shift, const float* save_mean, const float* save_invstd,
                        const float* gamma, float* dy, float* dres, float* dgamma, float* dbeta,
                        int rows, int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream) {
+  return tmr_bn_bwd_x(dz, y, z, scale, shift, save_mean, save_invstd, gamma, dy, dres, dgamma,
+                      dbeta, rows, c, relu, ws, ws_bytes, 0, stream);
+}
+
+TMR_API int tmr_bn_bwd_x(const float* dz, const float* y, const float* z, const float* scale,
+                         const float* shift, const float* save_mean, const float* save_invstd,
+                         const float* gamma, void* dyv, float* dres, float* dgamma, float* dbeta,
+                         int rows, int c, int relu, void* ws, size_t ws_bytes, int out_bf16,
+                         hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0 && c >= 4, "tmr_bn_bwd: channels %d must be a multiple of 4", c);
   TMR_CHECK_ARG(rows > 0, "tmr_bn_bwd: empty input");
   TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd: workspace too small");
@@ -745,13 +780,17 @@ TMR_API int tmr_bn_bwd(const float* dz, const float* y, const float* z, const fl
   long n4 = (long)rows * c / 4;
   int nb = ew_blocks(n4);
   int c4 = c / 4;
-#define TMR_BN_APPLY(M, D)                                                                        \
-  hipLaunchKernelGGL((bn_bwd_apply<M, D>), dim3(nb), dim3(NT), 0, stream, dz, y, z, scale, shift, \
-                     coef, dy, dres, n4, c4)
+#define TMR_BN_APPLY(M, D)                                                                     \
+  if (out_bf16)                                                                                  \
+    hipLaunchKernelGGL((bn_bwd_apply<M, D, __bf16>), dim3(nb), dim3(NT), 0, stream, dz, y, z,    \
+                       scale, shift, coef, (__bf16*)dyv, dres, n4, c4);                          \
+  else                                                                                           \
+    hipLaunchKernelGGL((bn_bwd_apply<M, D>), dim3(nb), dim3(NT), 0, stream, dz, y, z, scale,     \
+                       shift, coef, (float*)dyv, dres, n4, c4)
   if (dres) {
-    if (mask == 1) TMR_BN_APPLY(1, true); else if (mask == 2) TMR_BN_APPLY(2, true); else TMR_BN_APPLY(0, true);
+    if (mask == 1) { TMR_BN_APPLY(1, true); } else if (mask == 2) { TMR_BN_APPLY(2, true); } else { TMR_BN_APPLY(0, true); }
   } else {
-    if (mask == 1) TMR_BN_APPLY(1, false); else if (mask == 2) TMR_BN_APPLY(2, false); else TMR_BN_APPLY(0, false);
+    if (mask == 1) { TMR_BN_APPLY(1, false); } else if (mask == 2) { TMR_BN_APPLY(2, false); } else { TMR_BN_APPLY(0, false); }
   }
 #undef TMR_BN_APPLY
   TMR_CHECK_LAUNCH("bn_bwd_apply");
@@ -764,6 +803,16 @@ TMR_API int tmr_bn_bwd_maxpool(const float* dyp, const uint8_t* argmax, int n, i
                                const float* save_invstd, const float* gamma, float* dy,
                                float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
                                hipStream_t stream) {
+  return tmr_bn_bwd_maxpool_x(dyp, argmax, n, h, w, ho, wo, y, scale, shift, save_mean,
+                              save_invstd, gamma, dy, dgamma, dbeta, c, ws, ws_bytes, 0, stream);
+}
+
+TMR_API int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n, int h, int w,
+                                 int ho, int wo, const float* y, const float* scale,
+                                 const float* shift, const float* save_mean,
+                                 const float* save_invstd, const float* gamma, void* dyv,
+                                 float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                                 int out_bf16, hipStream_t stream) {
   const long rows_l = (long)n * h * w;
   TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows_l > 0 && rows_l < 0x7fffffffL,
                 "tmr_bn_bwd_maxpool: bad shape n=%d h=%d w=%d c=%d", n, h, w, c);
@@ -788,8 +837,12 @@ TMR_API int tmr_bn_bwd_maxpool(const float* dyp, const uint8_t* argmax, int n, i
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");
   const long n4 = rows_l * c / 4;
-  hipLaunchKernelGGL(stem_bwd_apply, dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg, y, scale, shift,
-                     coef, dy, n4, c / 4);
+  if (out_bf16)
+    hipLaunchKernelGGL(stem_bwd_apply<__bf16>, dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg, y, scale,
+                       shift, coef, (__bf16*)dyv, n4, c / 4);
+  else
+    hipLaunchKernelGGL(stem_bwd_apply<float>, dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg, y, scale,
+                       shift, coef, (float*)dyv, n4, c / 4);
   TMR_CHECK_LAUNCH("stem_bwd_apply");
   return 0;
 }
@@ -798,6 +851,15 @@ TMR_API int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, 
                              const float* save_mean, const float* save_invstd, const float* gamma,
                              float* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
                              size_t ws_bytes, hipStream_t stream) {
+  return tmr_bn_bwd_parts_x(g, y, parts, nparts, save_mean, save_invstd, gamma, dy, dgamma, dbeta,
+                            rows, c, ws, ws_bytes, 0, stream);
+}
+
+TMR_API int tmr_bn_bwd_parts_x(const float* g, const float* y, const void* parts, int nparts,
+                               const float* save_mean, const float* save_invstd,
+                               const float* gamma, void* dyv, float* dgamma, float* dbeta,
+                               int rows, int c, void* ws, size_t ws_bytes, int out_bf16,
+                               hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows > 0 && nparts > 0,
                 "tmr_bn_bwd_parts: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
   TMR_CHECK_ARG(ws && ws_bytes >= tmr_bn_parts_ws_bytes(nparts, c),
@@ -813,8 +875,12 @@ TMR_API int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, 
                      dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
   const long n4 = (long)rows * c / 4;
-  hipLaunchKernelGGL((bn_bwd_apply<0, false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
-                     nullptr, nullptr, nullptr, coef, dy, nullptr, n4, c / 4);
+  if (out_bf16)
+    hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g,
+                       y, nullptr, nullptr, nullptr, coef, (__bf16*)dyv, nullptr, n4, c / 4);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<0, false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
+                       nullptr, nullptr, nullptr, coef, (float*)dyv, nullptr, n4, c / 4);
   TMR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }

@@ -1,6 +1,8 @@
 // Implicit-GEMM convolution / GEMM engine: host side and C ABI (kernel template: gemm_kernel.h).
 #include "gemm_kernel.h"
 
+#include <type_traits>
+
 using namespace tmrg;
 
 namespace {
@@ -78,6 +80,21 @@ static inline int xld_of(const tmr_conv_desc* d) { return d->x_ld ? d->x_ld : d-
 static inline int yld_of(const tmr_conv_desc* d) { return d->y_ld ? d->y_ld : d->k; }
 static inline long span(long pixels, int ld, int width) { return pixels > 0 ? (pixels - 1) * ld + width : 0; }
 
+// element bytes of the conv operands (tmr_conv_desc.io: bf16-stored x / w / dy)
+static inline int esz_x(const tmr_conv_desc* d) { return (d->io & TMR_IO_X_BF16) ? 2 : 4; }
+static inline int esz_w(const tmr_conv_desc* d) { return (d->io & TMR_IO_W_BF16) ? 2 : 4; }
+static inline int esz_dy(const tmr_conv_desc* d) { return (d->io & TMR_IO_DY_BF16) ? 2 : 4; }
+template <typename T>
+static inline T* adv(T* p, long elems, int esz) {   // p + elems elements of esz bytes
+  return p ? (T*)((typename std::conditional<std::is_const<T>::value, const char*, char*>::type)p +
+                  elems * esz)
+           : p;
+}
+static uint32_t clamp_bytes_e(long elems, int esz) {
+  long b = elems * esz;
+  return b >= 0x80000000L ? 0x80000000u : (uint32_t)b;
+}
+
 static uint32_t clamp_bytes(long elems) {
   long b = elems * 4;
   return b >= 0x80000000L ? 0x80000000u : (uint32_t)b;
@@ -140,6 +157,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
                          const float* bias, float* y, float beta, GemmArgs& a, bool& al) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
+  TMR_CHECK_ARG(d->io == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
   a = GemmArgs{};
@@ -151,9 +169,10 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   set_grid(a, d->n, d->ho, d->wo);
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = xld_of(d); a.ldb = a.K; a.ldc = yld_of(d); a.beta = beta;
-  a.Abytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
+  a.Abytes = clamp_bytes_e(span((long)d->n * d->h * d->w, a.lds, d->c), esz_x(d));
   a.prec = d->math;
-  a.Bbytes = clamp_bytes((long)d->k * a.K);
+  a.Bbytes = clamp_bytes_e((long)d->k * a.K, esz_w(d));
+  a.sab = ((d->io & TMR_IO_X_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldc, d->k));
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
@@ -194,7 +213,7 @@ TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* 
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     GemmArgs a;
     bool al;
-    int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, bias, y + f0 * y_frame(d), beta, a, al);
+    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, bias, y + f0 * y_frame(d), beta, a, al);
     if (!rc) rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
     if (rc) return rc;
   }
@@ -212,7 +231,7 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     GemmArgs a;
     bool al;
-    int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, shift, y + f0 * y_frame(d), 0.f, a, al);
+    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, shift, y + f0 * y_frame(d), 0.f, a, al);
     if (rc) return rc;
     a.scale = scale;
     a.res = residual ? residual + f0 * y_frame(d) : nullptr;
@@ -257,7 +276,7 @@ TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     GemmArgs a;
     bool al;
-    int rc = conv_fwd_args(&c, x + f0 * x_frame(d), w_krsc, nullptr, y + f0 * y_frame(d), 0.f, a, al);
+    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, nullptr, y + f0 * y_frame(d), 0.f, a, al);
     if (!rc) rc = set_prologue(a, pro, d, true, false, 0);
     if (rc) return rc;
     a.stats = st;
@@ -311,9 +330,10 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
       set_grid(a, d->n, hg, wg);
       a.Hs = d->ho; a.Ws = d->wo; a.sy = 1; a.sx = 1;
       a.lds = yld_of(d); a.ldb = d->r * d->s * d->c; a.ldc = xld_of(d); a.beta = beta;
-      a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.lds, d->k));
+      a.Abytes = clamp_bytes_e(span((long)d->n * d->ho * d->wo, a.lds, d->k), esz_dy(d));
       a.prec = d->math;
-      a.Bbytes = clamp_bytes((long)d->k * d->r * d->s * d->c);
+      a.Bbytes = clamp_bytes_e((long)d->k * d->r * d->s * d->c, esz_w(d));
+      a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
       a.Cbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.ldc, d->c));
       a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
       // nothing to add -- unless the fused BN backward must still see (mask, sum) these pixels
@@ -357,7 +377,7 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
     fc_.nparts = 0;
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);
-    int rc = conv_dgrad_impl(&c, dy ? dy + f0 * y_frame(d) : nullptr, w_krsc,
+    int rc = conv_dgrad_impl(&c, adv(dy, f0 * y_frame(d), esz_dy(d)), w_krsc,
                              dx ? dx + f0 * x_frame(d) : nullptr, beta, stream, &fc_,
                              pro ? &pc : nullptr);
     if (rc) return rc;
@@ -421,7 +441,7 @@ TMR_API int tmr_conv2d_dgrad_pro(const tmr_conv_desc* d, const float* dy, const 
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);
-    int rc = conv_dgrad_impl(&c, dy + f0 * y_frame(d), w_krsc, dx + f0 * x_frame(d), beta, stream,
+    int rc = conv_dgrad_impl(&c, adv(dy, f0 * y_frame(d), esz_dy(d)), w_krsc, dx + f0 * x_frame(d), beta, stream,
                              nullptr, pro ? &pc : nullptr);
     if (rc) return rc;
   }
@@ -483,7 +503,7 @@ TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const f
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);
-    int rc = conv_wgrad_impl(&c, x + f0 * x_frame(d), dy + f0 * y_frame(d), dw_oihw, c_real,
+    int rc = conv_wgrad_impl(&c, adv(x, f0 * x_frame(d), esz_x(d)), adv(dy, f0 * y_frame(d), esz_dy(d)), dw_oihw, c_real,
                              f0 == 0 ? beta : 1.f, ws, ws_bytes, stream, pro ? &pc : nullptr);
     if (rc) return rc;
   }
@@ -513,9 +533,10 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
   a.lds = xld_of(d); a.ldb = yld_of(d); a.ldc = a.N; a.beta = 0.f;
   a.kchunk = kc; a.slab = slab;
-  a.Abytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldb, d->k));
+  a.Abytes = clamp_bytes_e(span((long)d->n * d->ho * d->wo, a.ldb, d->k), esz_dy(d));
   a.prec = d->math;
-  a.Bbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.lds, d->c));
+  a.Bbytes = clamp_bytes_e(span((long)d->n * d->h * d->w, a.lds, d->c), esz_x(d));
+  a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & TMR_IO_X_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(slab);
   bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0) && a.lds % 4 == 0 && a.ldb % 4 == 0;
   int rc = set_prologue(a, pro, d, true, true, 0);

@@ -102,6 +102,10 @@ struct GemmArgs {
   const float* pd_b;
   const float* pd_c;
   int pro;
+  // bf16-stored operands (bf16 math only): bit 0 = A, bit 1 = B holds bf16 values (2-byte
+  // elements; byte extents and offsets in bf16 units).  Exact w.r.t. the fp32-stored bf16 path:
+  // the loaders would round those operands to bf16 (RNE) anyway.
+  int sab;
 };
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -140,6 +144,17 @@ __device__ __forceinline__ float4 ld4v(__amdgpu_buffer_rsrc_t r, uint32_t off, b
   return v;
 }
 
+// 4 bf16 (8 bytes) at byte offset `off` of a bf16 tensor, carried raw in the .x/.y of a float4
+// slot (the fp32 loaders' register slot of 4 elements); OOB offsets read zeros
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ld4h(__amdgpu_buffer_rsrc_t r, uint32_t off, bool ok) {
+  // whole-vector bit_cast (as bld4): extracting the load's elements one by one makes hipcc
+  // (ROCm 7.2) emit one buffer_load_dword (checked in the .s)
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, ok ? off : OOB, 0, 0);
+  const float2 f = __builtin_bit_cast(float2, v);
+  return make_float4(f.x, f.y, 0.f, 0.f);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
@@ -157,9 +172,15 @@ __device__ __forceinline__ void tap_split(const GemmArgs& a, int tap, int& ri, i
 //           lane's 8-element k-fragment is one ds_read_b128, v_mfma_f32_32x32x16_bf16.
 //           M/N-contiguous operands are loaded as k-row pairs so the LDS writes are packed
 //           bf16x2 dwords (conflict-free); K-contiguous operands write bf16x4.
-template <int MODE, int BM, int BN, int WM, int WN, int BK, int VAR, int PREC = 0, int PRO = 0>
+template <int MODE, int BM, int BN, int WM, int WN, int BK, int VAR, int PREC = 0, int PRO = 0,
+          int SAB = 0>
 __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   constexpr bool AL = (VAR != 2);
+  // bf16-stored operands: 8-byte loads of 4 bf16 per slot (the fp32 slot of 4 elements, half the
+  // bytes, no conversion), written to LDS as they are
+  constexpr bool SA = (SAB & 1) != 0, SB = (SAB & 2) != 0;
+  constexpr uint32_t ESA = SA ? 2u : 4u, ESB = SB ? 2u : 4u;   // element bytes of A / B
+  static_assert(SAB == 0 || (PREC == 1 && PRO == 0 && AL), "bf16 storage: bf16 math, aligned");
   // operand prologues (GemmArgs::pro): X operand BN+ReLU on A (FWD) or B (WGRAD); dY operand BN
   // backward on A (DGRAD, WGRAD)
   constexpr bool PX_A = (PRO & 1) && MODE == MODE_FWD;
@@ -251,7 +272,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
       const uint32_t x = rem - y * a.dW.d;
       ay[q] = (int)y * a.sy;
       ax[q] = (int)x * a.sx;
-      apix[q] = ((uint32_t)(((int)n * a.Hs + ay[q]) * a.Ws + ax[q]) * (uint32_t)a.lds) * 4u;
+      apix[q] = ((uint32_t)(((int)n * a.Hs + ay[q]) * a.Ws + ax[q]) * (uint32_t)a.lds) * ESA;
     }
   }
   // WGRAD B: this thread's columns j -> (tap offset, channel), fixed for the whole kernel
@@ -269,7 +290,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
       tap_split(a, tap, ri, si);
       bdy[q] = a.oy0 + a.dyr * ri;
       bdx[q] = a.ox0 + a.dxs * si;
-      bcoff[q] = (uint32_t)c * 4u;
+      bcoff[q] = (uint32_t)c * ESB;
       bjok[q] = j < a.N && tap < a.ntaps;
     }
   }
@@ -297,7 +318,7 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
 #pragma unroll
     for (int p = 0; p < QB; ++p) {
       const int q = PREC ? 2 * p : 0;
-      const int c = bjok[q] ? (int)(bcoff[q] >> 2) : 0;
+      const int c = bjok[q] ? (int)(bcoff[q] / ESB) : 0;
       xsb[p] = *reinterpret_cast<const float4*>(a.px_scale + c);
       xhb[p] = *reinterpret_cast<const float4*>(a.px_shift + c);
     }
@@ -343,8 +364,9 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const int ys = ay[q] + dy, xs = ax[q] + dx;
         const bool ok = aok[q] && k < kend && tap < a.ntaps && (unsigned)ys < (unsigned)a.Hs &&
                         (unsigned)xs < (unsigned)a.Ws;
-        const uint32_t off = apix[q] + (uint32_t)(((dy * a.Ws + dx) * a.lds + c) * 4);
-        ra[q] = ld4v<AL>(rA, off, ok, kend - k);
+        const uint32_t off = apix[q] + (uint32_t)(((dy * a.Ws + dx) * a.lds + c) * (int)ESA);
+        if constexpr (SA) ra[q] = ld4h(rA, off, ok);
+        else ra[q] = ld4v<AL>(rA, off, ok, kend - k);
         if constexpr (PD_A) aux.ya[q] = ld4v<AL>(rY, off, ok, kend - k);
         if constexpr (PX_A || PD_A) {
           if (q == 0) aux.oka = 0;
@@ -369,8 +391,9 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const int krow = mn_krow(q, BM / 4), c4 = mn_c4(q, BM / 4);
         const int m = kb + krow, i = m0 + c4 * 4;
         const bool ok = (m < kend) && (i < a.M);
-        const uint32_t off = ((uint32_t)m * (uint32_t)a.ldb + (uint32_t)i) * 4u;
-        ra[q] = ld4v<AL>(rA, off, ok, a.M - i);
+        const uint32_t off = ((uint32_t)m * (uint32_t)a.ldb + (uint32_t)i) * ESA;
+        if constexpr (SA) ra[q] = ld4h(rA, off, ok);
+        else ra[q] = ld4v<AL>(rA, off, ok, a.M - i);
         if constexpr (PD_A) {
           aux.ya[q] = ld4v<AL>(rY, off, ok, a.M - i);
           if (q == 0) aux.oka = 0;
@@ -386,7 +409,9 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const int j = n0 + lin / KQ;
         const int k = kb + (lin % KQ) * 4;
         const bool ok = (j < a.N) && (k < kend);
-        rb[q] = ld4v<AL>(rB, ((uint32_t)j * (uint32_t)a.ldb + (uint32_t)k) * 4u, ok, kend - k);
+        const uint32_t off = ((uint32_t)j * (uint32_t)a.ldb + (uint32_t)k) * ESB;
+        if constexpr (SB) rb[q] = ld4h(rB, off, ok);
+        else rb[q] = ld4v<AL>(rB, off, ok, kend - k);
       }
     } else if (MODE == MODE_DGRAD) {  // B[k=(tap,co)][j=ci], ci contiguous
       int tapU = 0, cbU = kb;
@@ -404,8 +429,9 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const int k = kb + krow, j = n0 + c4 * 4;
         const bool ok = (k < kend) && (j < a.N);
         const uint32_t co = (uint32_t)(cbU + krow);
-        rb[q] = ld4v<AL>(rB, (co * (uint32_t)a.ldb + (uint32_t)rsU * (uint32_t)a.N + (uint32_t)j) * 4u,
-                         ok, a.N - j);
+        const uint32_t off = (co * (uint32_t)a.ldb + (uint32_t)rsU * (uint32_t)a.N + (uint32_t)j) * ESB;
+        if constexpr (SB) rb[q] = ld4h(rB, off, ok);
+        else rb[q] = ld4v<AL>(rB, off, ok, a.N - j);
       }
     } else {  // WGRAD: B[kk=m][j=(tap,c)] gathered from X
 #pragma unroll
@@ -421,9 +447,10 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
         const bool ok = m < kend && bjok[q] && (unsigned)ys < (unsigned)a.Hs &&
                         (unsigned)xs < (unsigned)a.Ws;
         const uint32_t off =
-            ((uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds) * 4u + bcoff[q];
+            ((uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds) * ESB + bcoff[q];
         const int j = n0 + mn_c4(q, BN / 4) * 4;
-        rb[q] = ld4v<AL>(rB, off, ok, a.N - j);
+        if constexpr (SB) rb[q] = ld4h(rB, off, ok);
+        else rb[q] = ld4v<AL>(rB, off, ok, a.N - j);
         if constexpr (PX_B) {
           if (q == 0) aux.okb = 0;
           aux.okb |= (uint32_t)ok << q;
@@ -449,19 +476,47 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
       t[((4 * c4 + 2) * LDK) / 2 + kp] = pack_bf16x2(v0.z, v1.z);
       t[((4 * c4 + 3) * LDK) / 2 + kp] = pack_bf16x2(v0.w, v1.w);
     };
+    // bf16-stored slots: 4 raw bf16 in .x/.y
+    auto kc_store16 = [&](__bf16* T, int lin, const float4& v) {
+      const int row = lin / KQ, kq = (lin % KQ) * 4;
+      *reinterpret_cast<uint2*>(&T[row * LDK + kq]) =
+          make_uint2(__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y));
+    };
+    auto mn_store16 = [&](__bf16* T, int q, int W4, const float4& v0, const float4& v1) {
+      const int kp = mn_krow(q, W4) >> 1, c4 = mn_c4(q, W4);
+      const uint32_t a0 = __builtin_bit_cast(uint32_t, v0.x), a1 = __builtin_bit_cast(uint32_t, v0.y);
+      const uint32_t b0 = __builtin_bit_cast(uint32_t, v1.x), b1 = __builtin_bit_cast(uint32_t, v1.y);
+      uint32_t* t = reinterpret_cast<uint32_t*>(T);
+      t[((4 * c4 + 0) * LDK) / 2 + kp] = (a0 & 0xffffu) | (b0 << 16);
+      t[((4 * c4 + 1) * LDK) / 2 + kp] = (a0 >> 16) | (b0 & 0xffff0000u);
+      t[((4 * c4 + 2) * LDK) / 2 + kp] = (a1 & 0xffffu) | (b1 << 16);
+      t[((4 * c4 + 3) * LDK) / 2 + kp] = (a1 >> 16) | (b1 & 0xffff0000u);
+    };
     if (A_KC) {
 #pragma unroll
-      for (int q = 0; q < RA; ++q) kc_store(Ah, tid + NT * q, ra[q]);
+      for (int q = 0; q < RA; ++q) {
+        if constexpr (SA) kc_store16(Ah, tid + NT * q, ra[q]);
+        else kc_store(Ah, tid + NT * q, ra[q]);
+      }
     } else {
 #pragma unroll
-      for (int q = 0; q < RA; q += 2) mn_store(Ah, q, BM / 4, ra[q], ra[q + 1]);
+      for (int q = 0; q < RA; q += 2) {
+        if constexpr (SA) mn_store16(Ah, q, BM / 4, ra[q], ra[q + 1]);
+        else mn_store(Ah, q, BM / 4, ra[q], ra[q + 1]);
+      }
     }
     if (B_KC) {
 #pragma unroll
-      for (int q = 0; q < RB; ++q) kc_store(Bh, tid + NT * q, rb[q]);
+      for (int q = 0; q < RB; ++q) {
+        if constexpr (SB) kc_store16(Bh, tid + NT * q, rb[q]);
+        else kc_store(Bh, tid + NT * q, rb[q]);
+      }
     } else {
 #pragma unroll
-      for (int q = 0; q < RB; q += 2) mn_store(Bh, q, BN / 4, rb[q], rb[q + 1]);
+      for (int q = 0; q < RB; q += 2) {
+        if constexpr (SB) mn_store16(Bh, q, BN / 4, rb[q], rb[q + 1]);
+        else mn_store(Bh, q, BN / 4, rb[q], rb[q + 1]);
+      }
     }
   };
 
@@ -1053,6 +1108,27 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
 template <int MODE, int BM, int BN, int WM, int WN, int BKT, int PREC = 0>
 int launch_cfg(const GemmArgs& a, int var, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
+  if constexpr (PREC == 1) {
+    if (a.sab) {   // bf16-stored operands (combinations checked by launch_gemm_t)
+      if constexpr (MODE == MODE_FWD) {
+        if (a.sab == 2 && var == 1)
+          hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 1, 1, 0, 2>), grid, blk, 0, st, a);
+        else if (a.sab == 2)
+          hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, 1, 0, 2>), grid, blk, 0, st, a);
+        else
+          hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, 1, 0, 3>), grid, blk, 0, st, a);
+      } else if constexpr (MODE == MODE_DGRAD) {
+        hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, 1, 0, 3>), grid, blk, 0, st, a);
+      } else {
+        if (a.sab == 1)
+          hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, 1, 0, 1>), grid, blk, 0, st, a);
+        else
+          hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, 1, 0, 3>), grid, blk, 0, st, a);
+      }
+      TMR_CHECK_LAUNCH("gemm_kernel");
+      return 0;
+    }
+  }
   if (a.pro) {   // operand prologues (var == 0, checked by launch_gemm_t)
     if constexpr (MODE == MODE_FWD) {
       hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, PREC, 1>), grid, blk, 0, st, a);
@@ -1147,6 +1223,12 @@ int launch_gemm_t(const GemmArgs& a, bool al, int splits, hipStream_t st) {
   int var = al ? (uniform ? 0 : 1) : 2;
   TMR_CHECK_ARG(!a.pro || var == 0,
                 "gemm: operand prologues need aligned operands with one tap per k-tile");
+  TMR_CHECK_ARG(!a.sab || (a.prec == TMR_MATH_BF16 && !a.pro &&
+                           (MODE == MODE_FWD ? ((a.sab == 2 && var <= 1) || (a.sab == 3 && var == 0))
+                            : MODE == MODE_DGRAD ? (a.sab == 3 && var == 0)
+                                                 : ((a.sab == 1 || a.sab == 3) && var == 0))),
+                "gemm: unsupported bf16-stored operand combination (sab %d, view %d, var %d)",
+                a.sab, MODE, var);
   TMR_CHECK_ARG(!a.pro || ((a.pro & 1) ? (MODE != MODE_DGRAD && a.px_scale && a.px_shift) : true),
                 "gemm: X-operand prologue needs scale/shift (forward or wgrad view)");
   TMR_CHECK_ARG(!a.pro || ((a.pro & 2) ? (MODE != MODE_FWD && a.pd_y && a.pd_a && a.pd_b && a.pd_c)

@@ -113,7 +113,8 @@ __global__ __launch_bounds__(NT) void avgpool_bwd_k(const float* __restrict__ dy
   }
 }
 
-__global__ void oihw_to_krsc_k(const float* __restrict__ w, float* __restrict__ wk, int k, int c,
+template <typename TO>
+__global__ void oihw_to_krsc_k(const float* __restrict__ w, TO* __restrict__ wk, int k, int c,
                                int rs, int cpad) {
   const long total = (long)k * rs * cpad;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -122,7 +123,7 @@ __global__ void oihw_to_krsc_k(const float* __restrict__ w, float* __restrict__ 
     const long t = i / cpad;
     const int tap = (int)(t % rs);
     const int ko = (int)(t / rs);
-    wk[i] = ci < c ? w[((long)ko * c + ci) * rs + tap] : 0.f;
+    wk[i] = (TO)(ci < c ? w[((long)ko * c + ci) * rs + tap] : 0.f);   // bf16: RNE
   }
 }
 
@@ -227,9 +228,18 @@ TMR_API int tmr_avgpool_bwd(const float* dy, float* dx, int n, int hw, int c, hi
 
 TMR_API int tmr_weight_oihw_to_krsc(const float* w, float* wk, int k, int c, int r, int s,
                                     int cpad, hipStream_t stream) {
+  return tmr_weight_oihw_to_krsc_x(w, wk, k, c, r, s, cpad, 0, stream);
+}
+
+TMR_API int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, int r, int s,
+                                      int cpad, int out_bf16, hipStream_t stream) {
   TMR_CHECK_ARG(cpad >= c, "tmr_weight_oihw_to_krsc: cpad < c");
-  hipLaunchKernelGGL(oihw_to_krsc_k, dim3(ew_blocks((long)k * r * s * cpad)), dim3(NT), 0, stream,
-                     w, wk, k, c, r * s, cpad);
+  if (out_bf16)
+    hipLaunchKernelGGL(oihw_to_krsc_k<__bf16>, dim3(ew_blocks((long)k * r * s * cpad)), dim3(NT), 0,
+                       stream, w, (__bf16*)wk, k, c, r * s, cpad);
+  else
+    hipLaunchKernelGGL(oihw_to_krsc_k<float>, dim3(ew_blocks((long)k * r * s * cpad)), dim3(NT), 0,
+                       stream, w, (float*)wk, k, c, r * s, cpad);
   TMR_CHECK_LAUNCH("oihw_to_krsc");
   return 0;
 }

@@ -70,23 +70,46 @@ _SUFFIX = {"fp32": "", "bf16": "_bf16"}
 MAX_FRAMES = 0
 
 
-def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math="fp32"):
+IO_X, IO_W, IO_DY = 1, 2, 4     # tmr_conv_desc.io: bf16-stored x / KRSC weights / dy
+
+
+def _io(x=None, w=None, dy=None):
+    """tmr_conv_desc.io from the operands' dtypes (bf16 storage of conv-operand-only tensors)."""
+    io = 0
+    for t, bit in ((x, IO_X), (w, IO_W), (dy, IO_DY)):
+        if t is not None and t.dtype == torch.bfloat16:
+            io |= bit
+    return io
+
+
+def _esz(t):
+    return t.element_size() if t is not None else 4
+
+
+def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math="fp32", io=0):
     pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
     wo = (w + 2 * pad_w - s) // stride + 1
+    if io and math != "bf16":
+        raise RuntimeError("bf16-stored conv operands need math='bf16'")
     return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
-                    MAX_FRAMES)
+                    MAX_FRAMES, io)
+
+
+def _req_op(t, name):
+    """A conv operand: fp32, or bf16 (stored rounded; bf16 math only)."""
+    return _req(t, name, torch.bfloat16 if t.dtype == torch.bfloat16 else f32)
 
 
 def conv_fwd(x, w_krsc, stride, pad, bias=None, out=None, beta=0.0, c_real=None, pad_w=None,
              math="fp32"):
     """x (N,H,W,C) NHWC (or channel-slice view), w_krsc (K,R,S,C) -> y (N,Ho,Wo,K);
     `out` may be a channel-slice view of a wider NHWC tensor (grouped convolution)."""
-    _req(w_krsc, "w")
+    _req_op(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, w_krsc))
     if out is None:
         out = _empty((n, d.ho, d.wo, k), x)
     d.x_ld = _nhwc_ld(x, "x")
@@ -104,11 +127,11 @@ def conv_fwd_fused(x, w_krsc, stride, pad, scale, shift, residual=None, relu=Tru
                    pad_w=None, math="fp32"):
     """Inference conv + BN(running stats) [+ residual] [+ ReLU] in one launch:
     [relu](conv(x, w_krsc) * scale + shift + residual) -> (N,Ho,Wo,K)."""
-    _req(x, "x"); _req(w_krsc, "w"); _req(scale, "scale"); _req(shift, "shift")
+    _req_op(x, "x"); _req_op(w_krsc, "w"); _req(scale, "scale"); _req(shift, "shift")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, w_krsc))
     out = _empty((n, d.ho, d.wo, k), x)
     if residual is not None:
         _req(residual, "residual")
@@ -140,17 +163,18 @@ def _prologue(xpro=None, dpro=None):
 def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32", xpro=None):
     """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts).
     xpro = (scale, shift): x is a pre-BN tensor read as relu(x*scale + shift) (0 at padding)."""
-    _req(x, "x"); _req(w_krsc, "w")
+    _req_op(x, "x"); _req_op(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, w_krsc))
     out = _empty((n, d.ho, d.wo, k), x)
     nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
     with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
                (n, h, w, c, k, r, stride),
-               4 * (n * h * w * c + k * r * s * c + n * d.ho * d.wo * k) + stats.numel() * 4):
+               _esz(x) * n * h * w * c + _esz(w_krsc) * k * r * s * c + 4 * n * d.ho * d.wo * k
+               + stats.numel() * 4):
         pro = _prologue(xpro)
         if pro is None:
             call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
@@ -178,19 +202,19 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices).
     dpro = (y, coef): dy is the masked BN-output gradient g, read as the BN backward
     A*g + B*y + C (tmr_bn_bwd_coefs)."""
-    _req(w_krsc, "w")
+    _req_op(w_krsc, "w")
     n, ho, wo, k = dy.shape
     k2, r, s, c = w_krsc.shape
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(None, w_krsc, dy))
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
-               4 * (n * ho * wo * k * (2 if dpro is not None else 1) + k * r * s * c
-                    + n * h * w * c * (2 if beta else 1))):
+               _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * k * r * s * c
+               + 4 * n * h * w * c * (2 if beta else 1)):
         pro = _prologue(None, dpro)
         if pro is None:
             call("tmr_conv2d_dgrad", ctypes.byref(d), dy, w_krsc, out, float(beta), stream_ptr())
@@ -204,11 +228,11 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
                      shift=None, out=None, beta=0.0, math="fp32", dpro=None):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts)."""
-    _req(w_krsc, "w"); _req(y, "y"); _req(mean, "mean")
+    _req_op(w_krsc, "w"); _req(y, "y"); _req(mean, "mean")
     n, ho, wo, k = dy.shape
     k2, r, s, c = w_krsc.shape
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math, io=_io(None, w_krsc, dy))
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
@@ -221,8 +245,8 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
         raise RuntimeError("tmr_conv2d_dgrad_bnbwd_parts failed")
     parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
-               4 * (n * ho * wo * k * (2 if dpro is not None else 1) + k * r * s * c
-                    + n * h * w * c * (3 if beta else 2) + (n * h * w * c if z is not None else 0))):
+               _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * k * r * s * c
+               + 4 * (n * h * w * c * (3 if beta else 2) + (n * h * w * c if z is not None else 0))):
         pro = _prologue(None, dpro)
         if pro is None:
             call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z,
@@ -235,16 +259,16 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     return out, parts, nparts
 
 
-def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma):
+def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma, bf16=False):
     """Stem backward: maxpool(3,2,1) backward + ReLU mask (from y) + BN backward in two passes
     over y; the maxpool's input gradient is never written.  -> (dy, dgamma, dbeta)."""
     n, h, w, c = y.shape
     _, ho, wo, _ = dyp.shape
     ws, nb = _bn_ws(n * h * w, c, y.device)
-    dy = torch.empty_like(y)
+    dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)
-    call("tmr_bn_bwd_maxpool", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma, dy,
-         dgamma, dbeta, c, ws, ctypes.c_size_t(nb), stream_ptr())
+    call("tmr_bn_bwd_maxpool_x", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma, dy,
+         dgamma, dbeta, c, ws, ctypes.c_size_t(nb), int(bf16), stream_ptr())
     return dy, dgamma, dbeta
 
 
@@ -276,16 +300,17 @@ def bn_bwd_coefs_dense(g, y, z, scale, shift, mean, inv, gamma, relu):
     return coef, dgamma, dbeta
 
 
-def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma):
-    """BN backward from conv_dgrad_bnbwd partials: g already masked -> (dy, dgamma, dbeta)."""
+def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma, bf16=False):
+    """BN backward from conv_dgrad_bnbwd partials: g already masked -> (dy, dgamma, dbeta);
+    bf16=True stores dy rounded (consumed only by the bf16-math dgrad / wgrad)."""
     c = y.shape[-1]
     rows = y.numel() // c
-    dy = torch.empty_like(y)
+    dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)
     nb = query("tmr_bn_parts_ws_bytes", int(nparts), c)
     ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=y.device)
-    call("tmr_bn_bwd_parts", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta, rows,
-         c, ws, ctypes.c_size_t(ws.numel() * 8), stream_ptr())
+    call("tmr_bn_bwd_parts_x", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta, rows,
+         c, ws, ctypes.c_size_t(ws.numel() * 8), int(bf16), stream_ptr())
     return dy, dgamma, dbeta
 
 
@@ -297,7 +322,7 @@ def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=
     n, h, w, c = x.shape
     k = dy.shape[3]
     c_real = c if c_real is None else c_real
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, None, dy))
     d.x_ld = _nhwc_ld(x, "x")
     d.y_ld = _nhwc_ld(dy, "dy")
     assert (d.ho, d.wo) == tuple(dy.shape[1:3])
@@ -307,8 +332,8 @@ def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=
     ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
     with _prof("conv_wgrad" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * c_real,
                (n, h, w, c, k, r, stride),
-               4 * (n * h * w * c + n * d.ho * d.wo * k * (2 if dpro is not None else 1)
-                    + k * r * s * c_real)):
+               _esz(x) * n * h * w * c + _esz(dy) * n * d.ho * d.wo * k * (2 if dpro is not None else 1)
+               + 4 * k * r * s * c_real):
         pro = _prologue(xpro, dpro)
         if pro is None:
             call("tmr_conv2d_wgrad", ctypes.byref(d), x, dy, out, int(c_real), float(beta), ws,
@@ -370,11 +395,13 @@ def col_sum(x, rows, cols, ld, out=None, beta=0.0):
 
 
 # --------------------------------------------------------------------- layout
-def weight_to_krsc(w, cpad=None):
+def weight_to_krsc(w, cpad=None, bf16=False):
+    """OIHW fp32 -> KRSC (channels zero-padded to cpad); bf16=True stores it rounded (RNE), for
+    the bf16-math convs (tmr_conv_desc.io TMR_IO_W_BF16)."""
     k, c, r, s = w.shape
     cpad = c if cpad is None else cpad
-    out = _empty((k, r, s, cpad), w)
-    call("tmr_weight_oihw_to_krsc", _req(w, "w"), out, k, c, r, s, cpad, stream_ptr())
+    out = _empty((k, r, s, cpad), w, dtype=torch.bfloat16 if bf16 else f32)
+    call("tmr_weight_oihw_to_krsc_x", _req(w, "w"), out, k, c, r, s, cpad, int(bf16), stream_ptr())
     return out
 
 
@@ -435,12 +462,15 @@ def bn_eval_params(gamma, beta, running_mean, running_var, eps):
     return scale, shift
 
 
-def bn_apply(y, scale, shift, residual=None, relu=True, out=None):
+def bn_apply(y, scale, shift, residual=None, relu=True, out=None, bf16=False):
+    """z = act(y*scale + shift (+ residual)); bf16=True stores z rounded (a tensor consumed only
+    as a bf16-math conv operand)."""
     c = y.shape[-1]
     rows = y.numel() // c
     if out is None:
-        out = torch.empty_like(y)
-    call("tmr_bn_apply", y, scale, shift, residual, out, rows, c, int(relu), stream_ptr())
+        out = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
+    call("tmr_bn_apply_x", y, scale, shift, residual, out, rows, c, int(relu),
+         int(out.dtype == torch.bfloat16), stream_ptr())
     return out
 
 
@@ -458,19 +488,19 @@ def bn_apply2(y, scale, shift, yr, rscale, rshift, relu=True, out=None):
 
 
 def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None, scale=None,
-           shift=None):
+           shift=None, bf16=False):
     """ReLU mask from the saved output z, or (z=None) recomputed from y with the forward's
-    scale/shift -- only valid when the forward had no residual."""
+    scale/shift -- only valid when the forward had no residual.  bf16=True: dy stored rounded."""
     c = y.shape[-1]
     rows = y.numel() // c
     ws, nb = _bn_ws(rows, c, y.device)
-    dy = torch.empty_like(y)
+    dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     dres = None
     if want_dres:
         dres = torch.empty_like(y) if dres_out is None else dres_out
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)
-    call("tmr_bn_bwd", dz, y, z if relu else None, scale, shift, mean, inv, gamma, dy, dres,
-         dgamma, dbeta, rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
+    call("tmr_bn_bwd_x", dz, y, z if relu else None, scale, shift, mean, inv, gamma, dy, dres,
+         dgamma, dbeta, rows, c, int(relu), ws, ctypes.c_size_t(nb), int(bf16), stream_ptr())
     return dy, dres, dgamma, dbeta
 
 

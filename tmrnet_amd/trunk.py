@@ -87,6 +87,17 @@ def _bn_momentum(bn):
 # ms/step.  Kept for the bf16 path and for A/B measurements.
 FOLD_BN = os.environ.get("TMR_FOLD_BN", "0") == "1"
 
+# bf16 math (configs C4/C5): the tensors consumed only as conv operands -- the KRSC weights, the
+# BN+ReLU outputs of each Bottleneck's first two units, every BatchNorm-backward output dy -- are
+# stored as bf16 (tmr_conv_desc.io).  Exact: the bf16 convs round those operands to bf16 (RNE)
+# when staging them anyway, so results are bit-identical to fp32 storage; the convs read half the
+# bytes with no conversion.  TMR_BF16_STORE=0 keeps them fp32 (A/B measurements).
+BF16_STORE = os.environ.get("TMR_BF16_STORE", "1") != "0"
+
+
+def _store16(math):
+    return math == "bf16" and BF16_STORE
+
 
 def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
              defer=False, branch=None, nbt=None):
@@ -103,10 +114,11 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     w = conv.weight
     k, c, r, s = w.shape
     cs = x.shape[3]
-    if r == 1 and s == 1 and c == cs:
+    s16 = _store16(math)
+    if r == 1 and s == 1 and c == cs and not s16:
         wk = w.detach().contiguous().view(k, 1, 1, c)   # OIHW == KRSC for 1x1
     else:
-        wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs)
+        wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs, bf16=s16)
     if training:
         # batch statistics come out of the conv epilogue (no separate pass over y)
         y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c, math=math,
@@ -133,7 +145,9 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     elif branch is not None:
         z = ops.bn_apply2(y, scale, shift, branch[0], branch[1], branch[2], relu)
     else:
-        z = ops.bn_apply(y, scale, shift, residual, relu)
+        # a non-residual unit's output is only ever a conv operand (next conv's forward and
+        # wgrad; the backward recomputes its ReLU mask from y): bf16 under bf16 math
+        z = ops.bn_apply(y, scale, shift, residual, relu, bf16=s16 and residual is None)
     if recs is not None:
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
         has_res = residual is not None or branch is not None
@@ -158,10 +172,11 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     dz is then gathered from it inside the BN backward."""
     conv, bn = rec["conv"], rec["bn"]
     dpro = None    # (y, coef): dy = A*g + B*y + C evaluated by the consumer convs' loaders
+    s16 = _store16(rec["math"])   # dy feeds only this conv's dgrad / wgrad
     if pool is not None:
         # the stem: maxpool backward + ReLU mask + BN backward without writing dz
         dy, dg, db = ops.bn_bwd_maxpool(pool[0], pool[1], rec["y"], rec["scale"], rec["shift"],
-                                        rec["mean"], rec["inv"], bn.weight.detach())
+                                        rec["mean"], rec["inv"], bn.weight.detach(), bf16=s16)
         dres = None
     elif FOLD_BN:
         rows = rec["y"].numel() // rec["y"].shape[-1]
@@ -178,13 +193,13 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
         dres = dz if want_dres else None
     elif parts is not None:
         dy, dg, db = ops.bn_bwd_parts(dz, rec["y"], parts[0], parts[1], rec["mean"], rec["inv"],
-                                      bn.weight.detach())
+                                      bn.weight.detach(), bf16=s16)
         dres = dz if want_dres else None
     else:
         dy, dres, dg, db = ops.bn_bwd(dz, rec["y"], rec["z"], rec["mean"], rec["inv"],
                                       bn.weight.detach(), rec["relu"], want_dres=want_dres,
                                       dres_out=dz if dres_inplace else None,
-                                      scale=rec["scale"], shift=rec["shift"])
+                                      scale=rec["scale"], shift=rec["shift"], bf16=s16)
     grads[bn.weight] = dg
     grads[bn.bias] = db
     x = rec["x"]
