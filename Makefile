@@ -8,7 +8,7 @@ CFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Itmrnet_amd/csr
 tmrnet_amd/libtmr.so: $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
 
-build/%.hip.o: tmrnet_amd/csrc/%.hip tmrnet_amd/csrc/common.h tmrnet_amd/csrc/gemm_kernel.h include/tmr.h
+build/%.hip.o: tmrnet_amd/csrc/%.hip tmrnet_amd/csrc/common.h tmrnet_amd/csrc/gemm_kernel.h tmrnet_amd/csrc/gemm16_kernel.h include/tmr.h
 	@mkdir -p build
 	$(HIPCC) $(CFLAGS) -c $< -o $@
 

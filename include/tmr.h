@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 3
+#define TMR_ABI_VERSION 4
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
@@ -67,6 +67,8 @@ typedef struct tmr_conv_desc {
 #define TMR_IO_X_BF16 1
 #define TMR_IO_W_BF16 2
 #define TMR_IO_DY_BF16 4
+#define TMR_IO_WT_BF16 8   /* dgrad only: w is the transposed bf16 weight copy Wt[Cin][R][S][Cout]
+                              (tmr_weight_oihw_to_crsk_x), read K-contiguous by the LDS-DMA engine */
 
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
 int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
@@ -284,6 +286,21 @@ int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n, int h, 
                          int out_bf16, hipStream_t stream);
 int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, int r, int s, int cpad,
                               int out_bf16, hipStream_t stream);
+/* bf16 operands of the LDS-DMA conv engine (every operand of a bf16-math conv stored bf16):
+ * the transposed weights of the dgrad view Wt[Cin][R][S][Cout] (TMR_IO_WT_BF16); a block output
+ * written fp32 (identity residual, ReLU mask) AND as a bf16 copy (next convs' operand) in one pass
+ * (tmr_bn_apply_dual; tmr_bn_apply2_x with z16 != NULL); the stem maxpool output as bf16 (it is
+ * only a conv operand). */
+int tmr_weight_oihw_to_crsk_x(const float* w, void* wt, int k, int c, int r, int s, int out_bf16,
+                              hipStream_t stream);
+int tmr_bn_apply_dual(const float* y, const float* scale, const float* shift, const float* residual,
+                      float* z, void* z16, int rows, int c, int relu, hipStream_t stream);
+int tmr_bn_apply2_x(const float* y, const float* scale, const float* shift, const float* yr,
+                    const float* rscale, const float* rshift, float* z, void* z16, int rows, int c,
+                    int relu, hipStream_t stream);
+int tmr_maxpool2d_fwd_bn_x(const float* x, const float* scale, const float* shift, void* y,
+                           uint8_t* argmax, int n, int h, int w, int c, int ho, int wo, int out_bf16,
+                           hipStream_t stream);
 
 /* ---------------- pooling (pool_layout.hip) --------------------------------------- */
 /* MaxPool2d(3,2,1) of share.maxpool (train_only_non-local_pretrained.py:207), NHWC */

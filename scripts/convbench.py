@@ -47,6 +47,12 @@ def main():
                          "conv but the stem")
     ap.add_argument("--math", choices=["fp32", "bf16"], default="fp32",
                     help="conv operand precision (bf16 = the C4/C5 configs)")
+    ap.add_argument("--io16", action="store_true",
+                    help="bf16 math with every operand stored bf16 (x, KRSC w, dy; dgrad reads the "
+                         "transposed CRSK copy): the LDS-DMA engine, as the bf16 train step")
+    ap.add_argument("--bnbwd", action="store_true",
+                    help="dgrad with the fused BN-backward epilogue (ReLU mask from z, per-tile "
+                         "partials), as the train step runs every dgrad but the stem's")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
@@ -62,10 +68,25 @@ def main():
         wk = torch.randn(cout, r, r, cs, device=dev)
         y = ops.conv_fwd(x, wk, st, pad)
         dy = torch.randn_like(y)
+        wdg, wt = wk, False
+        if args.io16:
+            args.math = "bf16"
+            wo = torch.randn(cout, cs, r, r, device=dev)
+            wk = ops.weight_to_krsc(wo, bf16=True)
+            dy = dy.to(torch.bfloat16)
+            if cin != 3:   # the stem's 4-channel input stays fp32 (register-staged gather)
+                x = x.to(torch.bfloat16)
+                wdg, wt = ops.weight_to_crsk(wo), True
+            else:
+                wdg = wk
         xpro = dpro = None
         if args.pro and cin != 3:
             xpro = (torch.rand(cs, device=dev) + 0.5, torch.randn(cs, device=dev) * 0.1)
             dpro = (torch.randn_like(y), torch.randn(3, cout, device=dev))
+        dx = torch.empty(n, h, w, cs, device=dev)
+        if args.bnbwd and cin != 3:
+            yb, zb = torch.randn_like(dx), torch.rand_like(dx) - 0.3
+            meanb = torch.randn(cs, device=dev)
         for kind in kinds:
             if kind == "dgrad" and cin == 3:
                 continue
@@ -74,8 +95,12 @@ def main():
                                                        math=mt))
                   if (args.stats or xpro is not None)
                   else (lambda: ops.conv_fwd(x, wk, st, pad, out=y, math=mt)),
-                  "dgrad": lambda: ops.conv_dgrad(dy, wk, (h, w), st, pad, out=x,
-                                                  beta=args.dgrad_beta, dpro=dpro, math=mt),
+                  "dgrad": (lambda: ops.conv_dgrad_bnbwd(dy, wdg, (h, w), st, pad, yb, meanb, 1,
+                                                         z=zb, out=dx, beta=args.dgrad_beta,
+                                                         math=mt, wt=wt))
+                  if args.bnbwd else
+                  (lambda: ops.conv_dgrad(dy, wdg, (h, w), st, pad, out=dx,
+                                          beta=args.dgrad_beta, dpro=dpro, math=mt, wt=wt)),
                   "wgrad": lambda: ops.conv_wgrad(x, dy, r, r, st, pad, c_real=cin, xpro=xpro,
                                                   dpro=dpro, math=mt)}[kind]
             fn()

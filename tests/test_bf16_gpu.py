@@ -182,7 +182,8 @@ def test_bf16_storage_bit_identical(dev, backbone, time_conv):
     B, T, L = 2, 5, 7
     frames, off, lt, labels = _inputs(B, T, L, seed=51)
     res = {}
-    saved = trunk.BF16_STORE
+    saved = trunk.BF16_STORE, trunk.FULL16
+    trunk.FULL16 = False   # the all-bf16 LDS-DMA path: test_bf16_full16_step
     try:
         for store in (True, False):
             trunk.BF16_STORE = store
@@ -207,7 +208,7 @@ def test_bf16_storage_bit_identical(dev, backbone, time_conv):
                 with torch.no_grad():
                     res["eval32"] = m(x4, lt.to(dev)).clone()
     finally:
-        trunk.BF16_STORE = saved
+        trunk.BF16_STORE, trunk.FULL16 = saved
     assert torch.equal(res[True][0], res[False][0])
     for n in res[True][1]:
         assert torch.equal(res[True][1][n], res[False][1][n]), n
@@ -249,9 +250,109 @@ def test_bf16_storage_conv_kernels(dev):
                     d32 = ops.conv_dgrad(dy, w32, (h, w), st, pad, math="bf16")
                     d16 = ops.conv_dgrad(dy16, w16, (h, w), st, pad, math="bf16")
                     assert torch.equal(d16, d32), ("dgrad", shp, mf)
-                for xa in ((xd, x16) if cin != 3 else (xd,)):
-                    g32 = ops.conv_wgrad(xd, dy, r, r, st, pad, c_real=cin, math="bf16")
-                    g16 = ops.conv_wgrad(xa, dy16, r, r, st, pad, c_real=cin, math="bf16")
-                    assert torch.equal(g16, g32), ("wgrad", shp, mf, xa.dtype)
+                    # the LDS-DMA engine (transposed bf16 weights): same k order -> same bits
+                    dt = ops.conv_dgrad(dy16, ops.weight_to_crsk(wd), (h, w), st, pad,
+                                        math="bf16", wt=True)
+                    assert torch.equal(dt, d32), ("dgrad wt", shp, mf)
+                g32 = ops.conv_wgrad(xd, dy, r, r, st, pad, c_real=cin, math="bf16")
+                g16 = ops.conv_wgrad(xd, dy16, r, r, st, pad, c_real=cin, math="bf16")
+                assert torch.equal(g16, g32), ("wgrad", shp, mf)
+                if cin != 3:
+                    # all-bf16 operands: the LDS-DMA engine, whose split-K plan (tile count) may
+                    # differ -> the same products summed in another order
+                    g16 = ops.conv_wgrad(x16, dy16, r, r, st, pad, c_real=cin, math="bf16")
+                    err = (g16 - g32).abs().max().item() / g32.abs().max().item()
+                    assert err < 2e-6, ("wgrad all-bf16", shp, mf, err)
     finally:
         ops.MAX_FRAMES = saved
+
+
+def _conv_ref16(x, wt, stride, pad):
+    """float64 conv of bf16-rounded operands (NHWC x, OIHW w) -> NHWC."""
+    xn = x.double().permute(0, 3, 1, 2)
+    y = torch.nn.functional.conv2d(xn, wt.double(), stride=stride, padding=pad)
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("case", [
+    # n, h, w, cin, cout, r, stride, pad, x channel offset in a wider tensor (0 = dense)
+    (2, 9, 11, 32, 64, 3, 1, 1, 0),      # 32 channels per tap: a k-tile spans two taps (TAPV)
+    (3, 10, 10, 16, 32, 3, 2, 1, 0),     # 16 per tap, stride 2, odd output width
+    (2, 7, 7, 8, 16, 3, 1, 1, 0),        # 8 per tap (one piece per tap)
+    (2, 13, 9, 64, 128, 1, 1, 0, 0),     # 1x1, M not a tile multiple
+    (1, 20, 20, 128, 64, 3, 2, 1, 0),    # strided 3x3 (dgrad parity classes), N = 64
+    (2, 8, 8, 64, 64, 3, 1, 1, 64),      # channel-slice operand (grouped conv), x_ld = 128
+    (5, 14, 14, 256, 256, 3, 1, 1, 0),   # 256x256 tiles
+    (2, 6, 6, 512, 1024, 1, 2, 0, 0),    # strided 1x1 with empty parity classes in dgrad
+])
+def test_gemm16_views(dev, case):
+    """The bf16 LDS-DMA engine (every operand bf16 in HBM) on its three views against float64
+    convolutions of the same bf16 operands: FWD / DGRAD / WGRAD, TAPV (k-tiles spanning taps),
+    partial tiles, strided parity classes and channel-slice operands.  FWD and DGRAD also
+    bit-identical to the register-staged bf16 engine (same k order)."""
+    n, h, w, cin, cout, r, st, pad, xoff = case
+    g = torch.Generator().manual_seed(71 + cin + cout)
+    wt = _r(torch.randn(cout, cin, r, r, generator=g) / (cin * r * r) ** 0.5)
+    xs = _r(torch.randn(n, h, w, cin + xoff, generator=g))
+    x16 = xs.to(dev).to(torch.bfloat16)[..., xoff:]
+    xd = xs.to(dev)[..., xoff:]
+    wd = wt.to(dev)
+    w16, w32 = ops.weight_to_krsc(wd, bf16=True), ops.weight_to_krsc(wd)
+    if xoff:   # channel-slice operand (the forward with BN statistics takes dense x only)
+        y16 = ops.conv_fwd(x16, w16, st, pad, math="bf16")
+    else:
+        y16, _, _ = ops.conv_fwd_bnstats(x16, w16, st, pad, math="bf16")
+    ref = _conv_ref16(xs[..., xoff:], wt, st, pad)
+    err = (y16.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, ("fwd", err)
+    y32 = ops.conv_fwd(xd.contiguous(), w32, st, pad, math="bf16")
+    assert torch.equal(y16, y32)
+    dy = _r(torch.randn(y16.shape, generator=g))
+    dy16 = dy.to(dev).to(torch.bfloat16)
+    dx = ops.conv_dgrad(dy16, ops.weight_to_crsk(wd), (h, w), st, pad, math="bf16", wt=True)
+    xr = xs[..., xoff:].double().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, stride=st, padding=pad)
+    yr.backward(dy.double().permute(0, 3, 1, 2))
+    dx_ref = xr.grad.permute(0, 2, 3, 1)
+    err = (dx.double().cpu() - dx_ref).abs().max().item() / dx_ref.abs().max().item()
+    assert err < 1e-5, ("dgrad", err)
+    if cout >= 32:   # the register-staged engine needs one tap per 32-deep k-tile
+        assert torch.equal(dx, ops.conv_dgrad(dy16, w16, (h, w), st, pad, math="bf16"))
+    dw = ops.conv_wgrad(x16, dy16, r, r, st, pad, math="bf16")
+    err = (dw.double().cpu() - wr.grad).abs().max().item() / wr.grad.abs().max().item()
+    assert err < 1e-5, ("wgrad", err)
+
+
+def test_bf16_full16_step(dev):
+    """The all-bf16-operand train step (trunk.FULL16: bf16 block-output copies, bf16 maxpool
+    output, transposed bf16 dgrad weights, every conv but the stem on the LDS-DMA engine) against
+    the register-staged bf16 step: the same operands rounded the same way; only the BN-statistic
+    tile partials and the wgrad split-K plans differ (summation order), so logits agree to fp32
+    rounding and gradients to the ill-conditioning of a 10-frame BN batch."""
+    from tmrnet_amd import trunk
+    B, T, L = 2, 5, 7
+    frames, off, lt, labels = _inputs(B, T, L, seed=53)
+    res = {}
+    saved = trunk.FULL16
+    try:
+        for full in (True, False):
+            trunk.FULL16 = full
+            torch.manual_seed(54)
+            m = tmrnet_amd.resnet_lstm(seq_len=T, precision="bf16").to(dev).train()
+            m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+            m.forced_head_mask = torch.ones(B, 512, device=dev)
+            x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
+            out = m(x4, lt.to(dev))
+            tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels.to(dev)).backward()
+            torch.cuda.synchronize()
+            res[full] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()})
+    finally:
+        trunk.FULL16 = saved
+    assert (res[True][0] - res[False][0]).abs().max().item() < 1e-4
+    assert torch.equal(res[True][0].argmax(1), res[False][0].argmax(1))
+    num = sum(((res[True][1][k] - res[False][1][k]).double() ** 2).sum() for k in res[True][1])
+    den = sum((res[False][1][k].double() ** 2).sum() for k in res[True][1])
+    assert (num / den).sqrt().item() < 1e-2
+    for k in res[True][1]:
+        assert torch.isfinite(res[True][1][k]).all(), k

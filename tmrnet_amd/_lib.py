@@ -67,6 +67,10 @@ SIGNATURES = {
     "tmr_bn_bwd_x": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, I, P],
     "tmr_bn_bwd_maxpool_x": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, I, P],
     "tmr_weight_oihw_to_krsc_x": [P, P, I, I, I, I, I, I, P],
+    "tmr_weight_oihw_to_crsk_x": [P, P, I, I, I, I, I, P],
+    "tmr_bn_apply_dual": [P, P, P, P, P, P, I, I, I, P],
+    "tmr_bn_apply2_x": [P, P, P, P, P, P, P, P, I, I, I, P],
+    "tmr_maxpool2d_fwd_bn_x": [P, P, P, P, P, I, I, I, I, I, I, I, P],
     "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
     "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],

@@ -157,11 +157,13 @@ __device__ __forceinline__ void st4(__bf16* p, long i4, float4 v) {
       make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
 }
 
-template <bool RES, bool RELU, typename TZ = float>
+// DUAL: z (fp32) and a bf16 (RNE) copy z16 -- a block output is both the next block's identity
+// residual (fp32) and the operand of its bf16-math convs (bf16, read by the LDS-DMA engine)
+template <bool RES, bool RELU, typename TZ = float, bool DUAL = false>
 __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift,
                                                  const float* __restrict__ res, TZ* __restrict__ z,
-                                                 long n4, int c4) {
+                                                 long n4, int c4, __bf16* __restrict__ z16 = nullptr) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cc = (int)(i % c4) * 4;
     float4 v = reinterpret_cast<const float4*>(y)[i];
@@ -179,19 +181,21 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, co
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
     }
     st4(z, i, v);
+    if (DUAL) st4(z16, i, v);
   }
 }
 
 // z = act(y*scale + shift + (yr*rscale + rshift)): the Bottleneck's BN3 + residual + ReLU with the
 // downsample branch's BatchNorm applied on the fly (its output is never materialised).  Same
 // fmaf/add/max sequence as bn_apply of the branch followed by bn_apply with that residual.
-template <bool RELU>
+template <bool RELU, bool DUAL = false>
 __global__ __launch_bounds__(NT) void bn_apply2_k(const float* __restrict__ y, const float* __restrict__ scale,
                                                   const float* __restrict__ shift,
                                                   const float* __restrict__ yr,
                                                   const float* __restrict__ rscale,
                                                   const float* __restrict__ rshift,
-                                                  float* __restrict__ z, long n4, int c4) {
+                                                  float* __restrict__ z, long n4, int c4,
+                                                  __bf16* __restrict__ z16) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cc = (int)(i % c4) * 4;
     float4 v = reinterpret_cast<const float4*>(y)[i];
@@ -208,6 +212,7 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const float* __restrict__ y, c
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
     }
     reinterpret_cast<float4*>(z)[i] = v;
+    if (DUAL) st4(z16, i, v);
   }
 }
 
@@ -719,17 +724,49 @@ TMR_API int tmr_bn_apply_x(const float* y, const float* scale, const float* shif
 TMR_API int tmr_bn_apply2(const float* y, const float* scale, const float* shift, const float* yr,
                           const float* rscale, const float* rshift, float* z, int rows, int c,
                           int relu, hipStream_t stream) {
+  return tmr_bn_apply2_x(y, scale, shift, yr, rscale, rshift, z, nullptr, rows, c, relu, stream);
+}
+
+TMR_API int tmr_bn_apply2_x(const float* y, const float* scale, const float* shift, const float* yr,
+                            const float* rscale, const float* rshift, float* z, void* z16,
+                            int rows, int c, int relu, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_bn_apply2: channels %d must be a multiple of 4", c);
   TMR_CHECK_ARG(y && scale && shift && yr && rscale && rshift && z, "tmr_bn_apply2: null operand");
   TMR_CHECK_ARG(yr != z, "tmr_bn_apply2: the branch input must not alias z");
   const long n4 = (long)rows * c / 4;
-  if (relu)
+  __bf16* h = (__bf16*)z16;
+  if (relu && h)
+    hipLaunchKernelGGL((bn_apply2_k<true, true>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+                       shift, yr, rscale, rshift, z, n4, c / 4, h);
+  else if (relu)
     hipLaunchKernelGGL((bn_apply2_k<true>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale, shift,
-                       yr, rscale, rshift, z, n4, c / 4);
+                       yr, rscale, rshift, z, n4, c / 4, h);
+  else if (h)
+    hipLaunchKernelGGL((bn_apply2_k<false, true>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+                       shift, yr, rscale, rshift, z, n4, c / 4, h);
   else
     hipLaunchKernelGGL((bn_apply2_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale, shift,
-                       yr, rscale, rshift, z, n4, c / 4);
+                       yr, rscale, rshift, z, n4, c / 4, h);
   TMR_CHECK_LAUNCH("bn_apply2");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply_dual(const float* y, const float* scale, const float* shift,
+                              const float* residual, float* z, void* z16, int rows, int c, int relu,
+                              hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_bn_apply_dual: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(y && scale && shift && z && z16, "tmr_bn_apply_dual: null operand");
+  const long n4 = (long)rows * c / 4;
+  const int nb = ew_blocks(n4), c4 = c / 4;
+  __bf16* h = (__bf16*)z16;
+  if (residual) {
+    if (relu) hipLaunchKernelGGL((bn_apply_k<true, true, float, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4, h);
+    else hipLaunchKernelGGL((bn_apply_k<true, false, float, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4, h);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_apply_k<false, true, float, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4, h);
+    else hipLaunchKernelGGL((bn_apply_k<false, false, float, true>), dim3(nb), dim3(NT), 0, stream, y, scale, shift, residual, z, n4, c4, h);
+  }
+  TMR_CHECK_LAUNCH("bn_apply_dual");
   return 0;
 }
 

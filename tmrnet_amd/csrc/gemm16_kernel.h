@@ -1,0 +1,441 @@
+// bf16 implicit-GEMM engine on LDS-DMA staging (gfx950).  The bf16-math conv views whose operands
+// are all stored as bf16 in HBM (tmr_conv_desc.io: x, dy and the weights -- the dgrad view reads a
+// transposed [Cin][R][S][Cout] weight copy, TMR_IO_WT_BF16) run here instead of gemm_kernel's
+// register-staged path:
+//
+//   * operands go global -> LDS with `buffer_load_dwordx4 ... lds` (LDS-DMA): no VGPR staging, no
+//     conversion, no ds_write; each lane's source address is its own, so the implicit-GEMM gather
+//     (pixel + tap offset, zero padding by out-of-range offsets -- an out-of-range LDS-DMA writes
+//     zeros) costs a few VALU ops per 16-B piece;
+//   * BK = 64 (four v_mfma_f32_32x32x16_bf16 k-steps per k-tile), two LDS stages: the k-tile t+1
+//     pieces are issued right after the barrier that publishes tile t and land under its MFMAs;
+//   * K-contiguous operands (FWD A/B, DGRAD A/B) use a [rows][64] image (128-B rows) with the
+//     16-B chunk index XOR-swizzled by (row >> 1) & 7: every ds_read_b128 lane group of the MFMA
+//     operand read hits 16 distinct bank quads.  The swizzle is applied to the SOURCE address of
+//     the LDS-DMA (the LDS image itself is lane-linear) and to the read;
+//   * the WGRAD operands are reduction-major in HBM (dY[m][co], X[pixel][c]): their image is
+//     [64 k-rows][R columns] and the MFMA fragments come from ds_read_b64_tr_b16 (a 4x16 block
+//     per 16 lanes, delivered column-major), two per 8-k fragment; chunks XOR-swizzled by k so
+//     each 32-lane half covers all 64 banks.
+//
+// Accumulator layout, XCD-aware tile order and the epilogue (BN statistics, fused BN backward,
+// beta, split-K slabs, dgrad parity scatter) are gemm_kernel's (epilogue_batched: branch-free
+// buffer accesses, each chunk of rows issuing all its loads first -- the fused BN-backward dgrads
+// are bound by that traffic), and the k order of the accumulation is the register-staged bf16
+// path's, so FWD / DGRAD results are bit-identical to it.
+#pragma once
+#include "gemm_kernel.h"
+
+namespace tmrg {
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+#define TMR_LDS_AS __attribute__((address_space(3)))
+
+// one 16-B LDS-DMA piece per lane: LDS dst = (wave-uniform) dst + 16 * lane
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, unsigned char* dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (TMR_LDS_AS void*)dst, 16, voff, 0, 0, 0);
+}
+
+// reduction-major image with R columns: chunk swizzle of k-row k
+template <int R>
+__device__ __forceinline__ int mn_swz(int k) {
+  return R >= 128 ? ((k & 3) << 2) : (((k >> 1) & 1) << 2);
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs a) {
+  constexpr int BK = 64;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr bool MN = (MODE == MODE_WGRAD);   // both operands reduction-major
+  constexpr int ABYTES = BM * BK * 2, BBYTES = BN * BK * 2, STAGE = ABYTES + BBYTES;
+  constexpr int NIA = ABYTES / (1024 * NW), NIB = BBYTES / (1024 * NW);   // pieces / wave / tile
+  static_assert(NIA >= 1 && NIB >= 1 && NIA * 1024 * NW == ABYTES && NIB * 1024 * NW == BBYTES,
+                "LDS-DMA pieces per wave");
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  static_assert(!MN || (BM >= 64 && BN >= 64), "reduction-major images need >= 64 columns");
+  constexpr int EPI = WM * BN * 2 * 4;
+  constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, hh = lane >> 5;
+
+  // XCD-aware tile order (gemm_kernel's)
+  const int nmt = (a.M + BM - 1) / BM;
+  const int nnt = (a.N + BN - 1) / BN;
+  const int nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    int xcd = bid & 7, loc = bid >> 3;
+    int q = nwg >> 3, r = nwg & 7;
+    int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    bid = (nwg >= 8) ? wg : bid;
+  }
+  const int m0 = (bid / nnt) * BM;
+  const int n0 = (bid % nnt) * BN;
+
+  int kbeg = 0, kend = a.K;
+  if (MODE == MODE_WGRAD) {
+    kbeg = blockIdx.y * a.kchunk;
+    kend = min(a.K, kbeg + a.kchunk);
+  }
+  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.A, a.Abytes);
+  const __amdgpu_buffer_rsrc_t rB = make_rsrc(a.B, a.Bbytes);
+  const int cmask = (1 << a.log2C) - 1;
+
+  // ---------------- per-lane piece state (fixed across k-tiles) ----------------
+  // K-contiguous pieces: piece q of this wave = image rows 8 * (wave + NW * q) .. + 7, lane -> row
+  // + lane / 8, chunk (lane & 7) ^ swizzle
+  auto kc_row = [&](int q) { return 8 * (wave + NW * q) + (lane >> 3); };
+  auto kc_chunk = [&](int q) { return (lane & 7) ^ ((kc_row(q) >> 1) & 7); };
+  // reduction-major pieces (R columns): piece q = 64 chunks = 512 / R k-rows of the image
+
+  // A: FWD / DGRAD gathered rows (pixel byte offset, y, x, in range)
+  uint32_t apix[MN ? 1 : NIA];
+  int ay[MN ? 1 : NIA], ax[MN ? 1 : NIA], ach[MN ? 1 : NIA];
+  bool aok[MN ? 1 : NIA];
+  // A: WGRAD dY columns (co byte offset), k-row of the piece
+  uint32_t aco[MN ? NIA : 1];
+  int akr[MN ? NIA : 1];
+  bool acok[MN ? NIA : 1];
+  if constexpr (!MN) {
+#pragma unroll
+    for (int q = 0; q < NIA; ++q) {
+      const int m = m0 + kc_row(q);
+      aok[q] = m < a.M;
+      const uint32_t mm = aok[q] ? (uint32_t)m : 0u;
+      const uint32_t n = fdiv(mm, a.dHW);
+      const uint32_t rem = mm - n * a.dHW.d;
+      const uint32_t y = fdiv(rem, a.dW);
+      const uint32_t x = rem - y * a.dW.d;
+      ay[q] = (int)y * a.sy;
+      ax[q] = (int)x * a.sx;
+      apix[q] = (uint32_t)(((int)n * a.Hs + ay[q]) * a.Ws + ax[q]) * (uint32_t)a.lds * 2u;
+      ach[q] = 8 * kc_chunk(q);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NIA; ++q) {
+      const int s = 64 * (wave + NW * q) + lane;
+      const int k = s / (BM / 8);
+      const int ch = (s % (BM / 8)) ^ mn_swz<BM>(k);
+      const int i = m0 + 8 * ch;
+      akr[q] = k;
+      acok[q] = i < a.M;
+      aco[q] = (uint32_t)i * 2u;
+    }
+  }
+  // B: FWD weight rows / DGRAD transposed-weight rows (row byte offset, chunk), WGRAD X columns
+  uint32_t brow[MN ? 1 : NIB];
+  int bch[MN ? 1 : NIB];
+  bool bok[NIB];
+  int bdy[MN ? NIB : 1], bdx[MN ? NIB : 1], bkr[MN ? NIB : 1];
+  uint32_t bco[MN ? NIB : 1];
+  if constexpr (!MN) {
+#pragma unroll
+    for (int q = 0; q < NIB; ++q) {
+      const int j = n0 + kc_row(q);
+      bok[q] = j < a.N;
+      const uint32_t jj = bok[q] ? (uint32_t)j : 0u;
+      brow[q] = jj * (uint32_t)(MODE == MODE_DGRAD ? a.ldbt : a.ldb) * 2u;
+      bch[q] = 8 * kc_chunk(q);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NIB; ++q) {
+      const int s = 64 * (wave + NW * q) + lane;
+      const int k = s / (BN / 8);
+      const int ch = (s % (BN / 8)) ^ mn_swz<BN>(k);
+      const int j = n0 + 8 * ch;
+      const int tap = a.ntaps == 1 ? 0 : (j >> a.log2C);
+      const int c = a.ntaps == 1 ? j : (j & cmask);
+      int ri, si;
+      tap_split(a, tap, ri, si);
+      bdy[q] = a.oy0 + a.dyr * ri;
+      bdx[q] = a.ox0 + a.dxs * si;
+      bco[q] = (uint32_t)c * 2u;
+      bok[q] = j < a.N && tap < a.ntaps;
+      bkr[q] = k;
+    }
+  }
+
+  // ---------------- stage one k-tile into LDS buffer `buf` ----------------
+  auto stage = [&](int kt, int buf) {
+    const int kb = kbeg + kt * BK;
+    unsigned char* As = smem + buf * STAGE;
+    unsigned char* Bs = As + ABYTES;
+    if constexpr (!MN) {
+      // tap of this k-tile (uniform unless TAPV)
+      int tapU = 0, cbU = kb, dyU = a.oy0, dxU = a.ox0;
+      if (!TAPV && a.ntaps != 1) {
+        tapU = kb >> a.log2C;
+        cbU = kb & cmask;
+        int ri, si;
+        tap_split(a, tapU, ri, si);
+        dyU = a.oy0 + a.dyr * ri;
+        dxU = a.ox0 + a.dxs * si;
+      }
+#pragma unroll
+      for (int q = 0; q < NIA; ++q) {
+        const int k = kb + ach[q];
+        int tap = tapU, c = cbU + ach[q], dy = dyU, dx = dxU;
+        if (TAPV) {
+          tap = k >> a.log2C;
+          c = k & cmask;
+          int ri, si;
+          tap_split(a, tap, ri, si);
+          dy = a.oy0 + a.dyr * ri;
+          dx = a.ox0 + a.dxs * si;
+        }
+        const int ys = ay[q] + dy, xs = ax[q] + dx;
+        const bool ok = aok[q] && k < kend && tap < a.ntaps && (unsigned)ys < (unsigned)a.Hs &&
+                        (unsigned)xs < (unsigned)a.Ws;
+        const uint32_t off = apix[q] + (uint32_t)(((dy * a.Ws + dx) * a.lds + c) * 2);
+        glds16(rA, As + 1024 * (wave + NW * q), ok ? off : OOB);
+      }
+      if constexpr (MODE == MODE_FWD) {
+        // B[j][k] = W[co][tap][c]: k-contiguous rows of the KRSC weights
+#pragma unroll
+        for (int q = 0; q < NIB; ++q) {
+          const int k = kb + bch[q];
+          const bool ok = bok[q] && k < kend;
+          glds16(rB, Bs + 1024 * (wave + NW * q), ok ? brow[q] + (uint32_t)k * 2u : OOB);
+        }
+      } else {
+        // B[j=ci][k=(tap,co)] = Wt[ci][rs(tap)][co]
+        int tapB = 0, coB = kb, rsB = 0;
+        if (!TAPV) {
+          if (a.ntaps != 1) {
+            tapB = kb >> a.log2C;
+            coB = kb & cmask;
+          }
+          int ri, si;
+          tap_split(a, tapB, ri, si);
+          rsB = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
+        }
+#pragma unroll
+        for (int q = 0; q < NIB; ++q) {
+          const int k = kb + bch[q];
+          int tap = tapB, co = coB + bch[q], rs = rsB;
+          if (TAPV) {
+            tap = k >> a.log2C;
+            co = k & cmask;
+            int ri, si;
+            tap_split(a, tap, ri, si);
+            rs = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
+          }
+          const bool ok = bok[q] && k < kend && tap < a.ntaps;
+          const uint32_t off = brow[q] + (uint32_t)((rs << a.log2C) + co) * 2u;
+          glds16(rB, Bs + 1024 * (wave + NW * q), ok ? off : OOB);
+        }
+      }
+    } else {
+      // WGRAD A[k=m][i=co] = dY[m][co]
+#pragma unroll
+      for (int q = 0; q < NIA; ++q) {
+        const int m = kb + akr[q];
+        const bool ok = acok[q] && m < kend;
+        glds16(rA, As + 1024 * (wave + NW * q), ok ? (uint32_t)m * (uint32_t)a.ldb * 2u + aco[q] : OOB);
+      }
+      // WGRAD B[k=m][j=(tap,c)] = X[src(m, tap)][c]
+#pragma unroll
+      for (int q = 0; q < NIB; ++q) {
+        const int m = kb + bkr[q];
+        const uint32_t mm = m < kend ? (uint32_t)m : 0u;
+        const uint32_t n = fdiv(mm, a.dHW);
+        const uint32_t rem = mm - n * a.dHW.d;
+        const uint32_t y = fdiv(rem, a.dW);
+        const uint32_t x = rem - y * a.dW.d;
+        const int ys = (int)y * a.sy + bdy[q], xs = (int)x * a.sx + bdx[q];
+        const bool ok = m < kend && bok[q] && (unsigned)ys < (unsigned)a.Hs &&
+                        (unsigned)xs < (unsigned)a.Ws;
+        const uint32_t off = (uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds * 2u + bco[q];
+        glds16(rB, Bs + 1024 * (wave + NW * q), ok ? off : OOB);
+      }
+    }
+  };
+
+  // ---------------- MFMA operand reads ----------------
+  // K-contiguous: row `row`, k-step s -> 8 k at chunk 2s + hh; the swizzle depends on row bits
+  // 1..3 only, which are l31's (the tile bases are multiples of 32)
+  const int kx = (l31 >> 1) & 7;
+  // reduction-major (tr reads): lane (g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3) supplies
+  // k-row 16s + 8(g >> 1) + 4t + q, columns cb + 16(g & 1) + 4p .. + 3
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  auto tr_frag = [&](const unsigned char* img, int R, int swz, int cb, int s) -> bf16x8 {
+    const int col = cb + 16 * (tg & 1) + 4 * tp;
+    const int k0 = 16 * s + 8 * (tg >> 1) + tq;
+    const uint32_t cbyte = (uint32_t)((((col >> 3) ^ swz) << 4) + (col & 7) * 2);
+    const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (TMR_LDS_AS s16x4_t*)(img + k0 * R * 2 + cbyte));
+    const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (TMR_LDS_AS s16x4_t*)(img + (k0 + 4) * R * 2 + cbyte));
+    const s16x8_t w = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, w);
+  };
+  const int swzA = mn_swz<BM>(tq), swzB = mn_swz<BN>(tq);
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int arow0 = wm * (BM / WM) + l31;
+  const int brow0 = wn * (BN / WN) + l31;
+  auto compute = [&](int buf) {
+    const unsigned char* As = smem + buf * STAGE;
+    const unsigned char* Bs = As + ABYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 av[TM], bv[TN];
+      const int ch = (2 * s + hh) ^ kx;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (!MN)
+          av[i] = *reinterpret_cast<const bf16x8*>(As + (arow0 + 32 * i) * 128 + (ch << 4));
+        else
+          av[i] = tr_frag(As, BM, swzA, wm * (BM / WM) + 32 * i, s);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (!MN)
+          bv[j] = *reinterpret_cast<const bf16x8*>(Bs + (brow0 + 32 * j) * 128 + (ch << 4));
+        else
+          bv[j] = tr_frag(Bs, BN, swzB, wn * (BN / WN) + 32 * j, s);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---------------- main loop: two LDS stages ----------------
+  // Iteration kt: wait for this wave's pieces of tile kt, barrier (every wave's pieces landed;
+  // every wave finished reading the other buffer in iteration kt-1), issue tile kt+1 into the
+  // other buffer, MFMAs on tile kt while it lands.
+  if (ntiles > 0) {
+    stage(0, 0);
+    for (int kt = 0; kt < ntiles; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < ntiles) stage(kt + 1, (kt + 1) & 1);
+      compute(kt & 1);
+    }
+  }
+  __syncthreads();   // LDS reads done (no LDS-DMA in flight) before the epilogue reuses smem
+
+  epilogue_batched<MODE, BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), m0, n0);
+}
+
+// ---------------------------------------------------------------- launch selection
+struct Cfg16 { int bm, bn; };
+constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64, 256}, {64, 64}};
+
+// Eligibility: bf16 math, every operand bf16 in HBM (sab 3; DGRAD with the transposed weights),
+// no operand prologue, 16-B pieces of 8 channels (channels per tap, row strides multiples of 8).
+inline bool use16(const GemmArgs& a, int mode) {
+  static const bool on = env_int("TMR_GEMM16", 1) != 0;   // A/B switch (experiments)
+  if (!on || a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
+  if (mode == MODE_DGRAD && !a.wt) return false;
+  if (a.lds % 8) return false;
+  if (mode == MODE_WGRAD) return a.M % 8 == 0 && a.log2C >= 3 && a.ldb % 8 == 0 && a.N % 8 == 0;
+  if (mode == MODE_FWD && a.ldb % 8) return false;
+  if (mode == MODE_DGRAD && a.ldbt % 8) return false;
+  return a.ntaps == 1 ? (a.K % 8 == 0 && (mode == MODE_FWD || a.log2C >= 3)) : a.log2C >= 3;
+}
+
+inline long cfg16_tiles(long M, long N, int c) {
+  return ((M + kCfgs16[c].bm - 1) / kCfgs16[c].bm) * ((N + kCfgs16[c].bn - 1) / kCfgs16[c].bn);
+}
+
+// Tile choice per view, from scripts/convbench.py --io16 --stats --bnbwd with each config forced
+// over the 23 ResNet-50 conv shapes x 3 views (profiles/r2/convbench16_cfgs/): 256x256 (8 waves,
+// one workgroup per CU) only pays for the long-reduction forwards and the largest wgrads; the
+// dgrads, whose fused BatchNorm-backward epilogue moves 12-16 B per output element, want the
+// occupancy of 128x128 / 256x64 tiles.
+inline int pick_cfg16(long M, long N, long K, int mode) {
+  static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
+  if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
+  (void)K;
+  int cfg;
+  if (mode == MODE_WGRAD) {
+    if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
+    else if (N <= 64) cfg = 3;
+    else if (M >= 256 && M <= 512 && N >= 2048) cfg = 0;
+    else if (M == 256 && N == 512) cfg = 0;
+    else cfg = 2;
+  } else if (N <= 64) {
+    cfg = M >= 256 ? 3 : 5;
+  } else if (mode == MODE_FWD && N >= 256 && M >= 256) {
+    cfg = 0;
+  } else {
+    cfg = 2;
+  }
+  if (mode != MODE_WGRAD && cfg16_tiles(M, N, cfg) < 256) {
+    for (const int c2 : {1, 2, 5}) {
+      if ((long)kCfgs16[c2].bm * kCfgs16[c2].bn >= (long)kCfgs16[cfg].bm * kCfgs16[cfg].bn ||
+          cfg16_tiles(M, N, c2) <= cfg16_tiles(M, N, cfg))
+        continue;
+      cfg = c2;
+      if (cfg16_tiles(M, N, cfg) >= 256) break;
+    }
+  }
+  return cfg;
+}
+
+// rows / columns of the output tile the launch for `a` will use (host planning: BN-partial rows,
+// wgrad split counts)
+inline int gemm_tile_bm(const GemmArgs& a, int mode) {
+  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode)].bm
+                        : kCfgs[pick_cfg(a.M, a.N, a.K, mode)].bm;
+}
+inline long gemm_tiles(const GemmArgs& a, int mode) {
+  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode))
+                        : cfg_tiles(a.M, a.N, pick_cfg(a.M, a.N, a.K, mode));
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
+int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
+  const dim3 blk(64 * WM * WN);
+  if (tapv)
+    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1>), grid, blk, 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0>), grid, blk, 0, st, a);
+  TMR_CHECK_LAUNCH("gemm16_kernel");
+  return 0;
+}
+
+template <int MODE>
+int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
+  TMR_CHECK_ARG(((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0,
+                "gemm (bf16 LDS-DMA path): operands must be 16-B aligned");
+  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE);
+  const Cfg16 c = kCfgs16[cfg];
+  dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
+  if (grid.x == 0) return 0;
+  // a k-tile of 64 spans several taps when the channels per tap are fewer (or not a multiple)
+  const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % 64) != 0;
+  if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
+  switch (cfg) {
+    case 0: return launch16_cfg<MODE, 256, 256, 2, 4>(a, tapv, grid, st);
+    case 1: return launch16_cfg<MODE, 256, 128, 4, 2>(a, tapv, grid, st);
+    case 2: return launch16_cfg<MODE, 128, 128, 2, 2>(a, tapv, grid, st);
+    case 3: return launch16_cfg<MODE, 256, 64, 4, 1>(a, tapv, grid, st);
+    case 4: return launch16_cfg<MODE, 64, 256, 1, 4>(a, tapv, grid, st);
+    default: return launch16_cfg<MODE, 64, 64, 2, 2>(a, tapv, grid, st);
+  }
+}
+
+}  // namespace tmrg

@@ -1,5 +1,5 @@
 // Implicit-GEMM convolution / GEMM engine: host side and C ABI (kernel template: gemm_kernel.h).
-#include "gemm_kernel.h"
+#include "gemm16_kernel.h"
 
 #include <type_traits>
 
@@ -82,7 +82,7 @@ static inline long span(long pixels, int ld, int width) { return pixels > 0 ? (p
 
 // element bytes of the conv operands (tmr_conv_desc.io: bf16-stored x / w / dy)
 static inline int esz_x(const tmr_conv_desc* d) { return (d->io & TMR_IO_X_BF16) ? 2 : 4; }
-static inline int esz_w(const tmr_conv_desc* d) { return (d->io & TMR_IO_W_BF16) ? 2 : 4; }
+static inline int esz_w(const tmr_conv_desc* d) { return (d->io & (TMR_IO_W_BF16 | TMR_IO_WT_BF16)) ? 2 : 4; }
 static inline int esz_dy(const tmr_conv_desc* d) { return (d->io & TMR_IO_DY_BF16) ? 2 : 4; }
 template <typename T>
 static inline T* adv(T* p, long elems, int esz) {   // p + elems elements of esz bytes
@@ -198,8 +198,10 @@ static tmr_conv_desc chunk_desc(const tmr_conv_desc* d, int nc) {
 }
 
 static int stats_parts_of(const tmr_conv_desc* d) {
-  const long M = (long)d->n * d->ho * d->wo;
-  return cdiv(M, kCfgs[pick_cfg(M, d->k, (long)d->r * d->s * d->c, MODE_FWD)].bm);
+  GemmArgs a;
+  bool al;
+  if (conv_fwd_args(d, nullptr, nullptr, nullptr, nullptr, 0.f, a, al)) return 0;
+  return cdiv(a.M, gemm_tile_bm(a, MODE_FWD));
 }
 
 static long x_frame(const tmr_conv_desc* d) { return (long)d->h * d->w * xld_of(d); }
@@ -304,6 +306,8 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
   const int lk = ilog2_exact(d->k);
   TMR_CHECK_ARG(lk >= 2, "tmr_conv2d_dgrad: output channels %d must be a power of two >= 4", d->k);
   TMR_CHECK_ARG(d->c % 4 == 0, "tmr_conv2d_dgrad: input channels %d must be a multiple of 4", d->c);
+  TMR_CHECK_ARG(!(d->io & TMR_IO_WT_BF16) || !(d->io & TMR_IO_W_BF16),
+                "tmr_conv2d_dgrad: TMR_IO_WT_BF16 and TMR_IO_W_BF16 are exclusive weight layouts");
   const int st = d->stride;
   // one launch per stride-parity class (ph,pw): rows h = st*y + ph
   for (int ph = 0; ph < st; ++ph) {
@@ -333,13 +337,17 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
       a.Abytes = clamp_bytes_e(span((long)d->n * d->ho * d->wo, a.lds, d->k), esz_dy(d));
       a.prec = d->math;
       a.Bbytes = clamp_bytes_e((long)d->k * d->r * d->s * d->c, esz_w(d));
-      a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
+      a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & (TMR_IO_W_BF16 | TMR_IO_WT_BF16)) ? 2 : 0);
+      if (d->io & TMR_IO_WT_BF16) {   // w = Wt[ci][r][s][co] (bf16)
+        a.wt = 1;
+        a.ldbt = d->r * d->s * d->k;
+      }
       a.Cbytes = clamp_bytes(span((long)d->n * d->h * d->w, a.ldc, d->c));
       a.oH = d->h; a.oW = d->w; a.osy = st; a.osx = st; a.oyc = ph; a.oxc = pw;
       // nothing to add -- unless the fused BN backward must still see (mask, sum) these pixels
       if (a.K == 0 && beta == 1.f && !fz) continue;
       if (fz) {
-        const long nmt = cdiv(a.M, kCfgs[pick_cfg(a.M, a.N, a.K, MODE_DGRAD)].bm);
+        const long nmt = cdiv(a.M, gemm_tile_bm(a, MODE_DGRAD));
         if (fz->count_only) { fz->nparts += nmt; continue; }
         a.bn_y = fz->y; a.bn_z = fz->z; a.bn_sc = fz->sc; a.bn_sh = fz->sh; a.bn_mean = fz->mean;
         a.bn_mask = fz->mask;
@@ -448,11 +456,28 @@ TMR_API int tmr_conv2d_dgrad_pro(const tmr_conv_desc* d, const float* dy, const 
   return 0;
 }
 
+// the WGRAD view of a conv (no pointers, no split plan)
+static void wgrad_fill(const tmr_conv_desc* d, GemmArgs& a) {
+  a = GemmArgs{};
+  a.M = d->k; a.N = d->r * d->s * d->c; a.K = d->n * d->ho * d->wo;
+  a.log2C = ilog2_exact(d->c);
+  set_taps(a, d->r, d->s);
+  a.oy0 = -d->pad; a.ox0 = -d->pad_w; a.dyr = 1; a.dxs = 1;
+  set_grid(a, d->n, d->ho, d->wo);
+  a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
+  a.lds = xld_of(d); a.ldb = yld_of(d); a.ldc = a.N; a.beta = 0.f;
+  a.Abytes = clamp_bytes_e(span((long)d->n * d->ho * d->wo, a.ldb, d->k), esz_dy(d));
+  a.prec = d->math;
+  a.Bbytes = clamp_bytes_e(span((long)d->n * d->h * d->w, a.lds, d->c), esz_x(d));
+  a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & TMR_IO_X_BF16) ? 2 : 0);
+}
+
 static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* slab) {
   const long Mred = (long)d->n * d->ho * d->wo;
   const long Mo = d->k, No = (long)d->r * d->s * d->c;
-  const TileCfg tc = kCfgs[pick_cfg(Mo, No, Mred, MODE_WGRAD)];
-  const long tiles = (long)cdiv(Mo, tc.bm) * cdiv(No, tc.bn);
+  GemmArgs a;
+  wgrad_fill(d, a);
+  const long tiles = gemm_tiles(a, MODE_WGRAD);
   // aim for ~target workgroups; at least minrows reduction rows per split
   static const long target = env_int("TMR_WGRAD_TARGET", 512);
   static const long minrows = env_int("TMR_WGRAD_MINROWS", 1024);
@@ -462,7 +487,7 @@ static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* sl
   if (maxsp < 1) maxsp = 1;
   if (sp > maxsp) sp = maxsp;
   long kc = (Mred + sp - 1) / sp;
-  kc = (kc + 31) / 32 * 32;  // multiple of every BK (16, 32)
+  kc = (kc + 63) / 64 * 64;  // multiple of every BK (16, 32, 64)
   sp = (Mred + kc - 1) / kc;
   *splits = (int)sp;
   *kchunk = (int)kc;
@@ -523,20 +548,11 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   TMR_CHECK_ARG(ws && ws_bytes >= (size_t)sp * slab * sizeof(float),
                 "tmr_conv2d_wgrad: workspace too small (%zu < %zu)", ws_bytes,
                 (size_t)sp * slab * sizeof(float));
-  GemmArgs a{};
+  GemmArgs a;
+  wgrad_fill(d, a);
+  (void)lc;
   a.A = dy; a.B = x; a.C = ws; a.bias = nullptr;
-  a.M = d->k; a.N = d->r * d->s * d->c; a.K = d->n * d->ho * d->wo;
-  a.log2C = lc;
-  set_taps(a, d->r, d->s);
-  a.oy0 = -d->pad; a.ox0 = -d->pad_w; a.dyr = 1; a.dxs = 1;
-  set_grid(a, d->n, d->ho, d->wo);
-  a.Hs = d->h; a.Ws = d->w; a.sy = d->stride; a.sx = d->stride;
-  a.lds = xld_of(d); a.ldb = yld_of(d); a.ldc = a.N; a.beta = 0.f;
   a.kchunk = kc; a.slab = slab;
-  a.Abytes = clamp_bytes_e(span((long)d->n * d->ho * d->wo, a.ldb, d->k), esz_dy(d));
-  a.prec = d->math;
-  a.Bbytes = clamp_bytes_e(span((long)d->n * d->h * d->w, a.lds, d->c), esz_x(d));
-  a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & TMR_IO_X_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(slab);
   bool al = aligned16(x) && aligned16(dy) && (d->k % 4 == 0) && a.lds % 4 == 0 && a.ldb % 4 == 0;
   int rc = set_prologue(a, pro, d, true, true, 0);

@@ -106,6 +106,9 @@ struct GemmArgs {
   // elements; byte extents and offsets in bf16 units).  Exact w.r.t. the fp32-stored bf16 path:
   // the loaders would round those operands to bf16 (RNE) anyway.
   int sab;
+  // DGRAD B operand is the transposed bf16 weight copy Wt[ci][r][s][co] (TMR_IO_WT_BF16; the
+  // LDS-DMA engine of gemm16_kernel.h only), row stride ldbt = R*S*Cout elements
+  int wt, ldbt;
 };
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -162,6 +165,442 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint
 __device__ __forceinline__ void tap_split(const GemmArgs& a, int tap, int& ri, int& si) {
   ri = (tap * a.tapSinv) >> 16;
   si = tap - ri * a.tapS;
+}
+
+// Epilogue, batched form: branch-free buffer accesses over C's extent, each chunk of ER rows
+// issuing all of its loads before consuming any (latency-bound short-reduction GEMMs).  Used by
+// gemm_kernel's 64x64 tiles and by every tile of the LDS-DMA engine.
+template <int MODE, int BM, int BN, int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&acc)[TM][TN],
+                                                 float* smem, int m0, int n0) {
+  const int tid = threadIdx.x;
+  // The epilogue's thread indices derive from an opaque copy of the thread id: otherwise the
+  // compiler computes its row/column offsets before the main loop and keeps them live (or
+  // spilled) across it.
+  int etid = tid;
+  asm volatile("" : "+v"(etid));
+  {
+  const int wm = (etid >> 6) / WN, wn = (etid >> 6) % WN;
+  const int l31 = etid & 31, hh = (etid & 63) >> 5;
+  // Branch-free: every access to C (and to the tensors laid out like C) goes through a buffer
+  // descriptor over C's extent; rows outside M and columns outside N get an out-of-range offset
+  // (loads return 0, stores are dropped).  Rows are handled in chunks of ER accumulator
+  // registers so each chunk's loads are issued back to back before any is consumed.
+  float* Cb = a.C;
+  if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
+  const __amdgpu_buffer_rsrc_t rC = make_rsrc(Cb, a.Cbytes);
+  const int col0 = n0 + wn * (BN / WN) + l31;
+  constexpr int ER = TN >= 4 ? 4 : 16 / (2 * TN);   // rows per chunk: 16 / 8 / 4 (TN = 1 / 2 / 4)
+  uint32_t cob[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    cob[j] = col0 + 32 * j < a.N ? (uint32_t)(col0 + 32 * j) * 4u : OOB;
+  // byte offset of accumulator row (i, r) in C; OOB outside M
+  auto row_off = [&](int i, int r) -> uint32_t {
+    const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    uint32_t pix = (uint32_t)row;
+    if (MODE == MODE_DGRAD) {   // output-pixel map of the parity class (identity when st == 1)
+      const uint32_t n = fdiv((uint32_t)row, a.dHW);
+      const uint32_t rem = row - n * a.dHW.d;
+      const uint32_t y = fdiv(rem, a.dW);
+      const uint32_t x = rem - y * a.dW.d;
+      pix = ((n * a.oH + y * a.osy + a.oyc) * a.oW + x * a.osx + a.oxc);
+    }
+    return row < a.M ? pix * (uint32_t)a.ldc * 4u : OOB;
+  };
+  // rob OOB + a column offset stays >= 2^31 (no wrap): still out of range
+  auto eoff = [&](uint32_t rob, int j) -> uint32_t { return cob[j] == OOB ? OOB : rob + cob[j]; };
+  auto st1 = [&](float v, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rC, off, 0, 0);
+  };
+  // Every chunk issues all of its loads (old C for beta, y / z of the fused BN backward, the
+  // residual of the fused forward) before consuming any; each row offset is computed once, in
+  // its chunk (kept out of the other phases so the offsets never stay live across them).
+  const bool has_beta = a.beta != 0.f;
+  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums.  Rows /
+  // columns outside the output hold acc == 0 (their operand loads returned zeros) and read
+  // bn_y == 0, so they add nothing to either sum.
+  if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
+    const __amdgpu_buffer_rsrc_t rY = make_rsrc(a.bn_y, a.Cbytes);
+    const __amdgpu_buffer_rsrc_t rZ = make_rsrc(a.bn_mask == 1 ? a.bn_z : a.bn_y, a.Cbytes);
+    const uint32_t zoob = a.bn_mask == 1 ? 0u : OOB;   // z is read only for mask 1
+    float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = col0 + 32 * j;
+      const bool okc = col < a.N;
+      mu[j] = okc ? a.bn_mean[col] : 0.f;
+      // keep test t = z + fmaf(y, bsc, bsh) > 0, branch-free over the mask modes:
+      // 1: z (bsc = bsh = 0); 2: y*scale+shift (z loads are out of range -> 0); 0: 1 > 0
+      bsc[j] = (okc && a.bn_mask == 2) ? a.bn_sc[col] : 0.f;
+      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : (a.bn_mask == 0 ? 1.f : 0.f);
+      cs[j] = 0.f;
+      cq[j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r0 = 0; r0 < 16; r0 += ER) {
+        uint32_t off[ER][TN];
+        float yv[ER][TN], zv[ER][TN];
+#pragma unroll
+        for (int r = 0; r < ER; ++r) {
+          const uint32_t ro = row_off(i, r0 + r);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            off[r][j] = eoff(ro, j);
+            yv[r][j] = bld1(rY, off[r][j]);
+            zv[r][j] = bld1(rZ, zoob | off[r][j]);
+          }
+        }
+        float old[ER][TN];
+#pragma unroll
+        for (int r = 0; r < ER; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) old[r][j] = has_beta ? bld1(rC, off[r][j]) : 0.f;
+#pragma unroll
+        for (int r = 0; r < ER; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float v = fmaf(a.beta, old[r][j], acc[i][j][r0 + r]);
+            const bool keep = zv[r][j] + fmaf(yv[r][j], bsc[j], bsh[j]) > 0.f;
+            v = keep ? v : 0.f;
+            st1(v, off[r][j]);
+            cs[j] += v;
+            cq[j] = fmaf(v, yv[r][j] - mu[j], cq[j]);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    float* red = smem;  // [WM][BN][2]; the main loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+      if (hh == 0) {
+        const int c = wn * (BN / WN) + 32 * j + l31;
+        red[(wm * BN + c) * 2] = cs[j];
+        red[(wm * BN + c) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * (BN / WN) + 32 * j + l31;
+        float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          t0 += red[(w * BN + c) * 2];
+          t1 += red[(w * BN + c) * 2 + 1];
+        }
+        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+      }
+    }
+    return;
+  }
+  // (2) bias
+  float bvals[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col0 + 32 * j;
+    bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
+  }
+  // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
+  // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
+  if (MODE == MODE_FWD && a.stats != nullptr) {
+    float* red = smem;  // main loop ended with a barrier: LDS is free
+    const int nrows = min(BM, a.M - m0);
+    const int rbase_w = m0 + wm * (BM / WM) + 4 * hh;
+    auto valid = [&](int i, int r) {
+      return rbase_w + 32 * i + (r & 3) + 8 * (r >> 2) < a.M;
+    };
+    float cs[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += valid(i, r) ? acc[i][j][r] + bvals[j] : 0.f;
+      t += __shfl_xor(t, 32, 64);
+      cs[j] = t;
+    }
+    if (hh == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
+    __syncthreads();
+    float mj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
+      mj[j] = t / (float)nrows;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[i][j][r] + bvals[j] - mj[j];
+          t += valid(i, r) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 32, 64);
+      cs[j] = t;
+    }
+    if (hh == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col0 + 32 * j;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
+        if (col < a.N)
+          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
+      }
+    }
+  }
+  // (3) beta, FWD inference epilogue (scale, residual, ReLU), stores
+  const bool has_res = MODE == MODE_FWD && a.res != nullptr;
+  const __amdgpu_buffer_rsrc_t rR = make_rsrc(has_res ? a.res : Cb, a.Cbytes);
+  float scj[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col0 + 32 * j;
+    scj[j] = (MODE == MODE_FWD && a.scale && col < a.N) ? a.scale[col] : 1.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r0 = 0; r0 < 16; r0 += ER) {
+      uint32_t off[ER][TN];
+      float old[ER][TN], rv[ER][TN];
+#pragma unroll
+      for (int r = 0; r < ER; ++r) {
+        const uint32_t ro = row_off(i, r0 + r);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          off[r][j] = eoff(ro, j);
+          old[r][j] = has_beta ? bld1(rC, off[r][j]) : 0.f;
+          rv[r][j] = has_res ? bld1(rR, off[r][j]) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < ER; ++r)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = fmaf(acc[i][j][r0 + r], scj[j], bvals[j]);
+          v = fmaf(a.beta, old[r][j], v);
+          if (MODE == MODE_FWD) {
+            v += rv[r][j];
+            if (a.relu) v = fmaxf(v, 0.f);
+          }
+          st1(v, off[r][j]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// Epilogue of the larger tiles: per-element guarded accesses (the batched branch-free form of the
+// 64x64 tiles pushes their main loops past the VGPR budget).  Shared by gemm_kernel and the bf16
+// LDS-DMA engine (gemm16_kernel.h).  smem: >= WM * BN * 2 floats, free (the main loop has ended
+// with a barrier and no LDS-DMA in flight).
+template <int MODE, int BM, int BN, int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void epilogue_guarded(const GemmArgs& a, floatx16 (&acc)[TM][TN],
+                                                 float* smem, int m0, int n0) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, hh = lane >> 5;
+  float* Cb = a.C;
+  if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
+  const int col0 = n0 + wn * (BN / WN) + l31;
+  // output row offset for accumulator register r of row-tile i (-1: outside M)
+  auto row_off = [&](int i, int r) -> long {
+    const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    if (row >= a.M) return -1;
+    if (MODE == MODE_DGRAD && a.osy != 0) {
+      uint32_t n = fdiv((uint32_t)row, a.dHW);
+      uint32_t rem = row - n * a.dHW.d;
+      uint32_t y = fdiv(rem, a.dW);
+      uint32_t x = rem - y * a.dW.d;
+      long pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
+      return pix * a.ldc;
+    }
+    return (long)row * a.ldc;
+  };
+  // (1) all reads of the old output first (beta), so they are issued back to back
+  if (a.beta != 0.f) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long ro = row_off(i, r);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = col0 + 32 * j;
+          if (ro >= 0 && col < a.N) acc[i][j][r] += a.beta * Cb[ro + col];
+        }
+      }
+  }
+  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums
+  if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
+    float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = col0 + 32 * j;
+      const bool okc = col < a.N;
+      mu[j] = okc ? a.bn_mean[col] : 0.f;
+      bsc[j] = (okc && a.bn_mask == 2) ? a.bn_sc[col] : 0.f;
+      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : 0.f;
+      cs[j] = 0.f;
+      cq[j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long ro = row_off(i, r);
+        if (ro < 0) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = col0 + 32 * j;
+          if (col >= a.N) continue;
+          float v = acc[i][j][r];
+          const float yv = a.bn_y[ro + col];
+          bool keep = true;
+          if (a.bn_mask == 1) keep = a.bn_z[ro + col] > 0.f;
+          else if (a.bn_mask == 2) keep = fmaf(yv, bsc[j], bsh[j]) > 0.f;
+          v = keep ? v : 0.f;
+          Cb[ro + col] = v;
+          cs[j] += v;
+          cq[j] = fmaf(v, yv - mu[j], cq[j]);
+        }
+      }
+    float* red = smem;  // [WM][BN][2]; the main loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+      if (hh == 0) {
+        const int c = wn * (BN / WN) + 32 * j + l31;
+        red[(wm * BN + c) * 2] = cs[j];
+        red[(wm * BN + c) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * (BN / WN) + 32 * j + l31;
+        float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          t0 += red[(w * BN + c) * 2];
+          t1 += red[(w * BN + c) * 2 + 1];
+        }
+        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+      }
+    }
+    return;
+  }
+  // (2) bias + stores
+  float bvals[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col0 + 32 * j;
+    bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
+  }
+  // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
+  // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
+  if (MODE == MODE_FWD && a.stats != nullptr) {
+    float* red = smem;  // main loop ended with a barrier: LDS is free
+    const int nrows = min(BM, a.M - m0);
+    const int rbase_w = m0 + wm * (BM / WM) + 4 * hh;
+    auto valid = [&](int i, int r) {
+      return rbase_w + 32 * i + (r & 3) + 8 * (r >> 2) < a.M;
+    };
+    float cs[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += valid(i, r) ? acc[i][j][r] + bvals[j] : 0.f;
+      t += __shfl_xor(t, 32, 64);
+      cs[j] = t;
+    }
+    if (hh == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
+    __syncthreads();
+    float mj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
+      mj[j] = t / (float)nrows;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[i][j][r] + bvals[j] - mj[j];
+          t += valid(i, r) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 32, 64);
+      cs[j] = t;
+    }
+    if (hh == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col0 + 32 * j;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
+        if (col < a.N)
+          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long ro = row_off(i, r);
+      if (ro < 0) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col0 + 32 * j;
+        if (col >= a.N) continue;
+        float v = acc[i][j][r] + bvals[j];
+        if (MODE == MODE_FWD) {
+          if (a.scale) v = fmaf(acc[i][j][r], a.scale[col], bvals[j]);
+          if (a.res) v += a.res[ro + col];
+          if (a.relu) v = fmaxf(v, 0.f);
+        }
+        Cb[ro + col] = v;
+      }
+    }
 }
 
 // VAR: 0 = aligned float4 loads, one tap per k-tile (channels per tap >= BK, or a plain GEMM)
@@ -688,420 +1127,9 @@ __global__ TMR_GEMM_LB void gemm_kernel(const GemmArgs a) {
   // buffer accesses, loads batched per chunk of rows.  Larger tiles: per-element guarded
   // accesses -- the batched form pushes their main loops past the VGPR budget (spills).
   if constexpr (TM * TN == 1) {
-  // The epilogue's thread indices derive from an opaque copy of the thread id: otherwise the
-  // compiler computes its row/column offsets before the main loop and keeps them live (or
-  // spilled) across it.
-  int etid = tid;
-  asm volatile("" : "+v"(etid));
-  {
-  const int wm = (etid >> 6) / WN, wn = (etid >> 6) % WN;
-  const int l31 = etid & 31, hh = (etid & 63) >> 5;
-  // Branch-free: every access to C (and to the tensors laid out like C) goes through a buffer
-  // descriptor over C's extent; rows outside M and columns outside N get an out-of-range offset
-  // (loads return 0, stores are dropped).  Rows are handled in chunks of ER accumulator
-  // registers so each chunk's loads are issued back to back before any is consumed.
-  float* Cb = a.C;
-  if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
-  const __amdgpu_buffer_rsrc_t rC = make_rsrc(Cb, a.Cbytes);
-  const int col0 = n0 + wn * (BN / WN) + l31;
-  constexpr int ER = TN >= 4 ? 4 : 16 / (2 * TN);   // rows per chunk: 16 / 8 / 4 (TN = 1 / 2 / 4)
-  uint32_t cob[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-    cob[j] = col0 + 32 * j < a.N ? (uint32_t)(col0 + 32 * j) * 4u : OOB;
-  // byte offset of accumulator row (i, r) in C; OOB outside M
-  auto row_off = [&](int i, int r) -> uint32_t {
-    const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-    uint32_t pix = (uint32_t)row;
-    if (MODE == MODE_DGRAD) {   // output-pixel map of the parity class (identity when st == 1)
-      const uint32_t n = fdiv((uint32_t)row, a.dHW);
-      const uint32_t rem = row - n * a.dHW.d;
-      const uint32_t y = fdiv(rem, a.dW);
-      const uint32_t x = rem - y * a.dW.d;
-      pix = ((n * a.oH + y * a.osy + a.oyc) * a.oW + x * a.osx + a.oxc);
-    }
-    return row < a.M ? pix * (uint32_t)a.ldc * 4u : OOB;
-  };
-  // rob OOB + a column offset stays >= 2^31 (no wrap): still out of range
-  auto eoff = [&](uint32_t rob, int j) -> uint32_t { return cob[j] == OOB ? OOB : rob + cob[j]; };
-  auto st1 = [&](float v, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rC, off, 0, 0);
-  };
-  // Every chunk issues all of its loads (old C for beta, y / z of the fused BN backward, the
-  // residual of the fused forward) before consuming any; each row offset is computed once, in
-  // its chunk (kept out of the other phases so the offsets never stay live across them).
-  const bool has_beta = a.beta != 0.f;
-  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums.  Rows /
-  // columns outside the output hold acc == 0 (their operand loads returned zeros) and read
-  // bn_y == 0, so they add nothing to either sum.
-  if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
-    const __amdgpu_buffer_rsrc_t rY = make_rsrc(a.bn_y, a.Cbytes);
-    const __amdgpu_buffer_rsrc_t rZ = make_rsrc(a.bn_mask == 1 ? a.bn_z : a.bn_y, a.Cbytes);
-    const uint32_t zoob = a.bn_mask == 1 ? 0u : OOB;   // z is read only for mask 1
-    float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = col0 + 32 * j;
-      const bool okc = col < a.N;
-      mu[j] = okc ? a.bn_mean[col] : 0.f;
-      // keep test t = z + fmaf(y, bsc, bsh) > 0, branch-free over the mask modes:
-      // 1: z (bsc = bsh = 0); 2: y*scale+shift (z loads are out of range -> 0); 0: 1 > 0
-      bsc[j] = (okc && a.bn_mask == 2) ? a.bn_sc[col] : 0.f;
-      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : (a.bn_mask == 0 ? 1.f : 0.f);
-      cs[j] = 0.f;
-      cq[j] = 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r0 = 0; r0 < 16; r0 += ER) {
-        uint32_t off[ER][TN];
-        float yv[ER][TN], zv[ER][TN];
-#pragma unroll
-        for (int r = 0; r < ER; ++r) {
-          const uint32_t ro = row_off(i, r0 + r);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            off[r][j] = eoff(ro, j);
-            yv[r][j] = bld1(rY, off[r][j]);
-            zv[r][j] = bld1(rZ, zoob | off[r][j]);
-          }
-        }
-        float old[ER][TN];
-#pragma unroll
-        for (int r = 0; r < ER; ++r)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) old[r][j] = has_beta ? bld1(rC, off[r][j]) : 0.f;
-#pragma unroll
-        for (int r = 0; r < ER; ++r)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            float v = fmaf(a.beta, old[r][j], acc[i][j][r0 + r]);
-            const bool keep = zv[r][j] + fmaf(yv[r][j], bsc[j], bsh[j]) > 0.f;
-            v = keep ? v : 0.f;
-            st1(v, off[r][j]);
-            cs[j] += v;
-            cq[j] = fmaf(v, yv[r][j] - mu[j], cq[j]);
-          }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    float* red = smem;  // [WM][BN][2]; the main loop ended with a barrier
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      cs[j] += __shfl_xor(cs[j], 32, 64);
-      cq[j] += __shfl_xor(cq[j], 32, 64);
-      if (hh == 0) {
-        const int c = wn * (BN / WN) + 32 * j + l31;
-        red[(wm * BN + c) * 2] = cs[j];
-        red[(wm * BN + c) * 2 + 1] = cq[j];
-      }
-    }
-    __syncthreads();
-    if (wm == 0 && hh == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = wn * (BN / WN) + 32 * j + l31;
-        float t0 = 0.f, t1 = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) {
-          t0 += red[(w * BN + c) * 2];
-          t1 += red[(w * BN + c) * 2 + 1];
-        }
-        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
-      }
-    }
-    return;
-  }
-  // (2) bias
-  float bvals[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = col0 + 32 * j;
-    bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
-  }
-  // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
-  // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
-  if (MODE == MODE_FWD && a.stats != nullptr) {
-    float* red = smem;  // main loop ended with a barrier: LDS is free
-    const int nrows = min(BM, a.M - m0);
-    const int rbase_w = m0 + wm * (BM / WM) + 4 * hh;
-    auto valid = [&](int i, int r) {
-      return rbase_w + 32 * i + (r & 3) + 8 * (r >> 2) < a.M;
-    };
-    float cs[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += valid(i, r) ? acc[i][j][r] + bvals[j] : 0.f;
-      t += __shfl_xor(t, 32, 64);
-      cs[j] = t;
-    }
-    if (hh == 0)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
-    __syncthreads();
-    float mj[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
-      mj[j] = t / (float)nrows;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = acc[i][j][r] + bvals[j] - mj[j];
-          t += valid(i, r) ? d * d : 0.f;
-        }
-      t += __shfl_xor(t, 32, 64);
-      cs[j] = t;
-    }
-    if (hh == 0)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
-    __syncthreads();
-    if (wm == 0 && hh == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = col0 + 32 * j;
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
-        if (col < a.N)
-          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
-      }
-    }
-  }
-  // (3) beta, FWD inference epilogue (scale, residual, ReLU), stores
-  const bool has_res = MODE == MODE_FWD && a.res != nullptr;
-  const __amdgpu_buffer_rsrc_t rR = make_rsrc(has_res ? a.res : Cb, a.Cbytes);
-  float scj[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = col0 + 32 * j;
-    scj[j] = (MODE == MODE_FWD && a.scale && col < a.N) ? a.scale[col] : 1.f;
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int r0 = 0; r0 < 16; r0 += ER) {
-      uint32_t off[ER][TN];
-      float old[ER][TN], rv[ER][TN];
-#pragma unroll
-      for (int r = 0; r < ER; ++r) {
-        const uint32_t ro = row_off(i, r0 + r);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          off[r][j] = eoff(ro, j);
-          old[r][j] = has_beta ? bld1(rC, off[r][j]) : 0.f;
-          rv[r][j] = has_res ? bld1(rR, off[r][j]) : 0.f;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < ER; ++r)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float v = fmaf(acc[i][j][r0 + r], scj[j], bvals[j]);
-          v = fmaf(a.beta, old[r][j], v);
-          if (MODE == MODE_FWD) {
-            v += rv[r][j];
-            if (a.relu) v = fmaxf(v, 0.f);
-          }
-          st1(v, off[r][j]);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
+    epilogue_batched<MODE, BM, BN, WM, WN, TM, TN>(a, acc, smem, m0, n0);
   } else {
-  float* Cb = a.C;
-  if (MODE == MODE_WGRAD) Cb += (long)blockIdx.y * a.slab;
-  const int col0 = n0 + wn * (BN / WN) + l31;
-  // output row offset for accumulator register r of row-tile i (-1: outside M)
-  auto row_off = [&](int i, int r) -> long {
-    const int row = m0 + wm * (BM / WM) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-    if (row >= a.M) return -1;
-    if (MODE == MODE_DGRAD && a.osy != 0) {
-      uint32_t n = fdiv((uint32_t)row, a.dHW);
-      uint32_t rem = row - n * a.dHW.d;
-      uint32_t y = fdiv(rem, a.dW);
-      uint32_t x = rem - y * a.dW.d;
-      long pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
-      return pix * a.ldc;
-    }
-    return (long)row * a.ldc;
-  };
-  // (1) all reads of the old output first (beta), so they are issued back to back
-  if (a.beta != 0.f) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long ro = row_off(i, r);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = col0 + 32 * j;
-          if (ro >= 0 && col < a.N) acc[i][j][r] += a.beta * Cb[ro + col];
-        }
-      }
-  }
-  // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums
-  if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
-    float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = col0 + 32 * j;
-      const bool okc = col < a.N;
-      mu[j] = okc ? a.bn_mean[col] : 0.f;
-      bsc[j] = (okc && a.bn_mask == 2) ? a.bn_sc[col] : 0.f;
-      bsh[j] = (okc && a.bn_mask == 2) ? a.bn_sh[col] : 0.f;
-      cs[j] = 0.f;
-      cq[j] = 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long ro = row_off(i, r);
-        if (ro < 0) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = col0 + 32 * j;
-          if (col >= a.N) continue;
-          float v = acc[i][j][r];
-          const float yv = a.bn_y[ro + col];
-          bool keep = true;
-          if (a.bn_mask == 1) keep = a.bn_z[ro + col] > 0.f;
-          else if (a.bn_mask == 2) keep = fmaf(yv, bsc[j], bsh[j]) > 0.f;
-          v = keep ? v : 0.f;
-          Cb[ro + col] = v;
-          cs[j] += v;
-          cq[j] = fmaf(v, yv - mu[j], cq[j]);
-        }
-      }
-    float* red = smem;  // [WM][BN][2]; the main loop ended with a barrier
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      cs[j] += __shfl_xor(cs[j], 32, 64);
-      cq[j] += __shfl_xor(cq[j], 32, 64);
-      if (hh == 0) {
-        const int c = wn * (BN / WN) + 32 * j + l31;
-        red[(wm * BN + c) * 2] = cs[j];
-        red[(wm * BN + c) * 2 + 1] = cq[j];
-      }
-    }
-    __syncthreads();
-    if (wm == 0 && hh == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = wn * (BN / WN) + 32 * j + l31;
-        float t0 = 0.f, t1 = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) {
-          t0 += red[(w * BN + c) * 2];
-          t1 += red[(w * BN + c) * 2 + 1];
-        }
-        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
-      }
-    }
-    return;
-  }
-  // (2) bias + stores
-  float bvals[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = col0 + 32 * j;
-    bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
-  }
-  // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
-  // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
-  if (MODE == MODE_FWD && a.stats != nullptr) {
-    float* red = smem;  // main loop ended with a barrier: LDS is free
-    const int nrows = min(BM, a.M - m0);
-    const int rbase_w = m0 + wm * (BM / WM) + 4 * hh;
-    auto valid = [&](int i, int r) {
-      return rbase_w + 32 * i + (r & 3) + 8 * (r >> 2) < a.M;
-    };
-    float cs[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += valid(i, r) ? acc[i][j][r] + bvals[j] : 0.f;
-      t += __shfl_xor(t, 32, 64);
-      cs[j] = t;
-    }
-    if (hh == 0)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
-    __syncthreads();
-    float mj[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
-      mj[j] = t / (float)nrows;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = acc[i][j][r] + bvals[j] - mj[j];
-          t += valid(i, r) ? d * d : 0.f;
-        }
-      t += __shfl_xor(t, 32, 64);
-      cs[j] = t;
-    }
-    if (hh == 0)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) red[wm * BN + wn * (BN / WN) + 32 * j + l31] = cs[j];
-    __syncthreads();
-    if (wm == 0 && hh == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = col0 + 32 * j;
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
-        if (col < a.N)
-          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const long ro = row_off(i, r);
-      if (ro < 0) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = col0 + 32 * j;
-        if (col >= a.N) continue;
-        float v = acc[i][j][r] + bvals[j];
-        if (MODE == MODE_FWD) {
-          if (a.scale) v = fmaf(acc[i][j][r], a.scale[col], bvals[j]);
-          if (a.res) v += a.res[ro + col];
-          if (a.relu) v = fmaxf(v, 0.f);
-        }
-        Cb[ro + col] = v;
-      }
-    }
+    epilogue_guarded<MODE, BM, BN, WM, WN, TM, TN>(a, acc, smem, m0, n0);
   }
 }
 
@@ -1236,6 +1264,8 @@ int launch_gemm_t(const GemmArgs& a, bool al, int splits, hipStream_t st) {
                 "gemm: dY-operand prologue needs y and coefficients (dgrad or wgrad view)");
   TMR_CHECK_ARG(uniform || (al && MODE == MODE_FWD),
                 "gemm: per-element taps need aligned channels and the forward view");
+  TMR_CHECK_ARG(!a.wt, "gemm: transposed bf16 weights (TMR_IO_WT_BF16) need the bf16 LDS-DMA "
+                "path: bf16 dy, 8-channel multiples, 16-B aligned operands");
   const int cfg = pick_cfg(a.M, a.N, a.K, MODE);
   const TileCfg c = kCfgs[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);

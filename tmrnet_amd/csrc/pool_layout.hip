@@ -6,6 +6,7 @@
 //    (train_only_non-local_pretrained.py:101-126 crop with per-clip seed,
 //    :335-341 Normalize constants), producing the NHWC4 layout the stem conv reads.
 #include "common.h"
+#include <type_traits>
 #include "tmr.h"
 
 namespace {
@@ -19,8 +20,8 @@ int ew_blocks(long n) {
 
 // BN: the input is the stem conv's pre-BN output; relu(x*scale + shift) is applied per loaded
 // element (the stem's BN+ReLU output is never materialised; same fmaf/max as bn_apply).
-template <bool BN>
-__global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x, float* __restrict__ y,
+template <bool BN, typename TY = float>
+__global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x, TY* __restrict__ y,
                                                     uchar4* __restrict__ am, int n, int h, int w,
                                                     int c4, int ho, int wo,
                                                     const float* __restrict__ scale,
@@ -61,7 +62,14 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x,
         if (v.w > best.w || isnan(v.w)) { best.w = v.w; bi.w = id; }
       }
     }
-    reinterpret_cast<float4*>(y)[i] = best;
+    if constexpr (std::is_same<TY, float>::value) {
+      reinterpret_cast<float4*>(y)[i] = best;
+    } else {   // bf16 (RNE): a tensor consumed only as a bf16-math conv operand
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      const bf16x2_t lo = {(__bf16)best.x, (__bf16)best.y}, hi = {(__bf16)best.z, (__bf16)best.w};
+      reinterpret_cast<uint2*>(y)[i] =
+          make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+    }
     am[i] = bi;
   }
 }
@@ -124,6 +132,22 @@ __global__ void oihw_to_krsc_k(const float* __restrict__ w, TO* __restrict__ wk,
     const int tap = (int)(t % rs);
     const int ko = (int)(t / rs);
     wk[i] = (TO)(ci < c ? w[((long)ko * c + ci) * rs + tap] : 0.f);   // bf16: RNE
+  }
+}
+
+// OIHW -> [Cin][R][S][Cout] (the transposed weights of the dgrad view, TMR_IO_WT_BF16); writes
+// along co are strided, the weights are small (<= 9.4 MB per tensor)
+template <typename TO>
+__global__ void oihw_to_crsk_k(const float* __restrict__ w, TO* __restrict__ wt, int k, int c,
+                               int rs) {
+  const long total = (long)k * rs * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ko = (int)(i % k);
+    const long t = i / k;
+    const int tap = (int)(t % rs);
+    const int ci = (int)(t / rs);
+    wt[i] = (TO)w[((long)ko * c + ci) * rs + tap];   // bf16: RNE
   }
 }
 
@@ -191,11 +215,21 @@ TMR_API int tmr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int n, 
 TMR_API int tmr_maxpool2d_fwd_bn(const float* x, const float* scale, const float* shift, float* y,
                                  uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
                                  hipStream_t stream) {
+  return tmr_maxpool2d_fwd_bn_x(x, scale, shift, y, argmax, n, h, w, c, ho, wo, 0, stream);
+}
+
+TMR_API int tmr_maxpool2d_fwd_bn_x(const float* x, const float* scale, const float* shift, void* y,
+                                   uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
+                                   int out_bf16, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd_bn: channels %d must be a multiple of 4", c);
   TMR_CHECK_ARG(scale && shift, "tmr_maxpool2d_fwd_bn: null BatchNorm scale/shift");
   const long total = (long)n * ho * wo * (c / 4);
-  hipLaunchKernelGGL(maxpool_fwd_k<true>, dim3(ew_blocks(total)), dim3(NT), 0, stream, x, y,
-                     (uchar4*)argmax, n, h, w, c / 4, ho, wo, scale, shift);
+  if (out_bf16)
+    hipLaunchKernelGGL((maxpool_fwd_k<true, __bf16>), dim3(ew_blocks(total)), dim3(NT), 0, stream, x,
+                       (__bf16*)y, (uchar4*)argmax, n, h, w, c / 4, ho, wo, scale, shift);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_k<true>), dim3(ew_blocks(total)), dim3(NT), 0, stream, x,
+                       (float*)y, (uchar4*)argmax, n, h, w, c / 4, ho, wo, scale, shift);
   TMR_CHECK_LAUNCH("maxpool_fwd_bn");
   return 0;
 }
@@ -244,6 +278,18 @@ TMR_API int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, in
   return 0;
 }
 
+TMR_API int tmr_weight_oihw_to_crsk_x(const float* w, void* wt, int k, int c, int r, int s,
+                                      int out_bf16, hipStream_t stream) {
+  TMR_CHECK_ARG(w && wt && k > 0 && c > 0 && r > 0 && s > 0, "tmr_weight_oihw_to_crsk_x: bad arguments");
+  if (out_bf16)
+    hipLaunchKernelGGL(oihw_to_crsk_k<__bf16>, dim3(ew_blocks((long)k * r * s * c)), dim3(NT), 0,
+                       stream, w, (__bf16*)wt, k, c, r * s);
+  else
+    hipLaunchKernelGGL(oihw_to_crsk_k<float>, dim3(ew_blocks((long)k * r * s * c)), dim3(NT), 0,
+                       stream, w, (float*)wt, k, c, r * s);
+  TMR_CHECK_LAUNCH("oihw_to_crsk");
+  return 0;
+}
 
 TMR_API int tmr_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, int cpad,
                              hipStream_t stream) {

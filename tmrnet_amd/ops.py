@@ -70,16 +70,28 @@ _SUFFIX = {"fp32": "", "bf16": "_bf16"}
 MAX_FRAMES = 0
 
 
-IO_X, IO_W, IO_DY = 1, 2, 4     # tmr_conv_desc.io: bf16-stored x / KRSC weights / dy
+IO_X, IO_W, IO_DY, IO_WT = 1, 2, 4, 8   # tmr_conv_desc.io: bf16-stored x / KRSC w / dy / CRSK w
 
 
-def _io(x=None, w=None, dy=None):
-    """tmr_conv_desc.io from the operands' dtypes (bf16 storage of conv-operand-only tensors)."""
+def _io(x=None, w=None, dy=None, wt=False):
+    """tmr_conv_desc.io from the operands' dtypes (bf16 storage of conv-operand-only tensors);
+    wt: w is the transposed [Cin][R][S][Cout] bf16 copy (dgrad view, weight_to_crsk)."""
     io = 0
-    for t, bit in ((x, IO_X), (w, IO_W), (dy, IO_DY)):
+    for t, bit in ((x, IO_X), (w, IO_WT if wt else IO_W), (dy, IO_DY)):
         if t is not None and t.dtype == torch.bfloat16:
             io |= bit
+    if wt and not io & IO_WT:
+        raise RuntimeError("transposed (CRSK) weights must be bf16")
     return io
+
+
+def _dgrad_w(w, wt):
+    """(k, r, s, c) of a dgrad weight operand: KRSC, or with wt the transposed CRSK copy."""
+    if wt:
+        c, r, s, k = w.shape
+    else:
+        k, r, s, c = w.shape
+    return k, r, s, c
 
 
 def _esz(t):
@@ -198,15 +210,16 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
 
 
 def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, math="fp32",
-               dpro=None):
+               dpro=None, wt=False):
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices).
     dpro = (y, coef): dy is the masked BN-output gradient g, read as the BN backward
-    A*g + B*y + C (tmr_bn_bwd_coefs)."""
+    A*g + B*y + C (tmr_bn_bwd_coefs).  wt: w_krsc is the transposed bf16 copy (C,R,S,K)
+    (weight_to_crsk; the bf16 LDS-DMA engine, with bf16 dy)."""
     _req_op(w_krsc, "w")
     n, ho, wo, k = dy.shape
-    k2, r, s, c = w_krsc.shape
+    k2, r, s, c = _dgrad_w(w_krsc, wt)
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(None, w_krsc, dy))
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(None, w_krsc, dy, wt))
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
@@ -225,14 +238,15 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
 
 
 def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scale=None,
-                     shift=None, out=None, beta=0.0, math="fp32", dpro=None):
+                     shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
-    y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts)."""
+    y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts).
+    wt: as conv_dgrad."""
     _req_op(w_krsc, "w"); _req(y, "y"); _req(mean, "mean")
     n, ho, wo, k = dy.shape
-    k2, r, s, c = w_krsc.shape
+    k2, r, s, c = _dgrad_w(w_krsc, wt)
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math, io=_io(None, w_krsc, dy))
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math, io=_io(None, w_krsc, dy, wt))
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
@@ -405,6 +419,15 @@ def weight_to_krsc(w, cpad=None, bf16=False):
     return out
 
 
+def weight_to_crsk(w, bf16=True):
+    """OIHW fp32 -> the transposed dgrad operand (Cin, R, S, Cout), bf16 (RNE): the weights of
+    the bf16 LDS-DMA engine's dgrad view (tmr_conv_desc.io TMR_IO_WT_BF16)."""
+    k, c, r, s = w.shape
+    out = _empty((c, r, s, k), w, dtype=torch.bfloat16 if bf16 else f32)
+    call("tmr_weight_oihw_to_crsk_x", _req(w, "w"), out, k, c, r, s, int(bf16), stream_ptr())
+    return out
+
+
 def nchw_to_nhwc(x, cpad=None):
     n, c, h, w = x.shape
     cpad = c if cpad is None else cpad
@@ -474,17 +497,30 @@ def bn_apply(y, scale, shift, residual=None, relu=True, out=None, bf16=False):
     return out
 
 
-def bn_apply2(y, scale, shift, yr, rscale, rshift, relu=True, out=None):
-    """act(y*scale + shift + (yr*rscale + rshift)): BN3 + the downsample branch's BN + ReLU."""
+def bn_apply_dual(y, scale, shift, residual=None, relu=True):
+    """bn_apply writing z in fp32 and a bf16 (RNE) copy in one pass -> (z, z16): a block output
+    is the next block's identity residual (fp32) and its bf16-math convs' operand (bf16)."""
+    c = y.shape[-1]
+    rows = y.numel() // c
+    z = torch.empty_like(y)
+    z16 = torch.empty_like(y, dtype=torch.bfloat16)
+    call("tmr_bn_apply_dual", y, scale, shift, residual, z, z16, rows, c, int(relu), stream_ptr())
+    return z, z16
+
+
+def bn_apply2(y, scale, shift, yr, rscale, rshift, relu=True, out=None, dual=False):
+    """act(y*scale + shift + (yr*rscale + rshift)): BN3 + the downsample branch's BN + ReLU.
+    dual=True -> (z, z16) with a bf16 copy (bn_apply_dual)."""
     c = y.shape[-1]
     rows = y.numel() // c
     if yr.shape != y.shape:
         raise RuntimeError("bn_apply2: branch shape %s != %s" % (tuple(yr.shape), tuple(y.shape)))
     if out is None:
         out = torch.empty_like(y)
-    call("tmr_bn_apply2", y, scale, shift, yr, rscale, rshift, out, rows, c, int(relu),
+    z16 = torch.empty_like(y, dtype=torch.bfloat16) if dual else None
+    call("tmr_bn_apply2_x", y, scale, shift, yr, rscale, rshift, out, z16, rows, c, int(relu),
          stream_ptr())
-    return out
+    return (out, z16) if dual else out
 
 
 def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None, scale=None,
@@ -515,14 +551,16 @@ def maxpool_fwd(x):
     return y, am
 
 
-def maxpool_fwd_bn(x, scale, shift):
-    """MaxPool2d(3,2,1)(relu(x*scale + shift)) with the BN+ReLU applied on load."""
+def maxpool_fwd_bn(x, scale, shift, bf16=False):
+    """MaxPool2d(3,2,1)(relu(x*scale + shift)) with the BN+ReLU applied on load; bf16=True stores
+    the output rounded (it is only a bf16-math conv operand)."""
     n, h, w, c = x.shape
     ho = (h + 2 - 3) // 2 + 1
     wo = (w + 2 - 3) // 2 + 1
-    y = _empty((n, ho, wo, c), x)
+    y = _empty((n, ho, wo, c), x, dtype=torch.bfloat16 if bf16 else f32)
     am = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
-    call("tmr_maxpool2d_fwd_bn", x, scale, shift, y, am, n, h, w, c, ho, wo, stream_ptr())
+    call("tmr_maxpool2d_fwd_bn_x", x, scale, shift, y, am, n, h, w, c, ho, wo, int(bf16),
+         stream_ptr())
     return y, am
 
 

@@ -99,15 +99,30 @@ def _store16(math):
     return math == "bf16" and BF16_STORE
 
 
+# bf16 math with EVERY conv operand bf16 in HBM (train mode; TMR_BF16_FULL=0 turns it off): the
+# block outputs are written fp32 (identity residual, ReLU mask) and as a bf16 copy in the same pass
+# (bn_apply_dual / bn_apply2 dual), the stem maxpool output as bf16 only (layer1.0 has a
+# downsample, so it is never a residual), and each conv's dgrad reads a transposed bf16 weight copy
+# (weight_to_crsk).  Every conv but the 4-channel stem then runs on the LDS-DMA engine
+# (gemm16_kernel.h).  Bit-identical to the register-staged bf16 path (same rounding of the same
+# operands), tests/test_bf16_gpu.py.
+FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
+
+
+def _full16(math):
+    return _store16(math) and FULL16 and not FOLD_BN
+
+
 def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
-             defer=False, branch=None, nbt=None):
+             defer=False, branch=None, nbt=None, dual=False):
     """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z.
 
     Train mode only: ``defer`` returns (y, scale, shift) instead of applying the BN -- the
     consumer applies it on load (the downsample branch inside its block's BN3 pass, the stem
     inside the maxpool, with FOLD_BN the next conv's loaders); ``branch`` = such a deferred
     (y, scale, shift) used as the residual; ``x`` may itself be a deferred (y, scale, shift) of a
-    ReLU unit, read through the conv's X-operand prologue."""
+    ReLU unit, read through the conv's X-operand prologue.  ``dual`` (block outputs under
+    _full16): returns (z fp32, z bf16 copy)."""
     xpro = None
     if isinstance(x, tuple):
         x, xpro = x[0], (x[1], x[2])
@@ -143,7 +158,9 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     if defer:
         z = None
     elif branch is not None:
-        z = ops.bn_apply2(y, scale, shift, branch[0], branch[1], branch[2], relu)
+        z = ops.bn_apply2(y, scale, shift, branch[0], branch[1], branch[2], relu, dual=dual)
+    elif dual:
+        z = ops.bn_apply_dual(y, scale, shift, residual, relu)
     else:
         # a non-residual unit's output is only ever a conv operand (next conv's forward and
         # wgrad; the backward recomputes its ReLU mask from y): bf16 under bf16 math
@@ -151,7 +168,11 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     if recs is not None:
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
         has_res = residual is not None or branch is not None
-        recs.append({"x": x, "xpro": xpro, "wk": wk, "y": y, "z": z if has_res else None,
+        # the dgrad view of a bf16-operand conv reads the transposed weights (LDS-DMA engine)
+        wt = (ops.weight_to_crsk(w.detach().contiguous())
+              if _full16(math) and x.dtype == torch.bfloat16 else None)
+        recs.append({"x": x, "xpro": xpro, "wk": wk, "wt": wt, "y": y,
+                     "z": (z[0] if dual else z) if has_res else None,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
                      "c_real": c, "math": math})
@@ -210,17 +231,20 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     dx, fused = None, None
     if need_dx:
         hw = (x.shape[1], x.shape[2])
+        wt = rec.get("wt") is not None
+        wdg = rec["wt"] if wt else rec["wk"]
         if fuse_prev is not None:
             p = fuse_prev
             mask = (1 if p["z"] is not None else 2) if p["relu"] else 0
-            dx, pp, npp = ops.conv_dgrad_bnbwd(dy, rec["wk"], hw, rec["stride"], rec["pad"],
+            dx, pp, npp = ops.conv_dgrad_bnbwd(dy, wdg, hw, rec["stride"], rec["pad"],
                                                p["y"], p["mean"], mask, z=p["z"],
                                                scale=p["scale"], shift=p["shift"], out=dx_out,
-                                               beta=dx_beta, math=rec["math"], dpro=dpro)
+                                               beta=dx_beta, math=rec["math"], dpro=dpro,
+                                               wt=wt)
             fused = (pp, npp)
         else:
-            dx = ops.conv_dgrad(dy, rec["wk"], hw, rec["stride"], rec["pad"], out=dx_out,
-                                beta=dx_beta, math=rec["math"], dpro=dpro)
+            dx = ops.conv_dgrad(dy, wdg, hw, rec["stride"], rec["pad"], out=dx_out,
+                                beta=dx_beta, math=rec["math"], dpro=dpro, wt=wt)
     return dx, dres, fused
 
 
@@ -235,39 +259,45 @@ class TrunkFn(torch.autograd.Function):
         nbt = []   # BatchNorm num_batches_tracked counters, incremented together at the end
         conv1, bn1, layers = share.trunk_parts()
         mt = share.precision
+        f16 = training and _full16(mt)
         if training:
             # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
             # mask from y, so the stem's BN output is never needed)
             y0, sc0, sh0 = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
                                     defer=True, nbt=nbt)
-            p, am = ops.maxpool_fwd_bn(y0, sc0, sh0)
+            p, am = ops.maxpool_fwd_bn(y0, sc0, sh0, bf16=f16)
             stem_hw = (y0.shape[1], y0.shape[2])
         else:
             z = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt, nbt=nbt)
             p, am = ops.maxpool_fwd(z)
             stem_hw = (z.shape[1], z.shape[2])
-        h = p
+        # h: the block input as the identity residual (fp32), hx: as the conv operand (the bf16
+        # copy under f16; the maxpool output is only ever a conv operand)
+        h, hx = (None, p) if f16 else (p, p)
         blocks = []
         for layer in layers:
             for blk in layer:
                 brec = [] if keep else None
                 fold = training and FOLD_BN
-                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt,
+                z1 = _conv_bn(hx, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt,
                               nbt=nbt, defer=fold)
                 z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec,
                               math=mt, nbt=nbt, defer=fold)
                 if blk.downsample is not None:
                     # train: the branch's BN is applied inside the BN3 pass (bn_apply2)
-                    idn = _conv_bn(h, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
+                    idn = _conv_bn(hx, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
                                    training, recs=brec, math=mt, defer=training, nbt=nbt)
                 else:
+                    if h is None:
+                        raise RuntimeError("identity residual of the stem output (no downsample)")
                     idn = h
                 if isinstance(idn, tuple):
                     h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, branch=idn,
-                                 recs=brec, math=mt, nbt=nbt)
+                                 recs=brec, math=mt, nbt=nbt, dual=f16)
                 else:
                     h = _conv_bn(z2, blk.conv3, blk.bn3, 1, 0, True, training, residual=idn,
-                                 recs=brec, math=mt, nbt=nbt)
+                                 recs=brec, math=mt, nbt=nbt, dual=f16)
+                h, hx = h if f16 else (h, h)
                 blocks.append((blk, brec))
         feat = ops.avgpool_fwd(h)
         if nbt:
