@@ -67,6 +67,9 @@ typedef struct tmr_conv_desc {
 #define TMR_IO_X_BF16 1
 #define TMR_IO_W_BF16 2
 #define TMR_IO_DY_BF16 4
+#define TMR_IO_Y_BF16 16   /* forward: y written as bf16 (RNE); the BatchNorm partials of
+                              tmr_conv2d_fwd_bnstats describe the rounded values (no beta/bias) */
+#define TMR_IO_BN_BF16 32  /* tmr_conv2d_dgrad_bnbwd: the y / z of the fused BN backward are bf16 */
 #define TMR_IO_WT_BF16 8   /* dgrad only: w is the transposed bf16 weight copy Wt[Cin][R][S][Cout]
                               (tmr_weight_oihw_to_crsk_x), read K-contiguous by the LDS-DMA engine */
 
@@ -301,6 +304,35 @@ int tmr_bn_apply2_x(const float* y, const float* scale, const float* shift, cons
 int tmr_maxpool2d_fwd_bn_x(const float* x, const float* scale, const float* shift, void* y,
                            uint8_t* argmax, int n, int h, int w, int c, int ho, int wo, int out_bf16,
                            hipStream_t stream);
+
+/* bf16-activation contract of the bf16 train step (TMR_MATH_BF16; tests/test_bf16_gpu.py,
+ * oracle.emulate_bf16_convs(activations=True)): every conv output y is stored rounded to bf16
+ * (TMR_IO_Y_BF16; BN statistics of the rounded values), every BatchNorm(+residual)(+ReLU) output
+ * z is computed in fp32 from the bf16 y / residual and stored rounded to bf16; gradients dz / dres
+ * stay fp32, dy (a conv operand) bf16.  "_a16" = y, z, residual (and the stem / avgpool inputs)
+ * are bf16 tensors; otherwise the arithmetic of the fp32 forms. */
+int tmr_bn_apply_a16(const void* y, const float* scale, const float* shift, const void* residual,
+                     void* z, int rows, int c, int relu, hipStream_t stream);
+int tmr_bn_apply2_a16(const void* y, const float* scale, const float* shift, const void* yr,
+                      const float* rscale, const float* rshift, void* z, int rows, int c, int relu,
+                      hipStream_t stream);
+int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const float* scale,
+                   const float* shift, const float* save_mean, const float* save_invstd,
+                   const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta, int rows,
+                   int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream);
+int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* parts, int nparts,
+                         const float* save_mean, const float* save_invstd, const float* gamma,
+                         void* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
+                         size_t ws_bytes, hipStream_t stream);
+int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho,
+                           int wo, const void* y, const float* scale, const float* shift,
+                           const float* save_mean, const float* save_invstd, const float* gamma,
+                           void* dy, float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                           hipStream_t stream);
+int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const float* shift, void* y,
+                             uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
+                             hipStream_t stream);
+int tmr_avgpool_fwd_a16(const void* x, float* y, int n, int hw, int c, hipStream_t stream);
 
 /* ---------------- pooling (pool_layout.hip) --------------------------------------- */
 /* MaxPool2d(3,2,1) of share.maxpool (train_only_non-local_pretrained.py:207), NHWC */

@@ -42,6 +42,10 @@ reference checkout, ``code/``):
                          build's TMR_MATH_BF16 contract on torch ops -- every trunk conv with
                          operands rounded to bf16 (RNE), exact products, accumulation in the
                          tensor dtype; fwd rounds (x, w), dgrad (dy, w), wgrad (x, dy).
+                         With activations=True (the ResNet-50 train step's bf16-activation
+                         contract, tmrnet_amd/trunk.py ACT16) every conv output and every
+                         Bottleneck output is also stored rounded to bf16 in train mode
+                         (straight-through: the rounding is storage, gradients pass unchanged).
 """
 import math
 
@@ -137,7 +141,10 @@ class Bottleneck(nn.Module):
         out = self.bn3(self.conv3(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        out = self.relu(out + identity)
+        if getattr(self, "round_out", False) and self.training:   # emulate_bf16_convs(activations)
+            out = _RoundFn.apply(out)
+        return out
 
 
 def make_layer(inplanes, planes, blocks, stride):
@@ -283,6 +290,18 @@ def bf16_round(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+class _RoundFn(torch.autograd.Function):
+    """Storage rounding to bf16 (RNE) with a straight-through gradient."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return bf16_round(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 class _Bf16ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, padding, groups):
@@ -308,30 +327,40 @@ class Bf16Conv2d(nn.Conv2d):
 
     def forward(self, x):
         assert self.bias is None
-        return _Bf16ConvFn.apply(x, self.weight, self.stride, self.padding, self.groups)
+        y = _Bf16ConvFn.apply(x, self.weight, self.stride, self.padding, self.groups)
+        if getattr(self, "round_out", False) and self.training:   # bf16-stored conv output
+            y = _RoundFn.apply(y)
+        return y
 
 
-def emulate_bf16_convs(module, skip=("fc1", "fc2")):
+def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False):
     """Switch every trunk Conv2d of `module` to bf16-operand math (class swap, so deepcopy
-    and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay."""
+    and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay.
+    activations=True: in train mode the conv outputs and the Bottleneck outputs are rounded to
+    bf16 as well (the bf16-activation contract of the ResNet-50 train step)."""
     for name, m in module.named_modules():
         if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
             m.__class__ = Bf16Conv2d
+            m.round_out = activations
+        elif isinstance(m, Bottleneck):
+            m.round_out = activations
     return module
 
 
 class TMRNetRef(nn.Module):
     """Inline `resnet_lstm` (train_only_non-local_pretrained.py:201-240); with
     time_conv=True the mutiConv variant (train_non-local_mutiConv_resnet.py:208-253).
-    precision='bf16': trunk convs with bf16 operands (emulate_bf16_convs)."""
+    precision='bf16': trunk convs with bf16 operands (emulate_bf16_convs); bf16_act (default: the
+    ResNet-50 backbone) adds the bf16 storage of conv and Bottleneck outputs in train mode."""
 
     def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50",
-                 precision="fp32"):
+                 precision="fp32", bf16_act=None):
         super().__init__()
         self.seq_len = seq_len
         self.share = resnet50_share() if backbone == "resnet50" else resnest50_share()
         if precision == "bf16":
-            emulate_bf16_convs(self.share)
+            emulate_bf16_convs(self.share, activations=(backbone == "resnet50"
+                                                         if bf16_act is None else bf16_act))
         self.lstm = nn.LSTM(2048, 512, batch_first=True)
         self.fc_c = nn.Linear(512, num_classes)
         self.fc_h_c = nn.Linear(1024, 512)

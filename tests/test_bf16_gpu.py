@@ -334,7 +334,8 @@ def test_bf16_full16_step(dev):
     B, T, L = 2, 5, 7
     frames, off, lt, labels = _inputs(B, T, L, seed=53)
     res = {}
-    saved = trunk.FULL16
+    saved = trunk.FULL16, trunk.ACT16
+    trunk.ACT16 = False   # the engine A/B; the bf16-activation contract: the fp64 tests above
     try:
         for full in (True, False):
             trunk.FULL16 = full
@@ -348,7 +349,7 @@ def test_bf16_full16_step(dev):
             torch.cuda.synchronize()
             res[full] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()})
     finally:
-        trunk.FULL16 = saved
+        trunk.FULL16, trunk.ACT16 = saved
     assert (res[True][0] - res[False][0]).abs().max().item() < 1e-4
     assert torch.equal(res[True][0].argmax(1), res[False][0].argmax(1))
     num = sum(((res[True][1][k] - res[False][1][k]).double() ** 2).sum() for k in res[True][1])

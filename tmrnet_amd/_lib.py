@@ -71,6 +71,13 @@ SIGNATURES = {
     "tmr_bn_apply_dual": [P, P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2_x": [P, P, P, P, P, P, P, P, I, I, I, P],
     "tmr_maxpool2d_fwd_bn_x": [P, P, P, P, P, I, I, I, I, I, I, I, P],
+    "tmr_bn_apply_a16": [P, P, P, P, P, I, I, I, P],
+    "tmr_bn_apply2_a16": [P, P, P, P, P, P, P, I, I, I, P],
+    "tmr_bn_bwd_a16": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
+    "tmr_bn_bwd_parts_a16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_bwd_maxpool_a16": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
+    "tmr_maxpool2d_fwd_bn_a16": [P, P, P, P, P, I, I, I, I, I, I, P],
+    "tmr_avgpool_fwd_a16": [P, P, I, I, I, P],
     "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
     "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],

@@ -159,14 +159,29 @@ __device__ __forceinline__ void st4(__bf16* p, long i4, float4 v) {
 
 // DUAL: z (fp32) and a bf16 (RNE) copy z16 -- a block output is both the next block's identity
 // residual (fp32) and the operand of its bf16-math convs (bf16, read by the LDS-DMA engine)
-template <bool RES, bool RELU, typename TZ = float, bool DUAL = false>
-__global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, const float* __restrict__ scale,
+// 4 consecutive elements of an fp32 or bf16 tensor as float4 (bf16 -> fp32 is exact)
+__device__ __forceinline__ float4 ld4(const float* p, long i4) {
+  return reinterpret_cast<const float4*>(p)[i4];
+}
+__device__ __forceinline__ float4 ld4(const __bf16* p, long i4) {
+  const uint2 u = reinterpret_cast<const uint2*>(p)[i4];
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ float ld1(const float* p, long i) { return p[i]; }
+__device__ __forceinline__ float ld1(const __bf16* p, long i) {
+  return __uint_as_float((uint32_t)reinterpret_cast<const unsigned short*>(p)[i] << 16);
+}
+
+// TY: element type of y and the residual (bf16 under the bf16-activation contract)
+template <bool RES, bool RELU, typename TZ = float, bool DUAL = false, typename TY = float>
+__global__ __launch_bounds__(NT) void bn_apply_k(const TY* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift,
-                                                 const float* __restrict__ res, TZ* __restrict__ z,
+                                                 const TY* __restrict__ res, TZ* __restrict__ z,
                                                  long n4, int c4, __bf16* __restrict__ z16 = nullptr) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cc = (int)(i % c4) * 4;
-    float4 v = reinterpret_cast<const float4*>(y)[i];
+    float4 v = ld4(y, i);
     const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
     const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
     v.x = fmaf(v.x, sc.x, sf.x);
@@ -174,7 +189,7 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, co
     v.z = fmaf(v.z, sc.z, sf.z);
     v.w = fmaf(v.w, sc.w, sf.w);
     if (RES) {
-      const float4 r = reinterpret_cast<const float4*>(res)[i];
+      const float4 r = ld4(res, i);
       v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
     if (RELU) {
@@ -188,18 +203,18 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const float* __restrict__ y, co
 // z = act(y*scale + shift + (yr*rscale + rshift)): the Bottleneck's BN3 + residual + ReLU with the
 // downsample branch's BatchNorm applied on the fly (its output is never materialised).  Same
 // fmaf/add/max sequence as bn_apply of the branch followed by bn_apply with that residual.
-template <bool RELU, bool DUAL = false>
-__global__ __launch_bounds__(NT) void bn_apply2_k(const float* __restrict__ y, const float* __restrict__ scale,
+template <bool RELU, bool DUAL = false, typename TY = float, typename TZ = float>
+__global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, const float* __restrict__ scale,
                                                   const float* __restrict__ shift,
-                                                  const float* __restrict__ yr,
+                                                  const TY* __restrict__ yr,
                                                   const float* __restrict__ rscale,
                                                   const float* __restrict__ rshift,
-                                                  float* __restrict__ z, long n4, int c4,
+                                                  TZ* __restrict__ z, long n4, int c4,
                                                   __bf16* __restrict__ z16) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cc = (int)(i % c4) * 4;
-    float4 v = reinterpret_cast<const float4*>(y)[i];
-    const float4 r = reinterpret_cast<const float4*>(yr)[i];
+    float4 v = ld4(y, i);
+    const float4 r = ld4(yr, i);
     const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
     const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
     const float4 rs = *reinterpret_cast<const float4*>(rscale + cc);
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const float* __restrict__ y, c
     if (RELU) {
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
     }
-    reinterpret_cast<float4*>(z)[i] = v;
+    st4(z, i, v);
     if (DUAL) st4(z16, i, v);
   }
 }
@@ -231,9 +246,9 @@ __device__ __forceinline__ float4 affine4(float4 v, float4 sc, float4 sf) {
 
 // WB: write the masked gradient back over dz (dres aliasing dz: the identity branch of a
 // residual block takes the masked gradient in place, and the apply pass needs no mask)
-template <int MASK, bool WB = false>
-__global__ __launch_bounds__(NT) void bn_bwd_partial(float* dz, const float* __restrict__ y,
-                                                     const float* __restrict__ z,
+template <int MASK, bool WB = false, typename TY = float>
+__global__ __launch_bounds__(NT) void bn_bwd_partial(float* dz, const TY* __restrict__ y,
+                                                     const TY* __restrict__ z,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift,
                                                      const float* __restrict__ mean, int rows, int c,
@@ -253,8 +268,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(float* dz, const float* __r
   for (int r = r0 + tr; r < r1; r += rthreads) {
     const long o = (long)r * c + ch;
     float4 g = *reinterpret_cast<const float4*>(dz + o);
-    const float4 v = *reinterpret_cast<const float4*>(y + o);
-    if (MASK == 1) g = relu_mask4(g, *reinterpret_cast<const float4*>(z + o));
+    const float4 v = ld4(y, o >> 2);
+    if (MASK == 1) g = relu_mask4(g, ld4(z, o >> 2));
     if (MASK == 2) g = relu_mask4(g, affine4(v, sc, sf));
     if (WB) *reinterpret_cast<float4*>(dz + o) = g;
     s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
@@ -320,9 +335,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
   }
 }
 
-template <int MASK, bool DRES, typename TD = float>
-__global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const float* __restrict__ y,
-                                                   const float* __restrict__ z,
+template <int MASK, bool DRES, typename TD = float, typename TY = float>
+__global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const TY* __restrict__ y,
+                                                   const TY* __restrict__ z,
                                                    const float* __restrict__ scale,
                                                    const float* __restrict__ shift,
                                                    const float* __restrict__ coef, TD* __restrict__ dy,
@@ -331,8 +346,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cc = (int)(i % c4) * 4;
     float4 g = reinterpret_cast<const float4*>(dz)[i];
-    const float4 v = reinterpret_cast<const float4*>(y)[i];
-    if (MASK == 1) g = relu_mask4(g, reinterpret_cast<const float4*>(z)[i]);
+    const float4 v = ld4(y, i);
+    if (MASK == 1) g = relu_mask4(g, ld4(z, i));
     if (MASK == 2)
       g = relu_mask4(g, affine4(v, *reinterpret_cast<const float4*>(scale + cc),
                                 *reinterpret_cast<const float4*>(shift + cc)));
@@ -529,8 +544,9 @@ __device__ __forceinline__ float4 stem_dz(const PoolGeo& pg, uint32_t r, int cq,
 // input pixel per channel (its argmax), so sum g and sum g*(y - mean) over the input pixels equal
 // the sums over pooled outputs of dyp * mask(y[argmax]) and that times (y[argmax] - mean): one
 // read of the pooled gradient and argmax plus one y element per channel, no gather of windows.
+template <typename TY = float>
 __global__ __launch_bounds__(NT) void stem_bwd_partial_pooled(
-    const PoolGeo pg, int h, int w, const float* __restrict__ y, const float* __restrict__ scale,
+    const PoolGeo pg, int h, int w, const TY* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, int prows, int c, int rpb,
     int cthreads, FastDiv dPHW, FastDiv dPW, double* __restrict__ part) {
   const int tc = threadIdx.x % cthreads, tr = threadIdx.x / cthreads;
@@ -556,7 +572,7 @@ __global__ __launch_bounds__(NT) void stem_bwd_partial_pooled(
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int iy = (int)oy * 2 - 1 + ids[e] / 3, ix = (int)ox * 2 - 1 + ids[e] % 3;
-      const float v = y[(((long)nn * h + iy) * w + ix) * c + ch + e];
+      const float v = ld1(y, (((long)nn * h + iy) * w + ix) * c + ch + e);
       const float g = fmaf(v, sc[e], sf[e]) > 0.f ? ds[e] : 0.f;
       s[e] += g;
       q[e] = fmaf(g, v - mu[e], q[e]);
@@ -581,8 +597,8 @@ __global__ __launch_bounds__(NT) void stem_bwd_partial_pooled(
   }
 }
 
-template <typename TD>
-__global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const float* __restrict__ y,
+template <typename TD, typename TY = float>
+__global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const TY* __restrict__ y,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift,
                                                      const float* __restrict__ coef,
@@ -591,7 +607,7 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const flo
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const int cq = (int)(i % c4);
     const int cc = cq * 4;
-    const float4 v = reinterpret_cast<const float4*>(y)[i];
+    const float4 v = ld4(y, i);
     const float4 g = relu_mask4(stem_dz(pg, (uint32_t)(i / c4), cq, c4),
                                 affine4(v, *reinterpret_cast<const float4*>(scale + cc),
                                         *reinterpret_cast<const float4*>(shift + cc)));
@@ -866,7 +882,7 @@ TMR_API int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n,
   Plan p = make_plan(prows, c);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
-  hipLaunchKernelGGL(stem_bwd_partial_pooled, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg, h, w,
+  hipLaunchKernelGGL(stem_bwd_partial_pooled<float>, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg, h, w,
                      y, scale, shift, save_mean, prows, c, p.rpb, p.cthreads,
                      make_fastdiv((uint32_t)(ho * wo)), make_fastdiv((uint32_t)wo), part);
   TMR_CHECK_LAUNCH("stem_bwd_partial_pooled");
@@ -913,10 +929,10 @@ TMR_API int tmr_bn_bwd_parts_x(const float* g, const float* y, const void* parts
   TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
   const long n4 = (long)rows * c / 4;
   if (out_bf16)
-    hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g,
+    hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g,
                        y, nullptr, nullptr, nullptr, coef, (__bf16*)dyv, nullptr, n4, c / 4);
   else
-    hipLaunchKernelGGL((bn_bwd_apply<0, false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
+    hipLaunchKernelGGL((bn_bwd_apply<0, false, float, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
                        nullptr, nullptr, nullptr, coef, (float*)dyv, nullptr, n4, c / 4);
   TMR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
@@ -974,5 +990,161 @@ TMR_API int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, con
   hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");
+  return 0;
+}
+
+// ---- bf16-activation forms (TMR_MATH_BF16 train step, include/tmr.h "_a16"): y, z and the
+// residual are bf16 tensors (the conv outputs rounded by their epilogue, the BN outputs rounded
+// here), the gradients dz / dres stay fp32, dy (a conv operand) is written bf16.  Same arithmetic
+// as the fp32 forms on the bf16 values.
+
+TMR_API int tmr_bn_apply_a16(const void* y, const float* scale, const float* shift,
+                             const void* residual, void* z, int rows, int c, int relu,
+                             hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && z, "tmr_bn_apply_a16: bad arguments (c %d)", c);
+  const long n4 = (long)rows * c / 4;
+  const int nb = ew_blocks(n4), c4 = c / 4;
+  const __bf16 *yb = (const __bf16*)y, *rb = (const __bf16*)residual;
+  __bf16* zb = (__bf16*)z;
+  if (rb) {
+    if (relu) hipLaunchKernelGGL((bn_apply_k<true, true, __bf16, false, __bf16>), dim3(nb), dim3(NT), 0, stream, yb, scale, shift, rb, zb, n4, c4, nullptr);
+    else hipLaunchKernelGGL((bn_apply_k<true, false, __bf16, false, __bf16>), dim3(nb), dim3(NT), 0, stream, yb, scale, shift, rb, zb, n4, c4, nullptr);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_apply_k<false, true, __bf16, false, __bf16>), dim3(nb), dim3(NT), 0, stream, yb, scale, shift, rb, zb, n4, c4, nullptr);
+    else hipLaunchKernelGGL((bn_apply_k<false, false, __bf16, false, __bf16>), dim3(nb), dim3(NT), 0, stream, yb, scale, shift, rb, zb, n4, c4, nullptr);
+  }
+  TMR_CHECK_LAUNCH("bn_apply_a16");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply2_a16(const void* y, const float* scale, const float* shift, const void* yr,
+                              const float* rscale, const float* rshift, void* z, int rows, int c,
+                              int relu, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_bn_apply2_a16: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(y && scale && shift && yr && rscale && rshift && z, "tmr_bn_apply2_a16: null operand");
+  TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_a16: the branch input must not alias z");
+  const long n4 = (long)rows * c / 4;
+  const __bf16 *yb = (const __bf16*)y, *rb = (const __bf16*)yr;
+  if (relu)
+    hipLaunchKernelGGL((bn_apply2_k<true, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
+                       stream, yb, scale, shift, rb, rscale, rshift, (__bf16*)z, n4, c / 4, nullptr);
+  else
+    hipLaunchKernelGGL((bn_apply2_k<false, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
+                       stream, yb, scale, shift, rb, rscale, rshift, (__bf16*)z, n4, c / 4, nullptr);
+  TMR_CHECK_LAUNCH("bn_apply2_a16");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const float* scale,
+                           const float* shift, const float* save_mean, const float* save_invstd,
+                           const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta,
+                           int rows, int c, int relu, void* ws, size_t ws_bytes,
+                           hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4, "tmr_bn_bwd_a16: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(rows > 0, "tmr_bn_bwd_a16: empty input");
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd_a16: workspace too small");
+  TMR_CHECK_ARG(!relu || z || (scale && shift),
+                "tmr_bn_bwd_a16: relu backward needs the saved output z or the forward scale/shift");
+  int mask = relu ? (z ? 1 : 2) : 0;
+  Plan p = make_plan(rows, c);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
+  const dim3 pg(p.nrb, p.cblocks);
+  float* dzw = const_cast<float*>(dz);
+  const __bf16 *yb = (const __bf16*)y, *zb = (const __bf16*)z;
+  if (dres == dz) {
+    if (mask == 1)
+      hipLaunchKernelGGL((bn_bwd_partial<1, true, __bf16>), pg, dim3(NT), 0, stream, dzw, yb, zb, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+    else if (mask == 2)
+      hipLaunchKernelGGL((bn_bwd_partial<2, true, __bf16>), pg, dim3(NT), 0, stream, dzw, yb, zb, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+    else
+      hipLaunchKernelGGL((bn_bwd_partial<0, false, __bf16>), pg, dim3(NT), 0, stream, dzw, yb, zb, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+    mask = 0;
+    dres = nullptr;
+  } else if (mask == 1)
+    hipLaunchKernelGGL((bn_bwd_partial<1, false, __bf16>), pg, dim3(NT), 0, stream, dzw, yb, zb, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  else if (mask == 2)
+    hipLaunchKernelGGL((bn_bwd_partial<2, false, __bf16>), pg, dim3(NT), 0, stream, dzw, yb, zb, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial<0, false, __bf16>), pg, dim3(NT), 0, stream, dzw, yb, zb, scale, shift, save_mean, rows, c, p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_bwd_partial");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  const long n4 = (long)rows * c / 4;
+  const int nb = ew_blocks(n4), c4 = c / 4;
+  __bf16* db = (__bf16*)dy;
+#define TMR_BN_APPLY16(M, D)                                                                    \
+  hipLaunchKernelGGL((bn_bwd_apply<M, D, __bf16, __bf16>), dim3(nb), dim3(NT), 0, stream, dz, yb, \
+                     zb, scale, shift, coef, db, dres, n4, c4)
+  if (dres) {
+    if (mask == 1) { TMR_BN_APPLY16(1, true); } else if (mask == 2) { TMR_BN_APPLY16(2, true); } else { TMR_BN_APPLY16(0, true); }
+  } else {
+    if (mask == 1) { TMR_BN_APPLY16(1, false); } else if (mask == 2) { TMR_BN_APPLY16(2, false); } else { TMR_BN_APPLY16(0, false); }
+  }
+#undef TMR_BN_APPLY16
+  TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* parts, int nparts,
+                                 const float* save_mean, const float* save_invstd,
+                                 const float* gamma, void* dy, float* dgamma, float* dbeta,
+                                 int rows, int c, void* ws, size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows > 0 && nparts > 0,
+                "tmr_bn_bwd_parts_a16: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_bn_parts_ws_bytes(nparts, c),
+                "tmr_bn_bwd_parts_a16: workspace too small (need tmr_bn_parts_ws_bytes)");
+  const SlabPlan sp = slab_plan(nparts, c);
+  double* slabs = (double*)ws;
+  float* coef = (float*)((char*)ws + slab_ws_bytes(nparts, c));
+  hipLaunchKernelGGL(parts_slab_k<1>, dim3(sp.groups, sp.nslabs), dim3(256), 0, stream, parts,
+                     nparts, c, sp.rows, slabs);
+  TMR_CHECK_LAUNCH("bn_parts_slab");
+  hipLaunchKernelGGL(bwd_final_slabs_k, dim3(sp.groups), dim3(SLAB_CH * SLAB_PH), 0, stream,
+                     (const double*)slabs, sp.nslabs, rows, c, save_mean, save_invstd, gamma,
+                     dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
+  const long n4 = (long)rows * c / 4;
+  hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
+                     stream, g, (const __bf16*)y, nullptr, nullptr, nullptr, coef, (__bf16*)dy,
+                     nullptr, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int n, int h, int w,
+                                   int ho, int wo, const void* y, const float* scale,
+                                   const float* shift, const float* save_mean,
+                                   const float* save_invstd, const float* gamma, void* dy,
+                                   float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                                   hipStream_t stream) {
+  const long rows_l = (long)n * h * w;
+  TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows_l > 0 && rows_l < 0x7fffffffL,
+                "tmr_bn_bwd_maxpool_a16: bad shape n=%d h=%d w=%d c=%d", n, h, w, c);
+  TMR_CHECK_ARG(ho == (h + 2 - 3) / 2 + 1 && wo == (w + 2 - 3) / 2 + 1,
+                "tmr_bn_bwd_maxpool_a16: pooled %dx%d is not MaxPool2d(3,2,1) of %dx%d", ho, wo, h, w);
+  const int rows = (int)rows_l;
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd_maxpool_a16: workspace too small");
+  PoolGeo pg;
+  pg.dyp = dyp; pg.am = (const uchar4*)argmax;
+  pg.dHW = make_fastdiv((uint32_t)(h * w)); pg.dW = make_fastdiv((uint32_t)w);
+  pg.ho = ho; pg.wo = wo;
+  const int prows = n * ho * wo;
+  Plan p = make_plan(prows, c);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
+  const __bf16* yb = (const __bf16*)y;
+  hipLaunchKernelGGL(stem_bwd_partial_pooled<__bf16>, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg,
+                     h, w, yb, scale, shift, save_mean, prows, c, p.rpb, p.cthreads,
+                     make_fastdiv((uint32_t)(ho * wo)), make_fastdiv((uint32_t)wo), part);
+  TMR_CHECK_LAUNCH("stem_bwd_partial_pooled");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  const long n4 = rows_l * c / 4;
+  hipLaunchKernelGGL((stem_bwd_apply<__bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg,
+                     yb, scale, shift, coef, (__bf16*)dy, n4, c / 4);
+  TMR_CHECK_LAUNCH("stem_bwd_apply");
   return 0;
 }

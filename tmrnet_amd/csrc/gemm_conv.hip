@@ -84,6 +84,8 @@ static inline long span(long pixels, int ld, int width) { return pixels > 0 ? (p
 static inline int esz_x(const tmr_conv_desc* d) { return (d->io & TMR_IO_X_BF16) ? 2 : 4; }
 static inline int esz_w(const tmr_conv_desc* d) { return (d->io & (TMR_IO_W_BF16 | TMR_IO_WT_BF16)) ? 2 : 4; }
 static inline int esz_dy(const tmr_conv_desc* d) { return (d->io & TMR_IO_DY_BF16) ? 2 : 4; }
+static inline int esz_y(const tmr_conv_desc* d) { return (d->io & TMR_IO_Y_BF16) ? 2 : 4; }
+static inline int esz_bn(const tmr_conv_desc* d) { return (d->io & TMR_IO_BN_BF16) ? 2 : 4; }
 template <typename T>
 static inline T* adv(T* p, long elems, int esz) {   // p + elems elements of esz bytes
   return p ? (T*)((typename std::conditional<std::is_const<T>::value, const char*, char*>::type)p +
@@ -174,6 +176,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.Bbytes = clamp_bytes_e((long)d->k * a.K, esz_w(d));
   a.sab = ((d->io & TMR_IO_X_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldc, d->k));
+  a.c16 = (d->io & TMR_IO_Y_BF16) ? 1 : 0;
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
 }
@@ -215,7 +218,11 @@ TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* 
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     GemmArgs a;
     bool al;
-    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, bias, y + f0 * y_frame(d), beta, a, al);
+    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, bias, adv(y, f0 * y_frame(d), esz_y(d)), beta, a, al);
+    if (!rc && a.c16 && (beta != 0.f || bias)) {
+      tmr_set_error("tmr_conv2d_fwd: a bf16 output (TMR_IO_Y_BF16) takes no beta / bias");
+      rc = 1;
+    }
     if (!rc) rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
     if (rc) return rc;
   }
@@ -235,6 +242,7 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
     bool al;
     int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, shift, y + f0 * y_frame(d), 0.f, a, al);
     if (rc) return rc;
+    TMR_CHECK_ARG(!a.c16, "tmr_conv2d_fwd_fused: the inference epilogue writes fp32 (no TMR_IO_Y_BF16)");
     a.scale = scale;
     a.res = residual ? residual + f0 * y_frame(d) : nullptr;
     a.relu = relu;
@@ -278,7 +286,7 @@ TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     GemmArgs a;
     bool al;
-    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, nullptr, y + f0 * y_frame(d), 0.f, a, al);
+    int rc = conv_fwd_args(&c, adv(x, f0 * x_frame(d), esz_x(d)), w_krsc, nullptr, adv(y, f0 * y_frame(d), esz_y(d)), 0.f, a, al);
     if (!rc) rc = set_prologue(a, pro, d, true, false, 0);
     if (rc) return rc;
     a.stats = st;
@@ -351,6 +359,7 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
         if (fz->count_only) { fz->nparts += nmt; continue; }
         a.bn_y = fz->y; a.bn_z = fz->z; a.bn_sc = fz->sc; a.bn_sh = fz->sh; a.bn_mean = fz->mean;
         a.bn_mask = fz->mask;
+        a.bn16 = (d->io & TMR_IO_BN_BF16) ? 1 : 0;
         a.bn_part = fz->part;
         fz->part += nmt * a.N;
         fz->nparts += nmt;
@@ -380,8 +389,8 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     BnBwdFuse fc_ = *fz;
-    fc_.y = fz->y ? fz->y + f0 * px_frame : nullptr;
-    fc_.z = fz->z ? fz->z + f0 * px_frame : nullptr;
+    fc_.y = adv(fz->y, f0 * px_frame, esz_bn(d));
+    fc_.z = adv(fz->z, f0 * px_frame, esz_bn(d));
     fc_.nparts = 0;
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);

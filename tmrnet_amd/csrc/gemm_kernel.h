@@ -109,7 +109,16 @@ struct GemmArgs {
   // DGRAD B operand is the transposed bf16 weight copy Wt[ci][r][s][co] (TMR_IO_WT_BF16; the
   // LDS-DMA engine of gemm16_kernel.h only), row stride ldbt = R*S*Cout elements
   int wt, ldbt;
+  // bf16 activations (TMR_MATH_BF16 train step): c16 -- the FWD output C is written as bf16 (RNE),
+  // and the BN statistics of the epilogue are those of the rounded values; bn16 -- the y / z read
+  // by the fused BN-backward epilogue of DGRAD are bf16
+  int c16, bn16;
 };
+
+__device__ __forceinline__ float bf16_rne(float v) { return (float)(__bf16)v; }
+__device__ __forceinline__ unsigned short bf16_bits(float v) {
+  return __builtin_bit_cast(unsigned short, (__bf16)v);
+}
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -210,9 +219,44 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
   };
   // rob OOB + a column offset stays >= 2^31 (no wrap): still out of range
   auto eoff = [&](uint32_t rob, int j) -> uint32_t { return cob[j] == OOB ? OOB : rob + cob[j]; };
+  const bool c16 = MODE == MODE_FWD && a.c16;
   auto st1 = [&](float v, uint32_t off) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rC, off, 0, 0);
   };
+  // bf16 tensors laid out like C are accessed a dword (two columns) per lane: lanes 2k, 2k+1 hold
+  // columns 2k, 2k+1 of accumulator rows r, r+1 (r even: adjacent output rows); the even lane
+  // moves the pair of row r, the odd lane that of row r+1, and the halves are swapped between the
+  // two lanes (DPP quad_perm [1,0,3,2]).  Needs an even N (conv channels: multiples of 8).
+  const bool odd = (l31 & 1) != 0;
+  auto poff = [&](uint32_t off_r, uint32_t off_r1) -> uint32_t {
+    const uint32_t o = odd ? off_r1 : off_r;
+    return o >= OOB ? OOB : (o >> 1) - (odd ? 2u : 0u);
+  };
+  auto swap1 = [](uint32_t w) -> uint32_t {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);
+  };
+  // the pair dword w loaded at poff -> (value of row r, value of row r+1) in this lane's column
+  auto unpair = [&](uint32_t w, float& vr, float& vr1) {
+    const uint32_t n = swap1(w);
+    vr = odd ? __uint_as_float(n & 0xffff0000u) : __uint_as_float(w << 16);
+    vr1 = odd ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(n << 16);
+  };
+  // store (row r: vr, row r+1: vr1) of this lane's column as bf16 pairs
+  auto st_pair = [&](float vr, float vr1, uint32_t off_r, uint32_t off_r1) {
+    const uint32_t mine = odd ? (uint32_t)bf16_bits(vr1) : (uint32_t)bf16_bits(vr);
+    const uint32_t other = odd ? (uint32_t)bf16_bits(vr) : (uint32_t)bf16_bits(vr1);
+    const uint32_t got = swap1(other);   // the neighbour's value of my pair's row
+    const uint32_t w = odd ? ((mine << 16) | got) : ((got << 16) | mine);
+    __builtin_amdgcn_raw_buffer_store_b32(w, rC, poff(off_r, off_r1), 0, 0);
+  };
+  if (c16) {   // the stored (rounded) values are the ones the BN statistics describe
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = bf16_rne(acc[i][j][r]);
+  }
   // Every chunk issues all of its loads (old C for beta, y / z of the fused BN backward, the
   // residual of the fused forward) before consuming any; each row offset is computed once, in
   // its chunk (kept out of the other phases so the offsets never stay live across them).
@@ -249,9 +293,29 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             off[r][j] = eoff(ro, j);
-            yv[r][j] = bld1(rY, off[r][j]);
-            zv[r][j] = bld1(rZ, zoob | off[r][j]);
+            if (!a.bn16) {
+              yv[r][j] = bld1(rY, off[r][j]);
+              zv[r][j] = bld1(rZ, zoob | off[r][j]);
+            }
           }
+        }
+        if (a.bn16) {   // bf16 y / z: one dword load per row pair, split between the lane pair
+          uint32_t yw[ER / 2][TN], zw[ER / 2][TN];
+#pragma unroll
+          for (int rp = 0; rp < ER / 2; ++rp)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const uint32_t po = poff(off[2 * rp][j], off[2 * rp + 1][j]);
+              yw[rp][j] = __builtin_amdgcn_raw_buffer_load_b32(rY, po, 0, 0);
+              zw[rp][j] = __builtin_amdgcn_raw_buffer_load_b32(rZ, zoob | po, 0, 0);
+            }
+#pragma unroll
+          for (int rp = 0; rp < ER / 2; ++rp)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              unpair(yw[rp][j], yv[2 * rp][j], yv[2 * rp + 1][j]);
+              unpair(zw[rp][j], zv[2 * rp][j], zv[2 * rp + 1][j]);
+            }
         }
         float old[ER][TN];
 #pragma unroll
@@ -392,6 +456,16 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
           rv[r][j] = has_res ? bld1(rR, off[r][j]) : 0.f;
         }
       }
+      if (c16) {   // bf16 output (no beta / residual / scale: checked on the host)
+#pragma unroll
+        for (int rp = 0; rp < ER / 2; ++rp)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            st_pair(acc[i][j][r0 + 2 * rp], acc[i][j][r0 + 2 * rp + 1], off[2 * rp][j],
+                    off[2 * rp + 1][j]);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < ER; ++r)
 #pragma unroll
@@ -452,6 +526,18 @@ __device__ __forceinline__ void epilogue_guarded(const GemmArgs& a, floatx16 (&a
         }
       }
   }
+  const bool c16 = MODE == MODE_FWD && a.c16;
+  if (c16) {   // the stored (rounded) values are the ones the BN statistics describe
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = bf16_rne(acc[i][j][r]);
+  }
+  auto bnv = [&](const float* p, long o) -> float {
+    return a.bn16 ? (float)reinterpret_cast<const __bf16*>(p)[o] : p[o];
+  };
   // (1c) fused BatchNorm backward partials (DGRAD): mask, store, per-column tile sums
   if (MODE == MODE_DGRAD && a.bn_part != nullptr) {
     float cs[TN], cq[TN], mu[TN], bsc[TN], bsh[TN];
@@ -476,9 +562,9 @@ __device__ __forceinline__ void epilogue_guarded(const GemmArgs& a, floatx16 (&a
           const int col = col0 + 32 * j;
           if (col >= a.N) continue;
           float v = acc[i][j][r];
-          const float yv = a.bn_y[ro + col];
+          const float yv = bnv(a.bn_y, ro + col);
           bool keep = true;
-          if (a.bn_mask == 1) keep = a.bn_z[ro + col] > 0.f;
+          if (a.bn_mask == 1) keep = bnv(a.bn_z, ro + col) > 0.f;
           else if (a.bn_mask == 2) keep = fmaf(yv, bsc[j], bsh[j]) > 0.f;
           v = keep ? v : 0.f;
           Cb[ro + col] = v;
@@ -598,7 +684,8 @@ __device__ __forceinline__ void epilogue_guarded(const GemmArgs& a, floatx16 (&a
           if (a.res) v += a.res[ro + col];
           if (a.relu) v = fmaxf(v, 0.f);
         }
-        Cb[ro + col] = v;
+        if (c16) reinterpret_cast<__bf16*>(Cb)[ro + col] = (__bf16)v;
+        else Cb[ro + col] = v;
       }
     }
 }

@@ -18,10 +18,19 @@ int ew_blocks(long n) {
   return (int)(b > 0 ? b : 1);
 }
 
+__device__ __forceinline__ float4 ldx4(const float* p, long i4) {
+  return reinterpret_cast<const float4*>(p)[i4];
+}
+__device__ __forceinline__ float4 ldx4(const __bf16* p, long i4) {   // bf16 -> fp32, exact
+  const uint2 u = reinterpret_cast<const uint2*>(p)[i4];
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+
 // BN: the input is the stem conv's pre-BN output; relu(x*scale + shift) is applied per loaded
 // element (the stem's BN+ReLU output is never materialised; same fmaf/max as bn_apply).
-template <bool BN, typename TY = float>
-__global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x, TY* __restrict__ y,
+template <bool BN, typename TY = float, typename TX = float>
+__global__ __launch_bounds__(NT) void maxpool_fwd_k(const TX* __restrict__ x, TY* __restrict__ y,
                                                     uchar4* __restrict__ am, int n, int h, int w,
                                                     int c4, int ho, int wo,
                                                     const float* __restrict__ scale,
@@ -47,7 +56,7 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_k(const float* __restrict__ x,
       for (int dx = 0; dx < 3; ++dx) {
         const int ix = ox * 2 - 1 + dx;
         if (ix < 0 || ix >= w) continue;
-        float4 v = reinterpret_cast<const float4*>(x)[(((long)nn * h + iy) * w + ix) * c4 + cq];
+        float4 v = ldx4(x, (((long)nn * h + iy) * w + ix) * c4 + cq);
         if (BN) {
           v.x = fmaxf(fmaf(v.x, sc.x, sf.x), 0.f);
           v.y = fmaxf(fmaf(v.y, sc.y, sf.y), 0.f);
@@ -90,7 +99,8 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_k(const float* __restrict__ dy
   }
 }
 
-__global__ __launch_bounds__(NT) void avgpool_fwd_k(const float* __restrict__ x, float* __restrict__ y, int n,
+template <typename TX = float>
+__global__ __launch_bounds__(NT) void avgpool_fwd_k(const TX* __restrict__ x, float* __restrict__ y, int n,
                                                     int hw, int c4) {
   const long total = (long)n * c4;
   const float inv = 1.0f / (float)hw;
@@ -98,9 +108,9 @@ __global__ __launch_bounds__(NT) void avgpool_fwd_k(const float* __restrict__ x,
     const int cq = (int)(i % c4);
     const long nn = i / c4;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* px = reinterpret_cast<const float4*>(x) + nn * hw * c4 + cq;
+    const long base = nn * hw * c4 + cq;
     for (int p = 0; p < hw; ++p) {
-      const float4 v = px[(long)p * c4];
+      const float4 v = ldx4(x, base + (long)p * c4);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     s.x *= inv; s.y *= inv; s.z *= inv; s.w *= inv;
@@ -234,6 +244,19 @@ TMR_API int tmr_maxpool2d_fwd_bn_x(const float* x, const float* scale, const flo
   return 0;
 }
 
+TMR_API int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const float* shift, void* y,
+                                     uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
+                                     hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd_bn_a16: channels %d must be a multiple of 4", c);
+  TMR_CHECK_ARG(scale && shift, "tmr_maxpool2d_fwd_bn_a16: null BatchNorm scale/shift");
+  const long total = (long)n * ho * wo * (c / 4);
+  hipLaunchKernelGGL((maxpool_fwd_k<true, __bf16, __bf16>), dim3(ew_blocks(total)), dim3(NT), 0,
+                     stream, (const __bf16*)x, (__bf16*)y, (uchar4*)argmax, n, h, w, c / 4, ho, wo,
+                     scale, shift);
+  TMR_CHECK_LAUNCH("maxpool_fwd_bn_a16");
+  return 0;
+}
+
 TMR_API int tmr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int n, int h,
                               int w, int c, int ho, int wo, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_bwd: channels %d must be a multiple of 4", c);
@@ -246,9 +269,17 @@ TMR_API int tmr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx,
 
 TMR_API int tmr_avgpool_fwd(const float* x, float* y, int n, int hw, int c, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool_fwd: channels %d must be a multiple of 4", c);
-  hipLaunchKernelGGL(avgpool_fwd_k, dim3(ew_blocks((long)n * c / 4)), dim3(NT), 0, stream, x, y, n,
+  hipLaunchKernelGGL(avgpool_fwd_k<float>, dim3(ew_blocks((long)n * c / 4)), dim3(NT), 0, stream, x, y, n,
                      hw, c / 4);
   TMR_CHECK_LAUNCH("avgpool_fwd");
+  return 0;
+}
+
+TMR_API int tmr_avgpool_fwd_a16(const void* x, float* y, int n, int hw, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool_fwd_a16: channels %d must be a multiple of 4", c);
+  hipLaunchKernelGGL(avgpool_fwd_k<__bf16>, dim3(ew_blocks((long)n * c / 4)), dim3(NT), 0, stream,
+                     (const __bf16*)x, y, n, hw, c / 4);
+  TMR_CHECK_LAUNCH("avgpool_fwd_a16");
   return 0;
 }
 

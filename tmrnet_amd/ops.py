@@ -71,6 +71,8 @@ MAX_FRAMES = 0
 
 
 IO_X, IO_W, IO_DY, IO_WT = 1, 2, 4, 8   # tmr_conv_desc.io: bf16-stored x / KRSC w / dy / CRSK w
+IO_Y, IO_BN = 16, 32    # bf16 conv output y (forward) / bf16 y, z of the fused BN backward (dgrad)
+BF16 = torch.bfloat16
 
 
 def _io(x=None, w=None, dy=None, wt=False):
@@ -172,15 +174,18 @@ def _prologue(xpro=None, dpro=None):
     return p
 
 
-def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32", xpro=None):
+def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32", xpro=None,
+                     y16=False):
     """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts).
-    xpro = (scale, shift): x is a pre-BN tensor read as relu(x*scale + shift) (0 at padding)."""
+    xpro = (scale, shift): x is a pre-BN tensor read as relu(x*scale + shift) (0 at padding).
+    y16: y stored rounded to bf16, the partials describing the rounded values (TMR_IO_Y_BF16)."""
     _req_op(x, "x"); _req_op(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
     assert c == c2, (x.shape, w_krsc.shape)
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, w_krsc))
-    out = _empty((n, d.ho, d.wo, k), x)
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math,
+                  io=_io(x, w_krsc) | (IO_Y if y16 else 0))
+    out = _empty((n, d.ho, d.wo, k), x, dtype=BF16 if y16 else f32)
     nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
     with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
@@ -241,12 +246,15 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
                      shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts).
-    wt: as conv_dgrad."""
-    _req_op(w_krsc, "w"); _req(y, "y"); _req(mean, "mean")
+    wt: as conv_dgrad.  y / z may be bf16 (the bf16-activation step, TMR_IO_BN_BF16)."""
+    _req_op(w_krsc, "w"); _req_op(y, "y"); _req(mean, "mean")
+    if z is not None and z.dtype != y.dtype:
+        raise RuntimeError("conv_dgrad_bnbwd: y and z must have one dtype")
     n, ho, wo, k = dy.shape
     k2, r, s, c = _dgrad_w(w_krsc, wt)
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math, io=_io(None, w_krsc, dy, wt))
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math,
+                  io=_io(None, w_krsc, dy, wt) | (IO_BN if y.dtype == BF16 else 0))
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
@@ -279,6 +287,12 @@ def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma, bf16=False):
     n, h, w, c = y.shape
     _, ho, wo, _ = dyp.shape
     ws, nb = _bn_ws(n * h * w, c, y.device)
+    if y.dtype == BF16:   # bf16 activations: dy is bf16 too
+        dy = torch.empty_like(y)
+        dgamma = _empty((c,), dyp); dbeta = _empty((c,), dyp)
+        call("tmr_bn_bwd_maxpool_a16", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma,
+             dy, dgamma, dbeta, c, ws, ctypes.c_size_t(nb), stream_ptr())
+        return dy, dgamma, dbeta
     dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)
     call("tmr_bn_bwd_maxpool_x", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma, dy,
@@ -319,10 +333,16 @@ def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma, bf16=False):
     bf16=True stores dy rounded (consumed only by the bf16-math dgrad / wgrad)."""
     c = y.shape[-1]
     rows = y.numel() // c
-    dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
-    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
     nb = query("tmr_bn_parts_ws_bytes", int(nparts), c)
     ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=y.device)
+    if y.dtype == BF16:   # bf16 activations: dy is bf16 too
+        dy = torch.empty_like(y)
+        dgamma = _empty((c,), g); dbeta = _empty((c,), g)
+        call("tmr_bn_bwd_parts_a16", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta,
+             rows, c, ws, ctypes.c_size_t(ws.numel() * 8), stream_ptr())
+        return dy, dgamma, dbeta
+    dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
+    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
     call("tmr_bn_bwd_parts_x", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta, rows,
          c, ws, ctypes.c_size_t(ws.numel() * 8), int(bf16), stream_ptr())
     return dy, dgamma, dbeta
@@ -490,6 +510,12 @@ def bn_apply(y, scale, shift, residual=None, relu=True, out=None, bf16=False):
     as a bf16-math conv operand)."""
     c = y.shape[-1]
     rows = y.numel() // c
+    if y.dtype == BF16:   # bf16 activations: y, residual and z bf16
+        if residual is not None and residual.dtype != BF16:
+            raise RuntimeError("bn_apply: a bf16 y takes a bf16 residual")
+        out = torch.empty_like(y) if out is None else out
+        call("tmr_bn_apply_a16", y, scale, shift, residual, out, rows, c, int(relu), stream_ptr())
+        return out
     if out is None:
         out = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     call("tmr_bn_apply_x", y, scale, shift, residual, out, rows, c, int(relu),
@@ -515,6 +541,13 @@ def bn_apply2(y, scale, shift, yr, rscale, rshift, relu=True, out=None, dual=Fal
     rows = y.numel() // c
     if yr.shape != y.shape:
         raise RuntimeError("bn_apply2: branch shape %s != %s" % (tuple(yr.shape), tuple(y.shape)))
+    if y.dtype == BF16:   # bf16 activations: y, yr and z bf16
+        if yr.dtype != BF16 or dual:
+            raise RuntimeError("bn_apply2: bf16 y takes a bf16 branch and writes one bf16 z")
+        out = torch.empty_like(y) if out is None else out
+        call("tmr_bn_apply2_a16", y, scale, shift, yr, rscale, rshift, out, rows, c, int(relu),
+             stream_ptr())
+        return out
     if out is None:
         out = torch.empty_like(y)
     z16 = torch.empty_like(y, dtype=torch.bfloat16) if dual else None
@@ -530,6 +563,15 @@ def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None, sca
     c = y.shape[-1]
     rows = y.numel() // c
     ws, nb = _bn_ws(rows, c, y.device)
+    if y.dtype == BF16:   # bf16 activations: y, z bf16; dz, dres fp32; dy bf16
+        dy = torch.empty_like(y)
+        dres = None
+        if want_dres:
+            dres = torch.empty_like(dz) if dres_out is None else dres_out
+        dgamma = _empty((c,), dz); dbeta = _empty((c,), dz)
+        call("tmr_bn_bwd_a16", dz, y, z if relu else None, scale, shift, mean, inv, gamma, dy, dres,
+             dgamma, dbeta, rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
+        return dy, dres, dgamma, dbeta
     dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     dres = None
     if want_dres:
@@ -557,8 +599,12 @@ def maxpool_fwd_bn(x, scale, shift, bf16=False):
     n, h, w, c = x.shape
     ho = (h + 2 - 3) // 2 + 1
     wo = (w + 2 - 3) // 2 + 1
-    y = _empty((n, ho, wo, c), x, dtype=torch.bfloat16 if bf16 else f32)
     am = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
+    if x.dtype == BF16:   # bf16 activations: the stem's bf16 y in, bf16 out
+        y = _empty((n, ho, wo, c), x, dtype=BF16)
+        call("tmr_maxpool2d_fwd_bn_a16", x, scale, shift, y, am, n, h, w, c, ho, wo, stream_ptr())
+        return y, am
+    y = _empty((n, ho, wo, c), x, dtype=torch.bfloat16 if bf16 else f32)
     call("tmr_maxpool2d_fwd_bn_x", x, scale, shift, y, am, n, h, w, c, ho, wo, int(bf16),
          stream_ptr())
     return y, am
@@ -575,7 +621,8 @@ def maxpool_bwd(dy, am, in_hw):
 def avgpool_fwd(x):
     n, h, w, c = x.shape
     y = _empty((n, c), x)
-    call("tmr_avgpool_fwd", x, y, n, h * w, c, stream_ptr())
+    call("tmr_avgpool_fwd_a16" if x.dtype == BF16 else "tmr_avgpool_fwd", x, y, n, h * w, c,
+         stream_ptr())
     return y
 
 

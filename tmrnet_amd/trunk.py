@@ -108,9 +108,22 @@ def _store16(math):
 # operands), tests/test_bf16_gpu.py.
 FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
 
+# bf16 activations (train mode, on top of FULL16; TMR_BF16_ACT=0 turns it off): every conv output
+# y is stored rounded to bf16 by its epilogue (the BN statistics are those of the rounded values)
+# and every BatchNorm(+residual)(+ReLU) output z is computed in fp32 and stored rounded to bf16 --
+# block outputs included, so the identity residual is the bf16 block output.  Gradients stay fp32
+# (dy, a conv operand, bf16).  This changes the numerics contract of the bf16 step (the oracle's
+# emulate_bf16_convs(activations=True) restates it); the HBM traffic of every BatchNorm pass and of
+# the conv epilogues halves.
+ACT16 = os.environ.get("TMR_BF16_ACT", "1") != "0"
+
 
 def _full16(math):
     return _store16(math) and FULL16 and not FOLD_BN
+
+
+def _act16(math):
+    return _full16(math) and ACT16
 
 
 def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
@@ -137,7 +150,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     if training:
         # batch statistics come out of the conv epilogue (no separate pass over y)
         y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c, math=math,
-                                                xpro=xpro)
+                                                xpro=xpro, y16=_act16(math))
         mean, inv, scale, shift = ops.bn_finalize(
             stats, nparts, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
             bn.running_var, _bn_momentum(bn), bn.eps)
@@ -163,7 +176,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         z = ops.bn_apply_dual(y, scale, shift, residual, relu)
     else:
         # a non-residual unit's output is only ever a conv operand (next conv's forward and
-        # wgrad; the backward recomputes its ReLU mask from y): bf16 under bf16 math
+        # wgrad; the backward recomputes its ReLU mask from y): bf16 under bf16 math (with bf16
+        # activations every z is bf16: the dtype of y decides)
         z = ops.bn_apply(y, scale, shift, residual, relu, bf16=s16 and residual is None)
     if recs is not None:
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
@@ -259,7 +273,8 @@ class TrunkFn(torch.autograd.Function):
         nbt = []   # BatchNorm num_batches_tracked counters, incremented together at the end
         conv1, bn1, layers = share.trunk_parts()
         mt = share.precision
-        f16 = training and _full16(mt)
+        a16 = training and _act16(mt)            # every activation bf16: no fp32 copies
+        f16 = training and _full16(mt) and not a16
         if training:
             # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
             # mask from y, so the stem's BN output is never needed)
