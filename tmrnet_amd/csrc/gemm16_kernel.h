@@ -43,7 +43,7 @@ __device__ __forceinline__ int mn_swz(int k) {
   return R >= 128 ? ((k & 3) << 2) : (((k >> 1) & 1) << 2);
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int TAPV>
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs a) {
   constexpr int BK = 64;
   constexpr int NW = WM * WN;
@@ -292,32 +292,41 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs 
 
   const int arow0 = wm * (BM / WM) + l31;
   const int brow0 = wn * (BN / WN) + l31;
-  auto compute = [&](int buf) {
+  // the operand fragments of k-step s of LDS buffer buf
+  auto frags = [&](int buf, int s, bf16x8 (&av)[TM], bf16x8 (&bv)[TN]) {
     const unsigned char* As = smem + buf * STAGE;
     const unsigned char* Bs = As + ABYTES;
+    const int ch = (2 * s + hh) ^ kx;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (!MN)
+        av[i] = *reinterpret_cast<const bf16x8*>(As + (arow0 + 32 * i) * 128 + (ch << 4));
+      else
+        av[i] = tr_frag(As, BM, swzA, wm * (BM / WM) + 32 * i, s);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (!MN)
+        bv[j] = *reinterpret_cast<const bf16x8*>(Bs + (brow0 + 32 * j) * 128 + (ch << 4));
+      else
+        bv[j] = tr_frag(Bs, BN, swzB, wn * (BN / WN) + 32 * j, s);
+    }
+  };
+  auto mfmas = [&](const bf16x8 (&av)[TM], const bf16x8 (&bv)[TN]) {
+    if (PIPE) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    if (PIPE) __builtin_amdgcn_s_setprio(0);
+  };
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       bf16x8 av[TM], bv[TN];
-      const int ch = (2 * s + hh) ^ kx;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        if constexpr (!MN)
-          av[i] = *reinterpret_cast<const bf16x8*>(As + (arow0 + 32 * i) * 128 + (ch << 4));
-        else
-          av[i] = tr_frag(As, BM, swzA, wm * (BM / WM) + 32 * i, s);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (!MN)
-          bv[j] = *reinterpret_cast<const bf16x8*>(Bs + (brow0 + 32 * j) * 128 + (ch << 4));
-        else
-          bv[j] = tr_frag(Bs, BN, swzB, wn * (BN / WN) + 32 * j, s);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      frags(buf, s, av, bv);
+      mfmas(av, bv);
     }
   };
 
@@ -325,13 +334,33 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs 
   // Iteration kt: wait for this wave's pieces of tile kt, barrier (every wave's pieces landed;
   // every wave finished reading the other buffer in iteration kt-1), issue tile kt+1 into the
   // other buffer, MFMAs on tile kt while it lands.
-  if (ntiles > 0) {
+  if (ntiles > 0 && PIPE == 0) {
     stage(0, 0);
     for (int kt = 0; kt < ntiles; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (kt + 1 < ntiles) stage(kt + 1, (kt + 1) & 1);
       compute(kt & 1);
+    }
+  } else if (ntiles > 0) {
+    // PIPE 1: the first k-step's fragment reads go out before the LDS-DMA issue of the next
+    // tile (its address arithmetic then overlaps their latency), each later k-step's reads
+    // before the previous k-step's MFMAs; MFMA clusters at raised priority
+    stage(0, 0);
+    for (int kt = 0; kt < ntiles; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int buf = kt & 1;
+      bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+      frags(buf, 0, a0, b0);
+      if (kt + 1 < ntiles) stage(kt + 1, buf ^ 1);
+      frags(buf, 1, a1, b1);
+      mfmas(a0, b0);
+      frags(buf, 2, a0, b0);
+      mfmas(a1, b1);
+      frags(buf, 3, a1, b1);
+      mfmas(a0, b0);
+      mfmas(a1, b1);
     }
   }
   __syncthreads();   // LDS reads done (no LDS-DMA in flight) before the epilogue reuses smem
