@@ -230,6 +230,14 @@ def main():
                                  "ms": round(v[2], 2)} for k, v in per_kind.items()},
                 "step_mfma_frac": round(fps / world * GFLOP_PER_FRAME.get(args.model, 0.0) * 1e9 /
                                         (peak * 1e12), 4)}
+        # per-launch roofline: each launch bound by max(FLOPs / MFMA peak, algorithmic bytes /
+        # HBM peak) -- the short-reduction convs and the fused BN-backward dgrads are HBM-bound, so
+        # `frac` (all FLOPs against the MFMA peak) understates how close the family is to its roof
+        att_ms = sum(max(r[1] / (peak * 1e12), r[5] / (HBM_PEAK_GBS * 1e9)) for r in recs) * 1e3
+        roof["attainable_ms"] = round(att_ms, 2)
+        roof["attainable_frac"] = round(att_ms / tot_ms, 4) if tot_ms > 0 else None
+        roof["hbm_bound_launches"] = sum(
+            1 for r in recs if r[5] / (HBM_PEAK_GBS * 1e9) > r[1] / (peak * 1e12))
 
     # whole-step HBM fraction: SURVEY.md §8d's activation-traffic model
     # (4 touches x 32.0 M activation elements per frame x dtype bytes) and the measured PMC bytes

@@ -190,8 +190,8 @@ def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
     with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
                (n, h, w, c, k, r, stride),
-               _esz(x) * n * h * w * c + _esz(w_krsc) * k * r * s * c + 4 * n * d.ho * d.wo * k
-               + stats.numel() * 4):
+               _esz(x) * n * h * w * c + _esz(w_krsc) * k * r * s * c
+               + out.element_size() * n * d.ho * d.wo * k + stats.numel() * 4):
         pro = _prologue(xpro)
         if pro is None:
             call("tmr_conv2d_fwd_bnstats", ctypes.byref(d), x, w_krsc, out, stats,
@@ -268,7 +268,8 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
                _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * k * r * s * c
-               + 4 * (n * h * w * c * (3 if beta else 2) + (n * h * w * c if z is not None else 0))):
+               + 4 * n * h * w * c * (2 if beta else 1)
+               + y.element_size() * n * h * w * c * (2 if z is not None else 1)):
         pro = _prologue(None, dpro)
         if pro is None:
             call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z,
