@@ -334,6 +334,23 @@ int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const float* shi
                              hipStream_t stream);
 int tmr_avgpool_fwd_a16(const void* x, float* y, int n, int hw, int c, hipStream_t stream);
 
+/* ---------------- input pipeline: frame resize (resize.hip) ----------------------- */
+/* transforms.Resize((250,250)) of the decoded PIL frame (Training TMRNet/
+ * train_only_non-local_pretrained.py:336, pil_loader :96-99) = Pillow's Image.resize(size,
+ * BILINEAR), bit-exact for 8-bit RGB.  Host (no GPU): the per-axis tables of Pillow's
+ * precompute_coeffs + normalize_coeffs_8bpc -- bounds [out][2] = (first input index, count),
+ * k [out][ksize] 22-bit fixed point, ksize = tmr_resize_ksize(in, out).  Device: in (n, h, w, 3)
+ * uint8 -> out (n, oh, ow, 3) uint8 through tmp (horizontal pass over input rows [y0, y1) -- the
+ * rows the vertical pass reads: y0 = bounds_v[0], y1 = bounds_v[2*(oh-1)] + bounds_v[2*oh-1]);
+ * a pass whose size does not change is skipped, as in Pillow.  Tables live in device memory. */
+int tmr_resize_ksize(int in_size, int out_size);
+int tmr_resize_coeffs(int in_size, int out_size, int32_t* bounds, int32_t* k, int ksize);
+size_t tmr_resize_tmp_bytes(int n, int h, int w, int oh, int ow);
+int tmr_resize_u8(const uint8_t* in, int n, int h, int w, uint8_t* tmp, size_t tmp_bytes,
+                  uint8_t* out, int oh, int ow, const int32_t* bounds_h, const int32_t* k_h,
+                  int ksize_h, const int32_t* bounds_v, const int32_t* k_v, int ksize_v, int y0,
+                  int y1, hipStream_t stream);
+
 /* ---------------- pooling (pool_layout.hip) --------------------------------------- */
 /* MaxPool2d(3,2,1) of share.maxpool (train_only_non-local_pretrained.py:207), NHWC */
 int tmr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int n, int h, int w, int c,

@@ -78,6 +78,10 @@ SIGNATURES = {
     "tmr_bn_bwd_maxpool_a16": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
     "tmr_maxpool2d_fwd_bn_a16": [P, P, P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd_a16": [P, P, I, I, I, P],
+    "tmr_resize_ksize": [I, I],
+    "tmr_resize_coeffs": [I, I, P, P, I],
+    "tmr_resize_tmp_bytes": [I, I, I, I, I],
+    "tmr_resize_u8": [P, I, I, I, P, SZ, P, I, I, P, P, I, P, P, I, I, I, P],
     "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
     "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],
@@ -153,6 +157,7 @@ _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,
     "tmr_clear_error": None,
     "tmr_conv2d_wgrad_ws_bytes": SZ,
+    "tmr_resize_tmp_bytes": SZ,
     "tmr_bn_ws_bytes": SZ,
     "tmr_bn_parts_ws_bytes": SZ,
     "tmr_sgd_chunk": ctypes.c_int64,

@@ -10,8 +10,9 @@ Reference: the transform classes of ``code/Training TMRNet/train_only_non-local_
 ``count // sequence_length`` (its own call counter) before drawing, so all T frames of a clip get
 the same crop / jitter / flip / angle.  The host part here is that rule, verbatim (Python's
 Mersenne Twister, same draw order); the pixels are produced by ``tmr_clip_augment`` in one pass
-over the resident uint8 frames, bit-exact to PIL (see augment.hip).  Resize and JPEG decoding
-stay on the host (frames arrive 250x250, as in the benchmark's synthetic input).
+over the resident uint8 frames, bit-exact to PIL (see augment.hip).  Frames come from files
+through tmrnet_amd.frames (PIL decode on host threads, Resize((250,250)) on the device, bit-exact
+to Pillow); the benchmark uses synthetic 250x250 frames.
 """
 import math
 import random
