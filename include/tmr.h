@@ -333,6 +333,8 @@ int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const float* shi
                              uint8_t* argmax, int n, int h, int w, int c, int ho, int wo,
                              hipStream_t stream);
 int tmr_avgpool_fwd_a16(const void* x, float* y, int n, int hw, int c, hipStream_t stream);
+/* fp32 -> bf16 (RNE) copy of a tensor consumed as a bf16 conv operand (n % 8 == 0) */
+int tmr_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
 
 /* ---------------- input pipeline: frame resize (resize.hip) ----------------------- */
 /* transforms.Resize((250,250)) of the decoded PIL frame (Training TMRNet/

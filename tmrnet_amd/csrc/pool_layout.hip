@@ -322,6 +322,28 @@ TMR_API int tmr_weight_oihw_to_crsk_x(const float* w, void* wt, int k, int c, in
   return 0;
 }
 
+// fp32 -> bf16 (RNE) copy: the bf16 conv operand of a tensor produced in fp32 (ResNeSt split-
+// attention / pool outputs), 8 elements per thread
+__global__ __launch_bounds__(NT) void cast_bf16_k(const float* __restrict__ x, __bf16* __restrict__ y,
+                                                  long n8) {
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const float4 a = reinterpret_cast<const float4*>(x)[2 * i];
+    const float4 b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+    const bf16x8_t v = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                        (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+    reinterpret_cast<bf16x8_t*>(y)[i] = v;
+  }
+}
+
+TMR_API int tmr_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream) {
+  TMR_CHECK_ARG(x && y && n >= 0 && n % 8 == 0, "tmr_cast_f32_bf16: n %ld must be a multiple of 8", n);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(cast_bf16_k, dim3(ew_blocks(n / 8)), dim3(NT), 0, stream, x, (__bf16*)y, n / 8);
+  TMR_CHECK_LAUNCH("cast_bf16");
+  return 0;
+}
+
 TMR_API int tmr_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, int cpad,
                              hipStream_t stream) {
   TMR_CHECK_ARG(cpad >= c, "tmr_nchw_to_nhwc: cpad < c");

@@ -449,6 +449,14 @@ def weight_to_crsk(w, bf16=True):
     return out
 
 
+def to_bf16(x):
+    """fp32 -> bf16 (RNE) copy (tmr_cast_f32_bf16): the bf16 conv operand of an fp32 tensor."""
+    _req(x, "x")
+    out = torch.empty_like(x, dtype=BF16)
+    call("tmr_cast_f32_bf16", x, out, ctypes.c_long(x.numel()), stream_ptr())
+    return out
+
+
 def nchw_to_nhwc(x, cpad=None):
     n, c, h, w = x.shape
     cpad = c if cpad is None else cpad

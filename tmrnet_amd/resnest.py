@@ -13,7 +13,15 @@ Each stage is an autograd node over HIP kernels, activations NHWC:
   * AvgPoolFn / MaxPoolFn / GlobalPoolFn
 Grouped convolutions run one GEMM launch per group on channel slices (pixel strides in
 tmr_conv_desc), so no channel shuffles are materialised.
+
+bf16 math in train mode (config C4): every conv but the 4-channel stem reads bf16 operands from
+HBM -- a bf16 copy of its input (written by the producing BN pass next to the fp32 tensor the
+residual / split attention / pools use, or cast once for split-attention and pool outputs), KRSC
+and transposed CRSK bf16 weights, bf16 dy -- and therefore runs on the LDS-DMA engine
+(gemm16_kernel.h).  The contract is unchanged (the bf16 convs round exactly those operands).
+TMR_BF16_FULL=0 keeps the register-staged path.
 """
+import os
 import math
 
 import torch
@@ -35,19 +43,27 @@ def _bn_train_or_eval(y, bn, training):
     return None, None, scale, shift
 
 
+FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
+
+
 class ConvBNActFn(torch.autograd.Function):
+    """x (fp32, autograd) and x16 (its bf16 copy or None, not differentiable) -> (z, z16): z16 is
+    the bf16 copy of z written by the same BN pass when the bf16 operand path is on (else None)."""
+
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, residual, bn, stride, pad, groups, relu, c_real, math):
+    def forward(ctx, x, x16, w, gamma, beta, residual, bn, stride, pad, groups, relu, c_real, math):
         x = x.contiguous()
         n, h, wd, cs = x.shape
         k, cg, r, s = w.shape
         kg = k // groups
         cgs = cs // groups                       # stored channels per group
         training = bn.training
-        wks = [ops.weight_to_krsc(w.detach()[g * kg:(g + 1) * kg].contiguous(), cpad=cgs)
+        f16 = x16 is not None
+        wks = [ops.weight_to_krsc(w.detach()[g * kg:(g + 1) * kg].contiguous(), cpad=cgs, bf16=f16)
                for g in range(groups)]
+        xc = x16 if f16 else x                   # the conv operand
         if groups == 1 and training:
-            y, stats, nparts = ops.conv_fwd_bnstats(x, wks[0], stride, pad, c_real=c_real,
+            y, stats, nparts = ops.conv_fwd_bnstats(xc, wks[0], stride, pad, c_real=c_real,
                                                     math=math)
             mean, inv, scale, shift = ops.bn_finalize(stats, nparts, gamma.detach(), beta.detach(),
                                                       bn.running_mean, bn.running_var, bn.momentum,
@@ -58,40 +74,56 @@ class ConvBNActFn(torch.autograd.Function):
             wo = (wd + 2 * pad - s) // stride + 1
             y = torch.empty((n, ho, wo, k), dtype=x.dtype, device=x.device)
             for g in range(groups):
-                ops.conv_fwd(x[..., g * cgs:(g + 1) * cgs], wks[g], stride, pad,
+                ops.conv_fwd(xc[..., g * cgs:(g + 1) * cgs], wks[g], stride, pad,
                              out=y[..., g * kg:(g + 1) * kg], c_real=min(cg, c_real), math=math)
             mean, inv, scale, shift = _bn_train_or_eval(y, bn, training)
-        z = ops.bn_apply(y, scale, shift, residual.contiguous() if residual is not None else None,
-                         relu)
+        res = residual.contiguous() if residual is not None else None
+        z16 = None
+        if f16 and training:   # z in fp32 (residual, split attention, pools) + its bf16 copy
+            z, z16 = ops.bn_apply_dual(y, scale, shift, res, relu)
+            ctx.mark_non_differentiable(z16)
+        else:
+            z = ops.bn_apply(y, scale, shift, res, relu)
+        # the dgrad view of the bf16 operand path reads transposed bf16 weights
+        wts = ([ops.weight_to_crsk(w.detach()[g * kg:(g + 1) * kg].contiguous())
+                for g in range(groups)] if f16 and training and cgs == cg else [])
         # without a residual the backward recomputes the ReLU mask from y and scale/shift
-        ctx.save_for_backward(x, y, z if residual is not None else None, scale, shift, mean, inv,
-                              gamma, *wks)
-        ctx.cfg = (stride, pad, groups, relu, c_real, residual is not None, r, s, math)
-        return z
+        ctx.save_for_backward(xc, y, z if residual is not None else None, scale, shift, mean, inv,
+                              gamma, *wks, *wts)
+        ctx.cfg = (stride, pad, groups, relu, c_real, residual is not None, r, s, math, f16,
+                   len(wts))
+        return z, z16
 
     @staticmethod
-    def backward(ctx, dz):
-        x, y, z, scale, shift, mean, inv, gamma, *wks = ctx.saved_tensors
-        stride, pad, groups, relu, c_real, has_res, r, s, math = ctx.cfg
+    def backward(ctx, dz, _dz16=None):
+        x, y, z, scale, shift, mean, inv, gamma, *ws = ctx.saved_tensors
+        stride, pad, groups, relu, c_real, has_res, r, s, math, f16, nwt = ctx.cfg
+        wks, wts = ws[:groups], ws[groups:]
         if mean is None:
             raise RuntimeError("backward through eval-mode BatchNorm is not supported")
         dz = dz.contiguous()
+        # dy only feeds this conv's dgrad / wgrad: bf16 on the bf16 operand path
         dy, dres, dg, db = ops.bn_bwd(dz, y, z, mean, inv, gamma.detach(), relu, want_dres=has_res,
-                                      scale=scale, shift=shift)
+                                      scale=scale, shift=shift, bf16=f16)
         n, h, wd, cs = x.shape
         k = y.shape[-1]
         kg, cgs = k // groups, cs // groups
         creal_g = min(c_real, cgs)
-        dw = torch.empty((k, creal_g, r, s), dtype=x.dtype, device=x.device)
-        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty((k, creal_g, r, s), dtype=torch.float32, device=x.device)
+        dx = torch.empty(x.shape, dtype=torch.float32, device=x.device) \
+            if ctx.needs_input_grad[0] else None
         for g in range(groups):
             dyg = dy[..., g * kg:(g + 1) * kg]
             ops.conv_wgrad(x[..., g * cgs:(g + 1) * cgs], dyg, r, s, stride, pad, c_real=creal_g,
                            out=dw[g * kg:(g + 1) * kg], math=math)
             if dx is not None:
-                ops.conv_dgrad(dyg, wks[g], (h, wd), stride, pad, out=dx[..., g * cgs:(g + 1) * cgs],
-                               math=math)
-        return dx, dw, dg, db, dres, None, None, None, None, None, None, None
+                if nwt:
+                    ops.conv_dgrad(dyg, wts[g], (h, wd), stride, pad,
+                                   out=dx[..., g * cgs:(g + 1) * cgs], math=math, wt=True)
+                else:
+                    ops.conv_dgrad(dyg, wks[g], (h, wd), stride, pad,
+                                   out=dx[..., g * cgs:(g + 1) * cgs], math=math)
+        return dx, None, dw, dg, db, dres, None, None, None, None, None, None, None
 
 
 class SplAtFn(torch.autograd.Function):
@@ -216,9 +248,20 @@ class GlobalPoolFn(torch.autograd.Function):
 
 def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=None,
                 math="fp32"):
-    return ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, residual, bn, stride, pad, groups,
-                             relu, c_real if c_real is not None else conv.weight.shape[1] * groups,
-                             math)
+    """conv -> BN -> (+residual) -> (ReLU).  On the bf16 operand path (bf16 math, train mode,
+    TMR_BF16_FULL) the conv reads x's bf16 copy: the one its producer attached (`_tmr_bf16`), else
+    a cast; the 4-channel stem input stays fp32 (register-staged gather)."""
+    x16 = None
+    if math == "bf16" and bn.training and FULL16 and x.shape[-1] % 8 == 0:
+        x16 = getattr(x, "_tmr_bf16", None)
+        if x16 is None:
+            x16 = ops.to_bf16(x.contiguous())
+    z, z16 = ConvBNActFn.apply(x, x16, conv.weight, bn.weight, bn.bias, residual, bn, stride, pad,
+                               groups, relu,
+                               c_real if c_real is not None else conv.weight.shape[1] * groups, math)
+    if z16 is not None:
+        z._tmr_bf16 = z16
+    return z
 
 
 # ------------------------------------------------------------------ modules
