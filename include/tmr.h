@@ -435,6 +435,22 @@ typedef struct tmr_sgd_tensor {
 int64_t tmr_sgd_chunk(void);
 int tmr_sgd_step_multi(const tmr_sgd_tensor* table, int ntensors, int64_t nblocks,
                        hipStream_t stream);
+/* Multi-tensor torch.optim.Adam step (the -o 1 optimizer, train_only_non-local_pretrained.py:644-645,
+ * code/models.py:63-68; amsgrad off): same table scheme as tmr_sgd_step_multi (chunks of
+ * tmr_sgd_chunk()), per tensor the moments m / v and the host-computed step_size = lr / (1 -
+ * beta1^step), bc2_sqrt = sqrt(1 - beta2^step). */
+typedef struct tmr_adam_tensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+  int64_t block_begin;
+  float beta1, beta2, eps, weight_decay, step_size, bc2_sqrt;
+  int32_t maximize, reserved;
+} tmr_adam_tensor;
+int tmr_adam_step_multi(const tmr_adam_tensor* table, int ntensors, int64_t nblocks,
+                        hipStream_t stream);
 /* LFB row table of get_long_feature (train_only_non-local_pretrained.py:293-311):
  * rows[b][k] = index of the first valid start >= max(start_b - k - 1, 0) in the sorted
  * valid-start list (== the reference's dict walk, incl. own-row fallback and

@@ -363,6 +363,45 @@ def test_sgd_optimizer_multi_tensor_matches_torch(dev):
         assert rel_err(a, b) < 1e-6
 
 
+def test_adam_optimizer_multi_tensor_matches_torch(dev):
+    """tmrnet_amd.Adam (one tmr_adam_step_multi launch per step; the reference's -o 1 optimizer,
+    train_only_non-local_pretrained.py:644-645) vs torch.optim.Adam in float64 over five steps:
+    groups with different lr / betas / eps / weight decay, chunk-straddling tensors, a parameter
+    without grad in one step, an lr change; state_dict keys interchange with torch's."""
+    import tmrnet_amd
+    g = torch.Generator().manual_seed(1)
+    shapes = [(3,), (8192,), (8193,), (70, 300), (1,), (5, 7)]
+    base = [torch.randn(s, generator=g) for s in shapes]
+    ours = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    ref = [torch.nn.Parameter(b.clone().double()) for b in base]
+
+    def groups(ps):
+        return [{"params": ps[0:2]},
+                {"params": ps[2:4], "lr": 3e-3, "betas": (0.8, 0.99)},
+                {"params": ps[4:5], "weight_decay": 1e-2},
+                {"params": ps[5:6], "eps": 1e-6}]
+    o1 = tmrnet_amd.Adam(groups(ours), lr=1e-3)
+    o2 = torch.optim.Adam(groups(ref), lr=1e-3)
+    for step in range(5):
+        if step == 3:
+            for a, b in zip(o1.param_groups, o2.param_groups):
+                a["lr"] *= 0.5; b["lr"] *= 0.5
+        for i, (a, b) in enumerate(zip(ours, ref)):
+            if i == 4 and step == 1:
+                a.grad = None; b.grad = None
+                continue
+            gr = torch.randn(a.shape, generator=g)
+            a.grad = gr.to(dev)
+            b.grad = gr.double()
+        o1.step(); o2.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ours, ref):
+        assert rel_err(a, b) < 2e-6
+    sd = o1.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+    assert float(sd["state"][4]["step"]) == 4.0
+
+
 @pytest.mark.parametrize("case", [
     # n, h, w, cin(dx channels), cout(dy channels), r, stride, pad, mask, beta
     (3, 14, 14, 64, 256, 1, 1, 0, 2, 0.0),     # conv3 dgrad -> conv2's BN (mask from y)

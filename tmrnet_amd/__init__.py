@@ -6,6 +6,6 @@ from .nlblock import NLBlock, LFBRows  # noqa: F401
 from .trunk import ResNet50Share, resnet50_share  # noqa: F401
 from .model import resnet_lstm, resnet_lstm_LFB, MemoryBankModel  # noqa: F401
 from .loss import CrossEntropyLoss  # noqa: F401
-from .optim import SGD  # noqa: F401
+from .optim import SGD, Adam  # noqa: F401
 
 __version__ = "0.1.0"

@@ -6,10 +6,9 @@ Training memory bank model/train_singlenet_phase_1fc.py:223-232 (the shipped mod
 feeds a 5-D tensor to Conv2d and raises): x (B,T,3,224,224) or (F,3,224,224) -> (F, num_class);
 the caller keeps outputs[T-1::T] (train_memorybank.py:262).
 """
-import torch
 
 from tmrnet_amd.model import MemoryBankModel
-from tmrnet_amd.optim import SGD
+from tmrnet_amd.optim import SGD, Adam
 
 
 class resnet_lstm(MemoryBankModel):  # noqa: N801  (reference name)
@@ -33,5 +32,5 @@ class resnet_lstm(MemoryBankModel):  # noqa: N801  (reference name)
             return SGD(groups, lr=a.lr / 10, momentum=a.momentum, dampening=a.dampening,
                        weight_decay=a.weightdecay, nesterov=a.nesterov)
         if a.opt == 1:
-            return torch.optim.Adam(groups, lr=a.lr / 10)
+            return Adam(groups, lr=a.lr / 10)
         return None

@@ -319,6 +319,35 @@ __global__ __launch_bounds__(256) void sgd_multi_k(const tmr_sgd_tensor* __restr
   }
 }
 
+// Multi-tensor Adam (torch.optim.Adam, amsgrad off): the table layout of SGD, moments m / v.
+// Per element the arithmetic of torch's _multi_tensor_adam: lerp of m toward the gradient
+// (weight 1 - beta1 < 0.5 branch), v = v * beta2 + (1 - beta2) * d * d, denom = sqrt(v) /
+// sqrt(bc2) + eps, p -= step_size * m / denom (step_size = lr / bc1 from the host, in double).
+__global__ __launch_bounds__(256) void adam_multi_k(const tmr_adam_tensor* __restrict__ tab, int nt) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].block_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const tmr_adam_tensor t = tab[lo];
+  const long base = (b - t.block_begin) * SGD_CHUNK;
+  const long end = base + SGD_CHUNK < t.n ? base + SGD_CHUNK : t.n;
+  const float w1 = 1.f - t.beta1, w2 = 1.f - t.beta2;
+  for (long i = base + threadIdx.x; i < end; i += 256) {
+    const float pv = t.p[i];
+    float d = t.maximize ? -t.g[i] : t.g[i];
+    if (t.weight_decay != 0.f) d = d + t.weight_decay * pv;
+    const float mo = t.m[i];
+    const float m = w1 < 0.5f ? mo + w1 * (d - mo) : d - (d - mo) * (1.f - w1);
+    const float v = t.v[i] * t.beta2 + w2 * (d * d);
+    t.m[i] = m;
+    t.v[i] = v;
+    const float denom = sqrtf(v) / t.bc2_sqrt + t.eps;
+    t.p[i] = pv - t.step_size * (m / denom);
+  }
+}
+
 int blocks_for(long n, int bs) {
   long b = (n + bs - 1) / bs;
   if (b > 8192) b = 8192;
@@ -441,6 +470,16 @@ TMR_API int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr,
 }
 
 TMR_API int64_t tmr_sgd_chunk(void) { return SGD_CHUNK; }
+
+TMR_API int tmr_adam_step_multi(const tmr_adam_tensor* table, int ntensors, int64_t nblocks,
+                                hipStream_t stream) {
+  if (ntensors == 0 || nblocks == 0) return 0;
+  TMR_CHECK_ARG(table && ntensors > 0 && nblocks > 0 && nblocks < (1L << 31),
+                "tmr_adam_step_multi: bad table (%d tensors, %ld blocks)", ntensors, (long)nblocks);
+  hipLaunchKernelGGL(adam_multi_k, dim3((unsigned)nblocks), dim3(256), 0, stream, table, ntensors);
+  TMR_CHECK_LAUNCH("adam_step_multi");
+  return 0;
+}
 
 TMR_API int tmr_sgd_step_multi(const tmr_sgd_tensor* table, int ntensors, int64_t nblocks,
                                hipStream_t stream) {

@@ -88,6 +88,77 @@ class SGD(torch.optim.Optimizer):
         return loss
 
 
+_ADAM_ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("n", "<i8"),
+                        ("block_begin", "<i8"), ("beta1", "<f4"), ("beta2", "<f4"), ("eps", "<f4"),
+                        ("weight_decay", "<f4"), ("step_size", "<f4"), ("bc2_sqrt", "<f4"),
+                        ("maximize", "<i4"), ("reserved", "<i4")])
+assert _ADAM_ENTRY.itemsize == 80   # sizeof(tmr_adam_tensor), include/tmr.h
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad off) on one multi-tensor launch per step (tmr_adam_step_multi):
+    the reference's -o 1 optimizer (train_only_non-local_pretrained.py:644-645, code/models.py:63-68:
+    default betas / eps, per-group lr).  State keys as torch's ('step', 'exp_avg', 'exp_avg_sq'),
+    so state_dict()s interchange; 'step' is a CPU float tensor as in torch."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 amsgrad=False, maximize=False):
+        if amsgrad:
+            raise NotImplementedError("Adam(amsgrad=True) is not used by the reference")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError("Invalid beta parameters: %s" % (betas,))
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=maximize)
+        super().__init__(params, defaults)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        entries, keep, dev, chunk = [], [], None, None
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
+                    raise RuntimeError("Adam: parameters must be contiguous fp32 GPU tensors")
+                if dev is None:
+                    dev = p.device
+                    chunk = int(query("tmr_sgd_chunk"))
+                elif p.device != dev:
+                    raise RuntimeError("Adam: all parameters must be on one device")
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                keep.append(g)
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                step = float(st["step"].item())
+                bc1 = 1.0 - b1 ** step
+                bc2 = 1.0 - b2 ** step
+                entries.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                st["exp_avg_sq"].data_ptr(), p.numel(), 0, b1, b2, group["eps"],
+                                group["weight_decay"], group["lr"] / bc1, bc2 ** 0.5,
+                                int(group["maximize"]), 0))
+        entries = [e for e in entries if e[4] > 0]
+        if not entries:
+            return loss
+        tab = np.array(entries, dtype=_ADAM_ENTRY)
+        nblk = (tab["n"] + chunk - 1) // chunk
+        tab["block_begin"] = np.concatenate([[0], np.cumsum(nblk)[:-1]])
+        # the step sizes change every step: upload the table each time (pinned, async)
+        host = torch.frombuffer(bytearray(tab.tobytes()), dtype=torch.uint8).pin_memory()
+        self._table_dev = host.to(dev, non_blocking=True)
+        self._keep = keep
+        call("tmr_adam_step_multi", self._table_dev, len(entries), int(nblk.sum()), stream_ptr(dev))
+        return loss
+
+
 def sgd_param_groups(model, lr):
     """Parameter groups of the reference's multi_optim=1 optimizer: `share` and `lstm` at the
     optimizer's default lr (the scripts pass lr/10), every later module at `lr`.
