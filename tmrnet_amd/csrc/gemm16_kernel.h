@@ -43,6 +43,152 @@ __device__ __forceinline__ int mn_swz(int k) {
   return R >= 128 ? ((k & 3) << 2) : (((k >> 1) & 1) << 2);
 }
 
+// Fused BatchNorm-backward epilogue of the DGRAD view through LDS (the tile is written to LDS in
+// row chunks, then each thread owns 8 consecutive columns of a row: 16-B / 32-B vector accesses of
+// y, z (bf16 or fp32), the old dx (beta) and the new dx, instead of one scalar access per
+// accumulator register).  Per row: beta, ReLU mask (z > 0, or y*scale+shift > 0, or none), store,
+// and per-column sums of g and g*(y - mean); the tile's column sums -> bn_part (one partial row per
+// m-tile, as epilogue_batched).
+template <int BM, int BN, int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (&acc)[TM][TN],
+                                                   float* lds, int lds_floats, int m0, int n0) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int LDC = BN + 4;                   // padded fp32 row of the staged tile
+  constexpr int CG = BN / 8;                    // column groups of 8
+  constexpr int RPP = NT / CG;                  // rows processed per pass over the chunk
+  static_assert(NT % CG == 0, "threads per column group");
+  int etid = threadIdx.x;
+  asm volatile("" : "+v"(etid));   // keep the epilogue's index math out of the main loop
+  const int lane = etid & 63, wave = etid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, hh = lane >> 5;
+  const int cg = etid % CG, rsub = etid / CG;
+  const int col = n0 + 8 * cg;
+  const bool okc = col < a.N;                   // N is a multiple of 8 (LDS-DMA engine)
+  // per-column coefficients of this thread's 8 columns
+  float mu[8], bsc[8], bsh[8], cs[8], cq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = okc ? col + e : 0;
+    mu[e] = okc ? a.bn_mean[c] : 0.f;
+    bsc[e] = (okc && a.bn_mask == 2) ? a.bn_sc[c] : 0.f;
+    bsh[e] = (okc && a.bn_mask == 2) ? a.bn_sh[c] : (a.bn_mask == 0 ? 1.f : 0.f);
+    cs[e] = 0.f;
+    cq[e] = 0.f;
+  }
+  const bool has_beta = a.beta != 0.f;
+  const int rchunk = min(BM, (lds_floats / LDC) / (BM / WM) * (BM / WM));   // whole wave rows
+  for (int r0 = 0; r0 < BM; r0 += rchunk) {
+    // (1) the waves whose rows lie in [r0, r0 + rchunk) stage their accumulators
+    __syncthreads();
+    const int wr0 = wm * (BM / WM);
+    if (wr0 >= r0 && wr0 < r0 + rchunk) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = wr0 - r0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            lds[row * LDC + wn * (BN / WN) + 32 * j + l31] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    // (2) rows of the chunk, 8 columns per thread
+    const int nrow = min(rchunk, BM - r0);
+    for (int rr = rsub; rr < nrow; rr += RPP) {
+      const int row = m0 + r0 + rr;
+      const bool ok = okc && row < a.M;
+      long pix = row;
+      if (ok && a.osy != 0) {   // the parity class's output pixel
+        const uint32_t n = fdiv((uint32_t)row, a.dHW);
+        const uint32_t rem = row - n * a.dHW.d;
+        const uint32_t y = fdiv(rem, a.dW);
+        const uint32_t x = rem - y * a.dW.d;
+        pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)x * a.osx + a.oxc;
+      }
+      const long off = pix * a.ldc + col;   // element offset in dx / y / z
+      float yv[8], zv[8], old[8];
+      if (ok) {
+        if (a.bn16) {
+          const uint4 yw = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.bn_y) + off);
+          const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            yv[2 * e] = __uint_as_float(yu[e] << 16);
+            yv[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
+          }
+          if (a.bn_mask == 1) {
+            const uint4 zw = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.bn_z) + off);
+            const uint32_t zu[4] = {zw.x, zw.y, zw.z, zw.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              zv[2 * e] = __uint_as_float(zu[e] << 16);
+              zv[2 * e + 1] = __uint_as_float(zu[e] & 0xffff0000u);
+            }
+          }
+        } else {
+          const float4 y0 = *reinterpret_cast<const float4*>(a.bn_y + off);
+          const float4 y1 = *reinterpret_cast<const float4*>(a.bn_y + off + 4);
+          yv[0] = y0.x; yv[1] = y0.y; yv[2] = y0.z; yv[3] = y0.w;
+          yv[4] = y1.x; yv[5] = y1.y; yv[6] = y1.z; yv[7] = y1.w;
+          if (a.bn_mask == 1) {
+            const float4 z0 = *reinterpret_cast<const float4*>(a.bn_z + off);
+            const float4 z1 = *reinterpret_cast<const float4*>(a.bn_z + off + 4);
+            zv[0] = z0.x; zv[1] = z0.y; zv[2] = z0.z; zv[3] = z0.w;
+            zv[4] = z1.x; zv[5] = z1.y; zv[6] = z1.z; zv[7] = z1.w;
+          }
+        }
+        if (a.bn_mask != 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) zv[e] = 0.f;
+        }
+        if (has_beta) {
+          const float4 c0 = *reinterpret_cast<const float4*>(a.C + off);
+          const float4 c1 = *reinterpret_cast<const float4*>(a.C + off + 4);
+          old[0] = c0.x; old[1] = c0.y; old[2] = c0.z; old[3] = c0.w;
+          old[4] = c1.x; old[5] = c1.y; old[6] = c1.z; old[7] = c1.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = 0.f;
+        }
+        const float4 a0 = *reinterpret_cast<const float4*>(lds + rr * LDC + 8 * cg);
+        const float4 a1 = *reinterpret_cast<const float4*>(lds + rr * LDC + 8 * cg + 4);
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = fmaf(a.beta, old[e], av[e]);
+          const bool keep = zv[e] + fmaf(yv[e], bsc[e], bsh[e]) > 0.f;
+          t = keep ? t : 0.f;
+          v[e] = t;
+          cs[e] += t;
+          cq[e] = fmaf(t, yv[e] - mu[e], cq[e]);
+        }
+        *reinterpret_cast<float4*>(a.C + off) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(a.C + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+  }
+  // (3) column sums over the RPP row slots -> bn_part
+  __syncthreads();
+  float* red = lds;   // [RPP][BN][2]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(rsub * BN + 8 * cg + e) * 2] = cs[e];
+    red[(rsub * BN + 8 * cg + e) * 2 + 1] = cq[e];
+  }
+  __syncthreads();
+  for (int c = etid; c < BN; c += NT) {
+    float t0 = 0.f, t1 = 0.f;
+    for (int q = 0; q < RPP; ++q) {
+      t0 += red[(q * BN + c) * 2];
+      t1 += red[(q * BN + c) * 2 + 1];
+    }
+    if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+  }
+}
+
 template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs a) {
   constexpr int BK = 64;
@@ -365,6 +511,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs 
   }
   __syncthreads();   // LDS reads done (no LDS-DMA in flight) before the epilogue reuses smem
 
+  // the LDS form stages whole wave row-blocks: (BM / WM) padded rows must fit (all configs but
+  // 256x256, which the dgrad tile rules never pick)
+  if constexpr (MODE == MODE_DGRAD && (BN + 4) * (BM / WM) * 4 <= SMEM) {
+    if (a.bn_part != nullptr) {
+      epilogue_lds_bnbwd<BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), SMEM / 4,
+                                                  m0, n0);
+      return;
+    }
+  }
   epilogue_batched<MODE, BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), m0, n0);
 }
 
