@@ -307,6 +307,17 @@ def test_gemm16_views(dev, case):
     assert err < 1e-5, ("fwd", err)
     y32 = ops.conv_fwd(xd.contiguous(), w32, st, pad, math="bf16")
     assert torch.equal(y16, y32)
+    if not xoff:   # bf16 output (TMR_IO_Y_BF16): the rounded accumulators, BN partials of those
+        yb, stb, npb = ops.conv_fwd_bnstats(x16, w16, st, pad, math="bf16", y16=True)
+        assert yb.dtype == torch.bfloat16 and torch.equal(yb, y32.to(torch.bfloat16))
+        c = yb.shape[-1]
+        mean, inv, _, _ = ops.bn_finalize(stb, npb, torch.ones(c, device=dev),
+                                          torch.zeros(c, device=dev), torch.zeros(c, device=dev),
+                                          torch.ones(c, device=dev), 0.1, 1e-5)
+        ye = yb.double().reshape(-1, c)
+        assert torch.allclose(mean.double(), ye.mean(0), rtol=1e-5, atol=1e-6)
+        var_ref = ye.var(0, unbiased=False)
+        assert torch.allclose((1.0 / inv.double() ** 2 - 1e-5), var_ref, rtol=1e-4, atol=1e-6)
     dy = _r(torch.randn(y16.shape, generator=g))
     dy16 = dy.to(dev).to(torch.bfloat16)
     dx = ops.conv_dgrad(dy16, ops.weight_to_crsk(wd), (h, w), st, pad, math="bf16", wt=True)
