@@ -190,7 +190,7 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 ? 4 : 2)) void gemm16_kernel(const GemmArgs a) {
   constexpr int BK = 64;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -525,7 +525,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm16_kernel(const GemmArgs 
 
 // ---------------------------------------------------------------- launch selection
 struct Cfg16 { int bm, bn; };
-constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64, 256}, {64, 64}};
+constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64, 256}, {64, 64},
+                              {256, 256}};   // 6: 256x256 as 16 waves (4x4, 64x64 per wave)
 
 // Eligibility: bf16 math, every operand bf16 in HBM (sab 3; DGRAD with the transposed weights),
 // no operand prologue, 16-B pieces of 8 channels (channels per tap, row strides multiples of 8).
@@ -545,10 +546,11 @@ inline long cfg16_tiles(long M, long N, int c) {
 }
 
 // Tile choice per view, from scripts/convbench.py --io16 --stats --bnbwd with each config forced
-// over the 23 ResNet-50 conv shapes x 3 views (profiles/r2/convbench16_cfgs/): 256x256 (8 waves,
-// one workgroup per CU) only pays for the long-reduction forwards and the largest wgrads; the
-// dgrads, whose fused BatchNorm-backward epilogue moves 12-16 B per output element, want the
-// occupancy of 128x128 / 256x64 tiles.
+// over the 23 ResNet-50 conv shapes x 3 views (profiles/r2/convbench16_cfgs/, cb16c/): 256x256
+// pays for the forwards and the wgrads with 256-512 output channels, as 16 waves (four per SIMD:
+// 5-20% over 8 waves, whose two waves per SIMD stall on the same barrier); the dgrads, whose
+// fused BatchNorm-backward epilogue moves 12-16 B per output element, want the occupancy of
+// 128x128 / 256x64 tiles.
 inline int pick_cfg16(long M, long N, long K, int mode) {
   static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
   if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
@@ -557,13 +559,12 @@ inline int pick_cfg16(long M, long N, long K, int mode) {
   if (mode == MODE_WGRAD) {
     if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
     else if (N <= 64) cfg = 3;
-    else if (M >= 256 && M <= 512 && N >= 2048) cfg = 0;
-    else if (M == 256 && N == 512) cfg = 0;
+    else if (M >= 256 && M <= 512 && N >= 256) cfg = 6;
     else cfg = 2;
   } else if (N <= 64) {
     cfg = M >= 256 ? 3 : 5;
   } else if (mode == MODE_FWD && N >= 256 && M >= 256) {
-    cfg = 0;
+    cfg = 6;   // 256x256 as 16 waves: four waves per SIMD hide the barrier / load waits
   } else {
     cfg = 2;
   }
@@ -618,6 +619,7 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
     case 2: return launch16_cfg<MODE, 128, 128, 2, 2>(a, tapv, grid, st);
     case 3: return launch16_cfg<MODE, 256, 64, 4, 1>(a, tapv, grid, st);
     case 4: return launch16_cfg<MODE, 64, 256, 1, 4>(a, tapv, grid, st);
+    case 6: return launch16_cfg<MODE, 256, 256, 4, 4>(a, tapv, grid, st);
     default: return launch16_cfg<MODE, 64, 64, 2, 2>(a, tapv, grid, st);
   }
 }
