@@ -190,7 +190,8 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1>
-__global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 ? 4 : 2)) void gemm16_kernel(const GemmArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && BM * BN <= 128 * 128) ? 4 : 2))
+void gemm16_kernel(const GemmArgs a) {
   constexpr int BK = 64;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -526,7 +527,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 ? 4 : 2)) void gemm16_
 // ---------------------------------------------------------------- launch selection
 struct Cfg16 { int bm, bn; };
 constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64, 256}, {64, 64},
-                              {256, 256}};   // 6: 256x256 as 16 waves (4x4, 64x64 per wave)
+                              {256, 256},    // 6: 256x256 as 16 waves (4x4, 64x64 per wave)
+                              {128, 128}};   // 7: 128x128 as 8 waves (4x2, 32x64 per wave)
 
 // Eligibility: bf16 math, every operand bf16 in HBM (sab 3; DGRAD with the transposed weights),
 // no operand prologue, 16-B pieces of 8 channels (channels per tap, row strides multiples of 8).
@@ -554,11 +556,13 @@ inline long cfg16_tiles(long M, long N, int c) {
 inline int pick_cfg16(long M, long N, long K, int mode) {
   static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
   if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
-  (void)K;
   int cfg;
   if (mode == MODE_WGRAD) {
     if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
     else if (N <= 64) cfg = 3;
+    // short reductions (layer3/4 spatial): 4x the tiles of 256x256 at the same occupancy, so
+    // fewer split-K slabs to write and reduce
+    else if (M >= 256 && N >= 256 && K <= 131072) cfg = 7;
     else if (M >= 256 && M <= 512 && N >= 256) cfg = 6;
     else cfg = 2;
   } else if (N <= 64) {
@@ -620,6 +624,7 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
     case 3: return launch16_cfg<MODE, 256, 64, 4, 1>(a, tapv, grid, st);
     case 4: return launch16_cfg<MODE, 64, 256, 1, 4>(a, tapv, grid, st);
     case 6: return launch16_cfg<MODE, 256, 256, 4, 4>(a, tapv, grid, st);
+    case 7: return launch16_cfg<MODE, 128, 128, 4, 2>(a, tapv, grid, st);
     default: return launch16_cfg<MODE, 64, 64, 2, 2>(a, tapv, grid, st);
   }
 }
