@@ -213,22 +213,15 @@ void gemm16_kernel(const GemmArgs a) {
   const int l31 = lane & 31, hh = lane >> 5;
 
   // XCD-aware tile order (gemm_kernel's)
-  const int nmt = (a.M + BM - 1) / BM;
   const int nnt = (a.N + BN - 1) / BN;
-  const int nwg = nmt * nnt;
-  int bid = blockIdx.x;
-  {
-    int xcd = bid & 7, loc = bid >> 3;
-    int q = nwg >> 3, r = nwg & 7;
-    int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-    bid = (nwg >= 8) ? wg : bid;
-  }
+  int bid, split;
+  xcd_work(bid, split);   // gemm_kernel.h
   const int m0 = (bid / nnt) * BM;
   const int n0 = (bid % nnt) * BN;
 
   int kbeg = 0, kend = a.K;
   if (MODE == MODE_WGRAD) {
-    kbeg = blockIdx.y * a.kchunk;
+    kbeg = split * a.kchunk;
     kend = min(a.K, kbeg + a.kchunk);
   }
   const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
@@ -521,7 +514,8 @@ void gemm16_kernel(const GemmArgs a) {
       return;
     }
   }
-  epilogue_batched<MODE, BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), m0, n0);
+  epilogue_batched<MODE, BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), m0, n0,
+                                                 split);
 }
 
 // ---------------------------------------------------------------- launch selection
