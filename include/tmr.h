@@ -72,6 +72,10 @@ typedef struct tmr_conv_desc {
 #define TMR_IO_BN_BF16 32  /* tmr_conv2d_dgrad_bnbwd: the y / z of the fused BN backward are bf16 */
 #define TMR_IO_WT_BF16 8   /* dgrad only: w is the transposed bf16 weight copy Wt[Cin][R][S][Cout]
                               (tmr_weight_oihw_to_crsk_x), read K-contiguous by the LDS-DMA engine */
+#define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the one io bit fp32 math takes): w is the
+                              transposed fp32 copy Wt[Cin][R][S][Cout] (tmr_weight_oihw_to_crsk_x,
+                              out_bf16 0); the fp32 LDS-DMA engine reads it K-contiguous.  dy, dx
+                              16-B aligned, Cin a multiple of 4 */
 
 /* y[n,ho,wo,k] = beta*y + sum x * w_krsc (+ bias[k]) */
 int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,

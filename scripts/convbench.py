@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--bnbwd", action="store_true",
                     help="dgrad with the fused BN-backward epilogue (ReLU mask from z, per-tile "
                          "partials), as the train step runs every dgrad but the stem's")
+    ap.add_argument("--wt32", action="store_true",
+                    help="fp32 dgrad on the LDS-DMA engine (transposed fp32 weights, "
+                         "TMR_IO_WT_F32), as the fp32 train step")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
@@ -79,6 +82,8 @@ def main():
                 wdg, wt = ops.weight_to_crsk(wo), True
             else:
                 wdg = wk
+        elif args.wt32 and cin != 3:
+            wdg, wt = ops.weight_to_crsk(torch.randn(cout, cs, r, r, device=dev), bf16=False), True
         xpro = dpro = None
         if args.pro and cin != 3:
             xpro = (torch.rand(cs, device=dev) + 0.5, torch.randn(cs, device=dev) * 0.1)

@@ -56,6 +56,38 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     assert rel_err(dw, wr.grad) < 2e-6
 
 
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] != 3])
+def test_conv_dgrad_fp32_transposed_weights(dev, case):
+    """fp32 dgrad on the LDS-DMA engine (transposed fp32 weights, TMR_IO_WT_F32) against float64
+    torch, and against the register-staged engine on the KRSC weights (same tolerance)."""
+    n, h, w, cin, cout, r, st, pad = case
+    g = torch.Generator().manual_seed(hash(case) % 997)
+    wt = torch.randn(cout, cin, r, r, generator=g, dtype=torch.float64) / np.sqrt(cout * r * r)
+    ho, wo = (h + 2 * pad - r) // st + 1, (w + 2 * pad - r) // st + 1
+    dy = torch.randn(n, cout, ho, wo, generator=g, dtype=torch.float64)
+    ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt, dy, stride=st, padding=pad)
+    wd = wt.float().to(dev).contiguous()
+    wc = ops.weight_to_crsk(wd, bf16=False)
+    assert wc.dtype == torch.float32 and wc.shape == (cin, r, r, cout)
+    dyd = dy.float().permute(0, 2, 3, 1).contiguous().to(dev)
+    dx = ops.conv_dgrad(dyd, wc, (h, w), st, pad, wt=True)
+    assert rel_err(dx.permute(0, 3, 1, 2), ref) < 2e-6
+    dxk = ops.conv_dgrad(dyd, ops.weight_to_krsc(wd), (h, w), st, pad)
+    assert rel_err(dx, dxk) < 2e-6
+    dx2 = ops.conv_dgrad(dyd, wc, (h, w), st, pad, out=dx.clone(), beta=1.0, wt=True)
+    assert rel_err(dx2, 2 * dx) < 1e-6
+
+
+def test_conv_fp32_transposed_weights_errors(dev):
+    """fp32 transposed weights with a bf16 operand, or with bf16 math, are refused."""
+    wc = ops.weight_to_crsk(torch.randn(64, 64, 1, 1, device=dev), bf16=False)
+    dy = torch.randn(1, 4, 4, 64, device=dev)
+    with pytest.raises(RuntimeError):
+        ops.conv_dgrad(dy.to(torch.bfloat16), wc, (4, 4), 1, 0, wt=True, math="bf16")
+    with pytest.raises(RuntimeError):
+        ops.conv_dgrad(dy, wc, (4, 4), 1, 0, wt=True, math="bf16")
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 2048, 2048), (7, 512, 64), (64, 7, 512), (33, 65, 17),
                                    (640, 512, 1024)])
 def test_gemms(dev, M, N, K):
@@ -410,16 +442,18 @@ def test_adam_optimizer_multi_tensor_matches_torch(dev):
     (2, 14, 14, 256, 512, 1, 2, 0, 1, 1.0),    # strided 1x1 downsample: tap-less classes
     (2, 9, 9, 64, 64, 3, 1, 1, 0, 0.0),        # no ReLU
 ])
-def test_conv_dgrad_fused_bn_backward(dev, case):
+@pytest.mark.parametrize("wtr", [False, True])
+def test_conv_dgrad_fused_bn_backward(dev, case, wtr):
     """conv_dgrad_bnbwd + bn_bwd_parts == conv_dgrad followed by bn_bwd (the separate passes):
-    the masked dx bit-exactly, dy / dgamma / dbeta to fp32 summation-order tolerance."""
+    the masked dx bit-exactly, dy / dgamma / dbeta to fp32 summation-order tolerance.  wtr: both
+    on the fp32 LDS-DMA engine (transposed fp32 weights; its LDS-staged fused epilogue)."""
     n, h, w, cin, cout, r, st, pad, mask, beta = case
     g = torch.Generator().manual_seed(11)
     ho = (h + 2 * pad - r) // st + 1
     wo = (w + 2 * pad - r) // st + 1
     dy = torch.randn(n, ho, wo, cout, generator=g).to(dev)
     wt = (torch.randn(cout, cin, r, r, generator=g) / np.sqrt(cout * r * r)).to(dev)
-    wk = ops.weight_to_krsc(wt)
+    wk = ops.weight_to_crsk(wt, bf16=False) if wtr else ops.weight_to_krsc(wt)
     y = torch.randn(n, h, w, cin, generator=g).to(dev)
     mean = y.view(-1, cin).mean(0)
     inv = 1.0 / (y.view(-1, cin).var(0, unbiased=False) + 1e-5).sqrt()
@@ -430,12 +464,13 @@ def test_conv_dgrad_fused_bn_backward(dev, case):
     z = torch.relu(y * scale + shift + res) if mask == 1 else None
     old = torch.randn(n, h, w, cin, generator=g).to(dev)
     # separate passes
-    dz = ops.conv_dgrad(dy, wk, (h, w), st, pad, out=old.clone(), beta=beta)
+    dz = ops.conv_dgrad(dy, wk, (h, w), st, pad, out=old.clone(), beta=beta, wt=wtr)
     dy_ref, dres_ref, dg_ref, db_ref = ops.bn_bwd(dz, y, z, mean, inv, gamma, mask != 0,
                                                   want_dres=True, scale=scale, shift=shift)
     # fused
     dzf, parts, npart = ops.conv_dgrad_bnbwd(dy, wk, (h, w), st, pad, y, mean, mask, z=z,
-                                              scale=scale, shift=shift, out=old.clone(), beta=beta)
+                                              scale=scale, shift=shift, out=old.clone(), beta=beta,
+                                              wt=wtr)
     dyf, dgf, dbf = ops.bn_bwd_parts(dzf, y, parts, npart, mean, inv, gamma)
     torch.cuda.synchronize()
     assert torch.equal(dzf, dres_ref)          # the masked BN-output gradient
@@ -443,22 +478,24 @@ def test_conv_dgrad_fused_bn_backward(dev, case):
     assert rel_err(dgf, dg_ref) < 1e-5 and rel_err(dbf, db_ref) < 1e-5
 
 
-def test_conv_dgrad_fused_bn_backward_frame_chunks(dev):
+@pytest.mark.parametrize("wtr", [False, True])
+def test_conv_dgrad_fused_bn_backward_frame_chunks(dev, wtr):
     """Partials stay in launch order across frame chunks (max_frames) and parity classes."""
     g = torch.Generator().manual_seed(12)
     n, h, w, cin, cout = 5, 14, 14, 128, 128
     dy = torch.randn(n, 7, 7, cout, generator=g).to(dev)
-    wk = ops.weight_to_krsc((torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(dev))
+    w0 = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(dev)
+    wk = ops.weight_to_crsk(w0, bf16=False) if wtr else ops.weight_to_krsc(w0)
     y = torch.randn(n, h, w, cin, generator=g).to(dev)
     mean = y.view(-1, cin).mean(0)
     inv = 1.0 / (y.view(-1, cin).var(0, unbiased=False) + 1e-5).sqrt()
     gamma = torch.ones(cin, device=dev)
     sc, sh = gamma * inv, -mean * inv
-    a = ops.conv_dgrad_bnbwd(dy, wk, (h, w), 2, 1, y, mean, 2, scale=sc, shift=sh)
+    a = ops.conv_dgrad_bnbwd(dy, wk, (h, w), 2, 1, y, mean, 2, scale=sc, shift=sh, wt=wtr)
     old = ops.MAX_FRAMES
     try:
         ops.MAX_FRAMES = 2
-        b = ops.conv_dgrad_bnbwd(dy, wk, (h, w), 2, 1, y, mean, 2, scale=sc, shift=sh)
+        b = ops.conv_dgrad_bnbwd(dy, wk, (h, w), 2, 1, y, mean, 2, scale=sc, shift=sh, wt=wtr)
     finally:
         ops.MAX_FRAMES = old
     ya = ops.bn_bwd_parts(a[0], y, a[1], a[2], mean, inv, gamma)[0]
@@ -514,7 +551,10 @@ def test_bn_fold_bit_identical(dev):
     """Train step with the BatchNorm folded into the conv loaders (tmr_conv_prologue: BN+ReLU of
     units 1-2 on the X operand, the BN backward on every dY operand) against the explicit passes
     (tmr_bn_apply / tmr_bn_bwd_parts / tmr_bn_bwd): same operand values by construction, same
-    GEMM arithmetic -> logits, every gradient and the running statistics bit-identical."""
+    GEMM arithmetic -> logits, every gradient and the running statistics bit-identical.  Both
+    on the register-staged engine (the LDS-DMA engine has no prologues; TMR_GEMM32=0 keeps the
+    explicit side's fp32 convs off it too, read per launch)."""
+    import os
     import tmrnet_amd
     from tmrnet_amd import trunk
     B, T, L = 2, 5, 7
@@ -525,6 +565,9 @@ def test_bn_fold_bit_identical(dev):
     labels = torch.randint(0, 7, (B,), generator=g).to(dev)
     res = {}
     saved = trunk.FOLD_BN
+    saved_dma, saved_env = trunk.DMA32, os.environ.get("TMR_GEMM32")
+    trunk.DMA32 = False
+    os.environ["TMR_GEMM32"] = "0"
     try:
         for fold in (True, False):
             trunk.FOLD_BN = fold
@@ -540,6 +583,11 @@ def test_bn_fold_bit_identical(dev):
                          {n: b.clone() for n, b in m.named_buffers()})
     finally:
         trunk.FOLD_BN = saved
+        trunk.DMA32 = saved_dma
+        if saved_env is None:
+            os.environ.pop("TMR_GEMM32", None)
+        else:
+            os.environ["TMR_GEMM32"] = saved_env
     assert torch.equal(res[True][0], res[False][0])
     for n in res[True][1]:
         assert torch.equal(res[True][1][n], res[False][1][n]), n

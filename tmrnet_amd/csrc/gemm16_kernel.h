@@ -25,6 +25,7 @@
 // path's, so FWD / DGRAD results are bit-identical to it.
 #pragma once
 #include "gemm_kernel.h"
+#include <type_traits>
 
 namespace tmrg {
 
@@ -189,19 +190,30 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1>
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// F32: the fp32 form of the engine (FWD / DGRAD views, every operand fp32 in HBM, GemmArgs::dma32).
+// The LDS images are byte-identical -- [rows][128 B], 16-B chunks of 4 floats instead of 8 bf16,
+// the same swizzle and LDS-DMA pieces -- so BK = 32 elements; each ds_read_b128 fragment holds 4
+// consecutive k of one row, lane half hh the chunk 2s + hh, and feeds 4 v_mfma_f32_32x32x2_f32
+// (MFMA t reduces k = 8s + t from half 0 and 8s + 4 + t from half 1: the same k for A and B).
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && BM * BN <= 128 * 128) ? 4 : 2))
 void gemm16_kernel(const GemmArgs a) {
-  constexpr int BK = 64;
+  constexpr uint32_t ES = F32 ? 4u : 2u;   // element bytes
+  constexpr int EPC = 16 / ES;             // elements per 16-B chunk
+  constexpr int BK = 128 / ES;             // elements per k-tile (128-B image rows)
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr bool MN = (MODE == MODE_WGRAD);   // both operands reduction-major
-  constexpr int ABYTES = BM * BK * 2, BBYTES = BN * BK * 2, STAGE = ABYTES + BBYTES;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;   // 128-B rows
   constexpr int NIA = ABYTES / (1024 * NW), NIB = BBYTES / (1024 * NW);   // pieces / wave / tile
   static_assert(NIA >= 1 && NIB >= 1 && NIA * 1024 * NW == ABYTES && NIB * 1024 * NW == BBYTES,
                 "LDS-DMA pieces per wave");
   static_assert(TM >= 1 && TN >= 1, "wave tile");
   static_assert(!MN || (BM >= 64 && BN >= 64), "reduction-major images need >= 64 columns");
+  static_assert(!(MN && F32), "fp32 LDS-DMA engine: FWD / DGRAD views only");
+  using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
   constexpr int EPI = WM * BN * 2 * 4;
   constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
@@ -257,8 +269,8 @@ void gemm16_kernel(const GemmArgs a) {
       const uint32_t x = rem - y * a.dW.d;
       ay[q] = (int)y * a.sy;
       ax[q] = (int)x * a.sx;
-      apix[q] = (uint32_t)(((int)n * a.Hs + ay[q]) * a.Ws + ax[q]) * (uint32_t)a.lds * 2u;
-      ach[q] = 8 * kc_chunk(q);
+      apix[q] = (uint32_t)(((int)n * a.Hs + ay[q]) * a.Ws + ax[q]) * (uint32_t)a.lds * ES;
+      ach[q] = EPC * kc_chunk(q);
     }
   } else {
 #pragma unroll
@@ -284,8 +296,8 @@ void gemm16_kernel(const GemmArgs a) {
       const int j = n0 + kc_row(q);
       bok[q] = j < a.N;
       const uint32_t jj = bok[q] ? (uint32_t)j : 0u;
-      brow[q] = jj * (uint32_t)(MODE == MODE_DGRAD ? a.ldbt : a.ldb) * 2u;
-      bch[q] = 8 * kc_chunk(q);
+      brow[q] = jj * (uint32_t)(MODE == MODE_DGRAD ? a.ldbt : a.ldb) * ES;
+      bch[q] = EPC * kc_chunk(q);
     }
   } else {
 #pragma unroll
@@ -337,7 +349,7 @@ void gemm16_kernel(const GemmArgs a) {
         const int ys = ay[q] + dy, xs = ax[q] + dx;
         const bool ok = aok[q] && k < kend && tap < a.ntaps && (unsigned)ys < (unsigned)a.Hs &&
                         (unsigned)xs < (unsigned)a.Ws;
-        const uint32_t off = apix[q] + (uint32_t)(((dy * a.Ws + dx) * a.lds + c) * 2);
+        const uint32_t off = apix[q] + (uint32_t)((dy * a.Ws + dx) * a.lds + c) * ES;
         glds16(rA, As + 1024 * (wave + NW * q), ok ? off : OOB);
       }
       if constexpr (MODE == MODE_FWD) {
@@ -346,7 +358,7 @@ void gemm16_kernel(const GemmArgs a) {
         for (int q = 0; q < NIB; ++q) {
           const int k = kb + bch[q];
           const bool ok = bok[q] && k < kend;
-          glds16(rB, Bs + 1024 * (wave + NW * q), ok ? brow[q] + (uint32_t)k * 2u : OOB);
+          glds16(rB, Bs + 1024 * (wave + NW * q), ok ? brow[q] + (uint32_t)k * ES : OOB);
         }
       } else {
         // B[j=ci][k=(tap,co)] = Wt[ci][rs(tap)][co]
@@ -372,7 +384,7 @@ void gemm16_kernel(const GemmArgs a) {
             rs = (a.wr0 + a.wst * ri) * a.wS + (a.ws0 + a.wst * si);
           }
           const bool ok = bok[q] && k < kend && tap < a.ntaps;
-          const uint32_t off = brow[q] + (uint32_t)((rs << a.log2C) + co) * 2u;
+          const uint32_t off = brow[q] + (uint32_t)((rs << a.log2C) + co) * ES;
           glds16(rB, Bs + 1024 * (wave + NW * q), ok ? off : OOB);
         }
       }
@@ -433,38 +445,52 @@ void gemm16_kernel(const GemmArgs a) {
   const int arow0 = wm * (BM / WM) + l31;
   const int brow0 = wn * (BN / WN) + l31;
   // the operand fragments of k-step s of LDS buffer buf
-  auto frags = [&](int buf, int s, bf16x8 (&av)[TM], bf16x8 (&bv)[TN]) {
+  auto frags = [&](int buf, int s, Frag (&av)[TM], Frag (&bv)[TN]) {
     const unsigned char* As = smem + buf * STAGE;
     const unsigned char* Bs = As + ABYTES;
     const int ch = (2 * s + hh) ^ kx;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if constexpr (!MN)
-        av[i] = *reinterpret_cast<const bf16x8*>(As + (arow0 + 32 * i) * 128 + (ch << 4));
-      else
+        av[i] = *reinterpret_cast<const Frag*>(As + (arow0 + 32 * i) * 128 + (ch << 4));
+      else if constexpr (!F32)
         av[i] = tr_frag(As, BM, swzA, wm * (BM / WM) + 32 * i, s);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       if constexpr (!MN)
-        bv[j] = *reinterpret_cast<const bf16x8*>(Bs + (brow0 + 32 * j) * 128 + (ch << 4));
-      else
+        bv[j] = *reinterpret_cast<const Frag*>(Bs + (brow0 + 32 * j) * 128 + (ch << 4));
+      else if constexpr (!F32)
         bv[j] = tr_frag(Bs, BN, swzB, wn * (BN / WN) + 32 * j, s);
     }
   };
-  auto mfmas = [&](const bf16x8 (&av)[TM], const bf16x8 (&bv)[TN]) {
+  auto mfmas = [&](const Frag (&av)[TM], const Frag (&bv)[TN]) {
     if (PIPE) __builtin_amdgcn_s_setprio(1);
+    if constexpr (F32) {
+      // t outermost: TM * TN independent accumulator chains between dependent MFMAs
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][t], bv[j][t], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
     if (PIPE) __builtin_amdgcn_s_setprio(0);
   };
+  // k-steps per k-tile: two 16-B chunks (lane halves) per step -> 16 bf16 or 8 floats
+  constexpr int KSTEPS = BK / (2 * EPC);
+  static_assert(KSTEPS == 4, "four k-steps per k-tile (the PIPE 1 schedule)");
   auto compute = [&](int buf) {
 #pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 av[TM], bv[TN];
+    for (int s = 0; s < KSTEPS; ++s) {
+      Frag av[TM], bv[TN];
       frags(buf, s, av, bv);
       mfmas(av, bv);
     }
@@ -491,7 +517,7 @@ void gemm16_kernel(const GemmArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       const int buf = kt & 1;
-      bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+      Frag a0[TM], b0[TN], a1[TM], b1[TN];
       frags(buf, 0, a0, b0);
       if (kt + 1 < ntiles) stage(kt + 1, buf ^ 1);
       frags(buf, 1, a1, b1);
@@ -526,8 +552,22 @@ constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64,
 
 // Eligibility: bf16 math, every operand bf16 in HBM (sab 3; DGRAD with the transposed weights),
 // no operand prologue, 16-B pieces of 8 channels (channels per tap, row strides multiples of 8).
+// fp32 form (GemmArgs::dma32, set by the conv entry points): FWD with every operand fp32 and
+// 16-B aligned, 4-channel pieces; DGRAD whenever the weights come transposed (wt: the engine is
+// the only reader of that layout, so eligibility is checked again by launch_gemm16_t).
+inline bool use32(const GemmArgs& a, int mode) {
+  // A/B switch for the forward view, read per launch (tests flip it in-process)
+  const bool on = env_int("TMR_GEMM32", 1) != 0;
+  if (a.prec != TMR_MATH_F32 || a.sab || a.pro || mode == MODE_WGRAD) return false;
+  if (mode == MODE_DGRAD) return a.wt != 0;
+  if (!on || !a.dma32) return false;
+  if ((((uintptr_t)a.A | (uintptr_t)a.B) & 15) != 0) return false;
+  return a.lds % 4 == 0 && a.ldb % 4 == 0 && a.log2C >= 2 && (a.ntaps != 1 || a.K % 4 == 0);
+}
+
 inline bool use16(const GemmArgs& a, int mode) {
   static const bool on = env_int("TMR_GEMM16", 1) != 0;   // A/B switch (experiments)
+  if (a.prec == TMR_MATH_F32) return use32(a, mode);
   if (!on || a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
   if (mode == MODE_DGRAD && !a.wt) return false;
   if (a.lds % 8) return false;
@@ -592,6 +632,16 @@ inline long gemm_tiles(const GemmArgs& a, int mode) {
 template <int MODE, int BM, int BN, int WM, int WN>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
+  if constexpr (MODE != MODE_WGRAD) {
+    if (a.prec == TMR_MATH_F32) {
+      if (tapv)
+        hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, 1>), grid, blk, 0, st, a);
+      else
+        hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, 1>), grid, blk, 0, st, a);
+      TMR_CHECK_LAUNCH("gemm16_kernel (fp32)");
+      return 0;
+    }
+  }
   if (tapv)
     hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1>), grid, blk, 0, st, a);
   else
@@ -603,13 +653,21 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
 template <int MODE>
 int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   TMR_CHECK_ARG(((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0,
-                "gemm (bf16 LDS-DMA path): operands must be 16-B aligned");
+                "gemm (LDS-DMA path): operands must be 16-B aligned");
+  const bool f32 = a.prec == TMR_MATH_F32;
+  TMR_CHECK_ARG(!f32 || (MODE != MODE_WGRAD && a.lds % 4 == 0 && a.log2C >= 2 &&
+                         (MODE == MODE_DGRAD ? (a.ldbt % 4 == 0 && a.N % 8 == 0 && a.ldc % 4 == 0 &&
+                                                ((uintptr_t)a.C & 15) == 0)
+                                             : a.ldb % 4 == 0)),
+                "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
   const int cfg = pick_cfg16(a.M, a.N, a.K, MODE);
   const Cfg16 c = kCfgs16[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
-  // a k-tile of 64 spans several taps when the channels per tap are fewer (or not a multiple)
-  const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % 64) != 0;
+  // a k-tile (64 bf16 / 32 fp32) spans several taps when the channels per tap are fewer (or not
+  // a multiple)
+  const int bk = f32 ? 32 : 64;
+  const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
   switch (cfg) {
     case 0: return launch16_cfg<MODE, 256, 256, 2, 4>(a, tapv, grid, st);

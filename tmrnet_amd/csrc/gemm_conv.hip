@@ -177,6 +177,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.sab = ((d->io & TMR_IO_X_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldc, d->k));
   a.c16 = (d->io & TMR_IO_Y_BF16) ? 1 : 0;
+  a.dma32 = d->math == TMR_MATH_F32;
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
 }
@@ -316,6 +317,11 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
   TMR_CHECK_ARG(d->c % 4 == 0, "tmr_conv2d_dgrad: input channels %d must be a multiple of 4", d->c);
   TMR_CHECK_ARG(!(d->io & TMR_IO_WT_BF16) || !(d->io & TMR_IO_W_BF16),
                 "tmr_conv2d_dgrad: TMR_IO_WT_BF16 and TMR_IO_W_BF16 are exclusive weight layouts");
+  TMR_CHECK_ARG(!(d->io & TMR_IO_WT_F32) || (d->math == TMR_MATH_F32 && d->io == TMR_IO_WT_F32),
+                "tmr_conv2d_dgrad: TMR_IO_WT_F32 (fp32 transposed weights) needs TMR_MATH_F32 and "
+                "no bf16-stored operand");
+  TMR_CHECK_ARG(d->io == 0 || d->io == TMR_IO_WT_F32 || d->math == TMR_MATH_BF16,
+                "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int st = d->stride;
   // one launch per stride-parity class (ph,pw): rows h = st*y + ph
   for (int ph = 0; ph < st; ++ph) {
@@ -346,7 +352,7 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
       a.prec = d->math;
       a.Bbytes = clamp_bytes_e((long)d->k * d->r * d->s * d->c, esz_w(d));
       a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & (TMR_IO_W_BF16 | TMR_IO_WT_BF16)) ? 2 : 0);
-      if (d->io & TMR_IO_WT_BF16) {   // w = Wt[ci][r][s][co] (bf16)
+      if (d->io & (TMR_IO_WT_BF16 | TMR_IO_WT_F32)) {   // w = Wt[ci][r][s][co] (bf16 / fp32)
         a.wt = 1;
         a.ldbt = d->r * d->s * d->k;
       }

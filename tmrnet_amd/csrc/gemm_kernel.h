@@ -113,6 +113,9 @@ struct GemmArgs {
   // and the BN statistics of the epilogue are those of the rounded values; bn16 -- the y / z read
   // by the fused BN-backward epilogue of DGRAD are bf16
   int c16, bn16;
+  // fp32 conv views eligible for the LDS-DMA engine (gemm16_kernel.h use32; set by the conv
+  // entry points, never by the plain GEMMs)
+  int dma32;
 };
 
 __device__ __forceinline__ float bf16_rne(float v) { return (float)(__bf16)v; }
@@ -1366,8 +1369,8 @@ int launch_gemm_t(const GemmArgs& a, bool al, int splits, hipStream_t st) {
                 "gemm: dY-operand prologue needs y and coefficients (dgrad or wgrad view)");
   TMR_CHECK_ARG(uniform || (al && MODE == MODE_FWD),
                 "gemm: per-element taps need aligned channels and the forward view");
-  TMR_CHECK_ARG(!a.wt, "gemm: transposed bf16 weights (TMR_IO_WT_BF16) need the bf16 LDS-DMA "
-                "path: bf16 dy, 8-channel multiples, 16-B aligned operands");
+  TMR_CHECK_ARG(!a.wt, "gemm: transposed weights (TMR_IO_WT_BF16 / TMR_IO_WT_F32) need the LDS-DMA "
+                "path: bf16 dy with 8-channel multiples, or fp32 dy, 16-B aligned operands");
   const int cfg = pick_cfg(a.M, a.N, a.K, MODE);
   const TileCfg c = kCfgs[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);

@@ -72,18 +72,24 @@ MAX_FRAMES = 0
 
 IO_X, IO_W, IO_DY, IO_WT = 1, 2, 4, 8   # tmr_conv_desc.io: bf16-stored x / KRSC w / dy / CRSK w
 IO_Y, IO_BN = 16, 32    # bf16 conv output y (forward) / bf16 y, z of the fused BN backward (dgrad)
+IO_WT32 = 64            # dgrad, fp32 math: w is the transposed fp32 copy (fp32 LDS-DMA engine)
 BF16 = torch.bfloat16
 
 
 def _io(x=None, w=None, dy=None, wt=False):
     """tmr_conv_desc.io from the operands' dtypes (bf16 storage of conv-operand-only tensors);
-    wt: w is the transposed [Cin][R][S][Cout] bf16 copy (dgrad view, weight_to_crsk)."""
+    wt: w is the transposed [Cin][R][S][Cout] copy (dgrad view, weight_to_crsk): bf16 with bf16
+    math (TMR_IO_WT_BF16), fp32 with fp32 operands (TMR_IO_WT_F32)."""
+    if wt and w.dtype == f32:
+        if (dy is not None and dy.dtype != f32) or (x is not None and x.dtype != f32):
+            raise RuntimeError("fp32 transposed (CRSK) weights need fp32 operands")
+        return IO_WT32
     io = 0
     for t, bit in ((x, IO_X), (w, IO_WT if wt else IO_W), (dy, IO_DY)):
         if t is not None and t.dtype == torch.bfloat16:
             io |= bit
     if wt and not io & IO_WT:
-        raise RuntimeError("transposed (CRSK) weights must be bf16")
+        raise RuntimeError("transposed (CRSK) weights must be bf16 or fp32")
     return io
 
 
@@ -104,8 +110,10 @@ def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math
     pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
     wo = (w + 2 * pad_w - s) // stride + 1
-    if io and math != "bf16":
+    if io and io != IO_WT32 and math != "bf16":
         raise RuntimeError("bf16-stored conv operands need math='bf16'")
+    if io & IO_WT32 and math != "fp32":
+        raise RuntimeError("fp32 transposed weights (TMR_IO_WT_F32) need math='fp32'")
     return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
                     MAX_FRAMES, io)
 
@@ -218,8 +226,8 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
                dpro=None, wt=False):
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices).
     dpro = (y, coef): dy is the masked BN-output gradient g, read as the BN backward
-    A*g + B*y + C (tmr_bn_bwd_coefs).  wt: w_krsc is the transposed bf16 copy (C,R,S,K)
-    (weight_to_crsk; the bf16 LDS-DMA engine, with bf16 dy)."""
+    A*g + B*y + C (tmr_bn_bwd_coefs).  wt: w_krsc is the transposed copy (C,R,S,K)
+    (weight_to_crsk; the LDS-DMA engine: bf16 with bf16 dy, or fp32 with fp32 math)."""
     _req_op(w_krsc, "w")
     n, ho, wo, k = dy.shape
     k2, r, s, c = _dgrad_w(w_krsc, wt)
@@ -441,8 +449,8 @@ def weight_to_krsc(w, cpad=None, bf16=False):
 
 
 def weight_to_crsk(w, bf16=True):
-    """OIHW fp32 -> the transposed dgrad operand (Cin, R, S, Cout), bf16 (RNE): the weights of
-    the bf16 LDS-DMA engine's dgrad view (tmr_conv_desc.io TMR_IO_WT_BF16)."""
+    """OIHW fp32 -> the transposed dgrad operand (Cin, R, S, Cout): the weights of the LDS-DMA
+    engine's dgrad view, bf16 (RNE; TMR_IO_WT_BF16) or fp32 (bf16=False; TMR_IO_WT_F32)."""
     k, c, r, s = w.shape
     out = _empty((c, r, s, k), w, dtype=torch.bfloat16 if bf16 else f32)
     call("tmr_weight_oihw_to_crsk_x", _req(w, "w"), out, k, c, r, s, int(bf16), stream_ptr())

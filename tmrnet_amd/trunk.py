@@ -118,6 +118,17 @@ FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
 ACT16 = os.environ.get("TMR_BF16_ACT", "1") != "0"
 
 
+# fp32 math: the dgrad view runs on the fp32 form of the LDS-DMA engine, reading a transposed fp32
+# weight copy (TMR_IO_WT_F32; the forward view takes that engine by itself).  TMR_GEMM32=0 keeps
+# both views on the register-staged engine (A/B measurements).  Not with FOLD_BN: the LDS-DMA
+# engine has no operand prologues.
+DMA32 = os.environ.get("TMR_GEMM32", "1") != "0"
+
+
+def _dma32(math):
+    return math == "fp32" and DMA32 and not FOLD_BN
+
+
 def _full16(math):
     return _store16(math) and FULL16 and not FOLD_BN
 
@@ -183,8 +194,12 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
         has_res = residual is not None or branch is not None
         # the dgrad view of a bf16-operand conv reads the transposed weights (LDS-DMA engine)
-        wt = (ops.weight_to_crsk(w.detach().contiguous())
-              if _full16(math) and x.dtype == torch.bfloat16 else None)
+        if _full16(math) and x.dtype == torch.bfloat16:
+            wt = ops.weight_to_crsk(w.detach().contiguous())
+        elif _dma32(math) and c % 8 == 0 and x.dtype == torch.float32:
+            wt = ops.weight_to_crsk(w.detach().contiguous(), bf16=False)
+        else:   # (the stem's 3 input channels: no dgrad)
+            wt = None
         recs.append({"x": x, "xpro": xpro, "wk": wk, "wt": wt, "y": y,
                      "z": (z[0] if dual else z) if has_res else None,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
