@@ -339,6 +339,11 @@ int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const float* shi
 int tmr_avgpool_fwd_a16(const void* x, float* y, int n, int hw, int c, hipStream_t stream);
 /* fp32 -> bf16 (RNE) copy of a tensor consumed as a bf16 conv operand (n % 8 == 0) */
 int tmr_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
+/* The stem input of the bf16 train step: NHWC4 fp32 pixels (tmr_crop_normalize / the augment
+ * output, 3 colours + 0) -> NHWC8 bf16 (RNE, channels 3-7 zero), so the 7x7 stem's 16-B pieces
+ * are one tap's 8 channels and the stem runs on the bf16 LDS-DMA engine.  Exact w.r.t. the
+ * bf16 math, which rounds x to bf16 anyway. */
+int tmr_nhwc4_to_bf16x8(const float* x4, void* y8, long npix, hipStream_t stream);
 
 /* ---------------- input pipeline: frame resize (resize.hip) ----------------------- */
 /* transforms.Resize((250,250)) of the decoded PIL frame (Training TMRNet/

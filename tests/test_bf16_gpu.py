@@ -425,3 +425,34 @@ def test_gemm16_dgrad_fused_bn_backward(dev, case):
     assert torch.equal(dzf, dres_ref)
     assert rel_err(dyf, dy_ref) < 1e-5
     assert rel_err(dgf, dg_ref) < 1e-5 and rel_err(dbf, db_ref) < 1e-5
+
+
+def test_stem_nhwc8_bf16_input(dev):
+    """The bf16 step's stem input (tmr_nhwc4_to_bf16x8): bit-exact bf16 (RNE) of the NHWC4 fp32
+    pixels with channels 3-7 zero; the 7x7/2 stem on it (bf16 LDS-DMA engine, forward and
+    wgrad) against float64 convs of the rounded operands (summation order only, 5e-6)."""
+    g = torch.Generator().manual_seed(21)
+    n, h, w = 3, 40, 36
+    x = torch.randn(n, 3, h, w, generator=g)
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    x8 = ops.nhwc4_to_bf16x8(x4)
+    want = torch.zeros(n, h, w, 8, dtype=torch.bfloat16)
+    want[..., :3] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    torch.cuda.synchronize()
+    assert x8.dtype == torch.bfloat16 and torch.equal(x8.cpu(), want)
+    wt = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
+    wk = ops.weight_to_krsc(wt.to(dev), cpad=8, bf16=True)
+    y = ops.conv_fwd(x8, wk, 2, 3, math="bf16")
+    xr = x.to(torch.bfloat16).double()
+    wr = wt.to(torch.bfloat16).double()
+    y_ref = F.conv2d(xr, wr, stride=2, padding=3)
+    assert rel_err(y.permute(0, 3, 1, 2), y_ref) < 5e-6
+    dy = torch.randn(y_ref.shape, generator=g).to(torch.bfloat16)
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev)
+    dw = ops.conv_wgrad(x8, dyd, 7, 7, 2, 3, c_real=3, math="bf16")
+    xg = xr.clone().requires_grad_(False)
+    wg = wr.clone().requires_grad_(True)
+    F.conv2d(xg, wg, stride=2, padding=3).backward(dy.double())
+    assert rel_err(dw, wg.grad) < 5e-6
+    with pytest.raises(RuntimeError):
+        ops.nhwc4_to_bf16x8(torch.randn(1, 4, 4, 3, device=dev))

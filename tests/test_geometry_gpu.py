@@ -145,9 +145,13 @@ def test_c5_geometry_step(dev, prec):
     # zeros are shared) counts the flips exactly.  One flip among 512 units measured 0.15
     # relative-L2 on every gradient downstream of it (fc_h_c, NLBlock, LSTM; the fp32 run of the
     # same geometry has none and meets the strict bound).  Each counted flip buys 0.2 slack.
+    # How many units sit that close to 0 is a property of the inputs, so the fp32 CPU oracle's
+    # own flip count (same emulated bf16 contract) sets the scale: at most twice it, or 3.
     dh, dh64 = m.fc_h_c.bias.grad.cpu(), r64.fc_h_c.bias.grad
     flips = int(((dh == 0) != (dh64 == 0)).sum())
-    assert flips <= (2 if prec == "bf16" else 0), flips
+    flips_cpu = int(((r.fc_h_c.bias.grad == 0) != (dh64 == 0)).sum())
+    _record("c5_%s_flips" % prec, {"hip": flips, "cpu_oracle": flips_cpu})
+    assert flips <= (max(3, 2 * flips_cpu) if prec == "bf16" else 0), (flips, flips_cpu)
     _check_grads(g(m), g(r), g(r64), "c5_%s_grads" % prec, slack=0.2 * flips)
 
 

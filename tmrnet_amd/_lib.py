@@ -79,6 +79,7 @@ SIGNATURES = {
     "tmr_maxpool2d_fwd_bn_a16": [P, P, P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd_a16": [P, P, I, I, I, P],
     "tmr_cast_f32_bf16": [P, P, ctypes.c_long, P],
+    "tmr_nhwc4_to_bf16x8": [P, P, ctypes.c_long, P],
     "tmr_adam_step_multi": [P, I, ctypes.c_int64, P],
     "tmr_resize_ksize": [I, I],
     "tmr_resize_coeffs": [I, I, P, P, I],

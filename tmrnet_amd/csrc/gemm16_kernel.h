@@ -192,11 +192,14 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-// F32: the fp32 form of the engine (FWD / DGRAD views, every operand fp32 in HBM, GemmArgs::dma32).
-// The LDS images are byte-identical -- [rows][128 B], 16-B chunks of 4 floats instead of 8 bf16,
-// the same swizzle and LDS-DMA pieces -- so BK = 32 elements; each ds_read_b128 fragment holds 4
+// F32: the fp32 form of the engine (every operand fp32 in HBM, GemmArgs::dma32).  The K-contiguous
+// images are byte-identical -- [rows][128 B], 16-B chunks of 4 floats instead of 8 bf16, the same
+// swizzle and LDS-DMA pieces -- so BK = 32 elements; each ds_read_b128 fragment holds 4
 // consecutive k of one row, lane half hh the chunk 2s + hh, and feeds 4 v_mfma_f32_32x32x2_f32
 // (MFMA t reduces k = 8s + t from half 0 and 8s + 4 + t from half 1: the same k for A and B).
+// WGRAD (reduction-major images [32 k-rows][R floats]): fragment element t of k-step s is
+// k = 8s + 2t + hh, one ds_read_b32 each; odd k-rows have their chunks XOR 8 (columns ^ 32), so
+// the two lane halves (rows k, k + 1) read disjoint bank halves.
 template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && BM * BN <= 128 * 128) ? 4 : 2))
 void gemm16_kernel(const GemmArgs a) {
@@ -212,7 +215,8 @@ void gemm16_kernel(const GemmArgs a) {
                 "LDS-DMA pieces per wave");
   static_assert(TM >= 1 && TN >= 1, "wave tile");
   static_assert(!MN || (BM >= 64 && BN >= 64), "reduction-major images need >= 64 columns");
-  static_assert(!(MN && F32), "fp32 LDS-DMA engine: FWD / DGRAD views only");
+  // reduction-major images: 16-B chunks per k-row
+  constexpr int CPRA = BM * (int)ES / 16, CPRB = BN * (int)ES / 16;
   using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
   constexpr int EPI = WM * BN * 2 * 4;
   constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
@@ -276,12 +280,12 @@ void gemm16_kernel(const GemmArgs a) {
 #pragma unroll
     for (int q = 0; q < NIA; ++q) {
       const int s = 64 * (wave + NW * q) + lane;
-      const int k = s / (BM / 8);
-      const int ch = (s % (BM / 8)) ^ mn_swz<BM>(k);
-      const int i = m0 + 8 * ch;
+      const int k = s / CPRA;
+      const int ch = (s % CPRA) ^ (F32 ? (k & 1) << 3 : mn_swz<BM>(k));
+      const int i = m0 + EPC * ch;
       akr[q] = k;
       acok[q] = i < a.M;
-      aco[q] = (uint32_t)i * 2u;
+      aco[q] = (uint32_t)i * ES;
     }
   }
   // B: FWD weight rows / DGRAD transposed-weight rows (row byte offset, chunk), WGRAD X columns
@@ -303,16 +307,16 @@ void gemm16_kernel(const GemmArgs a) {
 #pragma unroll
     for (int q = 0; q < NIB; ++q) {
       const int s = 64 * (wave + NW * q) + lane;
-      const int k = s / (BN / 8);
-      const int ch = (s % (BN / 8)) ^ mn_swz<BN>(k);
-      const int j = n0 + 8 * ch;
+      const int k = s / CPRB;
+      const int ch = (s % CPRB) ^ (F32 ? (k & 1) << 3 : mn_swz<BN>(k));
+      const int j = n0 + EPC * ch;
       const int tap = a.ntaps == 1 ? 0 : (j >> a.log2C);
       const int c = a.ntaps == 1 ? j : (j & cmask);
       int ri, si;
       tap_split(a, tap, ri, si);
       bdy[q] = a.oy0 + a.dyr * ri;
       bdx[q] = a.ox0 + a.dxs * si;
-      bco[q] = (uint32_t)c * 2u;
+      bco[q] = (uint32_t)c * ES;
       bok[q] = j < a.N && tap < a.ntaps;
       bkr[q] = k;
     }
@@ -394,7 +398,7 @@ void gemm16_kernel(const GemmArgs a) {
       for (int q = 0; q < NIA; ++q) {
         const int m = kb + akr[q];
         const bool ok = acok[q] && m < kend;
-        glds16(rA, As + 1024 * (wave + NW * q), ok ? (uint32_t)m * (uint32_t)a.ldb * 2u + aco[q] : OOB);
+        glds16(rA, As + 1024 * (wave + NW * q), ok ? (uint32_t)m * (uint32_t)a.ldb * ES + aco[q] : OOB);
       }
       // WGRAD B[k=m][j=(tap,c)] = X[src(m, tap)][c]
 #pragma unroll
@@ -408,7 +412,7 @@ void gemm16_kernel(const GemmArgs a) {
         const int ys = (int)y * a.sy + bdy[q], xs = (int)x * a.sx + bdx[q];
         const bool ok = m < kend && bok[q] && (unsigned)ys < (unsigned)a.Hs &&
                         (unsigned)xs < (unsigned)a.Ws;
-        const uint32_t off = (uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds * 2u + bco[q];
+        const uint32_t off = (uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds * ES + bco[q];
         glds16(rB, Bs + 1024 * (wave + NW * q), ok ? off : OOB);
       }
     }
@@ -433,6 +437,17 @@ void gemm16_kernel(const GemmArgs a) {
     return __builtin_bit_cast(bf16x8, w);
   };
   const int swzA = mn_swz<BM>(tq), swzB = mn_swz<BN>(tq);
+  // fp32 reduction-major fragment: element t = k-row 8s + 2t + hh of column cb + l31 (chunk
+  // swizzle of that row: hh << 3)
+  auto mn_frag32 = [&](const unsigned char* img, int R, int cb, int s) -> f32x4_t {
+    const int col = cb + l31;
+    const uint32_t cbyte = (uint32_t)((((col >> 2) ^ (hh << 3)) << 4) + (col & 3) * 4);
+    f32x4_t v;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      v[t] = *reinterpret_cast<const float*>(img + (8 * s + 2 * t + hh) * R * 4 + cbyte);
+    return v;
+  };
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -455,6 +470,8 @@ void gemm16_kernel(const GemmArgs a) {
         av[i] = *reinterpret_cast<const Frag*>(As + (arow0 + 32 * i) * 128 + (ch << 4));
       else if constexpr (!F32)
         av[i] = tr_frag(As, BM, swzA, wm * (BM / WM) + 32 * i, s);
+      else
+        av[i] = mn_frag32(As, BM, wm * (BM / WM) + 32 * i, s);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -462,6 +479,8 @@ void gemm16_kernel(const GemmArgs a) {
         bv[j] = *reinterpret_cast<const Frag*>(Bs + (brow0 + 32 * j) * 128 + (ch << 4));
       else if constexpr (!F32)
         bv[j] = tr_frag(Bs, BN, swzB, wn * (BN / WN) + 32 * j, s);
+      else
+        bv[j] = mn_frag32(Bs, BN, wn * (BN / WN) + 32 * j, s);
     }
   };
   auto mfmas = [&](const Frag (&av)[TM], const Frag (&bv)[TN]) {
@@ -558,10 +577,12 @@ constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64,
 inline bool use32(const GemmArgs& a, int mode) {
   // A/B switch for the forward view, read per launch (tests flip it in-process)
   const bool on = env_int("TMR_GEMM32", 1) != 0;
-  if (a.prec != TMR_MATH_F32 || a.sab || a.pro || mode == MODE_WGRAD) return false;
+  if (a.prec != TMR_MATH_F32 || a.sab || a.pro) return false;
   if (mode == MODE_DGRAD) return a.wt != 0;
   if (!on || !a.dma32) return false;
   if ((((uintptr_t)a.A | (uintptr_t)a.B) & 15) != 0) return false;
+  if (mode == MODE_WGRAD)
+    return a.M % 4 == 0 && a.log2C >= 2 && a.ldb % 4 == 0 && a.lds % 4 == 0 && a.N % 4 == 0;
   return a.lds % 4 == 0 && a.ldb % 4 == 0 && a.log2C >= 2 && (a.ntaps != 1 || a.K % 4 == 0);
 }
 
@@ -587,10 +608,22 @@ inline long cfg16_tiles(long M, long N, int c) {
 // 5-20% over 8 waves, whose two waves per SIMD stall on the same barrier); the dgrads, whose
 // fused BatchNorm-backward epilogue moves 12-16 B per output element, want the occupancy of
 // 128x128 / 256x64 tiles.
-inline int pick_cfg16(long M, long N, long K, int mode) {
+// fp32 (f32): measured separately (profiles/r2/convbench32_dma_cfgs/, wgrad32_cfgs/): the
+// wgrads with 64 output channels want 64-wide tiles, the big-FLOP wgrads (>= 100 GFLOP: 3x3,
+// strided downsample) 256x256 as 16 waves, the rest 128x128 as 8 waves; the N = 128 forwards and
+// the >= 512-column dgrads 128x128 as 8 waves.
+inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false) {
   static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
   if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
   int cfg;
+  if (f32 && mode == MODE_WGRAD) {
+    if (M <= 64) return (N <= 64 || N >= 512) ? 5 : 4;
+    if (N <= 64) return 5;
+    if (M >= 256 && N >= 256 && 2.0 * M * N * K >= 100e9) return 6;
+    return 7;
+  }
+  if (f32 && M >= 256 && ((mode == MODE_FWD && N == 128) || (mode == MODE_DGRAD && N >= 512)))
+    return cfg16_tiles(M, N, 7) >= 256 ? 7 : 2;
   if (mode == MODE_WGRAD) {
     if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
     else if (N <= 64) cfg = 3;
@@ -621,26 +654,24 @@ inline int pick_cfg16(long M, long N, long K, int mode) {
 // rows / columns of the output tile the launch for `a` will use (host planning: BN-partial rows,
 // wgrad split counts)
 inline int gemm_tile_bm(const GemmArgs& a, int mode) {
-  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode)].bm
+  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32)].bm
                         : kCfgs[pick_cfg(a.M, a.N, a.K, mode)].bm;
 }
 inline long gemm_tiles(const GemmArgs& a, int mode) {
-  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode))
+  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32))
                         : cfg_tiles(a.M, a.N, pick_cfg(a.M, a.N, a.K, mode));
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
-  if constexpr (MODE != MODE_WGRAD) {
-    if (a.prec == TMR_MATH_F32) {
-      if (tapv)
-        hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, 1>), grid, blk, 0, st, a);
-      else
-        hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, 1>), grid, blk, 0, st, a);
-      TMR_CHECK_LAUNCH("gemm16_kernel (fp32)");
-      return 0;
-    }
+  if (a.prec == TMR_MATH_F32) {
+    if (tapv)
+      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, 1>), grid, blk, 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, 1>), grid, blk, 0, st, a);
+    TMR_CHECK_LAUNCH("gemm16_kernel (fp32)");
+    return 0;
   }
   if (tapv)
     hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1>), grid, blk, 0, st, a);
@@ -655,12 +686,12 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   TMR_CHECK_ARG(((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0,
                 "gemm (LDS-DMA path): operands must be 16-B aligned");
   const bool f32 = a.prec == TMR_MATH_F32;
-  TMR_CHECK_ARG(!f32 || (MODE != MODE_WGRAD && a.lds % 4 == 0 && a.log2C >= 2 &&
+  TMR_CHECK_ARG(!f32 || (a.lds % 4 == 0 && a.log2C >= 2 &&
                          (MODE == MODE_DGRAD ? (a.ldbt % 4 == 0 && a.N % 8 == 0 && a.ldc % 4 == 0 &&
                                                 ((uintptr_t)a.C & 15) == 0)
                                              : a.ldb % 4 == 0)),
                 "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
-  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE);
+  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32);
   const Cfg16 c = kCfgs16[cfg];
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;

@@ -485,6 +485,7 @@ static void wgrad_fill(const tmr_conv_desc* d, GemmArgs& a) {
   a.prec = d->math;
   a.Bbytes = clamp_bytes_e(span((long)d->n * d->h * d->w, a.lds, d->c), esz_x(d));
   a.sab = ((d->io & TMR_IO_DY_BF16) ? 1 : 0) | ((d->io & TMR_IO_X_BF16) ? 2 : 0);
+  a.dma32 = d->math == TMR_MATH_F32;
 }
 
 static int wgrad_plan(const tmr_conv_desc* d, int* splits, int* kchunk, long* slab) {

@@ -344,6 +344,30 @@ TMR_API int tmr_cast_f32_bf16(const float* x, void* y, long n, hipStream_t strea
   return 0;
 }
 
+// stem input of the bf16 step: fp32 NHWC4 pixel (3 colours + zero) -> 8 bf16 (RNE; channels 4-7
+// zero), one 16-B read and one 16-B write per pixel
+__global__ __launch_bounds__(NT) void nhwc4_bf16x8_k(const float4* __restrict__ x,
+                                                     uint4* __restrict__ y, long npix) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < npix; i += (long)gridDim.x * NT) {
+    const float4 a = x[i];
+    const uint32_t w0 = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a.x) |
+                        ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a.y) << 16);
+    const uint32_t w1 = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a.z) |
+                        ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a.w) << 16);
+    y[i] = make_uint4(w0, w1, 0u, 0u);
+  }
+}
+
+TMR_API int tmr_nhwc4_to_bf16x8(const float* x4, void* y8, long npix, hipStream_t stream) {
+  TMR_CHECK_ARG(x4 && y8 && npix >= 0, "tmr_nhwc4_to_bf16x8: bad arguments");
+  TMR_CHECK_ARG((((uintptr_t)x4 | (uintptr_t)y8) & 15) == 0, "tmr_nhwc4_to_bf16x8: 16-B aligned pixels");
+  if (npix == 0) return 0;
+  hipLaunchKernelGGL(nhwc4_bf16x8_k, dim3(ew_blocks(npix)), dim3(NT), 0, stream,
+                     (const float4*)x4, (uint4*)y8, npix);
+  TMR_CHECK_LAUNCH("nhwc4_bf16x8");
+  return 0;
+}
+
 TMR_API int tmr_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, int cpad,
                              hipStream_t stream) {
   TMR_CHECK_ARG(cpad >= c, "tmr_nchw_to_nhwc: cpad < c");

@@ -457,6 +457,17 @@ def weight_to_crsk(w, bf16=True):
     return out
 
 
+def nhwc4_to_bf16x8(x4):
+    """(F,H,W,4) fp32 NHWC4 stem input -> (F,H,W,8) bf16 (tmr_nhwc4_to_bf16x8): the bf16 step's
+    stem operand (8-channel pieces for the LDS-DMA engine)."""
+    _req(x4, "x4")
+    if x4.dim() != 4 or x4.shape[3] != 4:
+        raise RuntimeError("nhwc4_to_bf16x8: expects (F,H,W,4), got %s" % (tuple(x4.shape),))
+    out = torch.empty(x4.shape[:3] + (8,), dtype=BF16, device=x4.device)
+    call("tmr_nhwc4_to_bf16x8", x4, out, x4.numel() // 4, stream_ptr())
+    return out
+
+
 def to_bf16(x):
     """fp32 -> bf16 (RNE) copy (tmr_cast_f32_bf16): the bf16 conv operand of an fp32 tensor."""
     _req(x, "x")

@@ -129,6 +129,11 @@ def _dma32(math):
     return math == "fp32" and DMA32 and not FOLD_BN
 
 
+# bf16 activations: the stem input as NHWC8 bf16 (TMR_BF16_STEM8=0: the NHWC4 fp32 input on the
+# register-staged engine, A/B measurements)
+STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
+
+
 def _full16(math):
     return _store16(math) and FULL16 and not FOLD_BN
 
@@ -291,9 +296,12 @@ class TrunkFn(torch.autograd.Function):
         a16 = training and _act16(mt)            # every activation bf16: no fp32 copies
         f16 = training and _full16(mt) and not a16
         if training:
+            # bf16 activations: the stem reads an NHWC8 bf16 copy of its input (8-channel
+            # pieces: the LDS-DMA engine; exact, the bf16 math rounds x anyway)
+            xs = ops.nhwc4_to_bf16x8(x4) if (a16 and STEM8) else x4
             # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
             # mask from y, so the stem's BN output is never needed)
-            y0, sc0, sh0 = _conv_bn(x4, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
+            y0, sc0, sh0 = _conv_bn(xs, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
                                     defer=True, nbt=nbt)
             p, am = ops.maxpool_fwd_bn(y0, sc0, sh0, bf16=f16)
             stem_hw = (y0.shape[1], y0.shape[2])
