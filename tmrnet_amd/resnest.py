@@ -44,6 +44,8 @@ def _bn_train_or_eval(y, bn, training):
 
 
 FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
+# the 4-channel stem input as NHWC8 bf16 on the bf16 operand path (trunk.STEM8's switch)
+STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -53,7 +55,8 @@ class ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, x16, w, gamma, beta, residual, bn, stride, pad, groups, relu, c_real, math):
         x = x.contiguous()
-        n, h, wd, cs = x.shape
+        n, h, wd, _ = x.shape
+        cs = (x16 if x16 is not None else x).shape[-1]   # stored channels of the conv operand
         k, cg, r, s = w.shape
         kg = k // groups
         cgs = cs // groups                       # stored channels per group
@@ -250,12 +253,14 @@ def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=
                 math="fp32"):
     """conv -> BN -> (+residual) -> (ReLU).  On the bf16 operand path (bf16 math, train mode,
     TMR_BF16_FULL) the conv reads x's bf16 copy: the one its producer attached (`_tmr_bf16`), else
-    a cast; the 4-channel stem input stays fp32 (register-staged gather)."""
+    a cast; the 4-channel stem input as an NHWC8 bf16 copy (tmr_nhwc4_to_bf16x8)."""
     x16 = None
     if math == "bf16" and bn.training and FULL16 and x.shape[-1] % 8 == 0:
         x16 = getattr(x, "_tmr_bf16", None)
         if x16 is None:
             x16 = ops.to_bf16(x.contiguous())
+    elif math == "bf16" and bn.training and FULL16 and STEM8 and x.shape[-1] == 4 and groups == 1:
+        x16 = ops.nhwc4_to_bf16x8(x.contiguous())
     z, z16 = ConvBNActFn.apply(x, x16, conv.weight, bn.weight, bn.bias, residual, bn, stride, pad,
                                groups, relu,
                                c_real if c_real is not None else conv.weight.shape[1] * groups, math)
