@@ -217,7 +217,7 @@ def main():
             a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
         peak = MFMA_F32_PEAK_TF if args.precision == "fp32" else MFMA_BF16_PEAK_TF
         roof = {"bound": "mfma",
-                "kernel": "gemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA)"
+                "kernel": "gemm16_kernel (LDS-DMA implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA)"
                           % ("f32" if args.precision == "fp32" else "bf16 operands, f32 acc"),
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
