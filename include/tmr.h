@@ -103,7 +103,8 @@ int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krs
  * gradient, and for a residual unit the identity branch's gradient -- and parts the per-tile
  * column sums (sum g, sum g*(y - mean)) as float2 [tmr_conv2d_dgrad_bnbwd_parts(d)][c], finished
  * by tmr_bn_bwd_parts.  Removes the separate statistics pass over (dz, y[, z]) of tmr_bn_bwd.
- * dx, y, z dense NHWC (x_ld == c). */
+ * dx, y, z dense NHWC (x_ld == c).  mask 3: z is the ReLU mask as bits (tmr_bn_apply_bits;
+ * fp32 dgrad with transposed weights, TMR_IO_WT_F32, and h*w*c a multiple of 32). */
 int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d);
 int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
                            float beta, const float* y, const float* z, const float* scale,
@@ -302,6 +303,15 @@ int tmr_weight_oihw_to_crsk_x(const float* w, void* wt, int k, int c, int r, int
                               hipStream_t stream);
 int tmr_bn_apply_dual(const float* y, const float* scale, const float* shift, const float* residual,
                       float* z, void* z16, int rows, int c, int relu, hipStream_t stream);
+/* Block outputs of the fp32 train step: tmr_bn_apply (residual optional) / tmr_bn_apply2 with
+ * ReLU, plus the ReLU mask as bits (element e = bit e % 32 of bits[e / 32]; ceil(rows*c/32)
+ * words) for the residual-gradient dgrads (tmr_conv2d_dgrad_bnbwd mask 3): 1/32 of z's bytes. */
+int tmr_bn_apply_bits(const float* y, const float* scale, const float* shift,
+                      const float* residual, float* z, uint32_t* bits, int rows, int c,
+                      hipStream_t stream);
+int tmr_bn_apply2_bits(const float* y, const float* scale, const float* shift, const float* yr,
+                       const float* rscale, const float* rshift, float* z, uint32_t* bits,
+                       int rows, int c, hipStream_t stream);
 int tmr_bn_apply2_x(const float* y, const float* scale, const float* shift, const float* yr,
                     const float* rscale, const float* rshift, float* z, void* z16, int rows, int c,
                     int relu, hipStream_t stream);

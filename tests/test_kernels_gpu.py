@@ -472,6 +472,13 @@ def test_conv_dgrad_fused_bn_backward(dev, case, wtr):
                                               scale=scale, shift=shift, out=old.clone(), beta=beta,
                                               wt=wtr)
     dyf, dgf, dbf = ops.bn_bwd_parts(dzf, y, parts, npart, mean, inv, gamma)
+    if wtr and mask == 1:
+        # the ReLU mask as bits (mask 3; bn_apply_bits): the same masked gradient and partials
+        _, bits = ops.bn_apply_bits(y, scale, shift, res)
+        dzb, partsb, npb = ops.conv_dgrad_bnbwd(dy, wk, (h, w), st, pad, y, mean, 3, z=bits,
+                                                out=old.clone(), beta=beta, wt=True)
+        torch.cuda.synchronize()
+        assert torch.equal(dzb, dzf) and torch.equal(partsb, parts) and npb == npart
     torch.cuda.synchronize()
     assert torch.equal(dzf, dres_ref)          # the masked BN-output gradient
     assert rel_err(dyf, dy_ref) < 1e-5
@@ -593,3 +600,38 @@ def test_bn_fold_bit_identical(dev):
         assert torch.equal(res[True][1][n], res[False][1][n]), n
     for n in res[True][2]:
         assert torch.equal(res[True][2][n], res[False][2][n]), n
+
+
+def _pack_bits(m):
+    """(numel,) bool -> int32 words, element e = bit e % 32 of word e // 32."""
+    m = m.reshape(-1).to(torch.int64)
+    m = torch.cat([m, torch.zeros((-m.numel()) % 32, dtype=torch.int64)]).view(-1, 32)
+    w = (m << torch.arange(32, dtype=torch.int64)).sum(1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+
+
+@pytest.mark.parametrize("rows,c", [(1000, 256), (77, 64), (3, 8)])
+def test_bn_apply_relu_bits(dev, rows, c):
+    """bn_apply_bits / bn_apply2_bits: z bit-identical to bn_apply / bn_apply2 (ReLU) and the
+    bits are exactly (z > 0) packed 32 per word (ragged tails included)."""
+    g = torch.Generator().manual_seed(rows + c)
+    y = torch.randn(rows, c, generator=g).to(dev)
+    res = torch.randn(rows, c, generator=g).to(dev)
+    yr = torch.randn(rows, c, generator=g).to(dev)
+    sc, sh = (torch.rand(c, generator=g) + 0.5).to(dev), torch.randn(c, generator=g).to(dev)
+    rs, rf = (torch.rand(c, generator=g) + 0.5).to(dev), torch.randn(c, generator=g).to(dev)
+    for resid in (res, None):
+        z, bits = ops.bn_apply_bits(y, sc, sh, resid)
+        zr = ops.bn_apply(y, sc, sh, resid, True)
+        torch.cuda.synchronize()
+        assert torch.equal(z, zr)
+        assert torch.equal(bits.cpu(), _pack_bits((zr > 0).cpu()))
+    z2, bits2 = ops.bn_apply2_bits(y, sc, sh, yr, rs, rf)
+    z2r = ops.bn_apply2(y, sc, sh, yr, rs, rf, True)
+    torch.cuda.synchronize()
+    assert torch.equal(z2, z2r) and torch.equal(bits2.cpu(), _pack_bits((z2r > 0).cpu()))
+    with pytest.raises(RuntimeError):
+        ops.conv_dgrad_bnbwd(torch.randn(1, 4, 4, 64, device=dev),
+                             ops.weight_to_krsc(torch.randn(64, 64, 1, 1, device=dev)), (4, 4), 1, 0,
+                             torch.randn(1, 4, 4, 64, device=dev), torch.zeros(64, device=dev), 3,
+                             z=ops.relu_bits_empty(torch.empty(1, 4, 4, 64, device=dev)))

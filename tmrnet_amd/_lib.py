@@ -70,6 +70,8 @@ SIGNATURES = {
     "tmr_weight_oihw_to_crsk_x": [P, P, I, I, I, I, I, P],
     "tmr_bn_apply_dual": [P, P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2_x": [P, P, P, P, P, P, P, P, I, I, I, P],
+    "tmr_bn_apply_bits": [P, P, P, P, P, P, I, I, P],
+    "tmr_bn_apply2_bits": [P, P, P, P, P, P, P, P, I, I, P],
     "tmr_maxpool2d_fwd_bn_x": [P, P, P, P, P, I, I, I, I, I, I, I, P],
     "tmr_bn_apply_a16": [P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2_a16": [P, P, P, P, P, P, P, I, I, I, P],

@@ -231,6 +231,60 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, cons
   }
 }
 
+// The ReLU mask of a block output as bits (tmr_bn_apply_bits / tmr_bn_apply2_bits): element e is
+// bit e % 32 of word e / 32.  The fp32 residual-gradient dgrads read it (mask 3) instead of
+// re-reading the 4-byte z.  Each lane holds 4 consecutive elements (one float4 index i); the 8
+// lanes of a word OR their nibbles.  Wave-uniform loop: the waves' lanes stay converged for the
+// shuffles.
+template <bool RES>
+__global__ __launch_bounds__(NT) void bn_apply_bits_k(const float* __restrict__ y,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      const float* __restrict__ res,
+                                                      const float* __restrict__ yr,
+                                                      const float* __restrict__ rscale,
+                                                      const float* __restrict__ rshift,
+                                                      float* __restrict__ z,
+                                                      uint32_t* __restrict__ bits, long n4, int c4) {
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * NT;
+  for (long base = blockIdx.x * (long)NT + (threadIdx.x & ~63); base < n4; base += stride) {
+    const long i = base + lane;
+    uint32_t nib = 0;
+    if (i < n4) {
+      const int cc = (int)(i % c4) * 4;
+      float4 v = ld4(y, i);
+      const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
+      const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
+      if (yr) {   // bn_apply2: the downsample branch's BatchNorm on the fly
+        const float4 r = ld4(yr, i);
+        const float4 rs = *reinterpret_cast<const float4*>(rscale + cc);
+        const float4 rf = *reinterpret_cast<const float4*>(rshift + cc);
+        v.x = fmaf(v.x, sc.x, sf.x) + fmaf(r.x, rs.x, rf.x);
+        v.y = fmaf(v.y, sc.y, sf.y) + fmaf(r.y, rs.y, rf.y);
+        v.z = fmaf(v.z, sc.z, sf.z) + fmaf(r.z, rs.z, rf.z);
+        v.w = fmaf(v.w, sc.w, sf.w) + fmaf(r.w, rs.w, rf.w);
+      } else {
+        v.x = fmaf(v.x, sc.x, sf.x); v.y = fmaf(v.y, sc.y, sf.y);
+        v.z = fmaf(v.z, sc.z, sf.z); v.w = fmaf(v.w, sc.w, sf.w);
+        if (RES) {
+          const float4 r = ld4(res, i);
+          v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+        }
+      }
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      st4(z, i, v);
+      nib = (uint32_t)(v.x > 0.f) | ((uint32_t)(v.y > 0.f) << 1) | ((uint32_t)(v.z > 0.f) << 2) |
+            ((uint32_t)(v.w > 0.f) << 3);
+    }
+    uint32_t w = nib << (4 * (lane & 7));
+    w |= (uint32_t)__shfl_xor((int)w, 1, 64);
+    w |= (uint32_t)__shfl_xor((int)w, 2, 64);
+    w |= (uint32_t)__shfl_xor((int)w, 4, 64);
+    if ((lane & 7) == 0 && i < n4) bits[i >> 3] = w;
+  }
+}
+
 // ReLU mask of the backward: MASK 0 = none, 1 = saved output z > 0, 2 = recomputed
 // fmaf(y, scale, shift) > 0 (bit-identical to the forward's z > 0 when there is no residual,
 // and saves reading z)
@@ -764,6 +818,37 @@ TMR_API int tmr_bn_apply2_x(const float* y, const float* scale, const float* shi
     hipLaunchKernelGGL((bn_apply2_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale, shift,
                        yr, rscale, rshift, z, n4, c / 4, h);
   TMR_CHECK_LAUNCH("bn_apply2");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply_bits(const float* y, const float* scale, const float* shift,
+                              const float* residual, float* z, uint32_t* bits, int rows, int c,
+                              hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && z && bits,
+                "tmr_bn_apply_bits: null operand or channels %d not a multiple of 4", c);
+  const long n4 = (long)rows * c / 4;
+  if (n4 == 0) return 0;
+  if (residual)
+    hipLaunchKernelGGL((bn_apply_bits_k<true>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+                       shift, residual, nullptr, nullptr, nullptr, z, bits, n4, c / 4);
+  else
+    hipLaunchKernelGGL((bn_apply_bits_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+                       shift, nullptr, nullptr, nullptr, nullptr, z, bits, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply_bits");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply2_bits(const float* y, const float* scale, const float* shift,
+                               const float* yr, const float* rscale, const float* rshift, float* z,
+                               uint32_t* bits, int rows, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && yr && rscale && rshift && z && bits,
+                "tmr_bn_apply2_bits: null operand or channels %d not a multiple of 4", c);
+  TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_bits: the branch input must not alias z");
+  const long n4 = (long)rows * c / 4;
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL((bn_apply_bits_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+                     shift, nullptr, yr, rscale, rshift, z, bits, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply2_bits");
   return 0;
 }
 

@@ -140,7 +140,12 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
             zv[4] = z1.x; zv[5] = z1.y; zv[6] = z1.z; zv[7] = z1.w;
           }
         }
-        if (a.bn_mask != 1) {
+        if (a.bn_mask == 3) {   // ReLU mask bits: this thread's 8 elements share one word
+          const uint32_t wrd = reinterpret_cast<const uint32_t*>(a.bn_z)[off >> 5];
+          const uint32_t b8 = wrd >> (off & 31);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) zv[e] = ((b8 >> e) & 1u) ? 1.f : 0.f;
+        } else if (a.bn_mask != 1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) zv[e] = 0.f;
         }
@@ -553,7 +558,7 @@ void gemm16_kernel(const GemmArgs a) {
   // the LDS form stages whole wave row-blocks: (BM / WM) padded rows must fit (all configs but
   // 256x256, which the dgrad tile rules never pick)
   if constexpr (MODE == MODE_DGRAD && (BN + 4) * (BM / WM) * 4 <= SMEM) {
-    if (a.bn_part != nullptr) {
+    if (a.bn_part != nullptr) {   // (the only form that reads mask-3 bits: launch_gemm16_t)
       epilogue_lds_bnbwd<BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), SMEM / 4,
                                                   m0, n0);
       return;
@@ -693,6 +698,11 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                 "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
   const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32);
   const Cfg16 c = kCfgs16[cfg];
+  // ReLU-mask bits are read by the LDS-staged BN-backward epilogue only (every dgrad tile but
+  // 256x256, whose wave row-blocks do not fit the staging buffer)
+  TMR_CHECK_ARG(a.bn_part == nullptr || a.bn_mask != 3 ||
+                    (MODE == MODE_DGRAD && f32 && !(c.bm == 256 && c.bn == 256)),
+                "gemm: ReLU-mask bits (mask 3) need the fp32 LDS-DMA dgrad (tile %dx%d)", c.bm, c.bn);
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   // a k-tile (64 bf16 / 32 fp32) spans several taps when the channels per tap are fewer (or not

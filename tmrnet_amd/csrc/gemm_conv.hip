@@ -396,7 +396,9 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     BnBwdFuse fc_ = *fz;
     fc_.y = adv(fz->y, f0 * px_frame, esz_bn(d));
-    fc_.z = adv(fz->z, f0 * px_frame, esz_bn(d));
+    // mask 3: z is bits, 32 elements per word (px_frame % 32 == 0, checked by the caller)
+    fc_.z = fz->mask == 3 ? (const float*)((const uint32_t*)fz->z + f0 * px_frame / 32)
+                          : adv(fz->z, f0 * px_frame, esz_bn(d));
     fc_.nparts = 0;
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);
@@ -439,8 +441,11 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd: null descriptor");
   TMR_CHECK_ARG(xld_of(d) == d->c, "tmr_conv2d_dgrad_bnbwd: dx must be dense (x_ld == c)");
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
-  TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift),
-                "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1) or scale/shift (2)", mask);
+  TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
+                "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
+  TMR_CHECK_ARG(mask != 3 || ((d->io & TMR_IO_WT_F32) && ((long)d->h * d->w * d->c) % 32 == 0),
+                "tmr_conv2d_dgrad_bnbwd: ReLU-mask bits (mask 3) need the fp32 LDS-DMA dgrad "
+                "(TMR_IO_WT_F32) and h*w*c a multiple of 32");
   const int np = tmr_conv2d_dgrad_bnbwd_parts(d);
   TMR_CHECK_ARG(np >= 0 && parts_bytes >= (size_t)np * d->c * sizeof(float2),
                 "tmr_conv2d_dgrad_bnbwd: parts buffer too small");

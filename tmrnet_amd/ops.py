@@ -256,7 +256,10 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts).
     wt: as conv_dgrad.  y / z may be bf16 (the bf16-activation step, TMR_IO_BN_BF16)."""
     _req_op(w_krsc, "w"); _req_op(y, "y"); _req(mean, "mean")
-    if z is not None and z.dtype != y.dtype:
+    if mask == 3:   # z = ReLU-mask bits of dx's shape (bn_apply_bits)
+        if z is None or z.dtype != torch.int32 or z.numel() * 32 < y.numel():
+            raise RuntimeError("conv_dgrad_bnbwd: mask 3 takes the int32 ReLU-mask bits of y's shape")
+    elif z is not None and z.dtype != y.dtype:
         raise RuntimeError("conv_dgrad_bnbwd: y and z must have one dtype")
     n, ho, wo, k = dy.shape
     k2, r, s, c = _dgrad_w(w_krsc, wt)
@@ -266,7 +269,8 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
-    if tuple(y.shape) != tuple(out.shape) or (z is not None and tuple(z.shape) != tuple(out.shape)):
+    if tuple(y.shape) != tuple(out.shape) or (z is not None and mask != 3
+                                              and tuple(z.shape) != tuple(out.shape)):
         raise RuntimeError("conv_dgrad_bnbwd: y/z must have dx's shape %s" % (tuple(out.shape),))
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
@@ -277,7 +281,8 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
                _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * k * r * s * c
                + 4 * n * h * w * c * (2 if beta else 1)
-               + y.element_size() * n * h * w * c * (2 if z is not None else 1)):
+               + y.element_size() * n * h * w * c * (2 if z is not None and mask != 3 else 1)
+               + (n * h * w * c // 8 if mask == 3 else 0)):
         pro = _prologue(None, dpro)
         if pro is None:
             call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z,
@@ -549,6 +554,35 @@ def bn_apply(y, scale, shift, residual=None, relu=True, out=None, bf16=False):
     call("tmr_bn_apply_x", y, scale, shift, residual, out, rows, c, int(relu),
          int(out.dtype == torch.bfloat16), stream_ptr())
     return out
+
+
+def relu_bits_empty(like):
+    """The ReLU-mask bit buffer of a tensor (tmr_bn_apply_bits): ceil(numel / 32) int32 words."""
+    return torch.empty(((like.numel() + 31) // 32,), dtype=torch.int32, device=like.device)
+
+
+def bn_apply_bits(y, scale, shift, residual=None):
+    """fp32 block output with ReLU: z = relu(y*scale + shift (+ residual)) and its ReLU mask as
+    bits (tmr_bn_apply_bits) -> (z, bits), for the mask-3 residual-gradient dgrads."""
+    _req(y, "y")
+    c = y.shape[-1]
+    z = torch.empty_like(y)
+    bits = relu_bits_empty(y)
+    call("tmr_bn_apply_bits", y, scale, shift, residual, z, bits, y.numel() // c, c, stream_ptr())
+    return z, bits
+
+
+def bn_apply2_bits(y, scale, shift, yr, rscale, rshift):
+    """bn_apply2 with ReLU, fp32, plus the ReLU mask as bits -> (z, bits)."""
+    _req(y, "y"); _req(yr, "yr")
+    if yr.shape != y.shape:
+        raise RuntimeError("bn_apply2_bits: branch shape %s != %s" % (tuple(yr.shape), tuple(y.shape)))
+    c = y.shape[-1]
+    z = torch.empty_like(y)
+    bits = relu_bits_empty(y)
+    call("tmr_bn_apply2_bits", y, scale, shift, yr, rscale, rshift, z, bits, y.numel() // c, c,
+         stream_ptr())
+    return z, bits
 
 
 def bn_apply_dual(y, scale, shift, residual=None, relu=True):

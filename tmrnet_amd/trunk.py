@@ -125,6 +125,10 @@ ACT16 = os.environ.get("TMR_BF16_ACT", "1") != "0"
 DMA32 = os.environ.get("TMR_GEMM32", "1") != "0"
 
 
+# the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
+BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
+
+
 def _dma32(math):
     return math == "fp32" and DMA32 and not FOLD_BN
 
@@ -184,8 +188,17 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
                                           bn.running_var, bn.eps)
         return ops.conv_fwd_fused(x, wk, stride, pad, scale, shift, residual, relu, c_real=c,
                                   math=math)
+    # fp32 block outputs on the LDS-DMA path also record their ReLU mask as bits: the dgrad that
+    # produces their gradient reads 1 bit instead of z's 4 bytes (mask 3)
+    zbits = None
+    bits = (recs is not None and relu and not dual and _dma32(math) and y.dtype == torch.float32
+            and (residual is not None or branch is not None) and BITS)
     if defer:
         z = None
+    elif branch is not None and bits:
+        z, zbits = ops.bn_apply2_bits(y, scale, shift, branch[0], branch[1], branch[2])
+    elif bits:
+        z, zbits = ops.bn_apply_bits(y, scale, shift, residual)
     elif branch is not None:
         z = ops.bn_apply2(y, scale, shift, branch[0], branch[1], branch[2], relu, dual=dual)
     elif dual:
@@ -206,7 +219,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         else:   # (the stem's 3 input channels: no dgrad)
             wt = None
         recs.append({"x": x, "xpro": xpro, "wk": wk, "wt": wt, "y": y,
-                     "z": (z[0] if dual else z) if has_res else None,
+                     "z": (z[0] if dual else z) if has_res else None, "zbits": zbits,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
                      "c_real": c, "math": math})
@@ -270,8 +283,11 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
         if fuse_prev is not None:
             p = fuse_prev
             mask = (1 if p["z"] is not None else 2) if p["relu"] else 0
+            zm = p["z"]
+            if mask == 1 and wt and p.get("zbits") is not None:
+                mask, zm = 3, p["zbits"]   # the ReLU mask as bits (fp32 LDS-DMA dgrad)
             dx, pp, npp = ops.conv_dgrad_bnbwd(dy, wdg, hw, rec["stride"], rec["pad"],
-                                               p["y"], p["mean"], mask, z=p["z"],
+                                               p["y"], p["mean"], mask, z=zm,
                                                scale=p["scale"], shift=p["shift"], out=dx_out,
                                                beta=dx_beta, math=rec["math"], dpro=dpro,
                                                wt=wt)
