@@ -16,7 +16,11 @@ def main():
     rank = int(os.environ["RANK"])
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo")
+    backend = os.environ.get("TMR_TEST_BACKEND", "gloo")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
     import tmrnet_amd
     from tmrnet_amd import ops
     from tmrnet_amd.ddp import GradAllReduce
@@ -25,7 +29,8 @@ def main():
     B, T, L = 2, 3, 5
     torch.manual_seed(0)
     m = tmrnet_amd.resnet_lstm(seq_len=T).to(dev).train()
-    red = GradAllReduce(m, dist, overlap=False)
+    # a one-rank RCCL run forces the collectives (world size 1 would skip them)
+    red = GradAllReduce(m, dist, overlap=False, force=dist.get_world_size() == 1)
     g = torch.Generator().manual_seed(10 + rank)
     frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
     off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)

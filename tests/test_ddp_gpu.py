@@ -57,3 +57,21 @@ def test_overlap_matches_post_backward():
     worst, n, early_off, early_on = float(f[1]), int(f[2]), int(f[3]), int(f[4])
     assert early_off == 0 and early_on == 16, line[0]    # one launch per bottleneck block
     assert n > 100 and worst < 1e-5, line[0]
+
+
+def test_overlap_on_rccl_one_rank():
+    """The overlapped exchange on the production backend: one rank over RCCL ("nccl"), the
+    collectives forced at world size 1 (GradAllReduce(force=True)) -- all-reduces issued from the
+    autograd thread during TrunkFn.backward, waited on the main thread.  A one-rank sum is the
+    identity, so both schedules must return the local gradients bit-exactly."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", TMR_TEST_BACKEND="nccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "tests/_ddp_overlap_worker.py"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("OVERLAP_REL_DIFF")]
+    assert len(line) == 1, p.stdout[-2000:]
+    f = line[0].split()
+    worst, early_off, early_on = float(f[1]), int(f[3]), int(f[4])
+    assert worst == 0.0 and early_off == 0 and early_on == 16, line[0]

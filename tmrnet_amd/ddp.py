@@ -27,8 +27,11 @@ _unflatten = torch._utils._unflatten_dense_tensors
 
 class GradAllReduce:
     def __init__(self, model, dist, bucket_bytes=25 * 1024 * 1024, broadcast_init=True,
-                 overlap=True):
+                 overlap=True, force=False):
+        """force: run the collectives even at world size 1 (a one-rank RCCL communicator: lets a
+        one-GPU box exercise the exchange path -- streams, early launches, waits -- on RCCL)."""
         self.dist = dist
+        self.force = bool(force)
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.buckets = []
         cur, size = [], 0
@@ -56,7 +59,7 @@ class GradAllReduce:
             set_grad_ready(share, self.grads_ready)
 
     def _multi(self):
-        return self.dist is not None and self.dist.get_world_size() > 1
+        return self.dist is not None and (self.force or self.dist.get_world_size() > 1)
 
     def grads_ready(self, pairs):
         """Launch the SUM of some final gradients while the backward is still running.
