@@ -105,8 +105,21 @@ def synth_inputs(args, rank, world, dev, nvar=2):
     return frames, bank, vs_d, offs, starts, labels
 
 
+def _dump_maps_at_exit(path):
+    """Diagnostics: write /proc/self/maps at interpreter exit (TMR_EXIT_MAPS=path), so a fault
+    in a native exit handler can be attributed to a library from its PC."""
+    import atexit
+
+    def dump():
+        with open("/proc/self/maps") as f, open(path, "w") as g:
+            g.write(f.read())
+    atexit.register(dump)
+
+
 def main():
     args = parse()
+    if os.environ.get("TMR_EXIT_MAPS"):
+        _dump_maps_at_exit(os.environ["TMR_EXIT_MAPS"])
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -252,8 +265,13 @@ def main():
                               / (HBM_PEAK_GBS * 1e9), 4) if traffic else None),
            "peak_gbs": HBM_PEAK_GBS}
 
+    # the CPU baseline runs on rank 0 after the GPU ranks are done (at N > 1 too: north_star asks
+    # for the CPU path next to every GPU count), so it never competes with a timed GPU step
+    if dist is not None:
+        dist.destroy_process_group()
+        dist = None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
 
     if rank == 0:
@@ -281,8 +299,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 def workload_name(args):
@@ -388,6 +404,9 @@ def cpu_baseline(args):
         pass
     return {"value": round(c2, 3), "unit": "frames/s", "cores": threads,
             "os_cpu_count": os.cpu_count(), "kind": "port", "cpu": model_name,
+            "threads_rule": ("OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS", "").isdigit()
+                             else "sched_getaffinity") + " (the job's host share; BASELINE.md "
+                            "section 4 names os.cpu_count(), which reports the whole host)",
             "c1_memory_bank_frames_per_s": round(c1, 3) if c1 is not None else None,
             "sample": "oracle fp32 train steps on the host (%s, fwd, CE-sum, bwd, SGD): value = C2 "
                       "model (TMRNetRef) at %d clips x %d frames, L=%d; c1 = memory-bank model "

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 4
+#define TMR_ABI_VERSION 5
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
@@ -61,6 +61,14 @@ typedef struct tmr_conv_desc {
                              / wgrad A).  Exact: the bf16 math rounds those operands to bf16 (RNE)
                              anyway, so a tensor consumed only as a conv operand may be stored
                              rounded.  Outputs (y, dx, dw) stay fp32. */
+  int groups;             /* nn.Conv2d groups (0 or 1: none).  c and k are the totals; group g reads
+                             input channels [g*c/G, (g+1)*c/G) and writes [g*k/G, (g+1)*k/G), i.e.
+                             the grouped 3x3 conv of ResNeSt's SplAtConv2d (radix 2,
+                             train_non-local_mutiConv_resnest.py:210-220).  Weights are torch's grouped
+                             layout per group block: KRSC (k, r, s, c/G), the transposed copy
+                             (G, c/G, r, s, k/G), OIHW gradients (k, c_real, r, s) with c_real the real
+                             input channels per group.  BatchNorm partials (stats / parts) keep rows
+                             over all channels.  No operand prologues, no ReLU-mask bits. */
 } tmr_conv_desc;
 #define TMR_MATH_F32 0
 #define TMR_MATH_BF16 1
@@ -417,6 +425,39 @@ int tmr_avgpool2d_fwd(const float* x, float* y, int n, int h, int w, int c, int 
 int tmr_avgpool2d_bwd(const float* dy, float* dx, int n, int h, int w, int c, int ho, int wo, int k,
                       int s, int p, int count_include_pad, hipStream_t stream);
 
+/* Split attention with bn0 + ReLU applied on load (the whole-trunk ResNeSt train step): y is the
+ * grouped conv's pre-BN output [n][hw][2c] (bf16 when act16, else fp32) and
+ * x_r = relu(y_r*scale + shift) -- rounded to bf16 under act16, the value a stored bf16 activation
+ * would hold -- is recomputed wherever it is read, so the post-BN tensor is never written.
+ *   gap_bn:   gap[n][c] = mean_hw(x_0 + x_1)
+ *   att:      att[n][r*c+j] = softmax over the radix pair of the fc2 logits zl [n][2c]
+ *   combine_bn: out[n,hw,j] = att_0*x_0 + att_1*x_1 (out bf16 when act16)
+ *   bwd_reduce_bn: per (frame, channel) over hw -- dzl (softmax backward of sum_hw dout*x_r) and
+ *             sums float [4][n][2c] = (sum m*dout, sum m, sum m*dout*(y-mean), sum m*(y-mean)),
+ *             m the ReLU mask; the bn0 input gradient g = m*(att*dout + dgap/hw) is known only after
+ *             the fc backward, and its BatchNorm sums are linear in these.
+ *   bn0_coefs: the BatchNorm sums of g from sums/att/dgap (frames in order) -> dgamma, dbeta and
+ *             coef [3][2c] with dy = coef0*(g - coef1 - (y - mean)*coef2)
+ *   bwd_apply_bn: dy[n,hw,j] (bf16 when act16: a conv operand) from dout, y, att, dgap, coef. */
+int tmr_splat_gap_bn(const void* y, const float* scale, const float* shift, float* gap, int n,
+                     int hw, int c, int act16, hipStream_t stream);
+int tmr_splat_att(const float* zl, float* att, int n, int c, hipStream_t stream);
+int tmr_splat_combine_bn(const void* y, const float* scale, const float* shift, const float* att,
+                         void* out, int n, int hw, int c, int act16, hipStream_t stream);
+int tmr_splat_bwd_reduce_bn(const float* dout, const void* y, const float* scale,
+                            const float* shift, const float* mean, const float* att, float* dzl,
+                            float* sums, int n, int hw, int c, int act16, hipStream_t stream);
+int tmr_splat_bn0_coefs(const float* att, const float* dgap, const float* sums, const float* mean,
+                        const float* invstd, const float* gamma, float* coef, float* dgamma,
+                        float* dbeta, int n, int hw, int c, hipStream_t stream);
+int tmr_splat_bwd_apply_bn(const float* dout, const void* y, const float* scale,
+                           const float* shift, const float* mean, const float* att,
+                           const float* dgap, const float* coef, void* dy, int n, int hw, int c,
+                           int act16, hipStream_t stream);
+/* tmr_avgpool2d_fwd on bf16 activations: fp32 sums of the bf16 inputs, the output rounded */
+int tmr_avgpool2d_fwd_a16(const void* x, void* y, int n, int h, int w, int c, int ho, int wo,
+                          int k, int s, int p, int count_include_pad, hipStream_t stream);
+
 /* ---------------- misc (head.hip) ------------------------------------------ */
 /* out[j] = beta*out[j] + sum_i x[i*ld + j]   (Linear bias grads) */
 int tmr_col_sum(const float* x, int rows, int cols, int ld, float* out, float beta,
@@ -496,6 +537,11 @@ int tmr_residual_mask(const float* base, const float* z, const float* mask, floa
 int tmr_mask_relu_fwd(const float* h, const float* mask, float* a, long n, hipStream_t stream);
 int tmr_mask_relu_bwd(const float* da, const float* a, const float* mask, float* dh, long n,
                       hipStream_t stream);
+/* x[i] = v (the exactly-zero fc1 bias gradient of the split attention) */
+int tmr_fill_f32(float* x, long n, float v, hipStream_t stream);
+/* *ptrs[i] += v for i < n: every BatchNorm num_batches_tracked counter of a train step
+ * (nn.BatchNorm2d's `num_batches_tracked += 1`) in one launch; ptrs is a DEVICE array */
+int tmr_counters_add(int64_t* const* ptrs, int n, int64_t v, hipStream_t stream);
 /* out = a*b*scalar[0] (b, scalar may be NULL) */
 int tmr_mul(const float* a, const float* b, const float* scalar, float* out, long n,
             hipStream_t stream);
@@ -592,6 +638,11 @@ int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, int h, co
 /* timeout word of the last persistent LSTM launch on ws (0 = every grid barrier completed);
  * synchronises the stream */
 int tmr_lstm_sync_status(const void* ws, unsigned* timeout_out, hipStream_t stream);
+/* *status |= 1 when the last persistent LSTM launch on ws gave up a grid barrier (its results are
+ * then invalid); enqueued on the stream, no synchronisation -- the caller reads the status word
+ * once per train step (tmrnet_amd/health.py) and raises.  TMR_LSTM_SPIN_LIMIT (env) overrides
+ * the barrier's spin limit (tests force a give-up with it). */
+int tmr_lstm_status_or(const void* ws, int32_t* status, hipStream_t stream);
 
 /* TimeConv (NLBlock_MutiConv6_3.py:43-79, generalised in L): the three Conv1d branches run
  * on tmr_conv2d_* (L as H, W=1); these kernels take the elementwise max of

@@ -42,10 +42,12 @@ reference checkout, ``code/``):
                          build's TMR_MATH_BF16 contract on torch ops -- every trunk conv with
                          operands rounded to bf16 (RNE), exact products, accumulation in the
                          tensor dtype; fwd rounds (x, w), dgrad (dy, w), wgrad (x, dy).
-                         With activations=True (the ResNet-50 train step's bf16-activation
-                         contract, tmrnet_amd/trunk.py ACT16) every conv output and every
-                         Bottleneck output is also stored rounded to bf16 in train mode
-                         (straight-through: the rounding is storage, gradients pass unchanged).
+                         With activations=True (the train step's bf16-activation contract,
+                         tmrnet_amd/trunk.py ACT16, both backbones) every conv output and every
+                         Bottleneck output -- for ResNeSt-50 also relu(bn0) and the output of
+                         the split attention and the avd pool output -- is stored rounded to
+                         bf16 in train mode (straight-through: the rounding is storage,
+                         gradients pass unchanged).
 """
 import math
 
@@ -202,6 +204,9 @@ class SplAtConv2d(nn.Module):
 
     def forward(self, x):
         x = self.relu(self.bn0(self.conv(x)))
+        rnd = getattr(self, "round_out", False) and self.training   # emulate_bf16_convs(activations)
+        if rnd:   # relu(bn0) as a stored bf16 activation (the HIP path recomputes it rounded)
+            x = _RoundFn.apply(x)
         b = x.shape[0]
         splits = torch.split(x, self.channels, dim=1)
         gap = F.adaptive_avg_pool2d(sum(splits), 1)
@@ -209,7 +214,8 @@ class SplAtConv2d(nn.Module):
         att = self.fc2(gap).view(b, 1, self.radix, -1).transpose(1, 2)
         att = F.softmax(att, dim=1).reshape(b, -1, 1, 1)
         atts = torch.split(att, self.channels, dim=1)
-        return sum(a * s_ for a, s_ in zip(atts, splits))
+        out = sum(a * s_ for a, s_ in zip(atts, splits))
+        return _RoundFn.apply(out) if rnd else out
 
 
 class BottleneckS(nn.Module):
@@ -231,13 +237,17 @@ class BottleneckS(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        rnd = getattr(self, "round_out", False) and self.training   # emulate_bf16_convs(activations)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.conv2(out)
         if self.avd:
             out = self.avd_layer(out)
+            if rnd:
+                out = _RoundFn.apply(out)
         out = self.bn3(self.conv3(out))
         res = self.downsample(x) if self.downsample is not None else x
-        return self.relu(out + res)
+        out = self.relu(out + res)
+        return _RoundFn.apply(out) if rnd else out
 
 
 def _make_layer_s(inplanes, planes, blocks, stride):
@@ -337,12 +347,13 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False):
     """Switch every trunk Conv2d of `module` to bf16-operand math (class swap, so deepcopy
     and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay.
     activations=True: in train mode the conv outputs and the Bottleneck outputs are rounded to
-    bf16 as well (the bf16-activation contract of the ResNet-50 train step)."""
+    bf16 as well (the bf16-activation contract of the train step; ResNeSt-50 also stores the
+    split attention's relu(bn0) input and output and the avd pool output as bf16)."""
     for name, m in module.named_modules():
         if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
             m.__class__ = Bf16Conv2d
             m.round_out = activations
-        elif isinstance(m, Bottleneck):
+        elif isinstance(m, (Bottleneck, BottleneckS, SplAtConv2d)):
             m.round_out = activations
     return module
 
@@ -350,8 +361,9 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False):
 class TMRNetRef(nn.Module):
     """Inline `resnet_lstm` (train_only_non-local_pretrained.py:201-240); with
     time_conv=True the mutiConv variant (train_non-local_mutiConv_resnet.py:208-253).
-    precision='bf16': trunk convs with bf16 operands (emulate_bf16_convs); bf16_act (default: the
-    ResNet-50 backbone) adds the bf16 storage of conv and Bottleneck outputs in train mode."""
+    precision='bf16': trunk convs with bf16 operands (emulate_bf16_convs); bf16_act (default on)
+    adds the bf16 storage of the train step's activations (conv and block outputs, ResNeSt's split
+    attention) in train mode."""
 
     def __init__(self, seq_len=10, num_classes=7, time_conv=False, backbone="resnet50",
                  precision="fp32", bf16_act=None):
@@ -359,8 +371,7 @@ class TMRNetRef(nn.Module):
         self.seq_len = seq_len
         self.share = resnet50_share() if backbone == "resnet50" else resnest50_share()
         if precision == "bf16":
-            emulate_bf16_convs(self.share, activations=(backbone == "resnet50"
-                                                         if bf16_act is None else bf16_act))
+            emulate_bf16_convs(self.share, activations=True if bf16_act is None else bf16_act)
         self.lstm = nn.LSTM(2048, 512, batch_first=True)
         self.fc_c = nn.Linear(512, num_classes)
         self.fc_h_c = nn.Linear(1024, 512)

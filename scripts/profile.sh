@@ -4,6 +4,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/${PROF_NAME:-prof}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+export TMR_EXIT_MAPS="$OUT/exit_maps.txt"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
   python3 "$R/bench.py" --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$OUT/bench.log" 2>&1
 rc=$?

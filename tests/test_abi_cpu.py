@@ -38,7 +38,7 @@ def test_python_binding_covers_header(built):
 def test_library_loads_and_reports_version(built):
     from tmrnet_amd import _lib
     h = _lib.lib()
-    assert h.tmr_abi_version() == 4
+    assert h.tmr_abi_version() == 5
     assert isinstance(h.tmr_last_error(), bytes)
 
 

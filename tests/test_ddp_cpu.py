@@ -91,7 +91,16 @@ def _accum_worker(rank, world, port, q):
         unused.weight.grad = torch.full_like(unused.weight, 5.0)
     red.all_reduce_sum()
     out = [None if p.grad is None else p.grad.numpy().copy() for p in m.parameters()]
-    q.put((rank, out))
+    # grads not cleared before the next backward (zero_grad(set_to_none=False)): the early launch
+    # is skipped -- with a one-time warning, and no collective is started
+    import warnings
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        red.overlap = True
+        red.grads_ready([(p, p.grad.clone()) for p in ps[2:]])
+        red.grads_ready([(p, p.grad.clone()) for p in ps[2:]])
+    warned = [x for x in w if issubclass(x.category, RuntimeWarning)]
+    q.put((rank, (out, len(warned), len(red.early))))
     dist.destroy_process_group()
 
 
@@ -108,7 +117,8 @@ def test_grad_accumulation_and_none_grads_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in range(world):
-        g = res[r]
+        g, nwarn, nearly = res[r]
+        assert nwarn == 1 and nearly == 0, (nwarn, nearly)
         for i in range(4):
             # sum over ranks (1, 2) of micro-batches (1, 2): (1+2) * (1+2) * (i+1)
             assert (g[i] == 9.0 * (i + 1)).all(), (r, i, g[i].ravel()[:3])

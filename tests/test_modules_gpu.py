@@ -85,6 +85,36 @@ def test_lstm_persistent_barrier_status(dev):
         assert rel(a, b) < 1e-4
 
 
+def test_lstm_giveup_is_loud(dev, monkeypatch):
+    """A persistent LSTM launch that gives up a grid barrier (forced: TMR_LSTM_SPIN_LIMIT=1, so
+    the first wait on another workgroup fails) is reported: the train step's optimizer raises
+    RuntimeError at its next step (tmrnet_amd/health.py), and health.check(sync=True) at once --
+    instead of training on a garbage recurrence."""
+    import tmrnet_amd
+    from tmrnet_amd import health
+    health.reset()
+    monkeypatch.setenv("TMR_LSTM_PERSIST", "1")
+    monkeypatch.setenv("TMR_LSTM_SPIN_LIMIT", "1")
+    torch.manual_seed(5)
+    m = tmrnet_amd.LSTM(2048, 512).to(dev)
+    opt = tmrnet_amd.SGD(m.parameters(), lr=1e-3, momentum=0.9)
+    x = torch.randn(64, 10, 2048, device=dev)
+    y, _ = m(x)
+    y.sum().backward()
+    opt.step()                      # schedules the status copy of this step
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="gave up a grid barrier"):
+        opt.step()                  # ... and raises on it one step later, without a sync
+    with pytest.raises(RuntimeError, match="gave up a grid barrier"):
+        health.check(sync=True)
+    health.reset()
+    monkeypatch.delenv("TMR_LSTM_SPIN_LIMIT")
+    y, _ = m(x)                     # default limit: no give-up, nothing raised
+    y.sum().backward()
+    opt.step()
+    health.check(sync=True)
+
+
 @pytest.mark.parametrize("B,L,rows", [(64, 300, True), (3, 40, False), (2, 1, False),
                                       (4, 33, True)])
 def test_nl_attn_split(dev, B, L, rows):

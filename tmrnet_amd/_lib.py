@@ -23,7 +23,7 @@ SZ = ctypes.c_size_t
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "pad_w",
-                 "x_ld", "y_ld", "math", "max_frames", "io")]
+                 "x_ld", "y_ld", "math", "max_frames", "io", "groups")]
 
 
 DP = ctypes.POINTER(ConvDesc)
@@ -116,6 +116,15 @@ SIGNATURES = {
     "tmr_splat_combine": [P, P, P, P, I, I, I, P],
     "tmr_splat_bwd": [P, P, P, P, I, I, I, P],
     "tmr_splat_bwd_apply": [P, P, P, P, I, I, I, P],
+    "tmr_splat_gap_bn": [P, P, P, P, I, I, I, I, P],
+    "tmr_splat_att": [P, P, I, I, P],
+    "tmr_splat_combine_bn": [P, P, P, P, P, I, I, I, I, P],
+    "tmr_splat_bwd_reduce_bn": [P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "tmr_splat_bn0_coefs": [P, P, P, P, P, P, P, P, P, I, I, I, P],
+    "tmr_splat_bwd_apply_bn": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "tmr_avgpool2d_fwd_a16": [P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "tmr_fill_f32": [P, L, F, P],
+    "tmr_counters_add": [P, I, ctypes.c_int64, P],
     "tmr_center_cols": [P, I, I, P, P, P],
     "tmr_axpy": [I, F, P, P, P],
     "tmr_avgpool2d_fwd": [P, P, I, I, I, I, I, I, I, I, I, I, P],
@@ -153,6 +162,7 @@ SIGNATURES = {
     "tmr_lstm_fwd": [P, I, I, I, I, P, P, P, P, P, P, P, P, SZ, P, SZ, P],
     "tmr_lstm_bwd": [P, P, I, I, I, I, P, P, P, P, SZ, P, P, P, P, P, P, SZ, P],
     "tmr_lstm_sync_status": [P, ctypes.POINTER(ctypes.c_uint), P],
+    "tmr_lstm_status_or": [P, P, P],
     "tmr_timeconv_max5_fwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_timeconv_max5_bwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],

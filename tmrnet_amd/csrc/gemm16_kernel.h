@@ -191,7 +191,7 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
       t0 += red[(q * BN + c) * 2];
       t1 += red[(q * BN + c) * 2 + 1];
     }
-    if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+    if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.part_ld + n0 + c] = make_float2(t0, t1);
   }
 }
 

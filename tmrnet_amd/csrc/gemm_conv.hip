@@ -211,9 +211,40 @@ static int stats_parts_of(const tmr_conv_desc* d) {
 static long x_frame(const tmr_conv_desc* d) { return (long)d->h * d->w * xld_of(d); }
 static long y_frame(const tmr_conv_desc* d) { return (long)d->ho * d->wo * yld_of(d); }
 
+// Grouped convolutions (tmr_conv_desc.groups = G > 1): group g reads input channels
+// [g*c/G, (g+1)*c/G) and writes output channels [g*k/G, (g+1)*k/G); each group is one launch on
+// channel slices (pixel strides = the whole tensors').  Weights per group are consecutive blocks
+// of (k/G)*(c/G)*r*s elements: KRSC (k, r, s, c/G), the transposed copy (G, c/G, r, s, k/G), and
+// OIHW gradients (k, c/G, r, s), i.e. torch's grouped Conv2d weight layout.
+static int ngroups(const tmr_conv_desc* d) { return d->groups > 1 ? d->groups : 1; }
+static int group_split(const tmr_conv_desc* d, tmr_conv_desc& g) {
+  const int G = ngroups(d);
+  TMR_CHECK_ARG(d->c % G == 0 && d->k % G == 0, "tmr_conv2d: channels %d / %d not divisible by %d groups",
+                d->c, d->k, G);
+  g = *d;
+  g.x_ld = xld_of(d);
+  g.y_ld = yld_of(d);
+  g.c = d->c / G;
+  g.k = d->k / G;
+  g.groups = 0;
+  return 0;
+}
+static long group_wsize(const tmr_conv_desc* g) { return (long)g->k * g->r * g->s * g->c; }
+
 TMR_API int tmr_conv2d_fwd(const tmr_conv_desc* d, const float* x, const float* w_krsc,
                            const float* bias, float* y, float beta, hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
+  if (ngroups(d) > 1) {
+    tmr_conv_desc g;
+    if (group_split(d, g)) return 1;
+    for (int i = 0; i < d->groups; ++i) {
+      const int rc = tmr_conv2d_fwd(&g, adv(x, (long)i * g.c, esz_x(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
+                                    bias ? bias + (long)i * g.k : nullptr,
+                                    adv(y, (long)i * g.k, esz_y(d)), beta, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   const int fc = frames_per_launch(d);
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
@@ -236,6 +267,19 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd_fused: null descriptor");
   TMR_CHECK_ARG(scale && shift, "tmr_conv2d_fwd_fused: null BatchNorm scale/shift");
   TMR_CHECK_ARG(!residual || residual != y, "tmr_conv2d_fwd_fused: residual must not alias y");
+  if (ngroups(d) > 1) {
+    tmr_conv_desc g;
+    if (group_split(d, g)) return 1;
+    for (int i = 0; i < d->groups; ++i) {
+      const long o = (long)i * g.k;
+      const int rc = tmr_conv2d_fwd_fused(&g, adv(x, (long)i * g.c, esz_x(d)),
+                                          adv(w_krsc, i * group_wsize(&g), esz_w(d)), scale + o,
+                                          shift + o, residual ? residual + o : nullptr, y + o, relu,
+                                          stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   const int fc = frames_per_launch(d);
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
@@ -258,10 +302,12 @@ TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
     tmr_set_error("tmr_conv2d_fwd_stats_parts: null or empty descriptor");
     return -1;
   }
-  const int fc = frames_per_launch(d);
+  tmr_conv_desc g = *d;
+  if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
+  const int fc = frames_per_launch(&g);
   int parts = 0;
-  for (int f0 = 0; f0 < d->n; f0 += fc) {
-    const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
+  for (int f0 = 0; f0 < g.n; f0 += fc) {
+    const tmr_conv_desc c = chunk_desc(&g, g.n - f0 < fc ? g.n - f0 : fc);
     parts += stats_parts_of(&c);
   }
   return parts;
@@ -272,17 +318,11 @@ TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const
   return tmr_conv2d_fwd_bnstats_pro(d, x, w_krsc, y, stats, stats_bytes, nullptr, stream);
 }
 
-TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
-                                       const float* w_krsc, float* y, void* stats,
-                                       size_t stats_bytes, const tmr_conv_prologue* pro,
-                                       hipStream_t stream) {
-  TMR_CHECK_ARG(d, "tmr_conv2d_fwd_bnstats: null descriptor");
-  TMR_CHECK_ARG(yld_of(d) == d->k, "tmr_conv2d_fwd_bnstats: output must be dense (y_ld == k)");
-  const size_t need = (size_t)tmr_conv2d_fwd_stats_parts(d) * d->k * sizeof(float4);
-  TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
-                stats_bytes, need);
+// stats: partial rows of part_ld columns (this launch's k columns at the pointer)
+static int fwd_bnstats_impl(const tmr_conv_desc* d, const float* x, const float* w_krsc, float* y,
+                            float4* st, int part_ld, const tmr_conv_prologue* pro,
+                            hipStream_t stream) {
   const int fc = frames_per_launch(d);
-  float4* st = (float4*)stats;
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
     GemmArgs a;
@@ -291,9 +331,34 @@ TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
     if (!rc) rc = set_prologue(a, pro, d, true, false, 0);
     if (rc) return rc;
     a.stats = st;
+    a.part_ld = part_ld;
     rc = launch_gemm<MODE_FWD>(a, al, 1, stream);
     if (rc) return rc;
-    st += (long)stats_parts_of(&c) * d->k;
+    st += (long)stats_parts_of(&c) * part_ld;
+  }
+  return 0;
+}
+
+TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
+                                       const float* w_krsc, float* y, void* stats,
+                                       size_t stats_bytes, const tmr_conv_prologue* pro,
+                                       hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_fwd_bnstats: null descriptor");
+  TMR_CHECK_ARG(yld_of(d) == d->k, "tmr_conv2d_fwd_bnstats: output must be dense (y_ld == k)");
+  const int np = tmr_conv2d_fwd_stats_parts(d);
+  TMR_CHECK_ARG(np >= 0, "tmr_conv2d_fwd_bnstats: bad descriptor");
+  const size_t need = (size_t)np * d->k * sizeof(float4);
+  TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
+                stats_bytes, need);
+  if (ngroups(d) == 1) return fwd_bnstats_impl(d, x, w_krsc, y, (float4*)stats, d->k, pro, stream);
+  TMR_CHECK_ARG(!pro, "tmr_conv2d_fwd_bnstats: operand prologues take no groups");
+  tmr_conv_desc g;
+  if (group_split(d, g)) return 1;
+  for (int i = 0; i < d->groups; ++i) {
+    const int rc = fwd_bnstats_impl(&g, adv(x, (long)i * g.c, esz_x(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
+                                    adv(y, (long)i * g.k, esz_y(d)), (float4*)stats + (long)i * g.k,
+                                    d->k, nullptr, stream);
+    if (rc) return rc;
   }
   return 0;
 }
@@ -306,6 +371,7 @@ struct BnBwdFuse {
   float2* part;
   long nparts;
   bool count_only;
+  int part_ld;   // columns per partial row (the total channels of a grouped dgrad)
 };
 
 static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
@@ -367,7 +433,8 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
         a.bn_mask = fz->mask;
         a.bn16 = (d->io & TMR_IO_BN_BF16) ? 1 : 0;
         a.bn_part = fz->part;
-        fz->part += nmt * a.N;
+        a.part_ld = fz->part_ld;
+        fz->part += nmt * fz->part_ld;
         fz->nparts += nmt;
       }
       bool al = aligned16(dy) && aligned16(w_krsc) && aligned16(dx) && a.lds % 4 == 0;
@@ -390,7 +457,7 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
                            float beta, BnBwdFuse* fz, hipStream_t stream,
                            const tmr_conv_prologue* pro = nullptr) {
   const int fc = frames_per_launch(d);
-  const long px_frame = (long)d->h * d->w * d->c;   // dense dx / y / z (checked by the caller)
+  const long px_frame = (long)d->h * d->w * xld_of(d);   // y / z laid out like dx
   float2* part0 = fz->part;
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
@@ -418,9 +485,12 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d) {
     tmr_set_error("tmr_conv2d_dgrad_bnbwd_parts: null or empty descriptor");
     return -1;
   }
+  tmr_conv_desc g = *d;
+  if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
   BnBwdFuse fz{};
   fz.count_only = true;
-  if (dgrad_bnbwd_run(d, nullptr, nullptr, nullptr, 1.f, &fz, nullptr)) return -1;
+  fz.part_ld = g.c;
+  if (dgrad_bnbwd_run(&g, nullptr, nullptr, nullptr, 1.f, &fz, nullptr)) return -1;
   return (int)fz.nparts;
 }
 
@@ -440,6 +510,8 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
                                        hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd: null descriptor");
   TMR_CHECK_ARG(xld_of(d) == d->c, "tmr_conv2d_dgrad_bnbwd: dx must be dense (x_ld == c)");
+  TMR_CHECK_ARG(ngroups(d) == 1 || (mask != 3 && !pro),
+                "tmr_conv2d_dgrad_bnbwd: a grouped dgrad takes no ReLU-mask bits / prologue");
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
                 "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
@@ -449,9 +521,27 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
   const int np = tmr_conv2d_dgrad_bnbwd_parts(d);
   TMR_CHECK_ARG(np >= 0 && parts_bytes >= (size_t)np * d->c * sizeof(float2),
                 "tmr_conv2d_dgrad_bnbwd: parts buffer too small");
+  if (ngroups(d) > 1) {
+    tmr_conv_desc g;
+    if (group_split(d, g)) return 1;
+    for (int i = 0; i < d->groups; ++i) {
+      const long o = (long)i * g.c;
+      BnBwdFuse fz{};
+      fz.y = adv(y, o, esz_bn(d)); fz.z = adv(z, o, esz_bn(d));
+      fz.sc = scale ? scale + o : nullptr; fz.sh = shift ? shift + o : nullptr; fz.mean = mean + o;
+      fz.mask = mask;
+      fz.part = (float2*)parts + o;
+      fz.part_ld = d->c;
+      const int rc = dgrad_bnbwd_run(&g, adv(dy, (long)i * g.k, esz_dy(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
+                                     dx + o, beta, &fz, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   BnBwdFuse fz{};
   fz.y = y; fz.z = z; fz.sc = scale; fz.sh = shift; fz.mean = mean; fz.mask = mask;
   fz.part = (float2*)parts;
+  fz.part_ld = d->c;
   return dgrad_bnbwd_run(d, dy, w_krsc, dx, beta, &fz, stream, pro);
 }
 
@@ -464,6 +554,17 @@ TMR_API int tmr_conv2d_dgrad_pro(const tmr_conv_desc* d, const float* dy, const 
                                  float* dx, float beta, const tmr_conv_prologue* pro,
                                  hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad: null descriptor");
+  if (ngroups(d) > 1) {
+    TMR_CHECK_ARG(!pro, "tmr_conv2d_dgrad: operand prologues take no groups");
+    tmr_conv_desc g;
+    if (group_split(d, g)) return 1;
+    for (int i = 0; i < d->groups; ++i) {
+      const int rc = tmr_conv2d_dgrad_pro(&g, adv(dy, (long)i * g.k, esz_dy(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
+                                          dx + (long)i * g.c, beta, nullptr, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   const int fc = frames_per_launch(d);
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);
@@ -521,9 +622,11 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
     tmr_set_error("tmr_conv2d_wgrad_ws_bytes: null or empty descriptor");
     return 0;
   }
+  tmr_conv_desc g = *d;
+  if (ngroups(d) > 1 && group_split(d, g)) return 0;   // one group's workspace, reused in turn
   int sp, kc;
   long slab;
-  const tmr_conv_desc c = chunk_desc(d, frames_per_launch(d));   // the largest chunk
+  const tmr_conv_desc c = chunk_desc(&g, frames_per_launch(&g));   // the largest chunk
   wgrad_plan(&c, &sp, &kc, &slab);
   return (size_t)sp * slab * sizeof(float);
 }
@@ -544,6 +647,18 @@ TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const f
                                  size_t ws_bytes, const tmr_conv_prologue* pro,
                                  hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_wgrad: null descriptor");
+  if (ngroups(d) > 1) {   // c_real = real input channels per group; dw (k, c_real, r, s)
+    TMR_CHECK_ARG(!pro, "tmr_conv2d_wgrad: operand prologues take no groups");
+    tmr_conv_desc g;
+    if (group_split(d, g)) return 1;
+    for (int i = 0; i < d->groups; ++i) {
+      const int rc = tmr_conv2d_wgrad_pro(&g, adv(x, (long)i * g.c, esz_x(d)), adv(dy, (long)i * g.k, esz_dy(d)),
+                                          dw_oihw + (long)i * g.k * c_real * g.r * g.s, c_real,
+                                          beta, ws, ws_bytes, nullptr, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   const int fc = frames_per_launch(d);
   for (int f0 = 0; f0 < d->n; f0 += fc) {
     const tmr_conv_desc c = chunk_desc(d, d->n - f0 < fc ? d->n - f0 : fc);

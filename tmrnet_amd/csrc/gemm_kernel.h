@@ -84,6 +84,9 @@ struct GemmArgs {
   const float* bn_mean;
   float2* bn_part;
   int bn_mask;
+  // row stride (columns) of the stats / bn_part partial rows: N, or the total channel count when
+  // this launch is one group of a grouped convolution (its columns are a slice of the rows)
+  int part_ld;
   // byte extents of A, B and C (buffer-descriptor range checks; C's also bounds the tensors
   // laid out like C: res, bn_y, bn_z; WGRAD: one split slab)
   uint32_t Abytes, Bbytes, Cbytes;
@@ -382,7 +385,7 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
           t0 += red[(w * BN + c) * 2];
           t1 += red[(w * BN + c) * 2 + 1];
         }
-        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.part_ld + n0 + c] = make_float2(t0, t1);
       }
     }
     return;
@@ -452,7 +455,7 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
 #pragma unroll
         for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
         if (col < a.N)
-          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
+          a.stats[(long)(m0 / BM) * a.part_ld + col] = make_float4((float)nrows, mj[j], t, 0.f);
       }
     }
   }
@@ -619,7 +622,7 @@ __device__ __forceinline__ void epilogue_guarded(const GemmArgs& a, floatx16 (&a
           t0 += red[(w * BN + c) * 2];
           t1 += red[(w * BN + c) * 2 + 1];
         }
-        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.N + n0 + c] = make_float2(t0, t1);
+        if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.part_ld + n0 + c] = make_float2(t0, t1);
       }
     }
     return;
@@ -689,7 +692,7 @@ __device__ __forceinline__ void epilogue_guarded(const GemmArgs& a, floatx16 (&a
 #pragma unroll
         for (int w = 0; w < WM; ++w) t += red[w * BN + wn * (BN / WN) + 32 * j + l31];
         if (col < a.N)
-          a.stats[(long)(m0 / BM) * a.N + col] = make_float4((float)nrows, mj[j], t, 0.f);
+          a.stats[(long)(m0 / BM) * a.part_ld + col] = make_float4((float)nrows, mj[j], t, 0.f);
       }
     }
   }

@@ -553,6 +553,33 @@ TMR_API int tmr_mul(const float* a, const float* b, const float* scalar, float* 
   return 0;
 }
 
+// ------------------------------------------------------------ small bookkeeping kernels
+namespace {
+__global__ void fill_k(float* __restrict__ x, long n, float v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+__global__ void counters_add_k(int64_t* const* __restrict__ ptrs, int n, int64_t v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) *ptrs[i] += v;
+}
+}  // namespace
+
+TMR_API int tmr_fill_f32(float* x, long n, float v, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fill_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, x, n, v);
+  TMR_CHECK_LAUNCH("fill_f32");
+  return 0;
+}
+
+TMR_API int tmr_counters_add(int64_t* const* ptrs, int n, int64_t v, hipStream_t stream) {
+  if (n <= 0) return 0;
+  TMR_CHECK_ARG(ptrs, "tmr_counters_add: null pointer table");
+  hipLaunchKernelGGL(counters_add_k, dim3(cdiv(n, NT)), dim3(NT), 0, stream, ptrs, n, v);
+  TMR_CHECK_LAUNCH("counters_add");
+  return 0;
+}
+
 // ------------------------------------------------------------ TimeConv max-of-5
 // NLBlock_MutiConv6_3.py:52-79: y = max over (x, conv3(x), conv5(x), conv7(x),
 // maxpool2(pad_left0(x))) with the first maximum winning (AdaptiveMaxPool2d / MaxPool1d

@@ -25,6 +25,11 @@ constexpr int HU = 8;          // hidden units per workgroup
 constexpr int NGC = 4 * HU;    // gate columns per workgroup
 constexpr int BBC = 16;        // clips per workgroup
 constexpr unsigned SPIN_LIMIT = 1u << 24;   // x s_sleep(1): ~0.5 s, then give up
+// TMR_LSTM_SPIN_LIMIT overrides it (tests force a give-up to check that it is reported)
+unsigned spin_limit() {
+  const char* v = getenv("TMR_LSTM_SPIN_LIMIT");
+  return v && v[0] ? (unsigned)strtoul(v, nullptr, 10) : SPIN_LIMIT;
+}
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -50,7 +55,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, uint32_t 
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
 
-__device__ bool grid_barrier(unsigned* sync, unsigned target) {
+__device__ bool grid_barrier(unsigned* sync, unsigned target, unsigned limit) {
   gu32* cnt = (gu32*)sync;
   gu32* tmo = (gu32*)(sync + 1);
   __shared__ int ok_s;
@@ -62,7 +67,7 @@ __device__ bool grid_barrier(unsigned* sync, unsigned target) {
     unsigned spins = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > SPIN_LIMIT ||
+      if (++spins > limit ||
           __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
         __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
@@ -88,7 +93,7 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_k(const float* __restrict__ 
                                                       float* __restrict__ acts,
                                                       float* __restrict__ hn,
                                                       float* __restrict__ cn, int B, int T,
-                                                      unsigned* sync) {
+                                                      unsigned* sync, unsigned limit) {
   constexpr int KG = 64;                 // k per register slice
   constexpr int HLD = LH + 4 * (LH / KG);  // padded h row: +4 floats per 64 (bank spread)
   __shared__ __attribute__((aligned(16))) float hs[BBC * HLD];
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_k(const float* __restrict__ 
         if (cn) cn[(long)cgb * LH + cj] = creg;
       }
     }
-    if (t + 1 < T && !grid_barrier(sync, (unsigned)((t + 1) * nwg))) return;
+    if (t + 1 < T && !grid_barrier(sync, (unsigned)((t + 1) * nwg), limit)) return;
   }
 }
 
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(256) void lstm_rec_bwd_k(const float* __restrict__ 
                                                       const float* __restrict__ acts,
                                                       float* __restrict__ dg,
                                                       float* __restrict__ hprev, int B, int T,
-                                                      unsigned* sync) {
+                                                      unsigned* sync, unsigned limit) {
   constexpr int G4 = 4 * LH;               // gate columns (2048)
   constexpr int KG = 64;                   // gate columns per register slice
   constexpr int NG = G4 / KG;              // 32 slices
@@ -282,7 +287,7 @@ __global__ __launch_bounds__(256) void lstm_rec_bwd_k(const float* __restrict__ 
       dc = dct * fg;
       hprev[((long)cgb * T + t) * LH + cj] = hp;
     }
-    if (t > 0 && !grid_barrier(sync, (unsigned)((T - t) * nwg))) return;
+    if (t > 0 && !grid_barrier(sync, (unsigned)((T - t) * nwg), limit)) return;
   }
 }
 
@@ -301,6 +306,11 @@ __global__ void copy_hprev_k(const float* __restrict__ y, float* __restrict__ hp
   const long bt = i / H;
   const int t = (int)(bt % T);
   hp[i] = t > 0 ? y[(bt - 1) * H + j] : 0.f;
+}
+
+// status |= timeout word of the last persistent launch on a workspace (stream-ordered, no sync)
+__global__ void status_or_k(const unsigned* __restrict__ sync, int* __restrict__ status) {
+  if (threadIdx.x == 0 && sync[1] != 0u) status[0] |= 1;
 }
 
 __global__ void copy_k(const float* __restrict__ a, float* __restrict__ o, int n) {
@@ -393,8 +403,9 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
     }
     dim3 grid(LH / HU, cdiv(b, BBC));
     const float* gxc = gx;
+    unsigned lim = spin_limit();
     void* args[] = {(void*)&gxc, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&hn,
-                    (void*)&cn, (void*)&b, (void*)&t, (void*)&sync};
+                    (void*)&cn, (void*)&b, (void*)&t, (void*)&sync, (void*)&lim};
     hipError_t e = hipLaunchCooperativeKernel((const void*)lstm_rec_fwd_k, grid, dim3(256), args,
                                               0, stream);
     if (e == hipSuccess) return 0;
@@ -463,8 +474,9 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
       return 2;
     }
     dim3 grid(LH / HU, cdiv(b, BBC));
+    unsigned lim = spin_limit();
     void* args[] = {(void*)&dy, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&dg,
-                    (void*)&hprev, (void*)&b, (void*)&t, (void*)&sync};
+                    (void*)&hprev, (void*)&b, (void*)&t, (void*)&sync, (void*)&lim};
     hipError_t e = hipLaunchCooperativeKernel((const void*)lstm_rec_bwd_k, grid, dim3(256), args,
                                               0, stream);
     if (e == hipSuccess) done = true;
@@ -518,5 +530,16 @@ TMR_API int tmr_lstm_sync_status(const void* ws, unsigned* timeout_out, hipStrea
     return 2;
   }
   *timeout_out = v[1];
+  return 0;
+}
+
+// Fold the timeout word of the last persistent launch on ws into a caller-owned device status
+// word (*status |= 1 after a give-up), enqueued on the stream: the caller checks the status at a
+// point where it synchronises anyway (tmrnet_amd/health.py: once per optimizer step), so a
+// give-up surfaces as an error instead of a silently wrong recurrence.
+TMR_API int tmr_lstm_status_or(const void* ws, int32_t* status, hipStream_t stream) {
+  TMR_CHECK_ARG(ws && status, "tmr_lstm_status_or: null pointer");
+  hipLaunchKernelGGL(status_or_k, dim3(1), dim3(64), 0, stream, (const unsigned*)ws, (int*)status);
+  TMR_CHECK_LAUNCH("lstm status_or");
   return 0;
 }

@@ -215,6 +215,283 @@ __global__ __launch_bounds__(NT) void avgpool2d_bwd_k(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split attention with bn0 + ReLU applied on load (the whole-trunk ResNeSt node, resnest.py).
+// The grouped conv's pre-BN output y2 [n][hw][2C] (bf16 under the bf16-activation contract, else
+// fp32) is the only stored tensor of the SplAtConv2d: x_r = relu(y2_r * scale + shift) -- rounded
+// to bf16 under act16, the value a stored bf16 activation would hold -- is recomputed wherever the
+// split attention reads it (GAP, weighted sum, both backward passes), so the post-BN tensor x is
+// never written and its backward (dx of the weighted sum, the ReLU mask, the BatchNorm backward of
+// bn0) runs as one reduction pass and one apply pass.
+template <typename T> struct Act;
+template <> struct Act<float> {
+  static __device__ __forceinline__ float4 ld(const float* p, long i4) {
+    return reinterpret_cast<const float4*>(p)[i4];
+  }
+  static __device__ __forceinline__ void st(float* p, long i4, float4 v) {
+    reinterpret_cast<float4*>(p)[i4] = v;
+  }
+  static __device__ __forceinline__ float rnd(float v) { return v; }
+};
+template <> struct Act<__bf16> {
+  static __device__ __forceinline__ float4 ld(const __bf16* p, long i4) {
+    const uint2 w = reinterpret_cast<const uint2*>(p)[i4];
+    return make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                       __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+  }
+  static __device__ __forceinline__ void st(__bf16* p, long i4, float4 v) {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    const b2 lo = {(__bf16)v.x, (__bf16)v.y}, hi = {(__bf16)v.z, (__bf16)v.w};
+    reinterpret_cast<uint2*>(p)[i4] = make_uint2(__builtin_bit_cast(uint32_t, lo),
+                                                 __builtin_bit_cast(uint32_t, hi));
+  }
+  static __device__ __forceinline__ float rnd(float v) { return (float)(__bf16)v; }
+};
+
+// x = rnd(relu(y * sc + sh)) per element of a channel quad
+template <typename T>
+__device__ __forceinline__ float4 bnrelu4(float4 y, float4 sc, float4 sh) {
+  return make_float4(Act<T>::rnd(fmaxf(fmaf(y.x, sc.x, sh.x), 0.f)), Act<T>::rnd(fmaxf(fmaf(y.y, sc.y, sh.y), 0.f)),
+                     Act<T>::rnd(fmaxf(fmaf(y.z, sc.z, sh.z), 0.f)), Act<T>::rnd(fmaxf(fmaf(y.w, sc.w, sh.w), 0.f)));
+}
+__device__ __forceinline__ float4 ld4f(const float* p, long i4) { return reinterpret_cast<const float4*>(p)[i4]; }
+
+// gap[n][c] = mean_hw (x0[n,hw,c] + x1[n,hw,c]) with x_r recomputed from y2 (splat_gap_k's block shape)
+template <typename T>
+__global__ __launch_bounds__(NT) void splat_gap_bn_k(const T* __restrict__ y, const float* __restrict__ sc,
+                                                     const float* __restrict__ sh, float* __restrict__ gap,
+                                                     int hw, int c4, int cols, int chunks) {
+  __shared__ Red4 lds[NT];
+  const int nn = blockIdx.x / chunks, cq = (blockIdx.x % chunks) * cols + threadIdx.x % cols;
+  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = NT / cols;
+  const bool live = cq < c4;
+  Red4 acc[1] = {{0.0, 0.0, 0.0, 0.0}};
+  if (live) {
+    const float4 s0 = ld4f(sc, cq), s1 = ld4f(sc, c4 + cq), h0 = ld4f(sh, cq), h1 = ld4f(sh, c4 + cq);
+    const long base = (long)nn * hw * 2 * c4;
+    for (int p = row; p < hw; p += rows) {
+      const long i = base + (long)p * 2 * c4;
+      red_add(acc[0], bnrelu4<T>(Act<T>::ld(y, i + cq), s0, h0));
+      red_add(acc[0], bnrelu4<T>(Act<T>::ld(y, i + c4 + cq), s1, h1));
+    }
+  }
+  red_rows<1>(acc, lds, col, row, cols, rows);
+  if (row == 0 && live) {
+    const double inv = 1.0 / (double)hw;
+    reinterpret_cast<float4*>(gap)[(long)nn * c4 + cq] =
+        make_float4((float)(acc[0].x * inv), (float)(acc[0].y * inv), (float)(acc[0].z * inv),
+                    (float)(acc[0].w * inv));
+  }
+}
+
+// att[n][r*C+c] = softmax over the radix pair of the fc2 logits zl
+__global__ __launch_bounds__(NT) void splat_att_k(const float* __restrict__ zl, float* __restrict__ att,
+                                                  int n, int C) {
+  const long total = (long)n * C;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long nn = i / C;
+    const int c = (int)(i - nn * C);
+    float a0, a1;
+    rsoft2(zl[nn * 2 * C + c], zl[nn * 2 * C + C + c], a0, a1);
+    att[nn * 2 * C + c] = a0;
+    att[nn * 2 * C + C + c] = a1;
+  }
+}
+
+// out[n,hw,c] = rnd(att0 * x0 + att1 * x1)
+template <typename T>
+__global__ __launch_bounds__(NT) void splat_combine_bn_k(const T* __restrict__ y, const float* __restrict__ sc,
+                                                         const float* __restrict__ sh, const float* __restrict__ att,
+                                                         T* __restrict__ out, int n, int hw, int c4) {
+  const long total = (long)n * hw * c4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long p = i / c4;
+    const int cq = (int)(i - p * c4);
+    const long nn = p / hw;
+    const float4 x0 = bnrelu4<T>(Act<T>::ld(y, p * 2 * c4 + cq), ld4f(sc, cq), ld4f(sh, cq));
+    const float4 x1 = bnrelu4<T>(Act<T>::ld(y, p * 2 * c4 + c4 + cq), ld4f(sc, c4 + cq), ld4f(sh, c4 + cq));
+    const float4 a0 = ld4f(att, nn * 2 * c4 + cq), a1 = ld4f(att, nn * 2 * c4 + c4 + cq);
+    Act<T>::st(out, i, make_float4(fmaf(a1.x, x1.x, a0.x * x0.x), fmaf(a1.y, x1.y, a0.y * x0.y),
+                                   fmaf(a1.z, x1.z, a0.z * x0.z), fmaf(a1.w, x1.w, a0.w * x0.w)));
+  }
+}
+
+// Backward reduction pass, per (frame, channel): for each radix r (x_r recomputed, m_r its ReLU
+// mask, d_r = y_r - mean_r)
+//   P_r = sum dout*x_r        -> dzl = softmax backward over the radix pair (weighted-sum -> att)
+//   S1 = sum m_r*dout, S2 = sum m_r, S3 = sum m_r*dout*d_r, S4 = sum m_r*d_r
+// The bn0 input gradient is g_r = m_r*(att_r*dout + dgap/hw) with dgap known only after the fc
+// backward; its BatchNorm sums over the frame are att_r*S1 + dgap/hw*S2 and att_r*S3 + dgap/hw*S4,
+// so one pass over (dout, y2) serves the attention and the BatchNorm backward.
+// sums: float [4][n][2C].
+template <typename T>
+__global__ __launch_bounds__(NT) void splat_bwd_reduce_bn_k(
+    const float* __restrict__ dout, const T* __restrict__ y, const float* __restrict__ sc,
+    const float* __restrict__ sh, const float* __restrict__ mean, const float* __restrict__ att,
+    float* __restrict__ dzl, float* __restrict__ sums, int n, int hw, int c4, int cols, int chunks) {
+  __shared__ Red4 lds[NT];
+  const int nn = blockIdx.x / chunks, cq = (blockIdx.x % chunks) * cols + threadIdx.x % cols;
+  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = NT / cols;
+  const bool live = cq < c4;
+  Red4 acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = {0.0, 0.0, 0.0, 0.0};
+  if (live) {
+    float4 s[2], h[2], mu[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      s[r] = ld4f(sc, r * c4 + cq); h[r] = ld4f(sh, r * c4 + cq); mu[r] = ld4f(mean, r * c4 + cq);
+    }
+    const long base = (long)nn * hw;
+    for (int p = row; p < hw; p += rows) {
+      const float4 g = ld4f(dout, (base + p) * c4 + cq);
+      const float gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const float4 yv = Act<T>::ld(y, (base + p) * 2 * c4 + r * c4 + cq);
+        const float ya[4] = {yv.x, yv.y, yv.z, yv.w};
+        const float sa[4] = {s[r].x, s[r].y, s[r].z, s[r].w}, ha[4] = {h[r].x, h[r].y, h[r].z, h[r].w};
+        const float ma[4] = {mu[r].x, mu[r].y, mu[r].z, mu[r].w};
+        double* a = &acc[5 * r].x;   // Red4 = 4 doubles: acc[5r + k].(x..w) = a[4k + e]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = fmaf(ya[e], sa[e], ha[e]);
+          const bool m = v > 0.f;
+          const float x = Act<T>::rnd(fmaxf(v, 0.f));
+          const double d = m ? (double)(ya[e] - ma[e]) : 0.0;
+          const double gm = m ? (double)gv[e] : 0.0;
+          a[e] = fma((double)gv[e], (double)x, a[e]);   // P
+          a[4 + e] += gm;                                // S1
+          a[8 + e] += m ? 1.0 : 0.0;                     // S2
+          a[12 + e] = fma(gm, (double)(ya[e] - ma[e]), a[12 + e]);   // S3
+          a[16 + e] += d;                                // S4
+        }
+      }
+    }
+  }
+  // tree-reduce the ten accumulators over the block's rows, one at a time through one LDS buffer
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    Red4 one[1] = {acc[k]};
+    red_rows<1>(one, lds, col, row, cols, rows);
+    acc[k] = one[0];
+    __syncthreads();
+  }
+  if (row == 0 && live) {
+    const int C = 4 * c4;
+    const long plane = (long)n * 2 * C;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * cq + e;
+      const long i0 = (long)nn * 2 * C + c;
+      const double p0 = (&acc[0].x)[e], p1 = (&acc[5].x)[e];
+      const double a0 = att[i0], a1 = att[i0 + C];
+      const double dot = a0 * p0 + a1 * p1;
+      dzl[i0] = (float)(a0 * (p0 - dot));
+      dzl[i0 + C] = (float)(a1 * (p1 - dot));
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          sums[k * plane + i0 + r * C] = (float)(&acc[5 * r + 1 + k].x)[e];
+    }
+  }
+}
+
+// per channel j of the 2C bn0 channels (r = j / C, c = j % C), frames summed in order:
+//   sg = sum_n att*S1 + dgap/hw*S2 = sum g,  sgx = sum_n att*S3 + dgap/hw*S4 = sum g*(y - mean)
+// -> dbeta = sg, dgamma = sgx*invstd, coef[3][2C] = (gamma*invstd, sg/N, invstd^2*sgx/N):
+//   dy = coef0 * (g - coef1 - (y - mean) * coef2)   (nn.BatchNorm2d's batch-statistics backward)
+__global__ __launch_bounds__(NT) void splat_bn0_coefs_k(const float* __restrict__ att, const float* __restrict__ dgap,
+                                                        const float* __restrict__ sums, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                                        float* __restrict__ coef, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta, int n, int hw, int C) {
+  const int j = blockIdx.x * NT + threadIdx.x;
+  if (j >= 2 * C) return;
+  const int c = j % C;
+  const long plane = (long)n * 2 * C;
+  const double ihw = 1.0 / (double)hw;
+  double sg = 0.0, sgx = 0.0;
+  for (int nn = 0; nn < n; ++nn) {
+    const long i = (long)nn * 2 * C + j;
+    const double a = att[i], dg = (double)dgap[(long)nn * C + c] * ihw;
+    sg += a * sums[i] + dg * sums[2 * plane + i];
+    sgx += a * sums[plane + i] + dg * sums[3 * plane + i];
+  }
+  (void)mean;
+  const double inv = invstd[j], N = (double)n * hw;
+  dbeta[j] = (float)sg;
+  dgamma[j] = (float)(sgx * inv);
+  coef[j] = (float)((double)gamma[j] * inv);
+  coef[2 * C + j] = (float)(sg / N);
+  coef[4 * C + j] = (float)(inv * inv * sgx / N);
+}
+
+// dy[n,hw,j] = coef0 * (g - coef1 - (y - mean) * coef2), g = m*(att*dout + dgap/hw)
+template <typename T>
+__global__ __launch_bounds__(NT) void splat_bwd_apply_bn_k(
+    const float* __restrict__ dout, const T* __restrict__ y, const float* __restrict__ sc,
+    const float* __restrict__ sh, const float* __restrict__ mean, const float* __restrict__ att,
+    const float* __restrict__ dgap, const float* __restrict__ coef, T* __restrict__ dy, int n,
+    int hw, int c4) {
+  const long total = (long)n * hw * 2 * c4;
+  const float ihw = 1.0f / (float)hw;
+  const int j4 = 2 * c4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const long p = i / j4;
+    const int jq = (int)(i - p * j4);
+    const int cq = jq < c4 ? jq : jq - c4;
+    const long nn = p / hw;
+    const float4 yv = Act<T>::ld(y, i);
+    const float4 g0 = ld4f(dout, p * c4 + cq);
+    const float4 a = ld4f(att, nn * j4 + jq);
+    const float4 dg = ld4f(dgap, nn * c4 + cq);
+    const float4 s = ld4f(sc, jq), h = ld4f(sh, jq), mu = ld4f(mean, jq);
+    const float4 k0 = ld4f(coef, jq), k1 = ld4f(coef, j4 + jq), k2 = ld4f(coef, 2 * j4 + jq);
+    auto one = [&](float yv_, float s_, float h_, float mu_, float g_, float a_, float dg_, float k0_,
+                   float k1_, float k2_) {
+      const float gg = fmaf(yv_, s_, h_) > 0.f ? fmaf(a_, g_, dg_ * ihw) : 0.f;
+      return k0_ * (gg - k1_ - (yv_ - mu_) * k2_);
+    };
+    Act<T>::st(dy, i, make_float4(one(yv.x, s.x, h.x, mu.x, g0.x, a.x, dg.x, k0.x, k1.x, k2.x),
+                                  one(yv.y, s.y, h.y, mu.y, g0.y, a.y, dg.y, k0.y, k1.y, k2.y),
+                                  one(yv.z, s.z, h.z, mu.z, g0.z, a.z, dg.z, k0.z, k1.z, k2.z),
+                                  one(yv.w, s.w, h.w, mu.w, g0.w, a.w, dg.w, k0.w, k1.w, k2.w)));
+  }
+}
+
+// AvgPool2d of bf16 activations (avd layer, avg_down): fp32 sums of the bf16 inputs, output rounded
+__global__ __launch_bounds__(NT) void avgpool2d_fwd_a16_k(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+                                                          int n, int h, int w, int c4, int ho, int wo,
+                                                          int k, int s, int p, int incl) {
+  const long total = (long)n * ho * wo * c4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int cq = (int)(i % c4);
+    long t = i / c4;
+    const int ox = (int)(t % wo);
+    t /= wo;
+    const int oy = (int)(t % ho);
+    const int nn = (int)(t / ho);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+    for (int dy = 0; dy < k; ++dy) {
+      const int iy = oy * s - p + dy;
+      if (iy < 0 || iy >= h) continue;
+      for (int dx = 0; dx < k; ++dx) {
+        const int ix = ox * s - p + dx;
+        if (ix < 0 || ix >= w) continue;
+        const float4 v = Act<__bf16>::ld(x, (((long)nn * h + iy) * w + ix) * c4 + cq);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        ++cnt;
+      }
+    }
+    const float inv = 1.0f / (float)(incl ? k * k : (cnt > 0 ? cnt : 1));
+    acc.x *= inv; acc.y *= inv; acc.z *= inv; acc.w *= inv;
+    Act<__bf16>::st(y, i, acc);
+  }
+}
+
 // one thread per column: rows are few (frames), columns <= 512
 __global__ __launch_bounds__(NT) void center_cols_k(const float* __restrict__ x, int rows, int cols,
                                                     float* __restrict__ center, float* __restrict__ xc) {
@@ -303,5 +580,97 @@ TMR_API int tmr_avgpool2d_bwd(const float* dy, float* dx, int n, int h, int w, i
   hipLaunchKernelGGL(avgpool2d_bwd_k, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
                      dy, dx, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
   TMR_CHECK_LAUNCH("avgpool2d_bwd");
+  return 0;
+}
+
+TMR_API int tmr_splat_gap_bn(const void* y, const float* scale, const float* shift, float* gap,
+                             int n, int hw, int c, int act16, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && n > 0 && hw > 0, "tmr_splat_gap_bn: bad shape n %d hw %d c %d", n, hw, c);
+  int cols, chunks;
+  red_shape(c / 4, cols, chunks);
+  if (act16)
+    hipLaunchKernelGGL(splat_gap_bn_k<__bf16>, dim3(n * chunks), dim3(NT), 0, stream,
+                       (const __bf16*)y, scale, shift, gap, hw, c / 4, cols, chunks);
+  else
+    hipLaunchKernelGGL(splat_gap_bn_k<float>, dim3(n * chunks), dim3(NT), 0, stream,
+                       (const float*)y, scale, shift, gap, hw, c / 4, cols, chunks);
+  TMR_CHECK_LAUNCH("splat_gap_bn");
+  return 0;
+}
+
+TMR_API int tmr_splat_att(const float* zl, float* att, int n, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && c > 0, "tmr_splat_att: bad shape n %d c %d", n, c);
+  hipLaunchKernelGGL(splat_att_k, dim3(blocks_for((long)n * c)), dim3(NT), 0, stream, zl, att, n, c);
+  TMR_CHECK_LAUNCH("splat_att");
+  return 0;
+}
+
+TMR_API int tmr_splat_combine_bn(const void* y, const float* scale, const float* shift,
+                                 const float* att, void* out, int n, int hw, int c, int act16,
+                                 hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_splat_combine_bn: channels %d must be a multiple of 4", c);
+  const int nb = blocks_for((long)n * hw * c / 4);
+  if (act16)
+    hipLaunchKernelGGL(splat_combine_bn_k<__bf16>, dim3(nb), dim3(NT), 0, stream, (const __bf16*)y,
+                       scale, shift, att, (__bf16*)out, n, hw, c / 4);
+  else
+    hipLaunchKernelGGL(splat_combine_bn_k<float>, dim3(nb), dim3(NT), 0, stream, (const float*)y,
+                       scale, shift, att, (float*)out, n, hw, c / 4);
+  TMR_CHECK_LAUNCH("splat_combine_bn");
+  return 0;
+}
+
+TMR_API int tmr_splat_bwd_reduce_bn(const float* dout, const void* y, const float* scale,
+                                    const float* shift, const float* mean, const float* att,
+                                    float* dzl, float* sums, int n, int hw, int c, int act16,
+                                    hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && n > 0 && hw > 0, "tmr_splat_bwd_reduce_bn: bad shape n %d hw %d c %d", n, hw, c);
+  int cols, chunks;
+  red_shape(c / 4, cols, chunks);
+  if (act16)
+    hipLaunchKernelGGL(splat_bwd_reduce_bn_k<__bf16>, dim3(n * chunks), dim3(NT), 0, stream, dout,
+                       (const __bf16*)y, scale, shift, mean, att, dzl, sums, n, hw, c / 4, cols, chunks);
+  else
+    hipLaunchKernelGGL(splat_bwd_reduce_bn_k<float>, dim3(n * chunks), dim3(NT), 0, stream, dout,
+                       (const float*)y, scale, shift, mean, att, dzl, sums, n, hw, c / 4, cols, chunks);
+  TMR_CHECK_LAUNCH("splat_bwd_reduce_bn");
+  return 0;
+}
+
+TMR_API int tmr_splat_bn0_coefs(const float* att, const float* dgap, const float* sums,
+                                const float* mean, const float* invstd, const float* gamma,
+                                float* coef, float* dgamma, float* dbeta, int n, int hw, int c,
+                                hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && hw > 0 && c > 0, "tmr_splat_bn0_coefs: bad shape n %d hw %d c %d", n, hw, c);
+  hipLaunchKernelGGL(splat_bn0_coefs_k, dim3(cdiv(2L * c, NT)), dim3(NT), 0, stream, att, dgap, sums,
+                     mean, invstd, gamma, coef, dgamma, dbeta, n, hw, c);
+  TMR_CHECK_LAUNCH("splat_bn0_coefs");
+  return 0;
+}
+
+TMR_API int tmr_splat_bwd_apply_bn(const float* dout, const void* y, const float* scale,
+                                   const float* shift, const float* mean, const float* att,
+                                   const float* dgap, const float* coef, void* dy, int n, int hw,
+                                   int c, int act16, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_splat_bwd_apply_bn: channels %d must be a multiple of 4", c);
+  const int nb = blocks_for((long)n * hw * 2 * c / 4);
+  if (act16)
+    hipLaunchKernelGGL(splat_bwd_apply_bn_k<__bf16>, dim3(nb), dim3(NT), 0, stream, dout,
+                       (const __bf16*)y, scale, shift, mean, att, dgap, coef, (__bf16*)dy, n, hw, c / 4);
+  else
+    hipLaunchKernelGGL(splat_bwd_apply_bn_k<float>, dim3(nb), dim3(NT), 0, stream, dout,
+                       (const float*)y, scale, shift, mean, att, dgap, coef, (float*)dy, n, hw, c / 4);
+  TMR_CHECK_LAUNCH("splat_bwd_apply_bn");
+  return 0;
+}
+
+TMR_API int tmr_avgpool2d_fwd_a16(const void* x, void* y, int n, int h, int w, int c, int ho,
+                                  int wo, int k, int s, int p, int count_include_pad,
+                                  hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_fwd_a16: channels %d must be a multiple of 4", c);
+  hipLaunchKernelGGL(avgpool2d_fwd_a16_k, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
+                     stream, (const __bf16*)x, (__bf16*)y, n, h, w, c / 4, ho, wo, k, s, p,
+                     count_include_pad);
+  TMR_CHECK_LAUNCH("avgpool2d_fwd_a16");
   return 0;
 }

@@ -19,6 +19,8 @@ Semantics kept from torch.optim + DataParallel:
 * ``p.grad is None`` stays None when it is None on every rank (torch.optim.SGD then skips the
   parameter); a presence flag per parameter rides in the same bucket, so no extra collective.
 """
+import warnings
+
 import torch
 
 _flatten = torch._utils._flatten_dense_tensors
@@ -53,6 +55,7 @@ class GradAllReduce:
         self.early_ids = set()  # params whose reduced gradient an early launch will deliver
         self.stale_ids = set()  # early-launched params touched again by a later backward
         self.overlap = bool(overlap) and self._multi()
+        self._warned_accum = False
         share = getattr(model, "share", None)
         if self.overlap and share is not None:
             from .trunk import set_grad_ready
@@ -79,6 +82,12 @@ class GradAllReduce:
             return
         # accumulating into an existing gradient: the launch would miss the earlier part
         if any(p.grad is not None for p in params):
+            if not self._warned_accum:
+                self._warned_accum = True
+                warnings.warn("GradAllReduce: trunk gradients already exist at backward time "
+                              "(zero_grad(set_to_none=False) or gradient accumulation), so the "
+                              "backward/all-reduce overlap is off for them; use "
+                              "optimizer.zero_grad(set_to_none=True) to keep it", RuntimeWarning)
             return
         flat = _flatten([g for _, g in pairs])
         self.early.append((params, flat, self.dist.all_reduce(flat, async_op=True)))

@@ -1,0 +1,79 @@
+"""Device-side health word of the train step: failures that kernels can only report on the device
+(today: a persistent LSTM launch that gave up a grid barrier, include/tmr.h tmr_lstm_status_or)
+are OR-ed into one int32 per device, stream-ordered and without a host sync.
+
+`check()` is called once per optimizer step (optim.SGD / Adam .step()).  It never stalls the
+stream: it starts an asynchronous copy of the word into pinned host memory and raises on the value
+of the PREVIOUS step's copy once that copy has landed (so a failure surfaces at most one step
+later, before the model trains on it for long).  `check(sync=True)` waits and checks now (tests,
+end of training).  Reference counterpart: the LSTM of train_only_non-local_pretrained.py:215,
+:230-231, which cannot fail this way on cuDNN.
+"""
+import torch
+
+from ._lib import call, stream_ptr
+
+_STATE = {}   # device index -> [status (device int32), host copy (pinned), event or None]
+
+LSTM_TIMEOUT = 1
+
+
+def status_word(device):
+    """The device status word (int32, zeroed at creation) kernels OR their failures into."""
+    idx = torch.device(device).index or 0
+    st = _STATE.get(idx)
+    if st is None:
+        dev = torch.device("cuda", idx)
+        word = torch.empty(1, dtype=torch.int32, device=dev)
+        call("tmr_fill_f32", word, 1, 0.0, stream_ptr(dev))   # all-zero bits = int32 0
+        st = _STATE[idx] = [word, torch.zeros(1, dtype=torch.int32, pin_memory=True), None]
+    return st[0]
+
+
+def note_lstm(ws):
+    """Enqueue status |= (timeout word of the persistent LSTM launch on ws)."""
+    call("tmr_lstm_status_or", ws, status_word(ws.device), stream_ptr())
+
+
+def _raise(v):
+    if v & LSTM_TIMEOUT:
+        raise RuntimeError("persistent LSTM kernel gave up a grid barrier (its recurrence results "
+                           "are invalid): the GPU was shared or oversubscribed -- rerun with "
+                           "TMR_LSTM_PERSIST=0 (per-step path) or free the device")
+    raise RuntimeError("device status word %#x" % v)
+
+
+def check(sync=False, device=None):
+    """Raise RuntimeError if a device-side failure was recorded (see module doc)."""
+    idxs = list(_STATE) if device is None else [torch.device(device).index or 0]
+    for idx in idxs:
+        st = _STATE.get(idx)
+        if st is None:
+            continue
+        status, host, ev = st
+        if sync:
+            torch.cuda.synchronize(status.device)
+            v = int(status.item())
+            if v:
+                _raise(v)
+            continue
+        if ev is not None and ev.query():
+            v = int(host.item())
+            if v:
+                _raise(v)
+            st[2] = None
+        if st[2] is None:
+            host.copy_(status, non_blocking=True)
+            e = torch.cuda.Event()
+            e.record()
+            st[2] = e
+
+
+def reset(device=None):
+    """Clear the recorded status (tests)."""
+    for idx, st in list(_STATE.items()):
+        if device is None or idx == (torch.device(device).index or 0):
+            torch.cuda.synchronize(st[0].device)
+            st[0].zero_()
+            st[1].zero_()
+            st[2] = None

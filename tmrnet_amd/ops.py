@@ -8,6 +8,7 @@ anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 import torch
 
 from ._lib import call, query, stream_ptr, ConvDesc, ConvPrologue
+from . import health
 import ctypes
 
 f32 = torch.float32
@@ -93,12 +94,17 @@ def _io(x=None, w=None, dy=None, wt=False):
     return io
 
 
-def _dgrad_w(w, wt):
-    """(k, r, s, c) of a dgrad weight operand: KRSC, or with wt the transposed CRSK copy."""
+def _dgrad_w(w, wt, groups=1):
+    """(k, r, s, c) totals of a dgrad weight operand: KRSC (k, r, s, c/groups), or with wt the
+    transposed copy (c, r, s, k) -- per group (groups, c/groups, r, s, k/groups)."""
+    if wt and groups > 1:
+        g, cg, r, s, kg = w.shape
+        return kg * g, r, s, cg * g
     if wt:
         c, r, s, k = w.shape
     else:
         k, r, s, c = w.shape
+        c *= groups
     return k, r, s, c
 
 
@@ -106,7 +112,8 @@ def _esz(t):
     return t.element_size() if t is not None else 4
 
 
-def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math="fp32", io=0):
+def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math="fp32", io=0,
+              groups=1):
     pad_w = pad if pad_w is None else pad_w
     ho = (h + 2 * pad - r) // stride + 1
     wo = (w + 2 * pad_w - s) // stride + 1
@@ -115,7 +122,7 @@ def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math
     if io & IO_WT32 and math != "fp32":
         raise RuntimeError("fp32 transposed weights (TMR_IO_WT_F32) need math='fp32'")
     return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
-                    MAX_FRAMES, io)
+                    MAX_FRAMES, io, groups if groups > 1 else 0)
 
 
 def _req_op(t, name):
@@ -183,22 +190,24 @@ def _prologue(xpro=None, dpro=None):
 
 
 def conv_fwd_bnstats(x, w_krsc, stride, pad, c_real=None, pad_w=None, math="fp32", xpro=None,
-                     y16=False):
+                     y16=False, groups=1):
     """conv_fwd whose epilogue also emits BatchNorm partials; returns (y, stats, nparts).
     xpro = (scale, shift): x is a pre-BN tensor read as relu(x*scale + shift) (0 at padding).
-    y16: y stored rounded to bf16, the partials describing the rounded values (TMR_IO_Y_BF16)."""
+    y16: y stored rounded to bf16, the partials describing the rounded values (TMR_IO_Y_BF16).
+    groups: a grouped conv (w_krsc (K, R, S, C/groups), torch's grouped layout); c_real is the
+    total real input channels."""
     _req_op(x, "x"); _req_op(w_krsc, "w")
     n, h, w, c = x.shape
     k, r, s, c2 = w_krsc.shape
-    assert c == c2, (x.shape, w_krsc.shape)
+    assert c == c2 * groups, (x.shape, w_krsc.shape, groups)
     d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math,
-                  io=_io(x, w_krsc) | (IO_Y if y16 else 0))
+                  io=_io(x, w_krsc) | (IO_Y if y16 else 0), groups=groups)
     out = _empty((n, d.ho, d.wo, k), x, dtype=BF16 if y16 else f32)
     nparts = query("tmr_conv2d_fwd_stats_parts", ctypes.byref(d))
     stats = torch.empty((nparts, k, 4), dtype=f32, device=x.device)
-    with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c),
+    with _prof("conv_fwd" + _SUFFIX[math], 2.0 * n * d.ho * d.wo * k * r * s * (c_real or c) / groups,
                (n, h, w, c, k, r, stride),
-               _esz(x) * n * h * w * c + _esz(w_krsc) * k * r * s * c
+               _esz(x) * n * h * w * c + _esz(w_krsc) * k * r * s * c2
                + out.element_size() * n * d.ho * d.wo * k + stats.numel() * 4):
         pro = _prologue(xpro)
         if pro is None:
@@ -223,23 +232,24 @@ def bn_finalize(stats, nparts, gamma, beta, running_mean, running_var, momentum,
 
 
 def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, math="fp32",
-               dpro=None, wt=False):
+               dpro=None, wt=False, groups=1):
     """dy (N,Ho,Wo,K), w_krsc (K,R,S,C) -> dx (N,H,W,C) (dy/out may be channel slices).
     dpro = (y, coef): dy is the masked BN-output gradient g, read as the BN backward
     A*g + B*y + C (tmr_bn_bwd_coefs).  wt: w_krsc is the transposed copy (C,R,S,K)
     (weight_to_crsk; the LDS-DMA engine: bf16 with bf16 dy, or fp32 with fp32 math)."""
     _req_op(w_krsc, "w")
     n, ho, wo, k = dy.shape
-    k2, r, s, c = _dgrad_w(w_krsc, wt)
+    k2, r, s, c = _dgrad_w(w_krsc, wt, groups)
     h, w = in_hw
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(None, w_krsc, dy, wt))
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(None, w_krsc, dy, wt),
+                  groups=groups)
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
-    with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
-               _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * k * r * s * c
+    with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c / groups, (n, h, w, c, k, r, stride),
+               _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * w_krsc.numel()
                + 4 * n * h * w * c * (2 if beta else 1)):
         pro = _prologue(None, dpro)
         if pro is None:
@@ -251,7 +261,7 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
 
 
 def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scale=None,
-                     shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False):
+                     shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False, groups=1):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts).
     wt: as conv_dgrad.  y / z may be bf16 (the bf16-activation step, TMR_IO_BN_BF16)."""
@@ -262,10 +272,10 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     elif z is not None and z.dtype != y.dtype:
         raise RuntimeError("conv_dgrad_bnbwd: y and z must have one dtype")
     n, ho, wo, k = dy.shape
-    k2, r, s, c = _dgrad_w(w_krsc, wt)
+    k2, r, s, c = _dgrad_w(w_krsc, wt, groups)
     h, w = in_hw
     d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math,
-                  io=_io(None, w_krsc, dy, wt) | (IO_BN if y.dtype == BF16 else 0))
+                  io=_io(None, w_krsc, dy, wt) | (IO_BN if y.dtype == BF16 else 0), groups=groups)
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
         out = _empty((n, h, w, c), dy)
@@ -278,8 +288,8 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     if nparts < 0:
         raise RuntimeError("tmr_conv2d_dgrad_bnbwd_parts failed")
     parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
-    with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c, (n, h, w, c, k, r, stride),
-               _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * k * r * s * c
+    with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c / groups, (n, h, w, c, k, r, stride),
+               _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * w_krsc.numel()
                + 4 * n * h * w * c * (2 if beta else 1)
                + y.element_size() * n * h * w * c * (2 if z is not None and mask != 3 else 1)
                + (n * h * w * c // 8 if mask == 3 else 0)):
@@ -363,14 +373,15 @@ def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma, bf16=False):
 
 
 def conv_wgrad(x, dy, r, s, stride, pad, c_real=None, out=None, beta=0.0, pad_w=None,
-               math="fp32", xpro=None, dpro=None):
+               math="fp32", xpro=None, dpro=None, groups=1):
     """x (N,H,W,C), dy (N,Ho,Wo,K) -> dW (K, c_real, R, S) in OIHW (x/dy may be channel slices).
     xpro = (scale, shift): x read as relu(x*scale + shift); dpro = (y, coef): dy read as the BN
-    backward A*dy + B*y + C."""
+    backward A*dy + B*y + C.  groups: c_real = real input channels per group."""
     n, h, w, c = x.shape
     k = dy.shape[3]
-    c_real = c if c_real is None else c_real
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, None, dy))
+    c_real = c // groups if c_real is None else c_real
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w, math=math, io=_io(x, None, dy),
+                  groups=groups)
     d.x_ld = _nhwc_ld(x, "x")
     d.y_ld = _nhwc_ld(dy, "dy")
     assert (d.ho, d.wo) == tuple(dy.shape[1:3])
@@ -459,6 +470,18 @@ def weight_to_crsk(w, bf16=True):
     k, c, r, s = w.shape
     out = _empty((c, r, s, k), w, dtype=torch.bfloat16 if bf16 else f32)
     call("tmr_weight_oihw_to_crsk_x", _req(w, "w"), out, k, c, r, s, int(bf16), stream_ptr())
+    return out
+
+
+def weight_to_crsk_grouped(w, groups, bf16=True):
+    """Grouped OIHW (K, C/G, R, S) -> the per-group transposed dgrad operand (G, C/G, R, S, K/G)."""
+    k, cg, r, s = w.shape
+    kg = k // groups
+    out = _empty((groups, cg, r, s, kg), w, dtype=torch.bfloat16 if bf16 else f32)
+    _req(w, "w")
+    for g in range(groups):
+        call("tmr_weight_oihw_to_crsk_x", w[g * kg:(g + 1) * kg], out[g], kg, cg, r, s, int(bf16),
+             stream_ptr())
     return out
 
 
@@ -895,6 +918,7 @@ def lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, train=True):
     ws = _ws(query("tmr_lstm_ws_bytes", B, T, I, H), x)
     call("tmr_lstm_fwd", x, B, T, I, H, w_ih, w_hh, b_ih, b_hh, y, hn, cn, saved,
          saved.numel() if saved is not None else 0, ws, ws.numel(), stream_ptr())
+    health.note_lstm(ws)   # a grid-barrier give-up is raised at the next optimizer step
     return y, hn, cn, saved, ws
 
 
@@ -909,6 +933,7 @@ def lstm_bwd(dy, x, w_ih, w_hh, y, saved, want_dx=True):
     ws = _ws(query("tmr_lstm_ws_bytes", B, T, I, H), x)
     call("tmr_lstm_bwd", dy, x, B, T, I, H, w_ih, w_hh, y, saved, saved.numel(), dx, dw_ih, dw_hh,
          db_ih, db_hh, ws, ws.numel(), stream_ptr())
+    health.note_lstm(ws)
     return dx, dw_ih, dw_hh, db_ih, db_hh, ws
 
 
@@ -951,3 +976,127 @@ def lstm_cell_bwd(dh_out_t, dh_rec, dc_next, act_t, c_t, c_prev, dg_t, dc_prev):
     B, H = c_t.shape
     call("tmr_lstm_cell_bwd", dh_out_t, dh_out_t.stride(0), dh_rec, dc_next, act_t, c_t, c_prev,
          dg_t, dg_t.stride(0), dc_prev, B, H, stream_ptr())
+
+
+# ------------------------------------------- ResNeSt split attention, bn0 applied on load
+def _act16(y):
+    if y.dtype not in (f32, BF16):
+        raise RuntimeError("split attention: y must be fp32 or bf16, got %s" % y.dtype)
+    return int(y.dtype == BF16)
+
+
+def splat_gap_bn(y2, scale, shift):
+    """gap[n][c] = mean_hw(x_0 + x_1), x_r = relu(bn0(y2_r)) recomputed (tmr_splat_gap_bn)."""
+    _req(y2, "y2", y2.dtype)
+    n, h, w, c2 = y2.shape
+    gap = _empty((n, c2 // 2), y2)
+    call("tmr_splat_gap_bn", y2, scale, shift, gap, n, h * w, c2 // 2, _act16(y2), stream_ptr())
+    return gap
+
+
+def splat_att(zl):
+    """r-softmax over the radix pair of the fc2 logits zl (n, 2C) -> att (n, 2C)."""
+    n, c2 = zl.shape
+    att = torch.empty_like(zl)
+    call("tmr_splat_att", _req(zl, "zl"), att, n, c2 // 2, stream_ptr())
+    return att
+
+
+def splat_combine_bn(y2, scale, shift, att):
+    """out = att_0*x_0 + att_1*x_1 (dtype of y2) -> (n, h, w, C)."""
+    _req(y2, "y2", y2.dtype)
+    n, h, w, c2 = y2.shape
+    out = torch.empty((n, h, w, c2 // 2), dtype=y2.dtype, device=y2.device)
+    call("tmr_splat_combine_bn", y2, scale, shift, att, out, n, h * w, c2 // 2, _act16(y2),
+         stream_ptr())
+    return out
+
+
+def splat_bwd_reduce_bn(dout, y2, scale, shift, mean, att):
+    """-> (dzl (n, 2C), sums (4, n, 2C)) of tmr_splat_bwd_reduce_bn."""
+    _req(dout, "dout"); _req(y2, "y2", y2.dtype)
+    n, h, w, c2 = y2.shape
+    if tuple(dout.shape) != (n, h, w, c2 // 2):
+        raise RuntimeError("splat_bwd_reduce_bn: dout %s vs y2 %s" % (tuple(dout.shape), tuple(y2.shape)))
+    dzl = _empty((n, c2), dout)
+    sums = _empty((4, n, c2), dout)
+    call("tmr_splat_bwd_reduce_bn", dout, y2, scale, shift, mean, att, dzl, sums, n, h * w, c2 // 2,
+         _act16(y2), stream_ptr())
+    return dzl, sums
+
+
+def splat_bn0_coefs(att, dgap, sums, mean, inv, gamma, hw):
+    """bn0 backward from the reduction sums -> (coef (3, 2C), dgamma, dbeta)."""
+    n, c2 = att.shape
+    coef = _empty((3, c2), att)
+    dgamma = _empty((c2,), att); dbeta = _empty((c2,), att)
+    call("tmr_splat_bn0_coefs", att, _req(dgap, "dgap"), sums, mean, inv, gamma, coef, dgamma, dbeta,
+         n, hw, c2 // 2, stream_ptr())
+    return coef, dgamma, dbeta
+
+
+def splat_bwd_apply_bn(dout, y2, scale, shift, mean, att, dgap, coef):
+    """dy2 (dtype of y2: the grouped conv's dgrad / wgrad operand) of tmr_splat_bwd_apply_bn."""
+    n, h, w, c2 = y2.shape
+    dy = torch.empty_like(y2)
+    call("tmr_splat_bwd_apply_bn", dout, y2, scale, shift, mean, att, dgap, coef, dy, n, h * w,
+         c2 // 2, _act16(y2), stream_ptr())
+    return dy
+
+
+def avgpool2d_fwd(x, k, s, p, count_include_pad, ceil_mode):
+    """nn.AvgPool2d on NHWC fp32 or bf16 (bf16: fp32 sums, rounded output) -> (y, geometry)."""
+    n, h, w, c = x.shape
+    ho, wo = pool_out(h, k, s, p, ceil_mode), pool_out(w, k, s, p, ceil_mode)
+    y = torch.empty((n, ho, wo, c), dtype=x.dtype, device=x.device)
+    name = "tmr_avgpool2d_fwd_a16" if x.dtype == BF16 else "tmr_avgpool2d_fwd"
+    call(name, _req(x, "x", x.dtype), y, n, h, w, c, ho, wo, k, s, p, int(count_include_pad),
+         stream_ptr())
+    return y
+
+
+def avgpool2d_bwd(dy, in_hw, k, s, p, count_include_pad):
+    """Gradient of avgpool2d_fwd (fp32) -> dx (n, h, w, c)."""
+    n, ho, wo, c = dy.shape
+    h, w = in_hw
+    dx = _empty((n, h, w, c), dy)
+    call("tmr_avgpool2d_bwd", _req(dy, "dy"), dx, n, h, w, c, ho, wo, k, s, p,
+         int(count_include_pad), stream_ptr())
+    return dx
+
+
+def pool_out(h, k, s, p, ceil):
+    """Output size of a pooling window (PyTorch's rule, incl. ceil_mode)."""
+    if not ceil:
+        return (h + 2 * p - k) // s + 1
+    o = -(-(h + 2 * p - k) // s) + 1
+    if (o - 1) * s >= h + p:   # last window must start inside the input
+        o -= 1
+    return o
+
+
+# ------------------------------------------------------------------- bookkeeping
+def zeros(shape, like):
+    """fp32 zeros on like's device from libtmr's fill kernel."""
+    out = torch.empty(shape, dtype=f32, device=like.device)
+    call("tmr_fill_f32", out, ctypes.c_long(out.numel()), 0.0, stream_ptr())
+    return out
+
+
+# device pointer tables of counter sets, keyed by their addresses; the entry holds the counters
+# themselves so their memory cannot be reused while the table points at it
+_COUNTER_TABLES = {}
+
+
+def counters_add_one(counters):
+    """counters[i] += 1 for every int64 counter (BatchNorm num_batches_tracked) in one launch."""
+    if not counters:
+        return
+    key = tuple(t.data_ptr() for t in counters)
+    ent = _COUNTER_TABLES.get(key)
+    if ent is None:
+        for t in counters:
+            _req(t, "counter", torch.int64)
+        tab = torch.tensor(key, dtype=torch.int64).to(counters[0].device)
+        ent = _COUNTER_TABLES[key] = (tab, list(counters))
+    call("tmr_counters_add", ent[0], len(counters), 1, stream_ptr())

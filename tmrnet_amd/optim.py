@@ -12,6 +12,7 @@ import numpy as np
 import torch
 
 from ._lib import call, query, stream_ptr
+from . import health
 
 _ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("buf", "<u8"), ("n", "<i8"),
                    ("block_begin", "<i8"), ("lr", "<f4"), ("momentum", "<f4"),
@@ -35,6 +36,7 @@ class SGD(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        health.check()   # device-side failures of earlier steps (no sync; health.py)
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -113,6 +115,7 @@ class Adam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        health.check()   # device-side failures of earlier steps (no sync; health.py)
         loss = None
         if closure is not None:
             with torch.enable_grad():

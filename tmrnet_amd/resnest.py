@@ -6,7 +6,23 @@ avg_down shortcut, avd pooling on strided blocks): same child names and state_di
 (``share.conv1.0.weight``, ``share.layer1.0.conv2.conv.weight``, ``...conv2.fc1.bias``, ...),
 25,434,240 parameters.
 
-Each stage is an autograd node over HIP kernels, activations NHWC:
+Train mode (fp32 math, or bf16 math under the bf16-activation contract): the whole trunk is ONE
+autograd node, `ResNeStTrunkFn`, built on trunk.py's conv-unit engine (the ResNet-50 TrunkFn's):
+  * every conv runs on the LDS-DMA implicit-GEMM engine with its BatchNorm statistics from the
+    epilogue -- the radix-2 grouped 3x3 included (tmr_conv_desc.groups: one launch per group on
+    channel slices, one BN-partial row over all channels);
+  * bf16 math stores every activation as bf16 (the C5 contract of trunk.py ACT16: conv outputs
+    rounded by their epilogue, BN(+residual)(+ReLU) outputs computed in fp32 and rounded);
+  * bn0 + ReLU of SplAtConv2d are applied on load by the split-attention kernels
+    (tmr_splat_*_bn): the post-BN tensor is never written, and its backward -- weighted-sum
+    gradient, ReLU mask and the bn0 BatchNorm backward -- is one reduction pass and one apply pass
+    that writes the grouped conv's dy;
+  * residual / branch gradients accumulate in the dgrad epilogues (beta = 1), each dgrad fused with
+    the backward of the BatchNorm that produced its input (conv2's with bn1, conv1's with the
+    previous block's bn3), so no PyTorch kernel sums gradients.
+Eval mode (and inference without grad) keeps the per-stage nodes below.
+
+Per-stage nodes (eval / legacy path), activations NHWC:
   * ConvBNActFn   -- (grouped) implicit-GEMM conv + BatchNorm (batch stats) + residual + ReLU
   * SplAtFn       -- split attention: radix-summed GAP, fc1 -> BN -> ReLU -> fc2 GEMMs,
                      r-softmax and weighted sum (and their backward)
@@ -249,6 +265,176 @@ class GlobalPoolFn(torch.autograd.Function):
         return ops.avgpool_bwd(dy.contiguous(), ctx.hw)
 
 
+class ResNeStTrunkFn(torch.autograd.Function):
+    """Whole ResNeSt-50 trunk, train mode, as one autograd node: x NHWC4 (F,224,224,4) -> (F,2048).
+
+    Forward per BottleneckS (train_non-local_mutiConv_resnest.py:210-220 -> resnest50()):
+    conv1+bn1+relu -> grouped conv + bn0 (deferred) -> split attention (fc1 -> bn1 -> relu -> fc2
+    -> r-softmax -> weighted sum) -> [avd AvgPool2d(3, s, 1)] -> conv3 + bn3 + [avg_down pool ->
+    conv -> bn] + relu.  The backward mirrors trunk.TrunkFn's."""
+
+    @staticmethod
+    def forward(ctx, x4, share, keep, *params):
+        from .trunk import _conv_bn, _act16
+        mt = share.precision
+        a16 = _act16(mt)
+        nbt = []
+        stem = []
+        c = share.conv1
+        # the stem input: NHWC8 bf16 under bf16 activations (the LDS-DMA engine's 8-channel pieces)
+        xs = ops.nhwc4_to_bf16x8(x4) if a16 else x4
+        z = _conv_bn(xs, c[0], c[1], 2, 1, True, True, recs=stem, math=mt, nbt=nbt)
+        z = _conv_bn(z, c[3], c[4], 1, 1, True, True, recs=stem, math=mt, nbt=nbt)
+        # share.bn1 + relu applied inside the maxpool (its backward recomputes the mask from y)
+        y0, sc0, sh0 = _conv_bn(z, c[6], share.bn1, 1, 1, True, True, recs=stem, math=mt,
+                                defer=True, nbt=nbt)
+        h, am = ops.maxpool_fwd_bn(y0, sc0, sh0)
+        stem_hw = (y0.shape[1], y0.shape[2])
+        blocks = []
+        for layer in (share.layer1, share.layer2, share.layer3, share.layer4):
+            for blk in layer:
+                rec = {"blk": blk, "in_hw": (h.shape[1], h.shape[2])}
+                r1, r2, r3, rd = [], [], [], []
+                z1 = _conv_bn(h, blk.conv1, blk.bn1, 1, 0, True, True, recs=r1, math=mt, nbt=nbt)
+                sp = blk.conv2
+                y2, sc2, sh2 = _conv_bn(z1, sp.conv, sp.bn0, sp.stride, 1, True, True, recs=r2,
+                                        math=mt, defer=True, nbt=nbt, groups=sp.radix)
+                out, spl = _splat_fwd(sp, y2, sc2, sh2, nbt)
+                if blk.avd:
+                    rec["avd_hw"] = (out.shape[1], out.shape[2])
+                    out = ops.avgpool2d_fwd(out, 3, blk.avd_stride, 1, True, False)
+                if blk.downsample is not None:
+                    pool, dconv, dbn = blk.downsample[0], blk.downsample[1], blk.downsample[2]
+                    xr = h
+                    if pool.kernel_size != 1:
+                        rec["pool"] = (pool.kernel_size, pool.stride)
+                        xr = ops.avgpool2d_fwd(h, pool.kernel_size, pool.stride, 0, False, True)
+                    idn = _conv_bn(xr, dconv, dbn, 1, 0, False, True, recs=rd, math=mt, defer=True,
+                                   nbt=nbt)
+                    h = _conv_bn(out, blk.conv3, blk.bn3, 1, 0, True, True, branch=idn, recs=r3,
+                                 math=mt, nbt=nbt)
+                else:
+                    h = _conv_bn(out, blk.conv3, blk.bn3, 1, 0, True, True, residual=h, recs=r3,
+                                 math=mt, nbt=nbt)
+                rec.update(r1=r1[0], r2=r2[0], r3=r3[0], rd=rd[0] if rd else None, spl=spl)
+                blocks.append(rec)
+        feat = ops.avgpool_fwd(h)
+        ops.counters_add_one(nbt)
+        ctx.keep = keep
+        if keep:
+            ctx.share, ctx.params = share, params
+            ctx.stem, ctx.pool, ctx.blocks = stem, (am, stem_hw), blocks
+            ctx.last_hw = (h.shape[1], h.shape[2])
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        from .trunk import _conv_bn_bwd, get_grad_ready
+        if not ctx.keep:
+            raise RuntimeError("trunk backward needs train mode and a forward with grad enabled")
+        grads = {}
+        g = ops.avgpool_bwd(dfeat.contiguous(), ctx.last_hw)   # grad at the last block output
+        blocks = ctx.blocks
+        pending = None     # BN-backward partials of g from the fused dgrad that produced it
+        ready = get_grad_ready(ctx.share)
+        while blocks:
+            rec = blocks.pop()
+            blk = rec["blk"]
+            prev3 = blocks[-1]["r3"] if blocks else None
+            # bn3 (+ReLU) backward; g (owned) becomes the masked gradient = the residual branch's
+            dout, dres, _ = _conv_bn_bwd(rec["r3"], g, grads, want_dres=True, dres_inplace=True,
+                                         parts=pending)
+            if blk.avd:
+                dout = ops.avgpool2d_bwd(dout, rec["avd_hw"], 3, blk.avd_stride, 1, True)
+            # split attention + bn0 backward -> dy of the grouped conv
+            r2 = rec["r2"]
+            dy2 = _splat_bwd(blk.conv2, rec["spl"], r2, dout, grads)
+            del dout
+            dz1, _, fz1 = _conv_bn_bwd(r2, None, grads, dy=dy2, fuse_prev=rec["r1"])
+            del dy2
+            if rec["rd"] is not None:
+                dxr, _, _ = _conv_bn_bwd(rec["rd"], dres, grads)
+                if "pool" in rec:
+                    k, st = rec["pool"]
+                    dxr = ops.avgpool2d_bwd(dxr, rec["in_hw"], k, st, 0, False)
+                _, _, pending = _conv_bn_bwd(rec["r1"], dz1, grads, parts=fz1, dx_out=dxr,
+                                             dx_beta=1.0, fuse_prev=prev3)
+                dx = dxr
+            else:
+                dx, _, pending = _conv_bn_bwd(rec["r1"], dz1, grads, parts=fz1, dx_out=dres,
+                                              dx_beta=1.0, fuse_prev=prev3)
+            del dz1, dres, rec
+            g = dx
+            if ready is not None:   # this block's parameter grads are final: start their exchange
+                ready([(p, grads[p]) for p in blk.parameters() if p in grads])
+        am, stem_hw = ctx.pool
+        st = ctx.stem
+        d2, _, f2 = _conv_bn_bwd(st[2], None, grads, pool=(g, am), fuse_prev=st[1])
+        d1, _, f1 = _conv_bn_bwd(st[1], d2, grads, parts=f2, fuse_prev=st[0])
+        _conv_bn_bwd(st[0], d1, grads, parts=f1, need_dx=False)
+        out = [grads.get(p) for p in ctx.params]
+        ctx.blocks = ctx.stem = None
+        return (None, None, None) + tuple(out)
+
+
+def _splat_fwd(sp, y2, sc, sh, nbt):
+    """Split attention of SplAtConv2d on the grouped conv's pre-BN output y2 (bn0 + ReLU applied
+    on load); fc1 -> BatchNorm runs on batch-centered GAP rows (see SplAtFn).  -> (out, saved)."""
+    n = y2.shape[0]
+    C = y2.shape[-1] // 2
+    inter = sp.fc1.weight.shape[0]
+    w1 = sp.fc1.weight.detach().reshape(inter, C)
+    w2 = sp.fc2.weight.detach().reshape(2 * C, inter)
+    gap = ops.splat_gap_bn(y2, sc, sh)
+    center = torch.empty((1, C), dtype=gap.dtype, device=gap.device)
+    gap_c = torch.empty_like(gap)
+    call("tmr_center_cols", gap, n, C, center, gap_c, stream_ptr())
+    h1 = ops.gemm_nt(gap_c, w1)
+    bn1 = sp.bn1
+    mean, inv, scale, shift = ops.bn_fwd_train(h1, bn1.weight.detach(), bn1.bias.detach(),
+                                               bn1.running_mean, bn1.running_var, bn1.momentum,
+                                               bn1.eps)
+    nbt.append(bn1.num_batches_tracked)
+    shift_back = ops.gemm_nt(center, w1, bias=sp.fc1.bias.detach())      # W1 c + b1
+    call("tmr_axpy", inter, float(bn1.momentum), shift_back, bn1.running_mean, stream_ptr())
+    a1 = ops.bn_apply(h1, scale, shift, None, True)
+    zl = ops.gemm_nt(a1, w2, bias=sp.fc2.bias.detach())
+    att = ops.splat_att(zl)
+    out = ops.splat_combine_bn(y2, sc, sh, att)
+    return out, {"gap": gap_c, "h1": h1, "a1": a1, "att": att, "mean": mean, "inv": inv}
+
+
+def _splat_bwd(sp, spl, r2, dout, grads):
+    """Backward of the split attention and of bn0 + ReLU -> dy2 (the grouped conv's output
+    gradient, dtype of y2); writes the fc1 / bn1 / fc2 / bn0 parameter gradients."""
+    y2 = r2["y"]
+    n, hh, ww, c2 = y2.shape
+    C = c2 // 2
+    inter = sp.fc1.weight.shape[0]
+    att = spl["att"]
+    dout = dout.contiguous()
+    dzl, sums = ops.splat_bwd_reduce_bn(dout, y2, r2["scale"], r2["shift"], r2["mean"], att)
+    grads[sp.fc2.weight] = ops.gemm_tn(dzl, spl["a1"]).view_as(sp.fc2.weight)
+    grads[sp.fc2.bias] = ops.col_sum(dzl, n, c2, c2)
+    da1 = ops.gemm_nn(dzl, sp.fc2.weight.detach().reshape(c2, inter))
+    dh1, _, dg1, dbt1 = ops.bn_bwd(da1, spl["h1"], spl["a1"], spl["mean"], spl["inv"],
+                                   sp.bn1.weight.detach(), True)
+    grads[sp.bn1.weight], grads[sp.bn1.bias] = dg1, dbt1
+    grads[sp.fc1.weight] = ops.gemm_tn(dh1, spl["gap"]).view_as(sp.fc1.weight)   # centered gap
+    grads[sp.fc1.bias] = ops.zeros((inter,), dh1)   # exactly 0 under batch-stat BN (SplAtFn)
+    dgap = ops.gemm_nn(dh1, sp.fc1.weight.detach().reshape(inter, C))
+    coef, dg0, db0 = ops.splat_bn0_coefs(att, dgap, sums, r2["mean"], r2["inv"],
+                                         sp.bn0.weight.detach(), hh * ww)
+    grads[sp.bn0.weight], grads[sp.bn0.bias] = dg0, db0
+    return ops.splat_bwd_apply_bn(dout, y2, r2["scale"], r2["shift"], r2["mean"], att, dgap, coef)
+
+
+def _trunk_node_ok(share):
+    """The whole-trunk node covers fp32 math and bf16 math under the bf16-activation contract."""
+    from .trunk import _act16, FOLD_BN
+    return not FOLD_BN and (share.precision == "fp32" or _act16(share.precision))
+
+
 def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=None,
                 math="fp32"):
     """conv -> BN -> (+residual) -> (ReLU).  On the bf16 operand path (bf16 math, train mode,
@@ -372,6 +558,11 @@ class ResNeSt50Share(nn.Sequential):
                 m.math = precision
 
     def features_nhwc4(self, x4):
+        if self.training and _trunk_node_ok(self):
+            params = list(self.parameters())
+            # grad mode is off inside autograd.Function.forward: decide here whether to save
+            keep = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+            return ResNeStTrunkFn.apply(x4, self, keep, *params)
         c, mt = self.conv1, self.precision
         h = conv_bn_act(x4, c[0], c[1], 2, 1, True, c_real=3, math=mt)
         h = conv_bn_act(h, c[3], c[4], 1, 1, True, math=mt)

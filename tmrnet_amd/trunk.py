@@ -147,7 +147,7 @@ def _act16(math):
 
 
 def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None, math="fp32",
-             defer=False, branch=None, nbt=None, dual=False):
+             defer=False, branch=None, nbt=None, dual=False, groups=1):
     """conv (NHWC implicit GEMM) -> BN -> (+residual) -> (ReLU); returns z.
 
     Train mode only: ``defer`` returns (y, scale, shift) instead of applying the BN -- the
@@ -155,7 +155,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     inside the maxpool, with FOLD_BN the next conv's loaders); ``branch`` = such a deferred
     (y, scale, shift) used as the residual; ``x`` may itself be a deferred (y, scale, shift) of a
     ReLU unit, read through the conv's X-operand prologue.  ``dual`` (block outputs under
-    _full16): returns (z fp32, z bf16 copy)."""
+    _full16): returns (z fp32, z bf16 copy).  ``groups``: a grouped conv
+    (train mode; ResNeSt's radix-2 3x3, tmr_conv_desc.groups)."""
     xpro = None
     if isinstance(x, tuple):
         x, xpro = x[0], (x[1], x[2])
@@ -165,12 +166,14 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     s16 = _store16(math)
     if r == 1 and s == 1 and c == cs and not s16:
         wk = w.detach().contiguous().view(k, 1, 1, c)   # OIHW == KRSC for 1x1
-    else:
-        wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs, bf16=s16)
+    else:   # (grouped: torch's (K, C/G, R, S) -> stacked per-group KRSC blocks (K, R, S, C/G))
+        wk = ops.weight_to_krsc(w.detach().contiguous(), cpad=cs // groups, bf16=s16)
+    if groups > 1 and not training:
+        raise RuntimeError("grouped convs run in the train-mode trunk only")
     if training:
         # batch statistics come out of the conv epilogue (no separate pass over y)
-        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c, math=math,
-                                                xpro=xpro, y16=_act16(math))
+        y, stats, nparts = ops.conv_fwd_bnstats(x, wk, stride, pad, c_real=c * groups, math=math,
+                                                xpro=xpro, y16=_act16(math), groups=groups)
         mean, inv, scale, shift = ops.bn_finalize(
             stats, nparts, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
             bn.running_var, _bn_momentum(bn), bn.eps)
@@ -212,7 +215,10 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
         # without a residual the backward recomputes the ReLU mask from y (scale/shift)
         has_res = residual is not None or branch is not None
         # the dgrad view of a bf16-operand conv reads the transposed weights (LDS-DMA engine)
-        if _full16(math) and x.dtype == torch.bfloat16:
+        if groups > 1 and ((_full16(math) and x.dtype == torch.bfloat16) or _dma32(math)):
+            wt = ops.weight_to_crsk_grouped(w.detach().contiguous(), groups,
+                                            bf16=x.dtype == torch.bfloat16)
+        elif _full16(math) and x.dtype == torch.bfloat16:
             wt = ops.weight_to_crsk(w.detach().contiguous())
         elif _dma32(math) and c % 8 == 0 and x.dtype == torch.float32:
             wt = ops.weight_to_crsk(w.detach().contiguous(), bf16=False)
@@ -222,12 +228,12 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
                      "z": (z[0] if dual else z) if has_res else None, "zbits": zbits,
                      "scale": scale, "shift": shift, "mean": mean, "inv": inv,
                      "stride": stride, "pad": pad, "relu": relu, "conv": conv, "bn": bn,
-                     "c_real": c, "math": math})
+                     "c_real": c, "math": math, "groups": groups})
     return (y, scale, shift) if defer else z
 
 
 def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
-                 dres_inplace=False, parts=None, fuse_prev=None, pool=None):
+                 dres_inplace=False, parts=None, fuse_prev=None, pool=None, dy=None):
     """BN backward, wgrad, dgrad (optionally accumulated into dx_out) of one conv+BN unit.
 
     parts: dz was produced by a fused dgrad (conv_dgrad_bnbwd): it is already ReLU-masked and
@@ -237,11 +243,15 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     fuse_prev: the unit whose BN output gradient this unit's dgrad produces -- its mask and
     partial sums are then computed in the dgrad epilogue; returned as the third value.
     pool: (pooled gradient, argmax) of the maxpool that consumed this unit's output (the stem);
-    dz is then gathered from it inside the BN backward."""
+    dz is then gathered from it inside the BN backward.
+    dy: the conv's output gradient computed by the caller (ResNeSt's split-attention backward
+    writes the grouped conv's dy with bn0's backward folded in): only wgrad and dgrad run here."""
     conv, bn = rec["conv"], rec["bn"]
     dpro = None    # (y, coef): dy = A*g + B*y + C evaluated by the consumer convs' loaders
     s16 = _store16(rec["math"])   # dy feeds only this conv's dgrad / wgrad
-    if pool is not None:
+    if dy is not None:
+        dres = None
+    elif pool is not None:
         # the stem: maxpool backward + ReLU mask + BN backward without writing dz
         dy, dg, db = ops.bn_bwd_maxpool(pool[0], pool[1], rec["y"], rec["scale"], rec["shift"],
                                         rec["mean"], rec["inv"], bn.weight.detach(), bf16=s16)
@@ -268,13 +278,15 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
                                       bn.weight.detach(), rec["relu"], want_dres=want_dres,
                                       dres_out=dz if dres_inplace else None,
                                       scale=rec["scale"], shift=rec["shift"], bf16=s16)
-    grads[bn.weight] = dg
-    grads[bn.bias] = db
+    if dy is None:
+        grads[bn.weight] = dg
+        grads[bn.bias] = db
     x = rec["x"]
     k, c, r, s = conv.weight.shape
+    grp = rec.get("groups", 1)
     grads[conv.weight] = ops.conv_wgrad(x, dy, r, s, rec["stride"], rec["pad"],
                                         c_real=rec["c_real"], math=rec["math"],
-                                        xpro=rec.get("xpro"), dpro=dpro)
+                                        xpro=rec.get("xpro"), dpro=dpro, groups=grp)
     dx, fused = None, None
     if need_dx:
         hw = (x.shape[1], x.shape[2])
@@ -290,11 +302,11 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
                                                p["y"], p["mean"], mask, z=zm,
                                                scale=p["scale"], shift=p["shift"], out=dx_out,
                                                beta=dx_beta, math=rec["math"], dpro=dpro,
-                                               wt=wt)
+                                               wt=wt, groups=grp)
             fused = (pp, npp)
         else:
             dx = ops.conv_dgrad(dy, wdg, hw, rec["stride"], rec["pad"], out=dx_out,
-                                beta=dx_beta, math=rec["math"], dpro=dpro, wt=wt)
+                                beta=dx_beta, math=rec["math"], dpro=dpro, wt=wt, groups=grp)
     return dx, dres, fused
 
 
@@ -354,8 +366,7 @@ class TrunkFn(torch.autograd.Function):
                 h, hx = h if f16 else (h, h)
                 blocks.append((blk, brec))
         feat = ops.avgpool_fwd(h)
-        if nbt:
-            torch._foreach_add_(nbt, 1)
+        ops.counters_add_one(nbt)
         ctx.keep = keep
         if keep:
             ctx.share = share
