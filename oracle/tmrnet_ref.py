@@ -396,6 +396,10 @@ class TMRNetRef(nn.Module):
         else:
             y_1 = self.nl_block(y, Lt, drop_mask=masks["nl"])
             h = self.fc_h_c(torch.cat([y, y_1], dim=1)) * masks["head"]
+            if "head_act" in masks:
+                # test hook: the head ReLU's active set taken from another run (the HIP step), so
+                # a pre-ReLU unit within rounding distance of 0 cannot take the other branch here
+                return self.fc_c(h * masks["head_act"])
         return self.fc_c(F.relu(h))
 
 

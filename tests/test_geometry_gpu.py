@@ -104,55 +104,85 @@ def test_c2_geometry_step_parity(dev):
             assert torch.equal(b.cpu(), rb[name]), name
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
-def test_c5_geometry_step(dev, prec):
-    """T=30, L=300 (C5), LFB rows from a resident bank, B=1 (30 frames); C5 runs bf16 conv
-    operands, the fp32 run of the same geometry is held to the strict bound."""
-    B, T, L = 1, 30, 300
-    torch.manual_seed(21)
-    m = tmrnet_amd.resnet_lstm(seq_len=T, precision=prec).to(dev).train()
-    r = ref.TMRNetRef(seq_len=T, precision=prec).train()
+def _head_act_spy(monkeypatch):
+    """Record the HIP head's post-ReLU activations (HeadFn -> ops.mask_relu_fwd)."""
+    rec = []
+    orig = ops.mask_relu_fwd
+
+    def spy(h, mask):
+        a = orig(h, mask)
+        rec.append(a.detach().clone())
+        return a
+    monkeypatch.setattr(ops, "mask_relu_fwd", spy)
+    return rec
+
+
+def _geometry_step(dev, monkeypatch, B, T, L, prec, seeds, backbone="resnet50", time_conv=False,
+                   nvid=2, vlen=None):
+    """One train step at a benchmarked geometry, LFB rows from a resident bank, dropout masks
+    injected on both sides.  Head ReLU: with bf16 operands both fp32 implementations sit ~1e-2
+    from float64 on the logits (rounding ties decided by fp32 summation order, amplified by
+    batch-statistic BN), so a pre-ReLU head unit that close to 0 can take the other branch and
+    move every gradient downstream of it (measured 0.15 relative L2 per flip).  Instead of paying
+    for such flips, the HIP step's own active set is forced on both oracles (masks["head_act"]),
+    and every parameter is held to the strict bound (no slack).  -> (e_hip, e_cpu) of the logits."""
+    torch.manual_seed(seeds)
+    m = tmrnet_amd.resnet_lstm(seq_len=T, precision=prec, backbone=backbone,
+                               time_conv=time_conv).to(dev).train()
+    r = ref.TMRNetRef(seq_len=T, precision=prec, backbone=backbone, time_conv=time_conv).train()
     r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
     r64 = _double_copy(r, None, B, T, L)
-    frames, off, _, labels = _inputs(B, T, L, seed=22)
-    bank, vs, starts, rows = _bank_rows(B, L, T, 23, nvid=2, vlen=2 * L)
+    frames, off, _, labels = _inputs(B, T, L, seed=seeds + 1)
+    bank, vs, starts, rows = _bank_rows(B, L, T, seeds + 2, nvid=nvid, vlen=vlen)
     lt = bank[rows.view(-1)].view(B, L, 512)
-    masks = _masks(B, 24)
+    masks = _masks(B, seeds + 3)
     m.nl_block.forced_mask = masks["nl"].to(dev)
     m.forced_head_mask = masks["head"].to(dev)
+    acts = _head_act_spy(monkeypatch)
     x4 = ops.crop_normalize(frames.to(dev), off.to(dev), T)
     out = m(x4, LFBRows(bank.to(dev), rows.to(torch.int32).to(dev)))
+    tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels.to(dev)).backward()
+    act = (acts[-1] > 0).double().cpu()
+    masks["head_act"] = act.float()
     x_ref = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224)
     out_r = r(x_ref, lt, masks=masks)
     out64 = r64(x_ref.double(), lt.double(), masks={k: v.double() for k, v in masks.items()})
     e_hip = (out.detach().cpu().double() - out64.detach()).abs().max().item()
     e_cpu = (out_r.detach().double() - out64.detach()).abs().max().item()
-    _record("c5_%s_logits" % prec, {"e_hip": e_hip, "e_cpu": e_cpu})
-    # bf16 rounding flips (fp32 summation order decides a tie-near rounding now and then) set the
-    # scale; the bound is the same scale-free one as the gradients'
+    _record("%s_%s_logits" % (backbone, prec), {"e_hip": e_hip, "e_cpu": e_cpu,
+                                                "head_active": int(act.sum())})
+    # the same scale-free bound as the gradients'
     assert e_hip <= GRAD_RATIO * e_cpu + 1e-5, (e_hip, e_cpu)
     top2 = out64.detach().topk(2, dim=1).values
     sure = (top2[:, 0] - top2[:, 1]) > 2 * max(e_hip, e_cpu)
     assert torch.equal(out.detach().cpu().argmax(1)[sure], out64.detach().argmax(1)[sure])
-    tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels.to(dev)).backward()
     ref.ce_sum_ref(out_r, labels).backward()
     ref.ce_sum_ref(out64, labels).backward()
     g = lambda mod: {n: p.grad for n, p in mod.named_parameters()}
-    # Head ReLU flips.  With bf16 operands both fp32 implementations sit ~2e-2 from float64 on
-    # the logits (chaotic rounding flips through 30-frame batch-stat BN), so a pre-ReLU head unit
-    # h_j within that distance of 0 can take the other sign: its whole gradient da_j is then kept
-    # or dropped.  fc_h_c.bias.grad IS dh, so a zero-pattern mismatch against float64 (dropout
-    # zeros are shared) counts the flips exactly.  One flip among 512 units measured 0.15
-    # relative-L2 on every gradient downstream of it (fc_h_c, NLBlock, LSTM; the fp32 run of the
-    # same geometry has none and meets the strict bound).  Each counted flip buys 0.2 slack.
-    # How many units sit that close to 0 is a property of the inputs, so the fp32 CPU oracle's
-    # own flip count (same emulated bf16 contract) sets the scale: at most twice it, or 3.
-    dh, dh64 = m.fc_h_c.bias.grad.cpu(), r64.fc_h_c.bias.grad
-    flips = int(((dh == 0) != (dh64 == 0)).sum())
-    flips_cpu = int(((r.fc_h_c.bias.grad == 0) != (dh64 == 0)).sum())
-    _record("c5_%s_flips" % prec, {"hip": flips, "cpu_oracle": flips_cpu})
-    assert flips <= (max(3, 2 * flips_cpu) if prec == "bf16" else 0), (flips, flips_cpu)
-    _check_grads(g(m), g(r), g(r64), "c5_%s_grads" % prec, slack=0.2 * flips)
+    scales = None
+    if backbone == "resnest50":
+        from tests.test_resnest_gpu import _zero_grad_scales
+        scales = _zero_grad_scales(g(r64))
+    _record("%s_%s_grads" % (backbone, prec),
+            {"rows": [(n, l2_err(t, g(r64)[n], (scales or {}).get(n)),
+                       l2_err(g(r)[n], g(r64)[n], (scales or {}).get(n))) for n, t in g(m).items()]})
+    _assert_vs_fp64(g(m), g(r), g(r64), "%s_%s_grads" % (backbone, prec), scales=scales)
+    return m
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_c5_geometry_step(dev, monkeypatch, prec):
+    """T=30, L=300 (C5), LFB rows from a resident bank, B=1 (30 frames); C5 runs bf16 conv
+    operands, the fp32 run of the same geometry is held to the same bound."""
+    _geometry_step(dev, monkeypatch, 1, 30, 300, prec, 21, nvid=2, vlen=600)
+
+
+def test_c4_geometry_step(dev, monkeypatch):
+    """C4's model at its own geometry (train_non-local_mutiConv_resnest.py:242-249): ResNeSt-50
+    + LSTM + NLBlock + TimeConv, bf16 under the bf16-activation contract (the whole-trunk
+    node), T=10, L=40, B=2 with LFB rows from a resident bank, against the float64 emulation."""
+    _geometry_step(dev, monkeypatch, 2, 10, 40, "bf16", 31, backbone="resnest50", time_conv=True,
+                   nvid=3)
 
 
 def _stem_stats64(x4, w, chans):
@@ -228,6 +258,83 @@ def test_c2_full_step_properties(dev):
             p.grad.abs().max().item() == 0]
     assert not zero, zero
     # (4) rows served from the resident bank == the dense gather (:293-313) through the model
+    m.eval()
+    with torch.no_grad():
+        o_rows = m(x4, LFBRows(bank, rows))
+        o_dense = m(x4, ops.lfb_gather(bank, rows))
+    assert torch.equal(o_rows, o_dense)
+
+
+def test_c4_full_step_properties(dev):
+    """The benchmarked C4 step itself (64 clips x 10 frames, L=40, ResNeSt-50 + TimeConv, bf16
+    under the bf16-activation contract), property-checked like the C2 step: the first stem BN's
+    running statistics against float64 (bf16-rounded operands and outputs), CE-sum and the fc_c
+    bias gradient from the GPU logits, finite non-trivial gradients for every trunk parameter,
+    bank rows == the dense gather."""
+    from tmrnet_amd.augment import ClipAugment
+    from tmrnet_amd.lfb import valid_starts
+    from tmrnet_amd.sampler import ClipSampler
+    B, T, L = 64, 10, 40
+    torch.manual_seed(0)
+    m = tmrnet_amd.resnet_lstm(seq_len=T, time_conv=True, backbone="resnest50",
+                               precision="bf16").to(dev).train()
+    w_stem = m.share.conv1[0].weight.detach().cpu().clone()
+    vs = valid_starts(T, [2500] * 40)
+    g = torch.Generator().manual_seed(3)
+    bank = (torch.rand(len(vs), 512, generator=g) * 2 - 1).to(dev)
+    starts = torch.from_numpy(ClipSampler(vs, B, seed=4).batch(0)).to(dev)
+    rows = ops.lfb_index(torch.tensor(vs, dtype=torch.int64, device=dev), starts, L)
+    g1 = torch.Generator().manual_seed(1)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g1, dtype=torch.uint8).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=torch.Generator().manual_seed(5)).to(dev)
+    x4 = ClipAugment(seq_len=T, use_flip=1)(frames)
+    masks = _masks(B, 6)
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    out = m(x4, LFBRows(bank, rows))
+    # (1) share.conv1[1] (the first stem BN) running statistics vs float64 of the bf16 contract:
+    # conv of bf16-rounded input / weights, output stored rounded to bf16
+    chans = [0, 9, 21, 31]
+    bn = m.share.conv1[1]
+    rm = bn.running_mean.detach().cpu().double()[chans]
+    rv = bn.running_var.detach().cpu().double()[chans]
+    xs = ref.bf16_round(x4.cpu()[..., :3]).permute(0, 3, 1, 2)
+    w64 = ref.bf16_round(w_stem[chans]).double()
+    s1 = torch.zeros(len(chans), dtype=torch.float64)
+    ys = []
+    for f0 in range(0, B * T, 64):
+        y = torch.nn.functional.conv2d(xs[f0:f0 + 64].double(), w64, stride=2, padding=1)
+        y = ref.bf16_round(y.float()).double()
+        ys.append(y.sum(dim=(0, 2, 3)))
+        s1 += ys[-1]
+    n = B * T * 112 * 112
+    mean64 = s1 / n
+    s2 = torch.zeros(len(chans), dtype=torch.float64)
+    for f0 in range(0, B * T, 64):
+        y = torch.nn.functional.conv2d(xs[f0:f0 + 64].double(), w64, stride=2, padding=1)
+        y = ref.bf16_round(y.float()).double()
+        s2 += ((y - mean64[None, :, None, None]) ** 2).sum(dim=(0, 2, 3))
+    var64 = s2 / (n - 1)
+    assert ((rm - 0.1 * mean64).abs() <= 1e-4 * (0.1 * mean64).abs().max() + 1e-6).all(), (rm, mean64)
+    assert ((rv - (0.9 + 0.1 * var64)).abs() <= 1e-4 * rv.abs()).all(), (rv, var64)
+    # (2) CE-sum and (3) the fc_c bias gradient from the GPU logits
+    loss = tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels)
+    o64 = out.detach().cpu().double()
+    lab = labels.cpu()
+    ce64 = (torch.logsumexp(o64, 1) - o64[torch.arange(B), lab]).sum().item()
+    assert abs(loss.item() - ce64) <= 1e-5 * abs(ce64)
+    loss.backward()
+    p64 = torch.softmax(o64, 1)
+    p64[torch.arange(B), lab] -= 1
+    db = m.fc_c.bias.grad.detach().cpu().double()
+    assert (db - p64.sum(0)).abs().max().item() <= 1e-5
+    bad = [n_ for n_, p in m.named_parameters() if p.grad is None or not torch.isfinite(p.grad).all()]
+    assert not bad, bad
+    # every trunk parameter but the split attention's fc1 biases (exactly 0 under batch-stat BN)
+    zero = [n_ for n_, p in m.named_parameters() if n_.startswith("share") and
+            not n_.endswith("fc1.bias") and p.grad.abs().max().item() == 0]
+    assert not zero, zero
+    # (4) rows served from the resident bank == the dense gather through the model
     m.eval()
     with torch.no_grad():
         o_rows = m(x4, LFBRows(bank, rows))

@@ -416,8 +416,8 @@ __global__ __launch_bounds__(NT) void splat_bn0_coefs_k(const float* __restrict_
   for (int nn = 0; nn < n; ++nn) {
     const long i = (long)nn * 2 * C + j;
     const double a = att[i], dg = (double)dgap[(long)nn * C + c] * ihw;
-    sg += a * sums[i] + dg * sums[2 * plane + i];
-    sgx += a * sums[plane + i] + dg * sums[3 * plane + i];
+    sg += a * sums[i] + dg * sums[plane + i];                    // att*S1 + dgap/hw*S2
+    sgx += a * sums[2 * plane + i] + dg * sums[3 * plane + i];   // att*S3 + dgap/hw*S4
   }
   (void)mean;
   const double inv = invstd[j], N = (double)n * hw;

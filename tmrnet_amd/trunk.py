@@ -249,7 +249,8 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     conv, bn = rec["conv"], rec["bn"]
     dpro = None    # (y, coef): dy = A*g + B*y + C evaluated by the consumer convs' loaders
     s16 = _store16(rec["math"])   # dy feeds only this conv's dgrad / wgrad
-    if dy is not None:
+    dy_given = dy is not None
+    if dy_given:
         dres = None
     elif pool is not None:
         # the stem: maxpool backward + ReLU mask + BN backward without writing dz
@@ -278,7 +279,7 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
                                       bn.weight.detach(), rec["relu"], want_dres=want_dres,
                                       dres_out=dz if dres_inplace else None,
                                       scale=rec["scale"], shift=rec["shift"], bf16=s16)
-    if dy is None:
+    if not dy_given:
         grads[bn.weight] = dg
         grads[bn.bias] = db
     x = rec["x"]
