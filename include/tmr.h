@@ -537,6 +537,13 @@ int tmr_residual_mask(const float* base, const float* z, const float* mask, floa
 int tmr_mask_relu_fwd(const float* h, const float* mask, float* a, long n, hipStream_t stream);
 int tmr_mask_relu_bwd(const float* da, const float* a, const float* mask, float* dh, long n,
                       hipStream_t stream);
+/* The LSTM output of each clip's last step, y.contiguous().view(-1, 512)[T-1::T]
+ * (train_only_non-local_pretrained.py:232): out (b, h) from y (b, t, h); and its backward for a
+ * tensor read by two consumers (the NLBlock query and the head, :235-236): dy (b, t, h) = d1 + d2
+ * at step t-1 (d2 may be NULL), 0 elsewhere -- one pass, no separate zero fill or add. */
+int tmr_seq_last(const float* y, float* out, int b, int t, int h, hipStream_t stream);
+int tmr_seq_last_bwd(const float* d1, const float* d2, float* dy, int b, int t, int h,
+                     hipStream_t stream);
 /* x[i] = v (the exactly-zero fc1 bias gradient of the split attention) */
 int tmr_fill_f32(float* x, long n, float v, hipStream_t stream);
 /* *ptrs[i] += v for i < n: every BatchNorm num_batches_tracked counter of a train step

@@ -1,9 +1,15 @@
+# one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
 set -o pipefail
-mkdir -p gpurun_out/r4c
-timeout -k 10 700 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_resnest_trunk_gpu.py tests/test_resnest_gpu.py tests/test_bf16_gpu.py tests/test_geometry_gpu.py tests/test_kernels_gpu.py -k "split or resnest or geometry or c4 or fused_bn_backward or grouped" > gpurun_out/r4c/pytest.txt 2>&1
-echo "pytest rc=$?"
-timeout -k 10 200 python scripts/convbench.py --kinds dgrad --bnbwd --wt32 --dgrad-beta 1 --reps 4 > gpurun_out/r4c/cb_new.txt 2>&1 && \
-TMR_LIB_PATH=tmrnet_amd/libtmr_ab.so timeout -k 10 200 python scripts/convbench.py --kinds dgrad --bnbwd --wt32 --dgrad-beta 1 --reps 4 > gpurun_out/r4c/cb_old.txt 2>&1 && \
-timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/r4c/c2.json 2> gpurun_out/r4c/c2.err && \
-timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --model resnest50 --precision bf16 > gpurun_out/r4c/c4.json 2> gpurun_out/r4c/c4.err
-echo "rc=$?"
+O=gpurun_out/r4f; mkdir -p $O
+R=$GRAFT_REPO_ROOT
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/pytest.txt 2>&1 && \
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 && \
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --model resnest50 --precision bf16 > $O/c4.json 2> $O/c4.err && \
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > $O/c2.json 2> $O/c2.err
+echo "main rc=$?"
+cd /tmp && export TMPDIR=/tmp
+for m in plain pinned lib conv lstm step; do
+  timeout -k 10 120 rocprofv3 --kernel-trace -d $R/$O/probe_$m -o run -- python3 $R/scripts/exit_probe.py $m > $R/$O/probe_$m.log 2>&1
+  rc=$?; echo "probe $m rc=$rc"
+  if [ $rc -ne 0 ]; then break; fi
+done

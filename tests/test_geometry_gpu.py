@@ -105,7 +105,7 @@ def test_c2_geometry_step_parity(dev):
 
 
 def _head_act_spy(monkeypatch):
-    """Record the HIP head's post-ReLU activations (HeadFn -> ops.mask_relu_fwd)."""
+    """Record the HIP head's post-ReLU activations (model.ClipHeadFn -> ops.mask_relu_fwd)."""
     rec = []
     orig = ops.mask_relu_fwd
 

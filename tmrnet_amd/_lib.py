@@ -124,6 +124,8 @@ SIGNATURES = {
     "tmr_splat_bwd_apply_bn": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "tmr_avgpool2d_fwd_a16": [P, P, I, I, I, I, I, I, I, I, I, I, P],
     "tmr_fill_f32": [P, L, F, P],
+    "tmr_seq_last": [P, P, I, I, I, P],
+    "tmr_seq_last_bwd": [P, P, P, I, I, I, P],
     "tmr_counters_add": [P, I, ctypes.c_int64, P],
     "tmr_center_cols": [P, I, I, P, P, P],
     "tmr_axpy": [I, F, P, P, P],

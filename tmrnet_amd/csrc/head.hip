@@ -565,6 +565,49 @@ __global__ void counters_add_k(int64_t* const* __restrict__ ptrs, int n, int64_t
 }
 }  // namespace
 
+// the LSTM output at the last step of each clip (y.view(-1, 512)[T-1::T]) and its gradient
+namespace {
+__global__ void seq_last_k(const float* __restrict__ y, float* __restrict__ out, int b, int t, int h) {
+  const long n = (long)b * h;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long bb = i / h;
+    out[i] = y[(bb * t + (t - 1)) * h + (i - bb * h)];
+  }
+}
+__global__ void seq_last_bwd_k(const float* __restrict__ d1, const float* __restrict__ d2,
+                               float* __restrict__ dy, int b, int t, int h) {
+  const long n = (long)b * t * h;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long j = i % h, bt = i / h;
+    const long bb = bt / t;
+    float v = 0.f;
+    if (bt - bb * t == t - 1) {
+      v = d1[bb * h + j];
+      if (d2) v += d2[bb * h + j];
+    }
+    dy[i] = v;
+  }
+}
+}  // namespace
+
+TMR_API int tmr_seq_last(const float* y, float* out, int b, int t, int h, hipStream_t stream) {
+  TMR_CHECK_ARG(b >= 0 && t > 0 && h > 0, "tmr_seq_last: bad shape b %d t %d h %d", b, t, h);
+  if (b == 0) return 0;
+  hipLaunchKernelGGL(seq_last_k, dim3(blocks_for((long)b * h, NT)), dim3(NT), 0, stream, y, out, b, t, h);
+  TMR_CHECK_LAUNCH("seq_last");
+  return 0;
+}
+
+TMR_API int tmr_seq_last_bwd(const float* d1, const float* d2, float* dy, int b, int t, int h,
+                             hipStream_t stream) {
+  TMR_CHECK_ARG(b >= 0 && t > 0 && h > 0 && d1, "tmr_seq_last_bwd: bad arguments");
+  if (b == 0) return 0;
+  hipLaunchKernelGGL(seq_last_bwd_k, dim3(blocks_for((long)b * t * h, NT)), dim3(NT), 0, stream, d1,
+                     d2, dy, b, t, h);
+  TMR_CHECK_LAUNCH("seq_last_bwd");
+  return 0;
+}
+
 TMR_API int tmr_fill_f32(float* x, long n, float v, hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(fill_k, dim3(blocks_for(n, NT)), dim3(NT), 0, stream, x, n, v);

@@ -378,6 +378,10 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
   const LstmWs L = lstm_ws(b, t, i, h);
   TMR_CHECK_ARG(ws && ws_bytes >= L.total, "tmr_lstm_fwd: workspace %zu < %zu bytes", ws_bytes,
                 L.total);
+  // the barrier words (arrival counter, timeout) start at 0 on every call, also on the per-step
+  // path and for empty inputs, so tmr_lstm_status_or never reads a stale or uninitialised word
+  TMR_CHECK_ARG(hipMemsetAsync((char*)ws + L.sync, 0, 16, stream) == hipSuccess,
+                "tmr_lstm_fwd: memset failed");
   float* cs = nullptr;
   float* acts = nullptr;
   if (saved) {
@@ -395,12 +399,8 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
   TMR_CHECK_LAUNCH("lstm bias");
   int rc = tmr_gemm_nt(b * t, 4 * h, i, x, i, w_ih, i, bias, gx, 4 * h, 0.f, stream);
   if (rc) return rc;
+  unsigned* sync = (unsigned*)(w + L.sync);
   if (persist_allowed() && lstm_persistent_shape(b, t, h)) {
-    unsigned* sync = (unsigned*)(w + L.sync);
-    if (hipMemsetAsync(sync, 0, 16, stream) != hipSuccess) {
-      tmr_set_error("tmr_lstm_fwd: memset failed");
-      return 2;
-    }
     dim3 grid(LH / HU, cdiv(b, BBC));
     const float* gxc = gx;
     unsigned lim = spin_limit();
@@ -450,6 +450,8 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
   const LstmWs L = lstm_ws(b, t, i, h);
   TMR_CHECK_ARG(ws && ws_bytes >= L.total, "tmr_lstm_bwd: workspace %zu < %zu bytes", ws_bytes,
                 L.total);
+  TMR_CHECK_ARG(hipMemsetAsync((char*)ws + L.sync, 0, 16, stream) == hipSuccess,
+                "tmr_lstm_bwd: memset failed");
   TMR_CHECK_ARG(saved_bytes >= tmr_lstm_saved_bytes(b, t, h),
                 "tmr_lstm_bwd: saved buffer %zu < %zu bytes", saved_bytes,
                 tmr_lstm_saved_bytes(b, t, h));
@@ -467,12 +469,8 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
     return 0;
   }
   bool done = false;
+  unsigned* sync = (unsigned*)(w + L.sync);   // zeroed above (see tmr_lstm_fwd)
   if (persist_allowed() && lstm_persistent_shape(b, t, h)) {
-    unsigned* sync = (unsigned*)(w + L.sync);
-    if (hipMemsetAsync(sync, 0, 16, stream) != hipSuccess) {
-      tmr_set_error("tmr_lstm_bwd: memset failed");
-      return 2;
-    }
     dim3 grid(LH / HU, cdiv(b, BBC));
     unsigned lim = spin_limit();
     void* args[] = {(void*)&dy, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&dg,

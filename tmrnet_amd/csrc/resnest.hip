@@ -11,6 +11,8 @@
 
 namespace {
 constexpr int NT = 256;
+// per-channel reductions over frames: 64 columns x 16 row groups per block
+constexpr int CC_COLS = 64, CC_RG = 16;
 
 int blocks_for(long n) {
   long b = (n + NT - 1) / NT;
@@ -402,23 +404,32 @@ __global__ __launch_bounds__(NT) void splat_bwd_reduce_bn_k(
 //   sg = sum_n att*S1 + dgap/hw*S2 = sum g,  sgx = sum_n att*S3 + dgap/hw*S4 = sum g*(y - mean)
 // -> dbeta = sg, dgamma = sgx*invstd, coef[3][2C] = (gamma*invstd, sg/N, invstd^2*sgx/N):
 //   dy = coef0 * (g - coef1 - (y - mean) * coef2)   (nn.BatchNorm2d's batch-statistics backward)
-__global__ __launch_bounds__(NT) void splat_bn0_coefs_k(const float* __restrict__ att, const float* __restrict__ dgap,
-                                                        const float* __restrict__ sums, const float* __restrict__ mean,
-                                                        const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                                        float* __restrict__ coef, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta, int n, int hw, int C) {
-  const int j = blockIdx.x * NT + threadIdx.x;
-  if (j >= 2 * C) return;
-  const int c = j % C;
+__global__ __launch_bounds__(CC_COLS * CC_RG) void splat_bn0_coefs_k(
+    const float* __restrict__ att, const float* __restrict__ dgap, const float* __restrict__ sums,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
+    float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta, int n, int hw,
+    int C) {
+  __shared__ double part[2][CC_RG][CC_COLS];
+  const int cl = threadIdx.x % CC_COLS, rg = threadIdx.x / CC_COLS;
+  const int j = blockIdx.x * CC_COLS + cl;
   const long plane = (long)n * 2 * C;
   const double ihw = 1.0 / (double)hw;
   double sg = 0.0, sgx = 0.0;
-  for (int nn = 0; nn < n; ++nn) {
-    const long i = (long)nn * 2 * C + j;
-    const double a = att[i], dg = (double)dgap[(long)nn * C + c] * ihw;
-    sg += a * sums[i] + dg * sums[plane + i];                    // att*S1 + dgap/hw*S2
-    sgx += a * sums[2 * plane + i] + dg * sums[3 * plane + i];   // att*S3 + dgap/hw*S4
+  if (j < 2 * C) {
+    const int c = j % C;
+    for (int nn = rg; nn < n; nn += CC_RG) {
+      const long i = (long)nn * 2 * C + j;
+      const double a = att[i], dg = (double)dgap[(long)nn * C + c] * ihw;
+      sg += a * sums[i] + dg * sums[plane + i];                    // att*S1 + dgap/hw*S2
+      sgx += a * sums[2 * plane + i] + dg * sums[3 * plane + i];   // att*S3 + dgap/hw*S4
+    }
   }
+  part[0][rg][cl] = sg;
+  part[1][rg][cl] = sgx;
+  __syncthreads();
+  if (rg != 0 || j >= 2 * C) return;
+  sg = 0.0; sgx = 0.0;
+  for (int q = 0; q < CC_RG; ++q) { sg += part[0][q][cl]; sgx += part[1][q][cl]; }
   (void)mean;
   const double inv = invstd[j], N = (double)n * hw;
   dbeta[j] = (float)sg;
@@ -492,16 +503,31 @@ __global__ __launch_bounds__(NT) void avgpool2d_fwd_a16_k(const __bf16* __restri
   }
 }
 
-// one thread per column: rows are few (frames), columns <= 512
-__global__ __launch_bounds__(NT) void center_cols_k(const float* __restrict__ x, int rows, int cols,
-                                                    float* __restrict__ center, float* __restrict__ xc) {
-  const int j = blockIdx.x * NT + threadIdx.x;
-  if (j >= cols) return;
+// Column means over the frames: block = 64 columns x 16 row groups (1024 threads), each thread
+// sums its rows in double, the 16 partial sums are added in a fixed order (deterministic).
+__global__ __launch_bounds__(CC_COLS * CC_RG) void center_cols_k(const float* __restrict__ x, int rows, int cols,
+                                                                 float* __restrict__ center, float* __restrict__ xc) {
+  __shared__ double part[CC_RG][CC_COLS];
+  __shared__ float mean_s[CC_COLS];
+  const int cl = threadIdx.x % CC_COLS, rg = threadIdx.x / CC_COLS;
+  const int j = blockIdx.x * CC_COLS + cl;
   double s = 0.0;
-  for (int i = 0; i < rows; ++i) s += x[(long)i * cols + j];
-  const float m = (float)(s / (double)rows);
-  center[j] = m;
-  for (int i = 0; i < rows; ++i) xc[(long)i * cols + j] = x[(long)i * cols + j] - m;
+  if (j < cols)
+    for (int i = rg; i < rows; i += CC_RG) s += x[(long)i * cols + j];
+  part[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0) {
+    double t = 0.0;
+    for (int q = 0; q < CC_RG; ++q) t += part[q][cl];
+    const float m = (float)(t / (double)rows);
+    mean_s[cl] = m;
+    if (j < cols) center[j] = m;
+  }
+  __syncthreads();
+  if (j < cols) {
+    const float m = mean_s[cl];
+    for (int i = rg; i < rows; i += CC_RG) xc[(long)i * cols + j] = x[(long)i * cols + j] - m;
+  }
 }
 
 __global__ __launch_bounds__(NT) void axpy_k(int n, float alpha, const float* __restrict__ x,
@@ -514,8 +540,8 @@ __global__ __launch_bounds__(NT) void axpy_k(int n, float alpha, const float* __
 TMR_API int tmr_center_cols(const float* x, int rows, int cols, float* center, float* xc,
                             hipStream_t stream) {
   TMR_CHECK_ARG(rows > 0 && cols > 0, "tmr_center_cols: bad shape %dx%d", rows, cols);
-  hipLaunchKernelGGL(center_cols_k, dim3((cols + NT - 1) / NT), dim3(NT), 0, stream, x, rows, cols,
-                     center, xc);
+  hipLaunchKernelGGL(center_cols_k, dim3(cdiv(cols, CC_COLS)), dim3(CC_COLS * CC_RG), 0, stream, x,
+                     rows, cols, center, xc);
   TMR_CHECK_LAUNCH("center_cols");
   return 0;
 }
@@ -642,8 +668,8 @@ TMR_API int tmr_splat_bn0_coefs(const float* att, const float* dgap, const float
                                 float* coef, float* dgamma, float* dbeta, int n, int hw, int c,
                                 hipStream_t stream) {
   TMR_CHECK_ARG(n > 0 && hw > 0 && c > 0, "tmr_splat_bn0_coefs: bad shape n %d hw %d c %d", n, hw, c);
-  hipLaunchKernelGGL(splat_bn0_coefs_k, dim3(cdiv(2L * c, NT)), dim3(NT), 0, stream, att, dgap, sums,
-                     mean, invstd, gamma, coef, dgamma, dbeta, n, hw, c);
+  hipLaunchKernelGGL(splat_bn0_coefs_k, dim3(cdiv(2L * c, CC_COLS)), dim3(CC_COLS * CC_RG), 0, stream,
+                     att, dgap, sums, mean, invstd, gamma, coef, dgamma, dbeta, n, hw, c);
   TMR_CHECK_LAUNCH("splat_bn0_coefs");
   return 0;
 }

@@ -15,6 +15,7 @@ class CESumFn(torch.autograd.Function):
         ctx.save_for_backward(dl)
         ctx.preds = preds
         ctx.mark_non_differentiable(preds)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for preds
         return loss.view(()), preds
 
     @staticmethod

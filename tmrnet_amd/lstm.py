@@ -35,12 +35,13 @@ class LSTMFn(torch.autograd.Function):
             ctx.save_for_backward(x, wi, wh, y, saved)
         hn, cn = hn.unsqueeze(0), cn.unsqueeze(0)
         ctx.mark_non_differentiable(hn, cn)
+        ctx.set_materialize_grads(False)   # no zero-filled gradients for h_n / c_n
         return y, hn, cn
 
     @staticmethod
     def backward(ctx, dy, dhn, dcn):
         x, wi, wh, y, saved = ctx.saved_tensors
-        dy = dy.contiguous() if dy is not None else torch.zeros_like(y)
+        dy = dy.contiguous() if dy is not None else ops.zeros(y.shape, y)
         dx, dw_ih, dw_hh, db_ih, db_hh, _ = ops.lstm_bwd(dy, x, wi, wh, y, saved,
                                                          want_dx=ctx.needs_input_grad[0])
         return dx, dw_ih, dw_hh, db_ih, db_hh

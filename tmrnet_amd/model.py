@@ -16,45 +16,62 @@ import torch.nn as nn
 import torch.nn.init as init
 
 from . import ops
+from ._lib import call, stream_ptr
 from .lstm import LSTM
 from .nlblock import NLBlock, LFBRows, _DropoutRNG
 from .trunk import ResNet50Share
 
 
-class HeadFn(torch.autograd.Function):
-    """cat([y, y1]) -> fc_h_c -> dropout(mask) -> ReLU -> fc_c (train_only_non-local_pretrained.py:236-239).
-    The concat is folded into two GEMMs on the column halves of fc_h_c.weight."""
+class ClipHeadFn(torch.autograd.Function):
+    """The clip branch after the LSTM as ONE autograd node (train_only_non-local_pretrained.py:
+    232-239): the last step of each clip y = lstm_out[:, T-1] (tmr_seq_last), the NLBlock on
+    (y, Lt) (tmr_nlblock_fwd/bwd, NLBlock_MutiConv6_3.py:10-40) and the head on cat(y, y_1).
+    y feeds both the NLBlock query and the head; the backward writes d(lstm_out) in one pass --
+    the two gradients of y summed at step T-1, zeros elsewhere (tmr_seq_last_bwd) -- so no zero
+    fill, scatter or add runs outside libtmr."""
 
     @staticmethod
-    def forward(ctx, y, y1, mask, wh, bh, wc, bc):
-        y = y.contiguous(); y1 = y1.contiguous()
-        B, D = y.shape
+    def forward(ctx, y_seq, lt, rows, nl_mask, L, head_mask, w1, b1, w2, b2, w3, b3, g, bt, w4, b4,
+                wh, bh, wc, bc):
+        y_seq = y_seq.contiguous()
+        B, T, H = y_seq.shape
+        y = torch.empty((B, H), dtype=y_seq.dtype, device=y_seq.device)
+        call("tmr_seq_last", y_seq, y, B, T, H, stream_ptr())
+        nlw = [t.detach().contiguous().reshape(-1) if t.dim() == 2 and t.shape[0] == 1
+               else t.detach().contiguous() for t in (w1, b1, w2, b2, w3, b3, g, bt, w4, b4)]
+        y1, saved = ops.nlblock_fwd(y, lt, rows, L, nl_mask, nlw)
         whd = wh.detach()
-        h = ops.gemm_nt(y, whd, bias=bh.detach(), K=D, ldb=2 * D)
-        ops.gemm_nt(y1, whd[:, D:], out=h, beta=1.0, K=D, ldb=2 * D)
-        a = ops.mask_relu_fwd(h, mask)
+        h = ops.gemm_nt(y, whd, bias=bh.detach(), K=H, ldb=2 * H)
+        ops.gemm_nt(y1, whd[:, H:], out=h, beta=1.0, K=H, ldb=2 * H)
+        a = ops.mask_relu_fwd(h, head_mask)
         logits = ops.gemm_nt(a, wc.detach(), bias=bc.detach())
-        ctx.save_for_backward(y, y1, mask, a, wh, wc)
+        ctx.save_for_backward(y, y1, lt, rows, nl_mask, saved, head_mask, a, wh, wc, *nlw)
+        ctx.cfg = (B, T, H, L, ctx.needs_input_grad[1] and rows is None, g.shape)
         return logits
 
     @staticmethod
     def backward(ctx, dl):
-        y, y1, mask, a, wh, wc = ctx.saved_tensors
+        y, y1, lt, rows, nl_mask, saved, head_mask, a, wh, wc, *nlw = ctx.saved_tensors
+        B, T, H, L, lt_grad, g_shape = ctx.cfg
         dl = dl.contiguous()
-        B, K = dl.shape
-        D = y.shape[1]
+        K = dl.shape[1]
         dwc = ops.gemm_tn(dl, a)
         dbc = ops.col_sum(dl, B, K, K)
         da = ops.gemm_nn(dl, wc.detach())
-        dh = ops.mask_relu_bwd(da, a, mask)
+        dh = ops.mask_relu_bwd(da, a, head_mask)
         whd = wh.detach()
-        dy = ops.gemm_nn(dh, whd, N=D, ldb=2 * D)
-        dy1 = ops.gemm_nn(dh, whd[:, D:], N=D, ldb=2 * D)
+        dy = ops.gemm_nn(dh, whd, N=H, ldb=2 * H)
+        dy1 = ops.gemm_nn(dh, whd[:, H:], N=H, ldb=2 * H)
         dwh = torch.empty_like(whd)
-        ops.gemm_tn(dh, y, out=dwh, N=D, ldc=2 * D)
-        ops.gemm_tn(dh, y1, out=dwh[:, D:], N=D, ldc=2 * D)
+        ops.gemm_tn(dh, y, out=dwh, N=H, ldc=2 * H)
+        ops.gemm_tn(dh, y1, out=dwh[:, H:], N=H, ldc=2 * H)
         dbh = ops.col_sum(dh, B, dh.shape[1], dh.shape[1])
-        return dy, dy1, None, dwh, dbh, dwc, dbc
+        dst, dlt, gr = ops.nlblock_bwd(dy1, y, lt, rows, L, nl_mask, saved, nlw, lt_grad)
+        dw1, db1, dw2, db2, dw3, db3, dg, dbt, dw4, db4 = gr
+        dy_seq = torch.empty((B, T, H), dtype=dl.dtype, device=dl.device)
+        call("tmr_seq_last_bwd", dy, dst, dy_seq, B, T, H, stream_ptr())
+        return (dy_seq, dlt, None, None, None, None, dw1, db1, dw2, db2, dw3, db3,
+                dg.view(g_shape), dbt.view(g_shape), dw4, db4, dwh, dbh, dwc, dbc)
 
 
 class LinearMaskFn(torch.autograd.Function):
@@ -127,21 +144,29 @@ class resnet_lstm(nn.Module):  # noqa: N801  (reference class name)
         T = self.seq_len
         feat = _frames_to_features(self.share, x)
         self.lstm.flatten_parameters()
-        y, _ = self.lstm(feat.view(-1, T, 2048))
-        y = y[:, T - 1, :]                      # == y.view(-1,512)[T-1::T]
+        y_seq, _ = self.lstm(feat.view(-1, T, 2048))   # y.view(-1,512)[T-1::T] inside ClipHeadFn
         Lt = long_feature
         if hasattr(self, "time_conv"):
             if isinstance(Lt, LFBRows):
                 Lt = Lt.dense()
             Lt = self.time_conv(Lt)
-        y_1 = self.nl_block(y, Lt)
+        nl = self.nl_block
+        if isinstance(Lt, LFBRows):
+            lt, rows, L = Lt.bank, Lt.rows, Lt.rows.shape[1]
+        else:
+            lt, rows, L = Lt.contiguous(), None, Lt.shape[1]
+        B = y_seq.shape[0]
+        nl_mask = nl.drop_mask(B, y_seq)
         mask = None
         if self.training and self.dropout.p > 0:
-            B = y.shape[0]
             mask = (self.forced_head_mask if self.forced_head_mask is not None
-                    else self._rng.mask(B * 512, self.dropout.p, y).view(B, 512))
-        return HeadFn.apply(y, y_1, mask, self.fc_h_c.weight, self.fc_h_c.bias,
-                            self.fc_c.weight, self.fc_c.bias)
+                    else self._rng.mask(B * 512, self.dropout.p, y_seq).view(B, 512))
+        return ClipHeadFn.apply(y_seq, lt, rows, nl_mask, L, mask,
+                                nl.linear1.weight, nl.linear1.bias, nl.linear2.weight,
+                                nl.linear2.bias, nl.linear3.weight, nl.linear3.bias,
+                                nl.layer_norm.weight, nl.layer_norm.bias, nl.linear4.weight,
+                                nl.linear4.bias, self.fc_h_c.weight, self.fc_h_c.bias,
+                                self.fc_c.weight, self.fc_c.bias)
 
 
 class resnet_lstm_LFB(nn.Module):  # noqa: N801

@@ -98,16 +98,21 @@ class NLBlock(nn.Module):
         self._rng = _DropoutRNG()
         self.forced_mask = None  # parity tests: externally supplied scaled mask (B,512)
 
+    def drop_mask(self, B, like):
+        """The Dropout(0.2) mask of this forward (scaled by 1/0.8), or None in eval mode."""
+        if not (self.training and self.dropout.p > 0):
+            return None
+        if self.forced_mask is not None:
+            return self.forced_mask
+        return self._rng.mask(B * 512, self.dropout.p, like).view(B, 512)
+
     def forward(self, St, Lt):
         B = St.shape[0]
         if isinstance(Lt, LFBRows):
             lt, rows, L = Lt.bank, Lt.rows, Lt.rows.shape[1]
         else:
             lt, rows, L = Lt.contiguous(), None, Lt.shape[1]
-        mask = None
-        if self.training and self.dropout.p > 0:
-            mask = (self.forced_mask if self.forced_mask is not None
-                    else self._rng.mask(B * 512, self.dropout.p, St).view(B, 512))
+        mask = self.drop_mask(B, St)
         return NLBlockFn.apply(St, lt, rows, mask, L,
                                self.linear1.weight, self.linear1.bias,
                                self.linear2.weight, self.linear2.bias,
