@@ -3,7 +3,8 @@ the train step and exit normally, so a profiled run can tell which one leaves th
 exit handler calling into a torn-down HSA runtime.
 
 usage: rocprofv3 --kernel-trace -d DIR -- python3 scripts/exit_probe.py MODE
-MODE: plain | pinned | lib | conv | lstm | step"""
+MODE: plain | pinned | lib | conv | lstm | lstm_reset | step
+(lstm_reset: hipDeviceReset from an interpreter atexit hook, i.e. before the C-level exit handlers)"""
 import os
 import sys
 
@@ -29,7 +30,12 @@ def main(mode):
         a = torch.randn(2, 16, 16, 64, device=dev)
         w = torch.randn(64, 1, 1, 64, device=dev)
         ops.conv_fwd(a, w, 1, 0)
-    if mode in ("lstm", "step"):
+    if mode == "lstm_reset":
+        import atexit
+        import ctypes
+        hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        atexit.register(lambda: hip.hipDeviceReset())
+    if mode in ("lstm", "lstm_reset", "step"):
         from tmrnet_amd import ops
         xs = torch.randn(64, 10, 2048, device=dev)
         wi = torch.randn(2048, 2048, device=dev) * 0.01

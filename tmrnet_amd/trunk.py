@@ -125,6 +125,12 @@ ACT16 = os.environ.get("TMR_BF16_ACT", "1") != "0"
 DMA32 = os.environ.get("TMR_GEMM32", "1") != "0"
 
 
+# downsample blocks' backward order: the strided downsample dgrad runs first (plain, beta 0; its
+# tap-less parity classes write zeros) and the previous block's BN backward is fused into conv1's
+# stride-1 dgrad (beta 1).  Bit-identical to the other order (dx = a + b either way); measured
+# 51.1 vs 51.6 ms of dgrads per C2 step (profiles/r3/bench_r4f/).  TMR_DS_FIRST=0: the old order.
+DS_FIRST = os.environ.get("TMR_DS_FIRST", "1") != "0"
+
 # the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
 BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
 
@@ -401,7 +407,13 @@ class TrunkFn(torch.autograd.Function):
                                           parts=pending, fuse_prev=r2 if fuse else None)
             dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1 if fuse else None)
             del dz2
-            if has_ds:
+            if has_ds and DS_FIRST:
+                # the strided downsample dgrad writes dx (its tap-less parity classes as zeros),
+                # the stride-1 conv1 dgrad accumulates into it with the fused BN backward
+                dx, _, _ = _conv_bn_bwd(rd, dres, grads)
+                _, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dx, dx_beta=1.0,
+                                             fuse_prev=prev3)
+            elif has_ds:
                 dx, _, _ = _conv_bn_bwd(r1, dz1, grads, parts=fz1)
                 _, _, pending = _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0,
                                              fuse_prev=prev3)
