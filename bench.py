@@ -206,8 +206,8 @@ def main():
     # ---- live roofline of the dominant kernel family (implicit-GEMM conv) ----
     roof = None
     # the committed PMC passes profile the default geometry (64 clips x 10 frames, L=40)
-    traffic = (load_traffic(args.model + ("" if args.precision == "fp32" else "_bf16"))
-               if (args.clips, args.seq, args.lfb) == (64, 10, 40) else None)
+    traffic = (load_traffic(args.model, args.precision, args.seq, args.lfb)
+               if args.clips == 64 else None)
     if not args.no_roofline:
         ops.PROF = []
         torch.cuda.synchronize()
@@ -237,6 +237,9 @@ def main():
                 # HBM bytes per conv call (PMC, per step / calls per step), same unit as achieved
                 "traffic": int(traffic["hbm_bytes_per_step"] / len(recs)) if traffic else None,
                 "traffic_source": traffic.get("source") if traffic else None,
+                # SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) over the conv
+                # launches of the same committed PMC record
+                "mfma_busy_frac": traffic.get("mfma_busy_frac") if traffic else None,
                 "alg_bytes_per_launch": int(tot_bytes / max(1, len(recs))),
                 "flops_per_launch": int(tot_flops / max(1, len(recs))),
                 "launches": len(recs), "avg_launch_ms": round(tot_ms / max(1, len(recs)), 4),
@@ -311,26 +314,38 @@ def workload_name(args):
     return "C2/C3: TMRNet ResNet50+LSTM+NLBlock train step"
 
 
-def load_traffic(model):
-    """HBM bytes of the conv kernels per step from the committed rocprofv3 PMC passes of this
-    workload (scripts/pmc.sh -> scripts/pmc_summary.py -> profiles/<round>/pmc_traffic_<model>.json:
-    FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE of gemm_kernel and the split-K
-    reductions (wgrad_reduce_kernel, wgrad_reduce_taps_kernel), per train step).  None when no PMC pass has been committed."""
+def load_traffic(model, precision, seq, lfb):
+    """HBM bytes (and MFMA-busy cycles) of the conv kernels per step from the committed rocprofv3
+    PMC passes of THIS workload (scripts/pmc.sh -> scripts/pmc_summary.py ->
+    profiles/<round>/pmc_traffic_<model>_<precision>_s<seq>_l<lfb>.json: FETCH_SIZE x2 (gfx950
+    wide-read correction) + WRITE_SIZE of the conv engines and the split-K reductions, per train
+    step; SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE).  Round-2 records (pmc_traffic_<model>[_bf16]
+    .json) cover the default geometry only.  None when no PMC pass has been committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic_%s.json" % model)))
+    names = ["pmc_traffic_%s_%s_s%d_l%d.json" % (model, precision, seq, lfb)]
+    if (seq, lfb) == (10, 40):
+        names.append("pmc_traffic_%s%s.json" % (model, "" if precision == "fp32" else "_bf16"))
+    files = []
+    for n in names:
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", n)))
+        if files:
+            break
     if not files:
         return None
     with open(files[-1]) as f:
         d = json.load(f)
     fams = d.get("families", {})
     # the conv family: gemm_kernel / tmrg::gemm_kernel (register-staged), tmrg::gemm16_kernel
-    # (bf16 LDS-DMA engine) and the split-K weight-gradient reductions
+    # (LDS-DMA engine) and the split-K weight-gradient reductions
     conv = [k for k in fams if any(t in k for t in ("gemm_kernel", "gemm16_kernel", "wgrad_reduce"))]
     if not conv:
         return None
     per_step = sum(fams[k]["hbm_bytes_per_step"] for k in conv)
+    busy = sum(fams[k].get("mfma_busy_cycles", 0.0) for k in conv)
+    gui = sum(fams[k].get("gui_active_cycles", 0.0) for k in conv)
     return {"hbm_bytes_per_step": per_step,
             "all_kernels_bytes_per_step": sum(f["hbm_bytes_per_step"] for f in fams.values()),
+            "mfma_busy_frac": round(busy / (gui / 8.0 * 1024.0), 4) if gui > 0 else None,
             "source": os.path.relpath(files[-1], ROOT)}
 
 

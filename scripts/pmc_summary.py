@@ -21,10 +21,14 @@ def family(name):
     return re.split(r"[<(]", n, 1)[0].strip()
 
 
-def read_pass(d, counter):
-    files = glob.glob(os.path.join(d, counter, "**", "*counter_collection.csv"), recursive=True)
+def read_pass(d, counter, optional=False, sub=None):
+    """Per-family sum of `counter` (and launch counts) from the pass in d/<sub or counter>."""
+    sub = sub or ("MFMA" if counter == "SQ_VALU_MFMA_BUSY_CYCLES" else counter)
+    files = glob.glob(os.path.join(d, sub, "**", "*counter_collection.csv"), recursive=True)
     if not files:
-        raise SystemExit("no counter_collection.csv under %s/%s" % (d, counter))
+        if optional:
+            return {}, {}
+        raise SystemExit("no counter_collection.csv under %s/%s" % (d, sub))
     per = defaultdict(float)     # family -> summed counter
     launches = defaultdict(set)  # family -> dispatch ids
     for fn in files:
@@ -54,6 +58,14 @@ def main():
         fams[fam] = {"launches": n, "read_bytes": int(rd), "write_bytes": int(wr),
                      "hbm_bytes_per_launch": int((rd + wr) / max(1, n)),
                      "hbm_bytes_per_step": int((rd + wr) / args.steps)}
+    busy, _ = read_pass(args.dir, "SQ_VALU_MFMA_BUSY_CYCLES", optional=True)
+    gui, _ = read_pass(args.dir, "GRBM_GUI_ACTIVE", optional=True, sub="MFMA")
+    for fam, d in fams.items():
+        if fam in busy and gui.get(fam, 0) > 0:
+            # busy cycles summed over all 1024 SIMDs / (kernel cycles = GUI_ACTIVE over 8 XCDs / 8)
+            d["mfma_busy_frac"] = round(busy[fam] / (gui[fam] / 8.0 * 1024.0), 4)
+            d["mfma_busy_cycles"] = busy[fam]
+            d["gui_active_cycles"] = gui[fam]
     out = {"model": args.model, "steps": args.steps,
            "what": "bench.py --steps 1 --warmup 1 (2 train steps + setup), rocprofv3 --pmc "
                    "FETCH_SIZE / WRITE_SIZE in separate passes, kernel-trace only",
