@@ -111,8 +111,9 @@ int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krs
  * gradient, and for a residual unit the identity branch's gradient -- and parts the per-tile
  * column sums (sum g, sum g*(y - mean)) as float2 [tmr_conv2d_dgrad_bnbwd_parts(d)][c], finished
  * by tmr_bn_bwd_parts.  Removes the separate statistics pass over (dz, y[, z]) of tmr_bn_bwd.
- * dx, y, z dense NHWC (x_ld == c).  mask 3: z is the ReLU mask as bits (tmr_bn_apply_bits;
- * fp32 dgrad with transposed weights, TMR_IO_WT_F32, and h*w*c a multiple of 32). */
+ * dx, y, z dense NHWC (x_ld == c).  mask 3: z is the ReLU mask as bits (tmr_bn_apply_bits /
+ * _bits_a16; the LDS-DMA dgrad with transposed weights, TMR_IO_WT_F32 or TMR_IO_WT_BF16, and
+ * h*w*c a multiple of 32). */
 int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d);
 int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
                            float beta, const float* y, const float* z, const float* scale,
@@ -338,6 +339,15 @@ int tmr_bn_apply_a16(const void* y, const float* scale, const float* shift, cons
 int tmr_bn_apply2_a16(const void* y, const float* scale, const float* shift, const void* yr,
                       const float* rscale, const float* rshift, void* z, int rows, int c, int relu,
                       hipStream_t stream);
+/* tmr_bn_apply_bits / tmr_bn_apply2_bits for bf16 activations: z bf16 and its ReLU mask as bits
+ * (taken from the rounded z, so mask 3 equals the mask-1 test z > 0) for the residual-gradient
+ * dgrads of the bf16 LDS-DMA engine (TMR_IO_WT_BF16, mask 3) */
+int tmr_bn_apply_bits_a16(const void* y, const float* scale, const float* shift,
+                          const void* residual, void* z, uint32_t* bits, int rows, int c,
+                          hipStream_t stream);
+int tmr_bn_apply2_bits_a16(const void* y, const float* scale, const float* shift, const void* yr,
+                           const float* rscale, const float* rshift, void* z, uint32_t* bits,
+                           int rows, int c, hipStream_t stream);
 int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const float* scale,
                    const float* shift, const float* save_mean, const float* save_invstd,
                    const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta, int rows,

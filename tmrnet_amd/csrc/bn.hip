@@ -236,15 +236,19 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, cons
 // re-reading the 4-byte z.  Each lane holds 4 consecutive elements (one float4 index i); the 8
 // lanes of a word OR their nibbles.  Wave-uniform loop: the waves' lanes stay converged for the
 // shuffles.
-template <bool RES>
-__global__ __launch_bounds__(NT) void bn_apply_bits_k(const float* __restrict__ y,
+// T: element type of y, the residual / branch input and z (bf16 under the bf16-activation contract:
+// the bit is taken from the stored, rounded value, so it equals the mask-1 test z > 0 exactly)
+__device__ __forceinline__ float stored(float v, const float*) { return v; }
+__device__ __forceinline__ float stored(float v, const __bf16*) { return (float)(__bf16)v; }
+template <bool RES, typename T = float>
+__global__ __launch_bounds__(NT) void bn_apply_bits_k(const T* __restrict__ y,
                                                       const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
-                                                      const float* __restrict__ res,
-                                                      const float* __restrict__ yr,
+                                                      const T* __restrict__ res,
+                                                      const T* __restrict__ yr,
                                                       const float* __restrict__ rscale,
                                                       const float* __restrict__ rshift,
-                                                      float* __restrict__ z,
+                                                      T* __restrict__ z,
                                                       uint32_t* __restrict__ bits, long n4, int c4) {
   const int lane = threadIdx.x & 63;
   const long stride = (long)gridDim.x * NT;
@@ -274,8 +278,9 @@ __global__ __launch_bounds__(NT) void bn_apply_bits_k(const float* __restrict__ 
       }
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
       st4(z, i, v);
-      nib = (uint32_t)(v.x > 0.f) | ((uint32_t)(v.y > 0.f) << 1) | ((uint32_t)(v.z > 0.f) << 2) |
-            ((uint32_t)(v.w > 0.f) << 3);
+      const T* tag = nullptr;
+      nib = (uint32_t)(stored(v.x, tag) > 0.f) | ((uint32_t)(stored(v.y, tag) > 0.f) << 1) |
+            ((uint32_t)(stored(v.z, tag) > 0.f) << 2) | ((uint32_t)(stored(v.w, tag) > 0.f) << 3);
     }
     uint32_t w = nib << (4 * (lane & 7));
     w |= (uint32_t)__shfl_xor((int)w, 1, 64);
@@ -829,10 +834,10 @@ TMR_API int tmr_bn_apply_bits(const float* y, const float* scale, const float* s
   const long n4 = (long)rows * c / 4;
   if (n4 == 0) return 0;
   if (residual)
-    hipLaunchKernelGGL((bn_apply_bits_k<true>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+    hipLaunchKernelGGL((bn_apply_bits_k<true, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
                        shift, residual, nullptr, nullptr, nullptr, z, bits, n4, c / 4);
   else
-    hipLaunchKernelGGL((bn_apply_bits_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+    hipLaunchKernelGGL((bn_apply_bits_k<false, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
                        shift, nullptr, nullptr, nullptr, nullptr, z, bits, n4, c / 4);
   TMR_CHECK_LAUNCH("bn_apply_bits");
   return 0;
@@ -846,9 +851,43 @@ TMR_API int tmr_bn_apply2_bits(const float* y, const float* scale, const float* 
   TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_bits: the branch input must not alias z");
   const long n4 = (long)rows * c / 4;
   if (n4 == 0) return 0;
-  hipLaunchKernelGGL((bn_apply_bits_k<false>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+  hipLaunchKernelGGL((bn_apply_bits_k<false, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
                      shift, nullptr, yr, rscale, rshift, z, bits, n4, c / 4);
   TMR_CHECK_LAUNCH("bn_apply2_bits");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply_bits_a16(const void* y, const float* scale, const float* shift,
+                                  const void* residual, void* z, uint32_t* bits, int rows, int c,
+                                  hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && z && bits,
+                "tmr_bn_apply_bits_a16: null operand or channels %d not a multiple of 4", c);
+  const long n4 = (long)rows * c / 4;
+  if (n4 == 0) return 0;
+  const __bf16* yb = (const __bf16*)y;
+  if (residual)
+    hipLaunchKernelGGL((bn_apply_bits_k<true, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, yb,
+                       scale, shift, (const __bf16*)residual, nullptr, nullptr, nullptr, (__bf16*)z,
+                       bits, n4, c / 4);
+  else
+    hipLaunchKernelGGL((bn_apply_bits_k<false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, yb,
+                       scale, shift, nullptr, nullptr, nullptr, nullptr, (__bf16*)z, bits, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply_bits_a16");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply2_bits_a16(const void* y, const float* scale, const float* shift,
+                                   const void* yr, const float* rscale, const float* rshift,
+                                   void* z, uint32_t* bits, int rows, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && yr && rscale && rshift && z && bits,
+                "tmr_bn_apply2_bits_a16: null operand or channels %d not a multiple of 4", c);
+  TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_bits_a16: the branch input must not alias z");
+  const long n4 = (long)rows * c / 4;
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL((bn_apply_bits_k<false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream,
+                     (const __bf16*)y, scale, shift, nullptr, (const __bf16*)yr, rscale, rshift,
+                     (__bf16*)z, bits, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply2_bits_a16");
   return 0;
 }
 

@@ -701,8 +701,9 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   // ReLU-mask bits are read by the LDS-staged BN-backward epilogue only (every dgrad tile but
   // 256x256, whose wave row-blocks do not fit the staging buffer)
   TMR_CHECK_ARG(a.bn_part == nullptr || a.bn_mask != 3 ||
-                    (MODE == MODE_DGRAD && f32 && !(c.bm == 256 && c.bn == 256)),
-                "gemm: ReLU-mask bits (mask 3) need the fp32 LDS-DMA dgrad (tile %dx%d)", c.bm, c.bn);
+                    (MODE == MODE_DGRAD && !(c.bm == 256 && c.bn == 256)),
+                "gemm: ReLU-mask bits (mask 3) need the LDS-DMA dgrad's LDS-staged epilogue (tile %dx%d)",
+                c.bm, c.bn);
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   // a k-tile (64 bf16 / 32 fp32) spans several taps when the channels per tap are fewer (or not

@@ -515,9 +515,10 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
                 "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
-  TMR_CHECK_ARG(mask != 3 || ((d->io & TMR_IO_WT_F32) && ((long)d->h * d->w * d->c) % 32 == 0),
-                "tmr_conv2d_dgrad_bnbwd: ReLU-mask bits (mask 3) need the fp32 LDS-DMA dgrad "
-                "(TMR_IO_WT_F32) and h*w*c a multiple of 32");
+  TMR_CHECK_ARG(mask != 3 || ((d->io & (TMR_IO_WT_F32 | TMR_IO_WT_BF16)) &&
+                              ((long)d->h * d->w * d->c) % 32 == 0),
+                "tmr_conv2d_dgrad_bnbwd: ReLU-mask bits (mask 3) need the LDS-DMA dgrad "
+                "(TMR_IO_WT_F32 / TMR_IO_WT_BF16) and h*w*c a multiple of 32");
   const int np = tmr_conv2d_dgrad_bnbwd_parts(d);
   TMR_CHECK_ARG(np >= 0 && parts_bytes >= (size_t)np * d->c * sizeof(float2),
                 "tmr_conv2d_dgrad_bnbwd: parts buffer too small");

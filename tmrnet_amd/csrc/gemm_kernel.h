@@ -1335,8 +1335,10 @@ inline int pick_cfg(long M, long N, long K, int mode) {
   // Plain GEMMs with few output rows (the LSTM input projection and its dgrad: M = B*T = 640,
   // N = K = 2048) leave most of the 256 CUs idle on the big tiles: step down through 256x128,
   // 128x128 and 64x64 until the grid has >= 256 workgroups.  (The conv views have M >= F*49 rows
-  // and never get here; WGRAD splits its reduction over blockIdx.y instead.)
-  if (mode != MODE_WGRAD && cfg_tiles(M, N, cfg) < 128) {
+  // and never get here; the conv WGRAD splits its reduction over blockIdx.y instead.  A plain
+  // A^T B GEMM (tmr_gemm_tn, WGRAD view without splits) with a short reduction -- the split
+  // attention's fc weight gradients over the frames, K = F -- steps down the same way.)
+  if ((mode != MODE_WGRAD || K <= 8192) && cfg_tiles(M, N, cfg) < 128) {
     const long area = (long)kCfgs[cfg].bm * kCfgs[cfg].bn;
     for (const int c2 : {4, 0, 3}) {
       if ((long)kCfgs[c2].bm * kCfgs[c2].bn >= area || cfg_tiles(M, N, c2) <= cfg_tiles(M, N, cfg))

@@ -133,6 +133,10 @@ DS_FIRST = os.environ.get("TMR_DS_FIRST", "1") != "0"
 
 # the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
 BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
+# ... and for the bf16-activation step (TMR_RELU_BITS16=1).  Off: the bf16 dgrads re-read the 2-byte
+# z, measured faster than the bits (C5 dgrads 56.6 vs 58.8 ms/step, C4 22.2 vs 23.1;
+# profiles/r3/bench_r4i/) -- the bits cost one dword load per row shared by 8 threads
+BITS16 = os.environ.get("TMR_RELU_BITS16", "0") == "1"
 
 
 def _dma32(math):
@@ -200,7 +204,10 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     # fp32 block outputs on the LDS-DMA path also record their ReLU mask as bits: the dgrad that
     # produces their gradient reads 1 bit instead of z's 4 bytes (mask 3)
     zbits = None
-    bits = (recs is not None and relu and not dual and _dma32(math) and y.dtype == torch.float32
+    # (bf16 activations too: the bits of the rounded z, tmr_bn_apply_bits_a16)
+    bits = (recs is not None and relu and not dual and
+            ((_dma32(math) and y.dtype == torch.float32) or
+             (_act16(math) and y.dtype == torch.bfloat16 and BITS16))
             and (residual is not None or branch is not None) and BITS)
     if defer:
         z = None
