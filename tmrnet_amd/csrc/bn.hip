@@ -157,6 +157,12 @@ __device__ __forceinline__ void st4(__bf16* p, long i4, float4 v) {
       make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
 }
 
+// channel group of element group i in rows of c groups: a mask when c is a power of two (every
+// conv channel count of the trunks), else a 64-bit remainder
+__device__ __forceinline__ int chan_of(long i, int c) {
+  return (c & (c - 1)) == 0 ? (int)(i & (long)(c - 1)) : (int)(i % c);
+}
+
 // DUAL: z (fp32) and a bf16 (RNE) copy z16 -- a block output is both the next block's identity
 // residual (fp32) and the operand of its bf16-math convs (bf16, read by the LDS-DMA engine)
 // 4 consecutive elements of an fp32 or bf16 tensor as float4 (bf16 -> fp32 is exact)
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const TY* __restrict__ y, const
                                                  const TY* __restrict__ res, TZ* __restrict__ z,
                                                  long n4, int c4, __bf16* __restrict__ z16 = nullptr) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    const int cc = (int)(i % c4) * 4;
+    const int cc = chan_of(i, c4) * 4;
     float4 v = ld4(y, i);
     const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
     const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, cons
                                                   TZ* __restrict__ z, long n4, int c4,
                                                   __bf16* __restrict__ z16) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    const int cc = (int)(i % c4) * 4;
+    const int cc = chan_of(i, c4) * 4;
     float4 v = ld4(y, i);
     const float4 r = ld4(yr, i);
     const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
@@ -256,7 +262,7 @@ __global__ __launch_bounds__(NT) void bn_apply_bits_k(const T* __restrict__ y,
     const long i = base + lane;
     uint32_t nib = 0;
     if (i < n4) {
-      const int cc = (int)(i % c4) * 4;
+      const int cc = chan_of(i, c4) * 4;
       float4 v = ld4(y, i);
       const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
       const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
@@ -403,7 +409,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
                                                    float* __restrict__ dres, long n4, int c4) {
   const int c = c4 * 4;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    const int cc = (int)(i % c4) * 4;
+    const int cc = chan_of(i, c4) * 4;
     float4 g = reinterpret_cast<const float4*>(dz)[i];
     const float4 v = ld4(y, i);
     if (MASK == 1) g = relu_mask4(g, ld4(z, i));
@@ -420,6 +426,46 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
     o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
     o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
     st4(dy, i, o);
+  }
+}
+
+// The BatchNorm-backward apply of the bf16-activation step, 8 elements per thread: g (fp32, already
+// ReLU-masked by the fused dgrad epilogue) 32 B, y (bf16) 16 B, dy (bf16) 16 B -- every access a
+// 16-B lane piece (the 4-wide form moved bf16 in 8-B pieces).  Same fmaf sequence as bn_bwd_apply.
+__global__ __launch_bounds__(NT) void bn_bwd_apply8_a16(const float* __restrict__ g,
+                                                        const __bf16* __restrict__ y,
+                                                        const float* __restrict__ coef,
+                                                        __bf16* __restrict__ dy, long n8, int c8) {
+  const int c = c8 * 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const int cc = chan_of(i, c8) * 8;
+    const float4 g0 = reinterpret_cast<const float4*>(g)[2 * i];
+    const float4 g1 = reinterpret_cast<const float4*>(g)[2 * i + 1];
+    const uint4 yw = reinterpret_cast<const uint4*>(y)[i];
+    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
+    float yv[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      yv[2 * e] = __uint_as_float(yu[e] << 16);
+      yv[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
+    }
+    uint32_t ow[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 A = *reinterpret_cast<const float4*>(coef + cc + 4 * h);
+      const float4 B = *reinterpret_cast<const float4*>(coef + c + cc + 4 * h);
+      const float4 C = *reinterpret_cast<const float4*>(coef + 2 * c + cc + 4 * h);
+      const float o0 = fmaf(A.x, gv[4 * h], fmaf(B.x, yv[4 * h], C.x));
+      const float o1 = fmaf(A.y, gv[4 * h + 1], fmaf(B.y, yv[4 * h + 1], C.y));
+      const float o2 = fmaf(A.z, gv[4 * h + 2], fmaf(B.z, yv[4 * h + 2], C.z));
+      const float o3 = fmaf(A.w, gv[4 * h + 3], fmaf(B.w, yv[4 * h + 3], C.w));
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      const bf16x2_t p = {(__bf16)o0, (__bf16)o1}, q = {(__bf16)o2, (__bf16)o3};
+      ow[2 * h] = __builtin_bit_cast(uint32_t, p);
+      ow[2 * h + 1] = __builtin_bit_cast(uint32_t, q);
+    }
+    reinterpret_cast<uint4*>(dy)[i] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
 }
 
@@ -1230,9 +1276,16 @@ TMR_API int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* part
                      dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
   const long n4 = (long)rows * c / 4;
-  hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
-                     stream, g, (const __bf16*)y, nullptr, nullptr, nullptr, coef, (__bf16*)dy,
-                     nullptr, n4, c / 4);
+  const char* w8 = getenv("TMR_BN8");   // A/B switch (0: the 4-wide form)
+  if (!(w8 && w8[0] == '0') && c % 8 == 0 && (((uintptr_t)g | (uintptr_t)y | (uintptr_t)dy) & 15) == 0) {
+    const long n8 = n4 / 2;
+    hipLaunchKernelGGL(bn_bwd_apply8_a16, dim3(ew_blocks(n8)), dim3(NT), 0, stream, g,
+                       (const __bf16*)y, coef, (__bf16*)dy, n8, c / 8);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
+                       stream, g, (const __bf16*)y, nullptr, nullptr, nullptr, coef, (__bf16*)dy,
+                       nullptr, n4, c / 4);
+  }
   TMR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }
