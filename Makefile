@@ -8,13 +8,17 @@ CFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Itmrnet_amd/csr
 tmrnet_amd/libtmr.so: $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
 
-build/%.hip.o: tmrnet_amd/csrc/%.hip tmrnet_amd/csrc/common.h tmrnet_amd/csrc/gemm_kernel.h tmrnet_amd/csrc/gemm16_kernel.h include/tmr.h
+# header dependencies from the compiler (-MMD: build/*.d); an edit of the LDS-DMA engine
+# (gemm16_kernel.h) rebuilds only the gemm16_<view>_<prec>.hip units
+build/%.hip.o: tmrnet_amd/csrc/%.hip
 	@mkdir -p build
-	$(HIPCC) $(CFLAGS) -c $< -o $@
+	$(HIPCC) $(CFLAGS) -MMD -MP -c $< -o $@
 
-build/%.cpp.o: tmrnet_amd/csrc/%.cpp tmrnet_amd/csrc/common.h include/tmr.h
+build/%.cpp.o: tmrnet_amd/csrc/%.cpp
 	@mkdir -p build
-	$(HIPCC) $(CFLAGS) -c $< -o $@
+	$(HIPCC) $(CFLAGS) -MMD -MP -c $< -o $@
+
+-include $(OBJ:.o=.d)
 
 clean:
 	rm -rf build tmrnet_amd/libtmr.so

@@ -24,7 +24,7 @@
 // are bound by that traffic), and the k order of the accumulation is the register-staged bf16
 // path's, so FWD / DGRAD results are bit-identical to it.
 #pragma once
-#include "gemm_kernel.h"
+#include "gemm16_select.h"
 #include <type_traits>
 
 namespace tmrg {
@@ -568,129 +568,23 @@ void gemm16_kernel(const GemmArgs a) {
                                                  split);
 }
 
-// ---------------------------------------------------------------- launch selection
-struct Cfg16 { int bm, bn; };
-constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64, 256}, {64, 64},
-                              {256, 256},    // 6: 256x256 as 16 waves (4x4, 64x64 per wave)
-                              {128, 128}};   // 7: 128x128 as 8 waves (4x2, 32x64 per wave)
-
-// Eligibility: bf16 math, every operand bf16 in HBM (sab 3; DGRAD with the transposed weights),
-// no operand prologue, 16-B pieces of 8 channels (channels per tap, row strides multiples of 8).
-// fp32 form (GemmArgs::dma32, set by the conv entry points): FWD with every operand fp32 and
-// 16-B aligned, 4-channel pieces; DGRAD whenever the weights come transposed (wt: the engine is
-// the only reader of that layout, so eligibility is checked again by launch_gemm16_t).
-inline bool use32(const GemmArgs& a, int mode) {
-  // A/B switch for the forward view, read per launch (tests flip it in-process)
-  const bool on = env_int("TMR_GEMM32", 1) != 0;
-  if (a.prec != TMR_MATH_F32 || a.sab || a.pro) return false;
-  if (mode == MODE_DGRAD) return a.wt != 0;
-  if (!on || !a.dma32) return false;
-  if ((((uintptr_t)a.A | (uintptr_t)a.B) & 15) != 0) return false;
-  if (mode == MODE_WGRAD)
-    return a.M % 4 == 0 && a.log2C >= 2 && a.ldb % 4 == 0 && a.lds % 4 == 0 && a.N % 4 == 0;
-  return a.lds % 4 == 0 && a.ldb % 4 == 0 && a.log2C >= 2 && (a.ntaps != 1 || a.K % 4 == 0);
-}
-
-inline bool use16(const GemmArgs& a, int mode) {
-  static const bool on = env_int("TMR_GEMM16", 1) != 0;   // A/B switch (experiments)
-  if (a.prec == TMR_MATH_F32) return use32(a, mode);
-  if (!on || a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
-  if (mode == MODE_DGRAD && !a.wt) return false;
-  if (a.lds % 8) return false;
-  if (mode == MODE_WGRAD) return a.M % 8 == 0 && a.log2C >= 3 && a.ldb % 8 == 0 && a.N % 8 == 0;
-  if (mode == MODE_FWD && a.ldb % 8) return false;
-  if (mode == MODE_DGRAD && a.ldbt % 8) return false;
-  return a.ntaps == 1 ? (a.K % 8 == 0 && (mode == MODE_FWD || a.log2C >= 3)) : a.log2C >= 3;
-}
-
-inline long cfg16_tiles(long M, long N, int c) {
-  return ((M + kCfgs16[c].bm - 1) / kCfgs16[c].bm) * ((N + kCfgs16[c].bn - 1) / kCfgs16[c].bn);
-}
-
-// Tile choice per view, from scripts/convbench.py --io16 --stats --bnbwd with each config forced
-// over the 23 ResNet-50 conv shapes x 3 views (profiles/r2/convbench16_cfgs/, cb16c/): 256x256
-// pays for the forwards and the wgrads with 256-512 output channels, as 16 waves (four per SIMD:
-// 5-20% over 8 waves, whose two waves per SIMD stall on the same barrier); the dgrads, whose
-// fused BatchNorm-backward epilogue moves 12-16 B per output element, want the occupancy of
-// 128x128 / 256x64 tiles.
-// fp32 (f32): measured separately (profiles/r2/convbench32_dma_cfgs/, wgrad32_cfgs/): the
-// wgrads with 64 output channels want 64-wide tiles, the big-FLOP wgrads (>= 100 GFLOP: 3x3,
-// strided downsample) 256x256 as 16 waves, the rest 128x128 as 8 waves; the N = 128 forwards and
-// the >= 512-column dgrads 128x128 as 8 waves.
-inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false) {
-  static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
-  if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
-  int cfg;
-  if (f32 && mode == MODE_WGRAD) {
-    if (M <= 64) return (N <= 64 || N >= 512) ? 5 : 4;
-    if (N <= 64) return 5;
-    if (M >= 256 && N >= 256 && 2.0 * M * N * K >= 100e9) return 6;
-    return 7;
-  }
-  if (f32 && M >= 256 && ((mode == MODE_FWD && N == 128) || (mode == MODE_DGRAD && N >= 512)))
-    return cfg16_tiles(M, N, 7) >= 256 ? 7 : 2;
-  if (mode == MODE_WGRAD) {
-    if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
-    else if (N <= 64) cfg = 3;
-    // short reductions (layer3/4 spatial): 4x the tiles of 256x256 at the same occupancy, so
-    // fewer split-K slabs to write and reduce
-    else if (M >= 256 && N >= 256 && K <= 131072) cfg = 7;
-    else if (M >= 256 && M <= 512 && N >= 256) cfg = 6;
-    else cfg = 2;
-  } else if (N <= 64) {
-    cfg = M >= 256 ? 3 : 5;
-  } else if (mode == MODE_FWD && N >= 256 && M >= 256) {
-    cfg = 6;   // 256x256 as 16 waves: four waves per SIMD hide the barrier / load waits
-  } else {
-    cfg = 2;
-  }
-  if (mode != MODE_WGRAD && cfg16_tiles(M, N, cfg) < 256) {
-    for (const int c2 : {1, 2, 5}) {
-      if ((long)kCfgs16[c2].bm * kCfgs16[c2].bn >= (long)kCfgs16[cfg].bm * kCfgs16[cfg].bn ||
-          cfg16_tiles(M, N, c2) <= cfg16_tiles(M, N, cfg))
-        continue;
-      cfg = c2;
-      if (cfg16_tiles(M, N, cfg) >= 256) break;
-    }
-  }
-  return cfg;
-}
-
-// rows / columns of the output tile the launch for `a` will use (host planning: BN-partial rows,
-// wgrad split counts)
-inline int gemm_tile_bm(const GemmArgs& a, int mode) {
-  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32)].bm
-                        : kCfgs[pick_cfg(a.M, a.N, a.K, mode)].bm;
-}
-inline long gemm_tiles(const GemmArgs& a, int mode) {
-  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32))
-                        : cfg_tiles(a.M, a.N, pick_cfg(a.M, a.N, a.K, mode));
-}
-
-template <int MODE, int BM, int BN, int WM, int WN>
+template <int MODE, int BM, int BN, int WM, int WN, int F32>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
-  if (a.prec == TMR_MATH_F32) {
-    if (tapv)
-      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, 1>), grid, blk, 0, st, a);
-    else
-      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, 1>), grid, blk, 0, st, a);
-    TMR_CHECK_LAUNCH("gemm16_kernel (fp32)");
-    return 0;
-  }
   if (tapv)
-    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, F32>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0>), grid, blk, 0, st, a);
-  TMR_CHECK_LAUNCH("gemm16_kernel");
+    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32>), grid, blk, 0, st, a);
+  TMR_CHECK_LAUNCH(F32 ? "gemm16_kernel (fp32)" : "gemm16_kernel");
   return 0;
 }
 
-template <int MODE>
+template <int MODE, int F32>
 int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   TMR_CHECK_ARG(((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0,
                 "gemm (LDS-DMA path): operands must be 16-B aligned");
-  const bool f32 = a.prec == TMR_MATH_F32;
+  constexpr bool f32 = F32 != 0;
+  TMR_CHECK_ARG((a.prec == TMR_MATH_F32) == f32, "gemm (LDS-DMA path): precision dispatch");
   TMR_CHECK_ARG(!f32 || (a.lds % 4 == 0 && a.log2C >= 2 &&
                          (MODE == MODE_DGRAD ? (a.ldbt % 4 == 0 && a.N % 8 == 0 && a.ldc % 4 == 0 &&
                                                 ((uintptr_t)a.C & 15) == 0)
@@ -712,15 +606,20 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
   switch (cfg) {
-    case 0: return launch16_cfg<MODE, 256, 256, 2, 4>(a, tapv, grid, st);
-    case 1: return launch16_cfg<MODE, 256, 128, 4, 2>(a, tapv, grid, st);
-    case 2: return launch16_cfg<MODE, 128, 128, 2, 2>(a, tapv, grid, st);
-    case 3: return launch16_cfg<MODE, 256, 64, 4, 1>(a, tapv, grid, st);
-    case 4: return launch16_cfg<MODE, 64, 256, 1, 4>(a, tapv, grid, st);
-    case 6: return launch16_cfg<MODE, 256, 256, 4, 4>(a, tapv, grid, st);
-    case 7: return launch16_cfg<MODE, 128, 128, 4, 2>(a, tapv, grid, st);
-    default: return launch16_cfg<MODE, 64, 64, 2, 2>(a, tapv, grid, st);
+    case 0: return launch16_cfg<MODE, 256, 256, 2, 4, F32>(a, tapv, grid, st);
+    case 1: return launch16_cfg<MODE, 256, 128, 4, 2, F32>(a, tapv, grid, st);
+    case 2: return launch16_cfg<MODE, 128, 128, 2, 2, F32>(a, tapv, grid, st);
+    case 3: return launch16_cfg<MODE, 256, 64, 4, 1, F32>(a, tapv, grid, st);
+    case 4: return launch16_cfg<MODE, 64, 256, 1, 4, F32>(a, tapv, grid, st);
+    case 6: return launch16_cfg<MODE, 256, 256, 4, 4, F32>(a, tapv, grid, st);
+    case 7: return launch16_cfg<MODE, 128, 128, 4, 2, F32>(a, tapv, grid, st);
+    default: return launch16_cfg<MODE, 64, 64, 2, 2, F32>(a, tapv, grid, st);
   }
+}
+
+template <int MODE, int F32>
+int launch_gemm16(const GemmArgs& a, int splits, hipStream_t st) {
+  return launch_gemm16_t<MODE, F32>(a, splits, st);
 }
 
 }  // namespace tmrg

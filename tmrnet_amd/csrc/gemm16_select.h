@@ -1,0 +1,120 @@
+// Host-side launch selection of the LDS-DMA implicit-GEMM engine (gemm16_kernel.h): eligibility
+// per view, tile rules, and the per-(view, precision) launchers instantiated in
+// gemm16_<view>_<prec>.hip.  The register-staged translation units include only this header, so
+// an edit of the engine rebuilds the six small engine units and nothing else.
+#pragma once
+#include "gemm_kernel.h"
+
+namespace tmrg {
+
+// ---------------------------------------------------------------- launch selection
+struct Cfg16 { int bm, bn; };
+constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64, 256}, {64, 64},
+                              {256, 256},    // 6: 256x256 as 16 waves (4x4, 64x64 per wave)
+                              {128, 128}};   // 7: 128x128 as 8 waves (4x2, 32x64 per wave)
+
+// Eligibility: bf16 math, every operand bf16 in HBM (sab 3; DGRAD with the transposed weights),
+// no operand prologue, 16-B pieces of 8 channels (channels per tap, row strides multiples of 8).
+// fp32 form (GemmArgs::dma32, set by the conv entry points): FWD with every operand fp32 and
+// 16-B aligned, 4-channel pieces; DGRAD whenever the weights come transposed (wt: the engine is
+// the only reader of that layout, so eligibility is checked again by launch_gemm16_t).
+inline bool use32(const GemmArgs& a, int mode) {
+  // A/B switch for the forward view, read per launch (tests flip it in-process)
+  const bool on = env_int("TMR_GEMM32", 1) != 0;
+  if (a.prec != TMR_MATH_F32 || a.sab || a.pro) return false;
+  if (mode == MODE_DGRAD) return a.wt != 0;
+  if (!on || !a.dma32) return false;
+  if ((((uintptr_t)a.A | (uintptr_t)a.B) & 15) != 0) return false;
+  if (mode == MODE_WGRAD)
+    return a.M % 4 == 0 && a.log2C >= 2 && a.ldb % 4 == 0 && a.lds % 4 == 0 && a.N % 4 == 0;
+  return a.lds % 4 == 0 && a.ldb % 4 == 0 && a.log2C >= 2 && (a.ntaps != 1 || a.K % 4 == 0);
+}
+
+inline bool use16(const GemmArgs& a, int mode) {
+  static const bool on = env_int("TMR_GEMM16", 1) != 0;   // A/B switch (experiments)
+  if (a.prec == TMR_MATH_F32) return use32(a, mode);
+  if (!on || a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
+  if (mode == MODE_DGRAD && !a.wt) return false;
+  if (a.lds % 8) return false;
+  if (mode == MODE_WGRAD) return a.M % 8 == 0 && a.log2C >= 3 && a.ldb % 8 == 0 && a.N % 8 == 0;
+  if (mode == MODE_FWD && a.ldb % 8) return false;
+  if (mode == MODE_DGRAD && a.ldbt % 8) return false;
+  return a.ntaps == 1 ? (a.K % 8 == 0 && (mode == MODE_FWD || a.log2C >= 3)) : a.log2C >= 3;
+}
+
+inline long cfg16_tiles(long M, long N, int c) {
+  return ((M + kCfgs16[c].bm - 1) / kCfgs16[c].bm) * ((N + kCfgs16[c].bn - 1) / kCfgs16[c].bn);
+}
+
+// Tile choice per view, from scripts/convbench.py --io16 --stats --bnbwd with each config forced
+// over the 23 ResNet-50 conv shapes x 3 views (profiles/r2/convbench16_cfgs/, cb16c/): 256x256
+// pays for the forwards and the wgrads with 256-512 output channels, as 16 waves (four per SIMD:
+// 5-20% over 8 waves, whose two waves per SIMD stall on the same barrier); the dgrads, whose
+// fused BatchNorm-backward epilogue moves 12-16 B per output element, want the occupancy of
+// 128x128 / 256x64 tiles.
+// fp32 (f32): measured separately (profiles/r2/convbench32_dma_cfgs/, wgrad32_cfgs/): the
+// wgrads with 64 output channels want 64-wide tiles, the big-FLOP wgrads (>= 100 GFLOP: 3x3,
+// strided downsample) 256x256 as 16 waves, the rest 128x128 as 8 waves; the N = 128 forwards and
+// the >= 512-column dgrads 128x128 as 8 waves.
+inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false) {
+  static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
+  if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
+  int cfg;
+  if (f32 && mode == MODE_WGRAD) {
+    if (M <= 64) return (N <= 64 || N >= 512) ? 5 : 4;
+    if (N <= 64) return 5;
+    if (M >= 256 && N >= 256 && 2.0 * M * N * K >= 100e9) return 6;
+    return 7;
+  }
+  if (f32 && M >= 256 && ((mode == MODE_FWD && N == 128) || (mode == MODE_DGRAD && N >= 512)))
+    return cfg16_tiles(M, N, 7) >= 256 ? 7 : 2;
+  if (mode == MODE_WGRAD) {
+    if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
+    else if (N <= 64) cfg = 3;
+    // short reductions (layer3/4 spatial): 4x the tiles of 256x256 at the same occupancy, so
+    // fewer split-K slabs to write and reduce
+    else if (M >= 256 && N >= 256 && K <= 131072) cfg = 7;
+    else if (M >= 256 && M <= 512 && N >= 256) cfg = 6;
+    else cfg = 2;
+  } else if (N <= 64) {
+    cfg = M >= 256 ? 3 : 5;
+  } else if (mode == MODE_FWD && N >= 256 && M >= 256) {
+    cfg = 6;   // 256x256 as 16 waves: four waves per SIMD hide the barrier / load waits
+  } else {
+    cfg = 2;
+  }
+  if (mode != MODE_WGRAD && cfg16_tiles(M, N, cfg) < 256) {
+    for (const int c2 : {1, 2, 5}) {
+      if ((long)kCfgs16[c2].bm * kCfgs16[c2].bn >= (long)kCfgs16[cfg].bm * kCfgs16[cfg].bn ||
+          cfg16_tiles(M, N, c2) <= cfg16_tiles(M, N, cfg))
+        continue;
+      cfg = c2;
+      if (cfg16_tiles(M, N, cfg) >= 256) break;
+    }
+  }
+  return cfg;
+}
+
+// rows / columns of the output tile the launch for `a` will use (host planning: BN-partial rows,
+// wgrad split counts)
+inline int gemm_tile_bm(const GemmArgs& a, int mode) {
+  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32)].bm
+                        : kCfgs[pick_cfg(a.M, a.N, a.K, mode)].bm;
+}
+inline long gemm_tiles(const GemmArgs& a, int mode) {
+  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32))
+                        : cfg_tiles(a.M, a.N, pick_cfg(a.M, a.N, a.K, mode));
+}
+
+// one view x precision per translation unit (gemm16_<view>_<prec>.hip, explicit instantiations:
+// they compile in parallel)
+template <int MODE, int F32>
+int launch_gemm16(const GemmArgs& a, int splits, hipStream_t st);
+extern template int launch_gemm16<MODE_FWD, 0>(const GemmArgs&, int, hipStream_t);
+extern template int launch_gemm16<MODE_FWD, 1>(const GemmArgs&, int, hipStream_t);
+extern template int launch_gemm16<MODE_DGRAD, 0>(const GemmArgs&, int, hipStream_t);
+extern template int launch_gemm16<MODE_DGRAD, 1>(const GemmArgs&, int, hipStream_t);
+extern template int launch_gemm16<MODE_WGRAD, 0>(const GemmArgs&, int, hipStream_t);
+extern template int launch_gemm16<MODE_WGRAD, 1>(const GemmArgs&, int, hipStream_t);
+
+}  // namespace tmrg

@@ -1,5 +1,5 @@
 // Implicit-GEMM convolution / GEMM engine: host side and C ABI (kernel template: gemm_kernel.h).
-#include "gemm16_kernel.h"
+#include "gemm16_select.h"
 
 #include <type_traits>
 
