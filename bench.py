@@ -219,9 +219,10 @@ def main():
         tot_flops = sum(r[1] for r in recs)
         tot_bytes = sum(r[5] for r in recs)
         if args.conv_table and rank == 0:
-            for kind, f, e0, e1, shp, _ in recs:
+            for kind, f, e0, e1, shp, nb in recs:
                 t = e0.elapsed_time(e1)
-                print("%-10s %-34s %8.3f ms %7.1f TF" % (kind, shp, t, f / (t * 1e-3) / 1e12),
+                print("%-10s %-34s %8.3f ms %7.1f TF %7.0f GB/s" % (kind, shp, t, f / (t * 1e-3) / 1e12,
+                                                                    nb / (t * 1e-3) / 1e9),
                       file=sys.stderr)
         achieved = tot_flops / (tot_ms * 1e-3) / 1e12
         per_kind = {}

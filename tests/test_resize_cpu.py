@@ -8,6 +8,7 @@ import os
 
 import numpy as np
 import pytest
+import torch
 from PIL import Image
 
 from oracle import resize_ref
@@ -73,3 +74,33 @@ def test_decode_matches_pil_loader(tmp_path):
     Image.fromarray(np.zeros((10, 10, 3), np.uint8), "RGB").save(bad)
     with pytest.raises(RuntimeError):
         frames.decode_frames(paths[:2] + [bad])
+
+
+def test_decode_pool_matches_pil_loader(tmp_path):
+    """DecodePool (pil_loader in worker processes writing a shared-memory batch) == decode_frames
+    frame by frame; the slot ring keeps an earlier batch intact while the next one decodes; a
+    worker's size mismatch is raised in the caller."""
+    from tmrnet_amd import frames
+    g = np.random.Generator(np.random.PCG64(7))
+    paths = []
+    for i in range(11):
+        img = g.integers(0, 256, (40, 56, 3), dtype=np.uint8)
+        p = str(tmp_path / ("p%d.%s" % (i, "jpg" if i % 3 else "png")))
+        Image.fromarray(img, "RGB").save(p, quality=85)
+        paths.append(p)
+    want = frames.decode_frames(paths, workers=2).numpy().copy()
+    with frames.DecodePool(workers=2, slots=2, chunk=3) as pool:
+        j0 = pool.submit(paths)
+        j1 = pool.submit(paths[::-1])
+        a = j0.result()
+        b = j1.result()
+        assert tuple(a.shape) == (11, 40, 56, 3) and a.dtype == torch.uint8
+        assert np.array_equal(a.numpy(), want)
+        assert np.array_equal(b.numpy(), want[::-1])
+        bad = str(tmp_path / "small.png")
+        Image.fromarray(np.zeros((8, 8, 3), np.uint8), "RGB").save(bad)
+        with pytest.raises(RuntimeError):
+            pool.decode(paths[:4] + [bad])
+        # a larger batch grows the slot's segment
+        c = pool.decode(paths * 3)
+        assert np.array_equal(c.numpy()[11:22], want)

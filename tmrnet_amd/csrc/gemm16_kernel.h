@@ -47,9 +47,219 @@ __device__ __forceinline__ int mn_swz(int k) {
 // Fused BatchNorm-backward epilogue of the DGRAD view through LDS (the tile is written to LDS in
 // row chunks, then each thread owns 8 consecutive columns of a row: 16-B / 32-B vector accesses of
 // y, z (bf16 or fp32), the old dx (beta) and the new dx, instead of one scalar access per
-// accumulator register).  Per row: beta, ReLU mask (z > 0, or y*scale+shift > 0, or none), store,
-// and per-column sums of g and g*(y - mean); the tile's column sums -> bn_part (one partial row per
-// m-tile, as epilogue_batched).
+// accumulator register).  Per row: beta, ReLU mask (z > 0, or y*scale+shift > 0, or bits, or
+// none), store, and per-column sums of g and g*(y - mean); the tile's column sums -> bn_part (one
+// partial row per m-tile, as epilogue_batched).
+//
+// The epilogue is HBM-bound (12-16 B per output element) and its rows are independent, so its
+// global operands are software-pipelined: the first D rows of each thread are loaded before the
+// main loop (they land under the MFMAs), and row t + D is issued right after row t is consumed.
+// Every (row, 8-column group) belongs to one thread, so reading the old dx of a later row before
+// this row's store cannot alias.  With loads issued one row at a time a thread keeps ~64 B in
+// flight and the launch is latency-bound (3.6 TB/s on the 56x56 residual dgrads).
+#ifndef TMR_EPI_DEPTH
+#define TMR_EPI_DEPTH 3
+#endif
+template <int BM, int BN, int WM, int WN, int SMEMB>
+struct LdsBnbwd {
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int LDC = BN + 4;                   // padded fp32 row of the staged tile
+  static constexpr int CG = BN / 8;                    // column groups of 8
+  static constexpr int RPP = NT / CG;                  // rows per pass over a chunk
+  static constexpr int WR = BM / WM;                   // rows of one wave row-block
+  static constexpr int RC0 = (SMEMB / 4 / LDC) / WR * WR;
+  // rows staged per chunk (whole row-blocks; configs where one row-block does not fit never run
+  // this epilogue)
+  static constexpr int RCH = RC0 < WR ? WR : (RC0 < BM ? RC0 : BM);
+  static constexpr int NCH = (BM + RCH - 1) / RCH;
+  static constexpr int PC = (RCH + RPP - 1) / RPP;     // row slots of a thread per chunk
+  static constexpr int NR = NCH * PC;                  // row slots of a thread
+  static constexpr int D = NR < TMR_EPI_DEPTH ? NR : TMR_EPI_DEPTH;   // rows in flight
+  static_assert(NT % CG == 0, "epilogue row partition");
+
+  struct In {         // one row's global operands as loaded
+    uint4 y0, y1, z0, z1, c0, c1;
+    uint32_t bits;
+    long off;
+    bool ok;
+  };
+
+  // issue the loads of row slot t (tile-relative row r)
+  __device__ __forceinline__ static void issue(const GemmArgs& a, int t, int m0, int n0, In& x) {
+    const int etid = threadIdx.x;
+    const int cg = etid % CG, rsub = etid / CG;
+    const int ci = t / PC, j = t % PC;
+    const int rr = rsub + j * RPP;                     // row within chunk ci
+    const int nrow = (BM - ci * RCH) < RCH ? (BM - ci * RCH) : RCH;
+    const int col = n0 + 8 * cg;
+    const int row = m0 + ci * RCH + rr;
+    x.ok = rr < nrow && col < a.N && row < a.M;
+    long pix = row;
+    if (x.ok && a.osy != 0) {   // the parity class's output pixel
+      const uint32_t n = fdiv((uint32_t)row, a.dHW);
+      const uint32_t rem = row - n * a.dHW.d;
+      const uint32_t y = fdiv(rem, a.dW);
+      const uint32_t xx = rem - y * a.dW.d;
+      pix = ((long)n * a.oH + (long)y * a.osy + a.oyc) * a.oW + (long)xx * a.osx + a.oxc;
+    }
+    x.off = pix * a.ldc + col;
+    if (!x.ok) return;
+    const long off = x.off;
+    if (a.bn16) {
+      x.y0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.bn_y) + off);
+      if (a.bn_mask == 1)
+        x.z0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.bn_z) + off);
+    } else {
+      x.y0 = *reinterpret_cast<const uint4*>(a.bn_y + off);
+      x.y1 = *reinterpret_cast<const uint4*>(a.bn_y + off + 4);
+      if (a.bn_mask == 1) {
+        x.z0 = *reinterpret_cast<const uint4*>(a.bn_z + off);
+        x.z1 = *reinterpret_cast<const uint4*>(a.bn_z + off + 4);
+      }
+    }
+    if (a.bn_mask == 3) x.bits = reinterpret_cast<const uint32_t*>(a.bn_z)[off >> 5];
+    if (a.beta != 0.f) {
+      x.c0 = *reinterpret_cast<const uint4*>(a.C + off);
+      x.c1 = *reinterpret_cast<const uint4*>(a.C + off + 4);
+    }
+  }
+
+  __device__ __forceinline__ static void prefetch(const GemmArgs& a, int m0, int n0, In (&pf)[D]) {
+#pragma unroll
+    for (int t = 0; t < D; ++t) issue(a, t, m0, n0, pf[t]);
+  }
+
+  template <int TM, int TN>
+  __device__ __forceinline__ static void run(const GemmArgs& a, floatx16 (&acc)[TM][TN], float* lds,
+                                             int m0, int n0, In (&pf)[D]) {
+    int etid = threadIdx.x;
+    asm volatile("" : "+v"(etid));   // keep the epilogue's index math out of the main loop
+    const int lane = etid & 63, wave = etid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int l31 = lane & 31, hh = lane >> 5;
+    const int cg = etid % CG, rsub = etid / CG;
+    const int col = n0 + 8 * cg;
+    const bool okc = col < a.N;                   // N is a multiple of 8 (LDS-DMA engine)
+    // per-column coefficients of this thread's 8 columns
+    float mu[8], bsc[8], bsh[8], cs[8], cq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = okc ? col + e : 0;
+      mu[e] = okc ? a.bn_mean[c] : 0.f;
+      bsc[e] = (okc && a.bn_mask == 2) ? a.bn_sc[c] : 0.f;
+      bsh[e] = (okc && a.bn_mask == 2) ? a.bn_sh[c] : (a.bn_mask == 0 ? 1.f : 0.f);
+      cs[e] = 0.f;
+      cq[e] = 0.f;
+    }
+    const bool has_beta = a.beta != 0.f;
+#pragma unroll
+    for (int ci = 0; ci < NCH; ++ci) {
+      // (1) the waves whose rows lie in chunk ci stage their accumulators
+      __syncthreads();
+      const int wr0 = wm * WR;
+      if (wr0 >= ci * RCH && wr0 < ci * RCH + RCH) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = wr0 - ci * RCH + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              lds[row * LDC + wn * (BN / WN) + 32 * j + l31] = acc[i][j][r];
+            }
+      }
+      __syncthreads();
+      // (2) this thread's rows of the chunk, 8 columns each
+#pragma unroll
+      for (int j = 0; j < PC; ++j) {
+        const int t = ci * PC + j;
+        In& x = pf[t % D];
+        if (x.ok) {
+          const long off = x.off;
+          float yv[8], zv[8], old[8];
+          if (a.bn16) {
+            const uint32_t yu[4] = {x.y0.x, x.y0.y, x.y0.z, x.y0.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              yv[2 * e] = __uint_as_float(yu[e] << 16);
+              yv[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
+            }
+            if (a.bn_mask == 1) {
+              const uint32_t zu[4] = {x.z0.x, x.z0.y, x.z0.z, x.z0.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                zv[2 * e] = __uint_as_float(zu[e] << 16);
+                zv[2 * e + 1] = __uint_as_float(zu[e] & 0xffff0000u);
+              }
+            }
+          } else {
+            const uint32_t yu[8] = {x.y0.x, x.y0.y, x.y0.z, x.y0.w, x.y1.x, x.y1.y, x.y1.z, x.y1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) yv[e] = __uint_as_float(yu[e]);
+            if (a.bn_mask == 1) {
+              const uint32_t zu[8] = {x.z0.x, x.z0.y, x.z0.z, x.z0.w, x.z1.x, x.z1.y, x.z1.z, x.z1.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) zv[e] = __uint_as_float(zu[e]);
+            }
+          }
+          if (a.bn_mask == 3) {   // ReLU mask bits: this thread's 8 elements share one word
+            const uint32_t b8 = x.bits >> (off & 31);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) zv[e] = ((b8 >> e) & 1u) ? 1.f : 0.f;
+          } else if (a.bn_mask != 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) zv[e] = 0.f;
+          }
+          if (has_beta) {
+            const uint32_t cu[8] = {x.c0.x, x.c0.y, x.c0.z, x.c0.w, x.c1.x, x.c1.y, x.c1.z, x.c1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) old[e] = __uint_as_float(cu[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) old[e] = 0.f;
+          }
+          const int rr = rsub + j * RPP;
+          const float4 a0 = *reinterpret_cast<const float4*>(lds + rr * LDC + 8 * cg);
+          const float4 a1 = *reinterpret_cast<const float4*>(lds + rr * LDC + 8 * cg + 4);
+          const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float tv = fmaf(a.beta, old[e], av[e]);
+            const bool keep = zv[e] + fmaf(yv[e], bsc[e], bsh[e]) > 0.f;
+            tv = keep ? tv : 0.f;
+            v[e] = tv;
+            cs[e] += tv;
+            cq[e] = fmaf(tv, yv[e] - mu[e], cq[e]);
+          }
+          *reinterpret_cast<float4*>(a.C + off) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(a.C + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+        if (t + D < NR) issue(a, t + D, m0, n0, x);   // the slot's next row
+      }
+    }
+    // (3) column sums over the RPP row slots -> bn_part
+    __syncthreads();
+    float* red = lds;   // [RPP][BN][2]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rsub * BN + 8 * cg + e) * 2] = cs[e];
+      red[(rsub * BN + 8 * cg + e) * 2 + 1] = cq[e];
+    }
+    __syncthreads();
+    for (int c = etid; c < BN; c += NT) {
+      float t0 = 0.f, t1 = 0.f;
+      for (int q = 0; q < RPP; ++q) {
+        t0 += red[(q * BN + c) * 2];
+        t1 += red[(q * BN + c) * 2 + 1];
+      }
+      if (n0 + c < a.N) a.bn_part[(long)(m0 / BM) * a.part_ld + n0 + c] = make_float2(t0, t1);
+    }
+  }
+};
+
+// The same epilogue with one row's loads at a time (no lookahead): the 8/16-wave tiles, which run
+// at a 128-VGPR budget that LdsBnbwd's extra row set would spill.
 template <int BM, int BN, int WM, int WN, int TM, int TN>
 __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (&acc)[TM][TN],
                                                    float* lds, int lds_floats, int m0, int n0) {
@@ -462,6 +672,19 @@ void gemm16_kernel(const GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // the LDS-staged BN-backward epilogue (whole wave row-blocks of (BM / WM) padded rows must fit:
+  // all configs but 256x256, which the dgrad tile rules never pick): its first rows' global
+  // operands are loaded now and land under the main loop
+  constexpr bool LDSEPI = MODE == MODE_DGRAD && (BN + 4) * (BM / WM) * 4 <= SMEM;
+  // prefetching form (LdsBnbwd) on the 4-wave tiles; the 8/16-wave ones (128-VGPR budget) keep
+  // epilogue_lds_bnbwd
+  constexpr bool PRE = LDSEPI && NW < 8;
+  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM>;
+  typename Epi::In pf[PRE ? Epi::D : 1];
+  if constexpr (PRE) {
+    if (a.bn_part != nullptr) Epi::prefetch(a, m0, n0, pf);
+  }
+
   const int arow0 = wm * (BM / WM) + l31;
   const int brow0 = wn * (BN / WN) + l31;
   // the operand fragments of k-step s of LDS buffer buf
@@ -555,12 +778,13 @@ void gemm16_kernel(const GemmArgs a) {
   }
   __syncthreads();   // LDS reads done (no LDS-DMA in flight) before the epilogue reuses smem
 
-  // the LDS form stages whole wave row-blocks: (BM / WM) padded rows must fit (all configs but
-  // 256x256, which the dgrad tile rules never pick)
-  if constexpr (MODE == MODE_DGRAD && (BN + 4) * (BM / WM) * 4 <= SMEM) {
+  if constexpr (LDSEPI) {
     if (a.bn_part != nullptr) {   // (the only form that reads mask-3 bits: launch_gemm16_t)
-      epilogue_lds_bnbwd<BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), SMEM / 4,
-                                                  m0, n0);
+      if constexpr (PRE)
+        Epi::run(a, acc, reinterpret_cast<float*>(smem), m0, n0, pf);
+      else
+        epilogue_lds_bnbwd<BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), SMEM / 4,
+                                                    m0, n0);
       return;
     }
   }

@@ -6,8 +6,11 @@ opens each frame file with PIL and converts it to RGB; the DataLoader workers th
 (tmrnet_amd.augment, on the device).  Here:
 
 * decode stays on the host, with the reference's own loader (PIL; libjpeg-turbo for JPEG) -- this
-  image has no GPU JPEG decoder -- in a thread pool (PIL releases the GIL while decoding), straight
-  into a pinned uint8 batch;
+  image has no GPU JPEG decoder -- either in a thread pool straight into a pinned uint8 batch, or
+  (``DecodePool``) in worker processes that write a shared-memory batch registered as pinned host
+  memory: the thread pool stops scaling at ~2.1k frames/s of 854x480 JPEGs (the GIL-held parts of
+  ``convert`` / ``asarray``; ``profiles/r3/bench_r5a/decode.jsonl``), the reference's own answer
+  is DataLoader worker processes (:682-688);
 * the batch is copied to HBM and resized there by ``tmr_resize_u8`` (resize.hip), bit-exact to
   Pillow's ``Image.resize((250, 250), BILINEAR)``: the per-axis fixed-point tables are computed
   once per input size on the host (``tmr_resize_coeffs``, Pillow's double arithmetic) and kept
@@ -17,7 +20,9 @@ opens each frame file with PIL and converts it to RGB; the DataLoader workers th
 ``tmrnet_amd.augment.augment_clips`` / ``ops.crop_normalize``.
 """
 import ctypes
+import multiprocessing as mp
 from concurrent.futures import ThreadPoolExecutor
+from multiprocessing import shared_memory
 
 import numpy as np
 import torch
@@ -105,9 +110,142 @@ def decode_frames(paths, workers=8, out=None):
     return out
 
 
-def load_frames(paths, device="cuda", size=RESIZE, workers=8):
-    """Files -> decoded (host, PIL) -> HBM -> resized on the device: (F, 250, 250, 3) uint8."""
-    host = decode_frames(paths, workers=workers)
+# ------------------------------------------------------------------ worker-process decode
+_W_SHM = {}   # worker process: shared-memory segments attached by name
+
+
+def _w_decode(name, nbytes, shape, first, paths):
+    """Worker task: pil_loader(paths[i]) -> frame first + i of the (F, H, W, 3) batch in segment
+    `name`.  Returns the number of frames written; a size mismatch raises (as decode_frames)."""
+    shm = _W_SHM.get(name)
+    if shm is None:
+        for old in _W_SHM.values():   # the pool grew its segment: drop the old attachment
+            old.close()
+        _W_SHM.clear()
+        # (spawned workers share the parent's resource tracker: the attachment's registration is
+        # the parent's, which unregisters it when it unlinks the segment)
+        shm = _W_SHM[name] = shared_memory.SharedMemory(name=name)
+    arr = np.ndarray(shape, dtype=np.uint8, buffer=shm.buf[:nbytes])
+    for i, p in enumerate(paths):
+        a = np.asarray(pil_loader(p))
+        if a.shape != tuple(shape[1:]):
+            raise RuntimeError("decode_frames: %s is %s, expected %s" % (p, a.shape, tuple(shape[1:])))
+        arr[first + i] = a
+    return len(paths)
+
+
+class DecodeJob:
+    """A batch in flight in a DecodePool: ``result()`` -> (F, H, W, 3) uint8 host tensor viewing the
+    pool's shared-memory slot (valid until that slot is reused, ``slots`` submissions later)."""
+
+    def __init__(self, pool, slot, shape, asyncs):
+        self.pool, self.slot, self.shape, self._asyncs = pool, slot, shape, asyncs
+
+    def result(self):
+        n = sum(r.get() for r in self._asyncs)   # re-raises a worker's exception
+        assert n == self.shape[0] - 1
+        return self.pool._view(self.slot, self.shape)
+
+
+class DecodePool:
+    """pil_loader (:96-99) in `workers` processes (the reference's DataLoader workers, :682-688)
+    writing into `slots` shared-memory batches; with CUDA present each segment is registered as
+    pinned host memory (hipHostRegister), so ``load_frames`` copies it to HBM without staging.
+
+    ``submit(paths)`` returns at once (decode of batch i + 1 overlaps the train step on batch i);
+    ``decode(paths)`` = ``submit(paths).result()``.  Workers are started with the spawn method (the
+    parent may hold a GPU context; forking it is unsafe) and never touch the GPU."""
+
+    def __init__(self, workers=8, slots=2, chunk=8):
+        self.workers, self.slots, self.chunk = max(1, workers), max(1, slots), max(1, chunk)
+        self._pool = mp.get_context("spawn").Pool(self.workers)
+        self._seg = [None] * self.slots   # (SharedMemory, nbytes, tensor view or None)
+        self._next = 0
+
+    def _segment(self, slot, nbytes):
+        cur = self._seg[slot]
+        if cur is not None and cur[1] >= nbytes:
+            return cur[0]
+        if cur is not None:
+            self._release(slot)
+        shm = shared_memory.SharedMemory(create=True, size=nbytes)
+        if torch.cuda.is_available():
+            rc = torch.cuda.cudart().cudaHostRegister(_buf_addr(shm), nbytes, 0)
+            if int(rc) != 0:
+                shm.close()
+                shm.unlink()
+                raise RuntimeError("DecodePool: hipHostRegister of %d bytes failed (%s)" % (nbytes, rc))
+        self._seg[slot] = [shm, nbytes, torch.cuda.is_available()]
+        return shm
+
+    def _release(self, slot):
+        cur = self._seg[slot]
+        if cur is None:
+            return
+        shm, _, registered = cur
+        self._seg[slot] = None
+        if registered:
+            torch.cuda.cudart().cudaHostUnregister(_buf_addr(shm))
+        shm.unlink()
+        try:
+            shm.close()
+        except BufferError:   # a caller still holds a view of it: the mapping lives until then
+            pass
+
+    def _view(self, slot, shape):
+        shm = self._seg[slot][0]
+        n = int(np.prod(shape))
+        return torch.frombuffer(shm.buf, dtype=torch.uint8, count=n).view(*shape)
+
+    def submit(self, paths):
+        paths = list(paths)
+        if not paths:
+            raise RuntimeError("decode_frames: no paths")
+        first = np.asarray(pil_loader(paths[0]))
+        shape = (len(paths),) + first.shape
+        nbytes = int(np.prod(shape))
+        slot = self._next
+        self._next = (self._next + 1) % self.slots
+        shm = self._segment(slot, nbytes)
+        np.ndarray(shape, dtype=np.uint8, buffer=shm.buf[:nbytes])[0] = first
+        asyncs = [self._pool.apply_async(_w_decode, (shm.name, nbytes, shape, i,
+                                                     paths[i:i + self.chunk]))
+                  for i in range(1, len(paths), self.chunk)]
+        return DecodeJob(self, slot, shape, asyncs)
+
+    def decode(self, paths):
+        return self.submit(paths).result()
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.terminate()
+            self._pool.join()
+            self._pool = None
+        for s in range(self.slots):
+            self._release(s)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _buf_addr(shm):
+    """Host address of a SharedMemory segment's mapping."""
+    return ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+
+
+def load_frames(paths, device="cuda", size=RESIZE, workers=8, pool=None):
+    """Files -> decoded (host, PIL; threads, or the processes of `pool`, a DecodePool) -> HBM ->
+    resized on the device: (F, 250, 250, 3) uint8."""
+    host = pool.decode(paths) if pool is not None else decode_frames(paths, workers=workers)
     dev = host.to(device, non_blocking=True)
     if tuple(host.shape[1:3]) == tuple(size):
         return dev
