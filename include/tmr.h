@@ -78,6 +78,11 @@ typedef struct tmr_conv_desc {
 #define TMR_IO_Y_BF16 16   /* forward: y written as bf16 (RNE); the BatchNorm partials of
                               tmr_conv2d_fwd_bnstats describe the rounded values (no beta/bias) */
 #define TMR_IO_BN_BF16 32  /* tmr_conv2d_dgrad_bnbwd: the y / z of the fused BN backward are bf16 */
+#define TMR_IO_G16 128     /* tmr_conv2d_dgrad_bnbwd, bf16 math on the LDS-DMA engine: dx -- the
+                              ReLU-masked BN-output gradient g -- is written as bf16 (RNE) and the
+                              partials describe the rounded values; beta 0, c a multiple of 8
+                              (the non-residual units of the bf16 train step; tmr_bn_bwd_parts_g16
+                              reads it) */
 #define TMR_IO_WT_BF16 8   /* dgrad only: w is the transposed bf16 weight copy Wt[Cin][R][S][Cout]
                               (tmr_weight_oihw_to_crsk_x), read K-contiguous by the LDS-DMA engine */
 #define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the one io bit fp32 math takes): w is the
@@ -353,6 +358,12 @@ int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const float* s
                    const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta, int rows,
                    int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream);
 int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* parts, int nparts,
+                         const float* save_mean, const float* save_invstd, const float* gamma,
+                         void* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
+                         size_t ws_bytes, hipStream_t stream);
+/* tmr_bn_bwd_parts_a16 with g stored bf16 (written by a TMR_IO_G16 dgrad); c a multiple of 8,
+ * g / y / dy 16-B aligned.  Replaces the same BatchNorm2d backward as tmr_bn_bwd_parts. */
+int tmr_bn_bwd_parts_g16(const void* g, const void* y, const void* parts, int nparts,
                          const float* save_mean, const float* save_invstd, const float* gamma,
                          void* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
                          size_t ws_bytes, hipStream_t stream);

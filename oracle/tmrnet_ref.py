@@ -138,8 +138,13 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x
+        rg = getattr(self, "round_grad", False) and self.training   # emulate_bf16_convs(grads)
         out = self.relu(self.bn1(self.conv1(x)))
+        if rg:
+            out = _GradRoundFn.apply(out)
         out = self.relu(self.bn2(self.conv2(out)))
+        if rg:
+            out = _GradRoundFn.apply(out)
         out = self.bn3(self.conv3(out))
         if self.downsample is not None:
             identity = self.downsample(x)
@@ -312,6 +317,20 @@ class _RoundFn(torch.autograd.Function):
         return g
 
 
+class _GradRoundFn(torch.autograd.Function):
+    """Identity whose gradient is stored rounded to bf16 (RNE): the bf16 train step keeps the
+    BN-output gradient of the non-residual units (relu(bn1), relu(bn2) of a Bottleneck) as bf16
+    (tmrnet_amd/trunk.py G16, TMR_IO_G16)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return bf16_round(g)
+
+
 class _Bf16ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, padding, groups):
@@ -343,18 +362,23 @@ class Bf16Conv2d(nn.Conv2d):
         return y
 
 
-def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False):
+def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=None):
     """Switch every trunk Conv2d of `module` to bf16-operand math (class swap, so deepcopy
     and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay.
     activations=True: in train mode the conv outputs and the Bottleneck outputs are rounded to
     bf16 as well (the bf16-activation contract of the train step; ResNeSt-50 also stores the
-    split attention's relu(bn0) input and output and the avd pool output as bf16)."""
+    split attention's relu(bn0) input and output and the avd pool output as bf16).
+    grads (default: activations): the ResNet-50 Bottleneck's relu(bn1) / relu(bn2) gradients are
+    rounded to bf16 in the backward (trunk.G16: the fused dgrad stores them bf16)."""
+    grads = activations if grads is None else grads
     for name, m in module.named_modules():
         if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
             m.__class__ = Bf16Conv2d
             m.round_out = activations
         elif isinstance(m, (Bottleneck, BottleneckS, SplAtConv2d)):
             m.round_out = activations
+            if isinstance(m, Bottleneck):
+                m.round_grad = grads
     return module
 
 

@@ -182,8 +182,9 @@ def test_bf16_storage_bit_identical(dev, backbone, time_conv):
     B, T, L = 2, 5, 7
     frames, off, lt, labels = _inputs(B, T, L, seed=51)
     res = {}
-    saved = trunk.BF16_STORE, trunk.FULL16
+    saved = trunk.BF16_STORE, trunk.FULL16, trunk.G16
     trunk.FULL16 = False   # the all-bf16 LDS-DMA path: test_bf16_full16_step
+    trunk.G16 = False      # (bf16 gradients need that path: fp32 storage keeps fp32 gradients)
     try:
         for store in (True, False):
             trunk.BF16_STORE = store
@@ -208,7 +209,7 @@ def test_bf16_storage_bit_identical(dev, backbone, time_conv):
                 with torch.no_grad():
                     res["eval32"] = m(x4, lt.to(dev)).clone()
     finally:
-        trunk.BF16_STORE, trunk.FULL16 = saved
+        trunk.BF16_STORE, trunk.FULL16, trunk.G16 = saved
     assert torch.equal(res[True][0], res[False][0])
     for n in res[True][1]:
         assert torch.equal(res[True][1][n], res[False][1][n]), n
@@ -425,6 +426,50 @@ def test_gemm16_dgrad_fused_bn_backward(dev, case):
     assert torch.equal(dzf, dres_ref)
     assert rel_err(dyf, dy_ref) < 1e-5
     assert rel_err(dgf, dg_ref) < 1e-5 and rel_err(dbf, db_ref) < 1e-5
+
+
+@pytest.mark.parametrize("case", [
+    # n, h, w, cin(dx channels), cout(dy channels), r, stride, pad
+    (3, 14, 14, 64, 256, 1, 1, 0),     # conv3 dgrad -> bn2's gradient (256x64 tiles)
+    (2, 14, 14, 128, 128, 3, 2, 1),    # strided 3x3 conv2 dgrad -> bn1's gradient: parity classes
+    (2, 20, 20, 256, 128, 3, 1, 1),    # 128x128 tiles
+])
+def test_gemm16_dgrad_g16(dev, case):
+    """TMR_IO_G16: the fused BN-backward dgrad storing the masked gradient g as bf16 (the
+    non-residual units of the bf16 step) writes exactly the RNE rounding of the fp32 path's g; its
+    BN partials are those of the rounded values (vs float64 sums); and the BN-backward apply
+    reading bf16 g (tmr_bn_bwd_parts_g16) is bit-identical to the fp32-g apply on the same
+    values and partials."""
+    n, h, w, cin, cout, r, st, pad = case
+    g = torch.Generator().manual_seed(17)
+    ho = (h + 2 * pad - r) // st + 1
+    wo = (w + 2 * pad - r) // st + 1
+    dy = _r(torch.randn(n, ho, wo, cout, generator=g)).to(dev).to(torch.bfloat16)
+    wt = (torch.randn(cout, cin, r, r, generator=g) / np.sqrt(cout * r * r)).to(dev)
+    wct = ops.weight_to_crsk(wt)
+    y = torch.randn(n, h, w, cin, generator=g).to(dev).to(torch.bfloat16)
+    ye = y.float()
+    mean = ye.view(-1, cin).mean(0)
+    inv = 1.0 / (ye.view(-1, cin).var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = (torch.rand(cin, generator=g) + 0.5).to(dev)
+    scale = gamma * inv
+    shift = (torch.randn(cin, generator=g) * 0.1).to(dev) - mean * scale
+    kw = dict(scale=scale, shift=shift, math="bf16", wt=True)
+    d32, p32, n32 = ops.conv_dgrad_bnbwd(dy, wct, (h, w), st, pad, y, mean, 2, **kw)
+    d16, p16, n16 = ops.conv_dgrad_bnbwd(dy, wct, (h, w), st, pad, y, mean, 2, g16=True, **kw)
+    torch.cuda.synchronize()
+    assert d16.dtype == torch.bfloat16 and n16 == n32
+    assert torch.equal(d16, d32.to(torch.bfloat16))
+    gd = d16.double().view(-1, cin)
+    want = torch.stack([gd.sum(0), (gd * (ye.double().view(-1, cin) - mean.double())).sum(0)], -1)
+    got = p16[:n16].double().sum(0)
+    assert (got - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
+    a = ops.bn_bwd_parts(d16, y, p16, n16, mean, inv, gamma)
+    b = ops.bn_bwd_parts(d16.float(), y, p16, n16, mean, inv, gamma)
+    torch.cuda.synchronize()
+    assert a[0].dtype == torch.bfloat16
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
 
 
 def test_stem_nhwc8_bf16_input(dev):

@@ -179,15 +179,16 @@ __device__ __forceinline__ float ld1(const __bf16* p, long i) {
   return __uint_as_float((uint32_t)reinterpret_cast<const unsigned short*>(p)[i] << 16);
 }
 
-// TY: element type of y and the residual (bf16 under the bf16-activation contract)
+// TY: element type of y and the residual (bf16 under the bf16-activation contract).  Two elements
+// per thread and iteration, both loaded before either is used (as bn_bwd_apply).
 template <bool RES, bool RELU, typename TZ = float, bool DUAL = false, typename TY = float>
 __global__ __launch_bounds__(NT) void bn_apply_k(const TY* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift,
                                                  const TY* __restrict__ res, TZ* __restrict__ z,
                                                  long n4, int c4, __bf16* __restrict__ z16 = nullptr) {
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+  const long stride = (long)gridDim.x * NT;
+  auto apply = [&](long i, float4 v, const float4 r) {
     const int cc = chan_of(i, c4) * 4;
-    float4 v = ld4(y, i);
     const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
     const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
     v.x = fmaf(v.x, sc.x, sf.x);
@@ -195,7 +196,6 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const TY* __restrict__ y, const
     v.z = fmaf(v.z, sc.z, sf.z);
     v.w = fmaf(v.w, sc.w, sf.w);
     if (RES) {
-      const float4 r = ld4(res, i);
       v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
     if (RELU) {
@@ -203,6 +203,19 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const TY* __restrict__ y, const
     }
     st4(z, i, v);
     if (DUAL) st4(z16, i, v);
+  };
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n4;
+    const float4 v0 = ld4(y, i);
+    const float4 r0 = RES ? ld4(res, i) : v0;
+    float4 v1 = v0, r1 = r0;
+    if (hj) {
+      v1 = ld4(y, j);
+      if (RES) r1 = ld4(res, j);
+    }
+    apply(i, v0, r0);
+    if (hj) apply(j, v1, r1);
   }
 }
 
@@ -217,10 +230,9 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, cons
                                                   const float* __restrict__ rshift,
                                                   TZ* __restrict__ z, long n4, int c4,
                                                   __bf16* __restrict__ z16) {
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+  const long stride = (long)gridDim.x * NT;
+  auto apply = [&](long i, float4 v, const float4 r) {
     const int cc = chan_of(i, c4) * 4;
-    float4 v = ld4(y, i);
-    const float4 r = ld4(yr, i);
     const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
     const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
     const float4 rs = *reinterpret_cast<const float4*>(rscale + cc);
@@ -234,6 +246,18 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, cons
     }
     st4(z, i, v);
     if (DUAL) st4(z16, i, v);
+  };
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n4;
+    const float4 v0 = ld4(y, i), r0 = ld4(yr, i);
+    float4 v1 = v0, r1 = r0;
+    if (hj) {
+      v1 = ld4(y, j);
+      r1 = ld4(yr, j);
+    }
+    apply(i, v0, r0);
+    if (hj) apply(j, v1, r1);
   }
 }
 
@@ -400,6 +424,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_final(const double* __restrict__ pa
   }
 }
 
+// Two elements per thread and iteration (i and i + the grid's stride), both elements' loads issued
+// before either is consumed: one element at a time kept 32 B in flight per thread and ran at
+// 5.2 TB/s (`profiles/r3/rocprof_r4g/`, the fp32 step's largest non-conv kernel).
 template <int MASK, bool DRES, typename TD = float, typename TY = float>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz, const TY* __restrict__ y,
                                                    const TY* __restrict__ z,
@@ -408,11 +435,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
                                                    const float* __restrict__ coef, TD* __restrict__ dy,
                                                    float* __restrict__ dres, long n4, int c4) {
   const int c = c4 * 4;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+  const long stride = (long)gridDim.x * NT;
+  auto apply = [&](long i, float4 g, const float4 v, const float4 zv) {
     const int cc = chan_of(i, c4) * 4;
-    float4 g = reinterpret_cast<const float4*>(dz)[i];
-    const float4 v = ld4(y, i);
-    if (MASK == 1) g = relu_mask4(g, ld4(z, i));
+    if (MASK == 1) g = relu_mask4(g, zv);
     if (MASK == 2)
       g = relu_mask4(g, affine4(v, *reinterpret_cast<const float4*>(scale + cc),
                                 *reinterpret_cast<const float4*>(shift + cc)));
@@ -426,22 +452,48 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const float* __restrict__ dz,
     o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
     o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
     st4(dy, i, o);
+  };
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n4;
+    const float4 g0 = reinterpret_cast<const float4*>(dz)[i];
+    const float4 v0 = ld4(y, i);
+    const float4 z0 = MASK == 1 ? ld4(z, i) : g0;
+    float4 g1 = g0, v1 = v0, z1 = z0;
+    if (hj) {
+      g1 = reinterpret_cast<const float4*>(dz)[j];
+      v1 = ld4(y, j);
+      if (MASK == 1) z1 = ld4(z, j);
+    }
+    apply(i, g0, v0, z0);
+    if (hj) apply(j, g1, v1, z1);
   }
 }
 
 // The BatchNorm-backward apply of the bf16-activation step, 8 elements per thread: g (fp32, already
 // ReLU-masked by the fused dgrad epilogue) 32 B, y (bf16) 16 B, dy (bf16) 16 B -- every access a
 // 16-B lane piece (the 4-wide form moved bf16 in 8-B pieces).  Same fmaf sequence as bn_bwd_apply.
-__global__ __launch_bounds__(NT) void bn_bwd_apply8_a16(const float* __restrict__ g,
+// TG: float, or __bf16 when g was stored bf16 by a TMR_IO_G16 dgrad (16 B of g per thread)
+__device__ __forceinline__ void ld_g8(const float* g, long i, float4& a, float4& b) {
+  a = reinterpret_cast<const float4*>(g)[2 * i];
+  b = reinterpret_cast<const float4*>(g)[2 * i + 1];
+}
+__device__ __forceinline__ void ld_g8(const __bf16* g, long i, float4& a, float4& b) {
+  const uint4 w = reinterpret_cast<const uint4*>(g)[i];
+  a = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                  __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+  b = make_float4(__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                  __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u));
+}
+template <typename TG = float>
+__global__ __launch_bounds__(NT) void bn_bwd_apply8_a16(const TG* __restrict__ g,
                                                         const __bf16* __restrict__ y,
                                                         const float* __restrict__ coef,
                                                         __bf16* __restrict__ dy, long n8, int c8) {
   const int c = c8 * 8;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+  const long stride = (long)gridDim.x * NT;
+  auto apply = [&](long i, const float4 g0, const float4 g1, const uint4 yw) {
     const int cc = chan_of(i, c8) * 8;
-    const float4 g0 = reinterpret_cast<const float4*>(g)[2 * i];
-    const float4 g1 = reinterpret_cast<const float4*>(g)[2 * i + 1];
-    const uint4 yw = reinterpret_cast<const uint4*>(y)[i];
     const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
     float yv[8];
@@ -466,6 +518,22 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply8_a16(const float* __restrict_
       ow[2 * h + 1] = __builtin_bit_cast(uint32_t, q);
     }
     reinterpret_cast<uint4*>(dy)[i] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  };
+  // two elements in flight per thread (bn_bwd_apply)
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n8;
+    float4 a0, a1;
+    ld_g8(g, i, a0, a1);
+    const uint4 ya = reinterpret_cast<const uint4*>(y)[i];
+    float4 b0 = a0, b1 = a1;
+    uint4 yb = ya;
+    if (hj) {
+      ld_g8(g, j, b0, b1);
+      yb = reinterpret_cast<const uint4*>(y)[j];
+    }
+    apply(i, a0, a1, ya);
+    if (hj) apply(j, b0, b1, yb);
   }
 }
 
@@ -710,10 +778,12 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const TY*
                                                      TD* __restrict__ dy, long n4, int c4) {
   const int c = c4 * 4;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    const int cq = (int)(i % c4);
+    const int cq = chan_of(i, c4);
     const int cc = cq * 4;
     const float4 v = ld4(y, i);
-    const float4 g = relu_mask4(stem_dz(pg, (uint32_t)(i / c4), cq, c4),
+    // (c4 a power of two -- the stem's 64 channels -- divides by a shift, not a 64-bit division)
+    const uint32_t row = (c4 & (c4 - 1)) == 0 ? (uint32_t)(i >> __builtin_ctz(c4)) : (uint32_t)(i / c4);
+    const float4 g = relu_mask4(stem_dz(pg, row, cq, c4),
                                 affine4(v, *reinterpret_cast<const float4*>(scale + cc),
                                         *reinterpret_cast<const float4*>(shift + cc)));
     const float4 A = *reinterpret_cast<const float4*>(coef + cc);
@@ -1279,7 +1349,7 @@ TMR_API int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* part
   const char* w8 = getenv("TMR_BN8");   // A/B switch (0: the 4-wide form)
   if (!(w8 && w8[0] == '0') && c % 8 == 0 && (((uintptr_t)g | (uintptr_t)y | (uintptr_t)dy) & 15) == 0) {
     const long n8 = n4 / 2;
-    hipLaunchKernelGGL(bn_bwd_apply8_a16, dim3(ew_blocks(n8)), dim3(NT), 0, stream, g,
+    hipLaunchKernelGGL(bn_bwd_apply8_a16<float>, dim3(ew_blocks(n8)), dim3(NT), 0, stream, g,
                        (const __bf16*)y, coef, (__bf16*)dy, n8, c / 8);
   } else {
     hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
@@ -1287,6 +1357,33 @@ TMR_API int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* part
                        nullptr, n4, c / 4);
   }
   TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+TMR_API int tmr_bn_bwd_parts_g16(const void* g, const void* y, const void* parts, int nparts,
+                                 const float* save_mean, const float* save_invstd,
+                                 const float* gamma, void* dy, float* dgamma, float* dbeta,
+                                 int rows, int c, void* ws, size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 8 == 0 && c >= 8 && rows > 0 && nparts > 0,
+                "tmr_bn_bwd_parts_g16: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
+  TMR_CHECK_ARG((((uintptr_t)g | (uintptr_t)y | (uintptr_t)dy) & 15) == 0,
+                "tmr_bn_bwd_parts_g16: g / y / dy must be 16-B aligned");
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_bn_parts_ws_bytes(nparts, c),
+                "tmr_bn_bwd_parts_g16: workspace too small (need tmr_bn_parts_ws_bytes)");
+  const SlabPlan sp = slab_plan(nparts, c);
+  double* slabs = (double*)ws;
+  float* coef = (float*)((char*)ws + slab_ws_bytes(nparts, c));
+  hipLaunchKernelGGL(parts_slab_k<1>, dim3(sp.groups, sp.nslabs), dim3(256), 0, stream, parts,
+                     nparts, c, sp.rows, slabs);
+  TMR_CHECK_LAUNCH("bn_parts_slab");
+  hipLaunchKernelGGL(bwd_final_slabs_k, dim3(sp.groups), dim3(SLAB_CH * SLAB_PH), 0, stream,
+                     (const double*)slabs, sp.nslabs, rows, c, save_mean, save_invstd, gamma,
+                     dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
+  const long n8 = (long)rows * c / 8;
+  hipLaunchKernelGGL(bn_bwd_apply8_a16<__bf16>, dim3(ew_blocks(n8)), dim3(NT), 0, stream,
+                     (const __bf16*)g, (const __bf16*)y, coef, (__bf16*)dy, n8, c / 8);
+  TMR_CHECK_LAUNCH("bn_bwd_apply_g16");
   return 0;
 }
 

@@ -57,6 +57,21 @@ __device__ __forceinline__ int mn_swz(int k) {
 // Every (row, 8-column group) belongs to one thread, so reading the old dx of a later row before
 // this row's store cannot alias.  With loads issued one row at a time a thread keeps ~64 B in
 // flight and the launch is latency-bound (3.6 TB/s on the 56x56 residual dgrads).
+// 8 consecutive elements of the fused BN-backward dgrad's output at element offset `off`: fp32, or
+// bf16 (already rounded values, GemmArgs::g16) as one 16-B store
+__device__ __forceinline__ void store_g8(const GemmArgs& a, long off, const float (&v)[8]) {
+  if (a.g16) {
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] = (__float_as_uint(v[2 * e]) >> 16) | (__float_as_uint(v[2 * e + 1]) & 0xffff0000u);
+    *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.C) + off) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    *reinterpret_cast<float4*>(a.C + off) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(a.C + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 #ifndef TMR_EPI_DEPTH
 #define TMR_EPI_DEPTH 3
 #endif
@@ -228,12 +243,12 @@ struct LdsBnbwd {
             float tv = fmaf(a.beta, old[e], av[e]);
             const bool keep = zv[e] + fmaf(yv[e], bsc[e], bsh[e]) > 0.f;
             tv = keep ? tv : 0.f;
+            if (a.g16) tv = bf16_rne(tv);   // stored bf16: the partials describe the stored g
             v[e] = tv;
             cs[e] += tv;
             cq[e] = fmaf(tv, yv[e] - mu[e], cq[e]);
           }
-          *reinterpret_cast<float4*>(a.C + off) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(a.C + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+          store_g8(a, off, v);
         }
         if (t + D < NR) issue(a, t + D, m0, n0, x);   // the slot's next row
       }
@@ -377,12 +392,12 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
           float t = fmaf(a.beta, old[e], av[e]);
           const bool keep = zv[e] + fmaf(yv[e], bsc[e], bsh[e]) > 0.f;
           t = keep ? t : 0.f;
+          if (a.g16) t = bf16_rne(t);
           v[e] = t;
           cs[e] += t;
           cq[e] = fmaf(t, yv[e] - mu[e], cq[e]);
         }
-        *reinterpret_cast<float4*>(a.C + off) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(a.C + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        store_g8(a, off, v);
       }
     }
   }
@@ -822,6 +837,11 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                     (MODE == MODE_DGRAD && !(c.bm == 256 && c.bn == 256)),
                 "gemm: ReLU-mask bits (mask 3) need the LDS-DMA dgrad's LDS-staged epilogue (tile %dx%d)",
                 c.bm, c.bn);
+  TMR_CHECK_ARG(!a.g16 || (MODE == MODE_DGRAD && a.bn_part != nullptr && a.beta == 0.f &&
+                           !(c.bm == 256 && c.bn == 256) && ((uintptr_t)a.C & 15) == 0 &&
+                           a.ldc % 8 == 0),
+                "gemm: a bf16 BN-backward gradient (TMR_IO_G16) needs the fused LDS-staged dgrad "
+                "epilogue, beta 0, 16-B aligned rows (tile %dx%d)", c.bm, c.bn);
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   // a k-tile (64 bf16 / 32 fp32) spans several taps when the channels per tap are fewer (or not

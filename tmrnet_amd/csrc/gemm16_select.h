@@ -66,7 +66,11 @@ inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false) {
     if (M >= 256 && N >= 256 && 2.0 * M * N * K >= 100e9) return 6;
     return 7;
   }
-  if (f32 && M >= 256 && ((mode == MODE_FWD && N == 128) || (mode == MODE_DGRAD && N >= 512)))
+  if (f32 && M >= 256 && mode == MODE_DGRAD && N >= 512) {
+    static const int wide = env_int("TMR_DGRAD32_WIDE_CFG", 7);   // A/B of this rule
+    return cfg16_tiles(M, N, wide) >= 256 ? wide : 2;
+  }
+  if (f32 && M >= 256 && mode == MODE_FWD && N == 128)
     return cfg16_tiles(M, N, 7) >= 256 ? 7 : 2;
   if (mode == MODE_WGRAD) {
     if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);

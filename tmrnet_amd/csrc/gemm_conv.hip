@@ -86,6 +86,7 @@ static inline int esz_w(const tmr_conv_desc* d) { return (d->io & (TMR_IO_W_BF16
 static inline int esz_dy(const tmr_conv_desc* d) { return (d->io & TMR_IO_DY_BF16) ? 2 : 4; }
 static inline int esz_y(const tmr_conv_desc* d) { return (d->io & TMR_IO_Y_BF16) ? 2 : 4; }
 static inline int esz_bn(const tmr_conv_desc* d) { return (d->io & TMR_IO_BN_BF16) ? 2 : 4; }
+static inline int esz_dx(const tmr_conv_desc* d) { return (d->io & TMR_IO_G16) ? 2 : 4; }
 template <typename T>
 static inline T* adv(T* p, long elems, int esz) {   // p + elems elements of esz bytes
   return p ? (T*)((typename std::conditional<std::is_const<T>::value, const char*, char*>::type)p +
@@ -432,6 +433,10 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
         a.bn_y = fz->y; a.bn_z = fz->z; a.bn_sc = fz->sc; a.bn_sh = fz->sh; a.bn_mean = fz->mean;
         a.bn_mask = fz->mask;
         a.bn16 = (d->io & TMR_IO_BN_BF16) ? 1 : 0;
+        if (d->io & TMR_IO_G16) {   // dx (g) stored bf16: C's extent in bytes of bf16
+          a.g16 = 1;
+          a.Cbytes = clamp_bytes_e(span((long)d->n * d->h * d->w, a.ldc, d->c), 2);
+        }
         a.bn_part = fz->part;
         a.part_ld = fz->part_ld;
         fz->part += nmt * fz->part_ld;
@@ -470,7 +475,7 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);
     int rc = conv_dgrad_impl(&c, adv(dy, f0 * y_frame(d), esz_dy(d)), w_krsc,
-                             dx ? dx + f0 * x_frame(d) : nullptr, beta, stream, &fc_,
+                             dx ? adv(dx, f0 * x_frame(d), esz_dx(d)) : nullptr, beta, stream, &fc_,
                              pro ? &pc : nullptr);
     if (rc) return rc;
     fz->part = fc_.part;
@@ -513,6 +518,11 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
   TMR_CHECK_ARG(ngroups(d) == 1 || (mask != 3 && !pro),
                 "tmr_conv2d_dgrad_bnbwd: a grouped dgrad takes no ReLU-mask bits / prologue");
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
+  TMR_CHECK_ARG(!(d->io & TMR_IO_G16) ||
+                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) && beta == 0.f &&
+                     ngroups(d) == 1 && !pro && d->c % 8 == 0),
+                "tmr_conv2d_dgrad_bnbwd: a bf16 gradient (TMR_IO_G16) needs bf16 math on the LDS-DMA "
+                "engine (TMR_IO_WT_BF16), beta 0, no groups / prologue, c a multiple of 8");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
                 "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
   TMR_CHECK_ARG(mask != 3 || ((d->io & (TMR_IO_WT_F32 | TMR_IO_WT_BF16)) &&

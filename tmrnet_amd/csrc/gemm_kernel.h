@@ -119,6 +119,10 @@ struct GemmArgs {
   // fp32 conv views eligible for the LDS-DMA engine (gemm16_kernel.h use32; set by the conv
   // entry points, never by the plain GEMMs)
   int dma32;
+  // DGRAD with the fused BN backward (LDS-DMA engine, LDS-staged epilogue): C -- the masked
+  // gradient g -- is stored as bf16 (RNE) and the partials describe the rounded values; no beta
+  // (TMR_IO_G16)
+  int g16;
 };
 
 __device__ __forceinline__ float bf16_rne(float v) { return (float)(__bf16)v; }

@@ -153,17 +153,20 @@ __global__ __launch_bounds__(NT) void splat_bwd_apply_k(const float* __restrict_
 }
 
 // general AvgPool2d on NHWC: divisor = k*k (count_include_pad) or #valid input cells
+// IT: index type (uint32_t when the element groups fit 31 bits: 64-bit divisions cost
+// ~100 instructions per element; tmr_avgpool2d_* pick it)
+template <typename IT>
 __global__ __launch_bounds__(NT) void avgpool2d_fwd_k(const float* __restrict__ x, float* __restrict__ y,
                                                       int n, int h, int w, int c4, int ho, int wo,
                                                       int k, int s, int p, int incl) {
-  const long total = (long)n * ho * wo * c4;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int cq = (int)(i % c4);
-    long t = i / c4;
-    const int ox = (int)(t % wo);
-    t /= wo;
-    const int oy = (int)(t % ho);
-    const int nn = (int)(t / ho);
+  const IT total = (IT) (long)n * ho * wo * c4;
+  for (IT i = (IT)blockIdx.x * NT + threadIdx.x; i < total; i += (IT)gridDim.x * NT) {
+    const int cq = (int)(i % (IT)c4);
+    IT t = i / (IT)c4;
+    const int ox = (int)(t % (IT)wo);
+    t /= (IT)wo;
+    const int oy = (int)(t % (IT)ho);
+    const int nn = (int)(t / (IT)ho);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int cnt = 0;
     for (int dy = 0; dy < k; ++dy) {
@@ -183,17 +186,20 @@ __global__ __launch_bounds__(NT) void avgpool2d_fwd_k(const float* __restrict__ 
   }
 }
 
+// IT: index type (uint32_t when the element groups fit 31 bits: 64-bit divisions cost
+// ~100 instructions per element; tmr_avgpool2d_* pick it)
+template <typename IT>
 __global__ __launch_bounds__(NT) void avgpool2d_bwd_k(const float* __restrict__ dy, float* __restrict__ dx,
                                                       int n, int h, int w, int c4, int ho, int wo,
                                                       int k, int s, int p, int incl) {
-  const long total = (long)n * h * w * c4;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int cq = (int)(i % c4);
-    long t = i / c4;
-    const int ix = (int)(t % w);
-    t /= w;
-    const int iy = (int)(t % h);
-    const int nn = (int)(t / h);
+  const IT total = (IT) (long)n * h * w * c4;
+  for (IT i = (IT)blockIdx.x * NT + threadIdx.x; i < total; i += (IT)gridDim.x * NT) {
+    const int cq = (int)(i % (IT)c4);
+    IT t = i / (IT)c4;
+    const int ix = (int)(t % (IT)w);
+    t /= (IT)w;
+    const int iy = (int)(t % (IT)h);
+    const int nn = (int)(t / (IT)h);
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
     // outputs oy with oy*s - p <= iy <= oy*s - p + k - 1
     const int oy0 = max(0, (iy + p - k + s) / s), oy1 = min(ho - 1, (iy + p) / s);
@@ -300,19 +306,21 @@ __global__ __launch_bounds__(NT) void splat_att_k(const float* __restrict__ zl, 
   }
 }
 
-// out[n,hw,c] = rnd(att0 * x0 + att1 * x1)
+// out[n,hw,c] = rnd(att0 * x0 + att1 * x1).  32-bit index math with magic-number division (the
+// host checks the element count; 64-bit divisions cost ~100 instructions per element)
 template <typename T>
 __global__ __launch_bounds__(NT) void splat_combine_bn_k(const T* __restrict__ y, const float* __restrict__ sc,
                                                          const float* __restrict__ sh, const float* __restrict__ att,
-                                                         T* __restrict__ out, int n, int hw, int c4) {
-  const long total = (long)n * hw * c4;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const long p = i / c4;
-    const int cq = (int)(i - p * c4);
-    const long nn = p / hw;
-    const float4 x0 = bnrelu4<T>(Act<T>::ld(y, p * 2 * c4 + cq), ld4f(sc, cq), ld4f(sh, cq));
-    const float4 x1 = bnrelu4<T>(Act<T>::ld(y, p * 2 * c4 + c4 + cq), ld4f(sc, c4 + cq), ld4f(sh, c4 + cq));
-    const float4 a0 = ld4f(att, nn * 2 * c4 + cq), a1 = ld4f(att, nn * 2 * c4 + c4 + cq);
+                                                         T* __restrict__ out, uint32_t total, FastDiv dc4,
+                                                         FastDiv dhw) {
+  const uint32_t c4 = dc4.d;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const uint32_t p = fdiv(i, dc4);
+    const uint32_t cq = i - p * c4;
+    const uint32_t nn = fdiv(p, dhw);
+    const float4 x0 = bnrelu4<T>(Act<T>::ld(y, (long)p * 2 * c4 + cq), ld4f(sc, cq), ld4f(sh, cq));
+    const float4 x1 = bnrelu4<T>(Act<T>::ld(y, (long)p * 2 * c4 + c4 + cq), ld4f(sc, c4 + cq), ld4f(sh, c4 + cq));
+    const float4 a0 = ld4f(att, (long)nn * 2 * c4 + cq), a1 = ld4f(att, (long)nn * 2 * c4 + c4 + cq);
     Act<T>::st(out, i, make_float4(fmaf(a1.x, x1.x, a0.x * x0.x), fmaf(a1.y, x1.y, a0.y * x0.y),
                                    fmaf(a1.z, x1.z, a0.z * x0.z), fmaf(a1.w, x1.w, a0.w * x0.w)));
   }
@@ -444,20 +452,19 @@ template <typename T>
 __global__ __launch_bounds__(NT) void splat_bwd_apply_bn_k(
     const float* __restrict__ dout, const T* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ mean, const float* __restrict__ att,
-    const float* __restrict__ dgap, const float* __restrict__ coef, T* __restrict__ dy, int n,
-    int hw, int c4) {
-  const long total = (long)n * hw * 2 * c4;
-  const float ihw = 1.0f / (float)hw;
-  const int j4 = 2 * c4;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const long p = i / j4;
-    const int jq = (int)(i - p * j4);
-    const int cq = jq < c4 ? jq : jq - c4;
-    const long nn = p / hw;
+    const float* __restrict__ dgap, const float* __restrict__ coef, T* __restrict__ dy,
+    uint32_t total, FastDiv dj4, FastDiv dhw) {
+  const uint32_t j4 = dj4.d, c4 = j4 / 2;
+  const float ihw = 1.0f / (float)dhw.d;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const uint32_t p = fdiv(i, dj4);
+    const uint32_t jq = i - p * j4;
+    const uint32_t cq = jq < c4 ? jq : jq - c4;
+    const uint32_t nn = fdiv(p, dhw);
     const float4 yv = Act<T>::ld(y, i);
-    const float4 g0 = ld4f(dout, p * c4 + cq);
-    const float4 a = ld4f(att, nn * j4 + jq);
-    const float4 dg = ld4f(dgap, nn * c4 + cq);
+    const float4 g0 = ld4f(dout, (long)p * c4 + cq);
+    const float4 a = ld4f(att, (long)nn * j4 + jq);
+    const float4 dg = ld4f(dgap, (long)nn * c4 + cq);
     const float4 s = ld4f(sc, jq), h = ld4f(sh, jq), mu = ld4f(mean, jq);
     const float4 k0 = ld4f(coef, jq), k1 = ld4f(coef, j4 + jq), k2 = ld4f(coef, 2 * j4 + jq);
     auto one = [&](float yv_, float s_, float h_, float mu_, float g_, float a_, float dg_, float k0_,
@@ -473,17 +480,20 @@ __global__ __launch_bounds__(NT) void splat_bwd_apply_bn_k(
 }
 
 // AvgPool2d of bf16 activations (avd layer, avg_down): fp32 sums of the bf16 inputs, output rounded
+// IT: index type (uint32_t when the element groups fit 31 bits: 64-bit divisions cost
+// ~100 instructions per element; tmr_avgpool2d_* pick it)
+template <typename IT>
 __global__ __launch_bounds__(NT) void avgpool2d_fwd_a16_k(const __bf16* __restrict__ x, __bf16* __restrict__ y,
                                                           int n, int h, int w, int c4, int ho, int wo,
                                                           int k, int s, int p, int incl) {
-  const long total = (long)n * ho * wo * c4;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int cq = (int)(i % c4);
-    long t = i / c4;
-    const int ox = (int)(t % wo);
-    t /= wo;
-    const int oy = (int)(t % ho);
-    const int nn = (int)(t / ho);
+  const IT total = (IT) (long)n * ho * wo * c4;
+  for (IT i = (IT)blockIdx.x * NT + threadIdx.x; i < total; i += (IT)gridDim.x * NT) {
+    const int cq = (int)(i % (IT)c4);
+    IT t = i / (IT)c4;
+    const int ox = (int)(t % (IT)wo);
+    t /= (IT)wo;
+    const int oy = (int)(t % (IT)ho);
+    const int nn = (int)(t / (IT)ho);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int cnt = 0;
     for (int dy = 0; dy < k; ++dy) {
@@ -593,7 +603,11 @@ TMR_API int tmr_splat_bwd_apply(const float* dout, const float* att, const float
 TMR_API int tmr_avgpool2d_fwd(const float* x, float* y, int n, int h, int w, int c, int ho, int wo,
                               int k, int s, int p, int count_include_pad, hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_fwd: channels %d must be a multiple of 4", c);
-  hipLaunchKernelGGL(avgpool2d_fwd_k, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
+  if ((long)n * ho * wo * c / 4 < (1L << 31))
+    hipLaunchKernelGGL(avgpool2d_fwd_k<uint32_t>, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
+                     stream, x, y, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
+  else
+    hipLaunchKernelGGL(avgpool2d_fwd_k<long>, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
                      stream, x, y, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
   TMR_CHECK_LAUNCH("avgpool2d_fwd");
   return 0;
@@ -603,7 +617,11 @@ TMR_API int tmr_avgpool2d_bwd(const float* dy, float* dx, int n, int h, int w, i
                               int wo, int k, int s, int p, int count_include_pad,
                               hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_bwd: channels %d must be a multiple of 4", c);
-  hipLaunchKernelGGL(avgpool2d_bwd_k, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
+  if ((long)n * h * w * c / 4 < (1L << 31))
+    hipLaunchKernelGGL(avgpool2d_bwd_k<uint32_t>, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
+                     dy, dx, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
+  else
+    hipLaunchKernelGGL(avgpool2d_bwd_k<long>, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
                      dy, dx, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
   TMR_CHECK_LAUNCH("avgpool2d_bwd");
   return 0;
@@ -634,14 +652,18 @@ TMR_API int tmr_splat_att(const float* zl, float* att, int n, int c, hipStream_t
 TMR_API int tmr_splat_combine_bn(const void* y, const float* scale, const float* shift,
                                  const float* att, void* out, int n, int hw, int c, int act16,
                                  hipStream_t stream) {
-  TMR_CHECK_ARG(c % 4 == 0, "tmr_splat_combine_bn: channels %d must be a multiple of 4", c);
-  const int nb = blocks_for((long)n * hw * c / 4);
+  TMR_CHECK_ARG(c % 4 == 0 && n > 0 && hw > 0, "tmr_splat_combine_bn: bad shape n %d hw %d c %d "
+                "(channels a multiple of 4)", n, hw, c);
+  const long total = (long)n * hw * c / 4;
+  TMR_CHECK_ARG(total < (1L << 31), "tmr_splat_combine_bn: %ld element groups exceed 2^31", total);
+  const int nb = blocks_for(total);
+  const FastDiv dc4 = make_fastdiv((uint32_t)(c / 4)), dhw = make_fastdiv((uint32_t)hw);
   if (act16)
     hipLaunchKernelGGL(splat_combine_bn_k<__bf16>, dim3(nb), dim3(NT), 0, stream, (const __bf16*)y,
-                       scale, shift, att, (__bf16*)out, n, hw, c / 4);
+                       scale, shift, att, (__bf16*)out, (uint32_t)total, dc4, dhw);
   else
     hipLaunchKernelGGL(splat_combine_bn_k<float>, dim3(nb), dim3(NT), 0, stream, (const float*)y,
-                       scale, shift, att, (float*)out, n, hw, c / 4);
+                       scale, shift, att, (float*)out, (uint32_t)total, dc4, dhw);
   TMR_CHECK_LAUNCH("splat_combine_bn");
   return 0;
 }
@@ -678,14 +700,20 @@ TMR_API int tmr_splat_bwd_apply_bn(const float* dout, const void* y, const float
                                    const float* shift, const float* mean, const float* att,
                                    const float* dgap, const float* coef, void* dy, int n, int hw,
                                    int c, int act16, hipStream_t stream) {
-  TMR_CHECK_ARG(c % 4 == 0, "tmr_splat_bwd_apply_bn: channels %d must be a multiple of 4", c);
-  const int nb = blocks_for((long)n * hw * 2 * c / 4);
+  TMR_CHECK_ARG(c % 4 == 0 && n > 0 && hw > 0, "tmr_splat_bwd_apply_bn: bad shape n %d hw %d c %d "
+                "(channels a multiple of 4)", n, hw, c);
+  const long total = (long)n * hw * 2 * c / 4;
+  TMR_CHECK_ARG(total < (1L << 31), "tmr_splat_bwd_apply_bn: %ld element groups exceed 2^31", total);
+  const int nb = blocks_for(total);
+  const FastDiv dj4 = make_fastdiv((uint32_t)(2 * c / 4)), dhw = make_fastdiv((uint32_t)hw);
   if (act16)
     hipLaunchKernelGGL(splat_bwd_apply_bn_k<__bf16>, dim3(nb), dim3(NT), 0, stream, dout,
-                       (const __bf16*)y, scale, shift, mean, att, dgap, coef, (__bf16*)dy, n, hw, c / 4);
+                       (const __bf16*)y, scale, shift, mean, att, dgap, coef, (__bf16*)dy,
+                       (uint32_t)total, dj4, dhw);
   else
     hipLaunchKernelGGL(splat_bwd_apply_bn_k<float>, dim3(nb), dim3(NT), 0, stream, dout,
-                       (const float*)y, scale, shift, mean, att, dgap, coef, (float*)dy, n, hw, c / 4);
+                       (const float*)y, scale, shift, mean, att, dgap, coef, (float*)dy,
+                       (uint32_t)total, dj4, dhw);
   TMR_CHECK_LAUNCH("splat_bwd_apply_bn");
   return 0;
 }
@@ -694,7 +722,12 @@ TMR_API int tmr_avgpool2d_fwd_a16(const void* x, void* y, int n, int h, int w, i
                                   int wo, int k, int s, int p, int count_include_pad,
                                   hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_fwd_a16: channels %d must be a multiple of 4", c);
-  hipLaunchKernelGGL(avgpool2d_fwd_a16_k, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
+  if ((long)n * ho * wo * c / 4 < (1L << 31))
+    hipLaunchKernelGGL(avgpool2d_fwd_a16_k<uint32_t>, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
+                     stream, (const __bf16*)x, (__bf16*)y, n, h, w, c / 4, ho, wo, k, s, p,
+                     count_include_pad);
+  else
+    hipLaunchKernelGGL(avgpool2d_fwd_a16_k<long>, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
                      stream, (const __bf16*)x, (__bf16*)y, n, h, w, c / 4, ho, wo, k, s, p,
                      count_include_pad);
   TMR_CHECK_LAUNCH("avgpool2d_fwd_a16");

@@ -74,6 +74,7 @@ MAX_FRAMES = 0
 IO_X, IO_W, IO_DY, IO_WT = 1, 2, 4, 8   # tmr_conv_desc.io: bf16-stored x / KRSC w / dy / CRSK w
 IO_Y, IO_BN = 16, 32    # bf16 conv output y (forward) / bf16 y, z of the fused BN backward (dgrad)
 IO_WT32 = 64            # dgrad, fp32 math: w is the transposed fp32 copy (fp32 LDS-DMA engine)
+IO_G16 = 128            # fused BN-backward dgrad: g (dx) written bf16 (non-residual bf16 units)
 BF16 = torch.bfloat16
 
 
@@ -261,10 +262,12 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
 
 
 def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scale=None,
-                     shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False, groups=1):
+                     shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False, groups=1,
+                     g16=False):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts).
-    wt: as conv_dgrad.  y / z may be bf16 (the bf16-activation step, TMR_IO_BN_BF16)."""
+    wt: as conv_dgrad.  y / z may be bf16 (the bf16-activation step, TMR_IO_BN_BF16).
+    g16: dx_masked stored bf16, the partials those of the rounded values (TMR_IO_G16)."""
     _req_op(w_krsc, "w"); _req_op(y, "y"); _req(mean, "mean")
     if mask == 3:   # z = ReLU-mask bits of dx's shape (bn_apply_bits)
         if z is None or z.dtype != torch.int32 or z.numel() * 32 < y.numel():
@@ -275,10 +278,13 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     k2, r, s, c = _dgrad_w(w_krsc, wt, groups)
     h, w = in_hw
     d = conv_desc(n, h, w, c, k, r, s, stride, pad, math=math,
-                  io=_io(None, w_krsc, dy, wt) | (IO_BN if y.dtype == BF16 else 0), groups=groups)
+                  io=_io(None, w_krsc, dy, wt) | (IO_BN if y.dtype == BF16 else 0)
+                  | (IO_G16 if g16 else 0), groups=groups)
     assert (d.ho, d.wo) == (ho, wo), ((d.ho, d.wo), (ho, wo))
     if out is None:
-        out = _empty((n, h, w, c), dy)
+        out = _empty((n, h, w, c), dy, dtype=BF16 if g16 else f32)
+    elif out.dtype != (BF16 if g16 else f32):
+        raise RuntimeError("conv_dgrad_bnbwd: dx must be %s" % ("bf16 (g16)" if g16 else "fp32"))
     if tuple(y.shape) != tuple(out.shape) or (z is not None and mask != 3
                                               and tuple(z.shape) != tuple(out.shape)):
         raise RuntimeError("conv_dgrad_bnbwd: y/z must have dx's shape %s" % (tuple(out.shape),))
@@ -290,7 +296,7 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c / groups, (n, h, w, c, k, r, stride),
                _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * w_krsc.numel()
-               + 4 * n * h * w * c * (2 if beta else 1)
+               + (2 if g16 else 4) * n * h * w * c * (2 if beta else 1)
                + y.element_size() * n * h * w * c * (2 if z is not None and mask != 3 else 1)
                + (n * h * w * c // 8 if mask == 3 else 0)):
         pro = _prologue(None, dpro)
@@ -359,11 +365,12 @@ def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma, bf16=False):
     rows = y.numel() // c
     nb = query("tmr_bn_parts_ws_bytes", int(nparts), c)
     ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=y.device)
-    if y.dtype == BF16:   # bf16 activations: dy is bf16 too
+    if y.dtype == BF16:   # bf16 activations: dy is bf16 too (g bf16 from a g16 dgrad, or fp32)
         dy = torch.empty_like(y)
-        dgamma = _empty((c,), g); dbeta = _empty((c,), g)
-        call("tmr_bn_bwd_parts_a16", g, y, parts, int(nparts), mean, inv, gamma, dy, dgamma, dbeta,
-             rows, c, ws, ctypes.c_size_t(ws.numel() * 8), stream_ptr())
+        dgamma = _empty((c,), mean); dbeta = _empty((c,), mean)
+        call("tmr_bn_bwd_parts_g16" if g.dtype == BF16 else "tmr_bn_bwd_parts_a16", g, y, parts,
+             int(nparts), mean, inv, gamma, dy, dgamma, dbeta, rows, c, ws,
+             ctypes.c_size_t(ws.numel() * 8), stream_ptr())
         return dy, dgamma, dbeta
     dy = torch.empty_like(y, dtype=torch.bfloat16 if bf16 else y.dtype)
     dgamma = _empty((c,), y); dbeta = _empty((c,), y)

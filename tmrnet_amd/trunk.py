@@ -131,6 +131,12 @@ DMA32 = os.environ.get("TMR_GEMM32", "1") != "0"
 # 51.1 vs 51.6 ms of dgrads per C2 step (profiles/r3/bench_r4f/).  TMR_DS_FIRST=0: the old order.
 DS_FIRST = os.environ.get("TMR_DS_FIRST", "1") != "0"
 
+# bf16-activation step: the masked BN-output gradient of the non-residual units (bn1, bn2 of every
+# Bottleneck) stored bf16 by the fused dgrad (TMR_IO_G16; the residual stream's gradient stays
+# fp32) -- halves the bytes of the dgrad store and of the BN-backward apply's read of g.  The
+# contract (oracle.emulate_bf16_convs(grads=True)) rounds the gradient at those two points.
+G16 = os.environ.get("TMR_G16", "1") != "0"
+
 # the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
 BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
 # ... and for the bf16-activation step (TMR_RELU_BITS16=1).  Off: the bf16 dgrads re-read the 2-byte
@@ -246,7 +252,7 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
 
 
 def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
-                 dres_inplace=False, parts=None, fuse_prev=None, pool=None, dy=None):
+                 dres_inplace=False, parts=None, fuse_prev=None, pool=None, dy=None, g16=False):
     """BN backward, wgrad, dgrad (optionally accumulated into dx_out) of one conv+BN unit.
 
     parts: dz was produced by a fused dgrad (conv_dgrad_bnbwd): it is already ReLU-masked and
@@ -258,7 +264,9 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     pool: (pooled gradient, argmax) of the maxpool that consumed this unit's output (the stem);
     dz is then gathered from it inside the BN backward.
     dy: the conv's output gradient computed by the caller (ResNeSt's split-attention backward
-    writes the grouped conv's dy with bn0's backward folded in): only wgrad and dgrad run here."""
+    writes the grouped conv's dy with bn0's backward folded in): only wgrad and dgrad run here.
+    g16: the fused dgrad may store fuse_prev's masked gradient as bf16 (TMR_IO_G16) when that unit
+    has no residual and the dgrad runs on the bf16 LDS-DMA engine (the bf16-activation step)."""
     conv, bn = rec["conv"], rec["bn"]
     dpro = None    # (y, coef): dy = A*g + B*y + C evaluated by the consumer convs' loaders
     s16 = _store16(rec["math"])   # dy feeds only this conv's dgrad / wgrad
@@ -312,11 +320,14 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
             zm = p["z"]
             if mask == 1 and wt and p.get("zbits") is not None:
                 mask, zm = 3, p["zbits"]   # the ReLU mask as bits (fp32 LDS-DMA dgrad)
+            gb = (g16 and G16 and mask == 2 and dx_out is None and dx_beta == 0.0 and wt and
+                  grp == 1 and dpro is None and p["y"].dtype == torch.bfloat16 and
+                  p["y"].shape[-1] % 8 == 0)
             dx, pp, npp = ops.conv_dgrad_bnbwd(dy, wdg, hw, rec["stride"], rec["pad"],
                                                p["y"], p["mean"], mask, z=zm,
                                                scale=p["scale"], shift=p["shift"], out=dx_out,
                                                beta=dx_beta, math=rec["math"], dpro=dpro,
-                                               wt=wt, groups=grp)
+                                               wt=wt, groups=grp, g16=gb)
             fused = (pp, npp)
         else:
             dx = ops.conv_dgrad(dy, wdg, hw, rec["stride"], rec["pad"], out=dx_out,
@@ -411,8 +422,9 @@ class TrunkFn(torch.autograd.Function):
             prev3 = blocks[-1][1][-1] if (blocks and fuse) else None
             # g (owned here) becomes the masked pre-ReLU gradient = the identity-branch grad
             dz2, dres, fz2 = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True,
-                                          parts=pending, fuse_prev=r2 if fuse else None)
-            dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1 if fuse else None)
+                                          parts=pending, fuse_prev=r2 if fuse else None, g16=True)
+            dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1 if fuse else None,
+                                       g16=True)
             del dz2
             if has_ds and DS_FIRST:
                 # the strided downsample dgrad writes dx (its tap-less parity classes as zeros),
