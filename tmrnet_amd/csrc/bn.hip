@@ -1319,6 +1319,11 @@ TMR_API int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const 
                      zb, scale, shift, coef, db, dres, n4, c4)
   if (dres) {
     if (mask == 1) { TMR_BN_APPLY16(1, true); } else if (mask == 2) { TMR_BN_APPLY16(2, true); } else { TMR_BN_APPLY16(0, true); }
+  } else if (mask == 0 && c % 8 == 0 && (((uintptr_t)dz | (uintptr_t)y | (uintptr_t)dy) & 15) == 0) {
+    // no mask left to apply (the downsample branch's BN, or a mask already written back): the
+    // 8-wide apply of the parts path (same coefficients, same fmaf sequence)
+    hipLaunchKernelGGL(bn_bwd_apply8_a16<float>, dim3(ew_blocks(n4 / 2)), dim3(NT), 0, stream, dz,
+                       yb, coef, db, n4 / 2, c / 8);
   } else {
     if (mask == 1) { TMR_BN_APPLY16(1, false); } else if (mask == 2) { TMR_BN_APPLY16(2, false); } else { TMR_BN_APPLY16(0, false); }
   }
