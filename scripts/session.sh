@@ -1,11 +1,8 @@
 # one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
 set -o pipefail
-O=gpurun_out/r5k; mkdir -p $O
-for i in 1 2; do
-timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --model resnest50 --precision bf16 > $O/c4_new$i.json 2> $O/c4_new$i.err || exit $?
-TMR_LIB_PATH=tmrnet_amd/libtmr_prev.so timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --model resnest50 --precision bf16 > $O/c4_prev$i.json 2> $O/c4_prev$i.err || exit $?
-done
+O=gpurun_out/r5n; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "stem or fused_bn_stats" -m gpu > $O/pytest_stem.txt 2>&1 || exit $?
+TMR_STEM_DIRECT=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --conv-table > $O/c2_stem.json 2> $O/c2_stem_table.txt || exit $?
+TMR_STEM_DIRECT=0 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --conv-table > $O/c2_nostem.json 2> $O/c2_nostem_table.txt || exit $?
+TMR_STEM_DIRECT=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > $O/c2_stem2.json 2> $O/c2_stem2.err
 echo "main rc=$?"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_bf16_gpu.py tests/test_kernels_gpu.py tests/test_geometry_gpu.py -m gpu > $O/pytest.txt 2>&1 && \
-timeout -k 10 300 python bench.py --no-cpu-baseline --steps 6 --precision bf16 --seq 30 --lfb 300 > $O/c5.json 2> $O/c5.err
-echo "tail rc=$?"

@@ -675,3 +675,32 @@ def test_bn_apply_relu_bits_bf16(dev, rows, c):
                                           out=old.clone(), beta=1.0, math="bf16", wt=True)
         torch.cuda.synchronize()
         assert n1 == n3 and torch.equal(d1, d3) and torch.equal(p1[:n1], p3[:n3])
+
+
+def test_stem_direct_fwd_bnstats(dev, monkeypatch):
+    """The fp32 7x7/2 stem with BatchNorm statistics as a direct convolution over its 147 real
+    (tap, channel) pairs (stem.hip, the train step's 224x224 geometry) against float64: the
+    output, and the BN statistics from its per-output-row partials; the implicit-GEMM engine
+    (TMR_STEM_DIRECT=0) agrees to fp32 summation order.  Six frames: 672 output rows, more than
+    the persistent grid's 512 workgroups, so workgroups run the prefetched second row."""
+    n = 6
+    g = torch.Generator().manual_seed(12)
+    x = torch.relu(torch.randn(n, 3, 224, 224, generator=g)) + 0.5
+    wt = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    wk = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=4)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    y, stats, nparts = ops.conv_fwd_bnstats(x4, wk, 2, 3, c_real=3)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    y0, stats0, nparts0 = ops.conv_fwd_bnstats(x4, wk, 2, 3, c_real=3)
+    torch.cuda.synchronize()
+    assert nparts == 4 * n * 112 and tuple(y.shape) == (n, 112, 112, 64)
+    ref = F.conv2d(x.double(), wt.double(), stride=2, padding=3).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-6 and rel_err(y0, ref) < 1e-6
+    yd = ref.reshape(-1, 64)
+    for st_, np_ in ((stats, nparts), (stats0, nparts0)):
+        ones, zeros = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+        rm, rv = zeros.clone(), ones.clone()
+        mean, inv, _, _ = ops.bn_finalize(st_, np_, ones, zeros, rm, rv, 0.1, 1e-5)
+        assert rel_err(mean, yd.mean(0)) < 1e-6
+        assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5

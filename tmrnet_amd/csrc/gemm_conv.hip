@@ -298,11 +298,24 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
   return 0;
 }
 
+// The fp32 7x7/2 stem with BatchNorm statistics runs as a direct convolution over its 147 real
+// (tap, channel) pairs (stem.hip): a partial row per output row and wave.  TMR_STEM_DIRECT=0: the
+// implicit-GEMM engine (A/B, tests).
+int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const float* w_krsc,
+                         float* y, void* stats, hipStream_t stream);
+static bool stem_direct(const tmr_conv_desc* d) {
+  return env_int("TMR_STEM_DIRECT", 1) != 0 && d->math == TMR_MATH_F32 && d->io == 0 &&
+         ngroups(d) == 1 && d->c == 4 && d->k == 64 && d->r == 7 && d->s == 7 && d->stride == 2 &&
+         d->pad == 3 && d->pad_w == 3 && d->wo == 112 && d->w <= 226 && xld_of(d) == 4 &&
+         yld_of(d) == 64;
+}
+
 TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
   if (!d || d->n <= 0) {
     tmr_set_error("tmr_conv2d_fwd_stats_parts: null or empty descriptor");
     return -1;
   }
+  if (stem_direct(d)) return 4 * d->n * d->ho;
   tmr_conv_desc g = *d;
   if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
   const int fc = frames_per_launch(&g);
@@ -351,6 +364,8 @@ TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
   const size_t need = (size_t)np * d->k * sizeof(float4);
   TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
                 stats_bytes, need);
+  if (!pro && stem_direct(d))
+    return tmr_stem_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, y, stats, stream);
   if (ngroups(d) == 1) return fwd_bnstats_impl(d, x, w_krsc, y, (float4*)stats, d->k, pro, stream);
   TMR_CHECK_ARG(!pro, "tmr_conv2d_fwd_bnstats: operand prologues take no groups");
   tmr_conv_desc g;

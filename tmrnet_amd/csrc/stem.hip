@@ -1,0 +1,170 @@
+// The fp32 7x7/2 stem convolution of the train step (conv1 + its BatchNorm statistics) as a
+// direct convolution: share.conv1 of train_only_non-local_pretrained.py:204-214 (torchvision
+// resnet50, 3 -> 64 channels, 224x224 -> 112x112).
+//
+// On the implicit-GEMM engine the stem's reduction is 49 taps x 4 channels (the NHWC4 input's
+// zero 4th channel) padded to 7 k-tiles of 32: 147 useful of 224 multiplied (the engine's
+// 16-B pieces cannot pack 3 channels per tap).  Here a persistent workgroup (two per CU) computes
+// output rows of one frame (112 pixels x 64 channels) from an LDS copy of the 7 input rows each
+// reads -- the next row's patch is fetched into registers under the current row's MFMAs and
+// published to the other half of a double buffer -- with the weights staged once and the
+// reduction over exactly the 147 real (tap, channel) pairs:
+//   * input patch, channel- and column-parity-planar: X[kh][c][col & 1][col >> 1] for the padded
+//     columns col = iw + 3 (0 outside the image) -- the 32 lanes of an MFMA operand read
+//     consecutive words (column 2*ow + kw: parity kw & 1, half ow + kw / 2);
+//   * weights k-major: W[k][co], k = (kh * 7 + kw) * 3 + c (148 rows, the last 0);
+//   * v_mfma_f32_32x32x2_f32, each wave 32 output pixels x 64 channels, 74 k-steps;
+//   * epilogue: y (NHWC, 64 channels) and each wave's BatchNorm partial (n, mean, M2) per channel
+//     over its 32 (last wave: 16) pixels -- the conv epilogue's statistics format, combined by
+//     tmr_bn_finalize -- with no cross-wave exchange, so a row needs a single barrier.
+#include "common.h"
+#include "tmr.h"
+
+namespace {
+
+constexpr int SW = 112;          // output width
+constexpr int XH = 7;            // input rows per output row
+constexpr int XHALF = 116;       // padded columns / 2 (230 used)
+constexpr int KR = 148;          // 147 real reduction rows + 1 zero row (k-steps of 2)
+
+typedef float floatx16_t __attribute__((ext_vector_type(16)));
+
+// LDS offset in the patch image of reduction row k = (kh * 7 + kw) * 3 + c at output column 0
+__host__ __device__ constexpr int kx_of(int k) {
+  return k >= 147 ? 0
+                  : ((((k / 3) / 7) * 3 + k % 3) * 2 + ((k / 3) % 7 & 1)) * XHALF + ((k / 3) % 7 >> 1);
+}
+
+__global__ __launch_bounds__(256, 2) void stem_fwd_k(const float* __restrict__ x,
+                                                     const float* __restrict__ w_krsc,
+                                                     float* __restrict__ y,
+                                                     float4* __restrict__ stats, int h, int wd,
+                                                     int ho, int rows) {
+  constexpr int XS = XH * 3 * 2 * XHALF;
+  __shared__ float Xs[2 * XS];   // 2 x 19.5 KB: the patch of this row and of the next
+  __shared__ float Ws[KR * 64];  // 37.9 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // weights, once per (persistent) workgroup: KRSC (64, 7, 7, 4) -> k-major [k][co] over the 3
+  // real channels (consecutive threads: consecutive co, conflict-free LDS writes)
+  for (int i = tid; i < 64 * 49; i += 256) {
+    const int co = i & 63, tap = i >> 6;
+    const float4 v = reinterpret_cast<const float4*>(w_krsc)[co * 49 + tap];
+    Ws[(tap * 3 + 0) * 64 + co] = v.x;
+    Ws[(tap * 3 + 1) * 64 + co] = v.y;
+    Ws[(tap * 3 + 2) * 64 + co] = v.z;
+  }
+  if (tid < 64) Ws[147 * 64 + tid] = 0.f;
+  // input rows ih = 2 * oh - 3 + kh, columns iw = col - 3 (NHWC4: 3 real channels); each thread
+  // holds its pieces of the next row's patch in registers while the current row computes
+  constexpr int NP = XH * 2 * XHALF, PPT = (NP + 255) / 256;
+  float4 pv[PPT];
+  auto fetch = [&](int row) {
+    const int oh = row % ho, n = row / ho;
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int i = tid + 256 * q;
+      const int kh = i / (2 * XHALF), col = i % (2 * XHALF);
+      const int ih = 2 * oh - 3 + kh, iw = col - 3;
+      pv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NP && ih >= 0 && ih < h && iw >= 0 && iw < wd)
+        pv[q] = reinterpret_cast<const float4*>(x)[((long)n * h + ih) * wd + iw];
+    }
+  };
+  auto publish = [&](float* X) {
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int i = tid + 256 * q;
+      if (i < NP) {
+        const int kh = i / (2 * XHALF), col = i % (2 * XHALF);
+        const int base = (kh * 3) * 2 * XHALF + (col & 1) * XHALF + (col >> 1);
+        X[base] = pv[q].x;
+        X[base + 2 * XHALF] = pv[q].y;
+        X[base + 4 * XHALF] = pv[q].z;
+      }
+    }
+  };
+  const int l31 = lane & 31, hh = lane >> 5;
+  const int ow = 32 * wave + l31;
+  const int owc = ow < SW ? ow : SW - 1;   // clamped read (rows >= 112 are dropped)
+  const int cnt = wave == 3 ? SW - 96 : 32;   // this wave's valid output pixels
+  int row = blockIdx.x, buf = 0;
+  if (row < rows) fetch(row);
+  for (; row < rows; row += gridDim.x, buf ^= 1) {
+    // the other buffer was last read two rows ago, before the previous row's barrier
+    float* X = Xs + buf * XS;
+    publish(X);
+    __syncthreads();   // the patch (and, the first time, the weights) visible
+    if (row + (int)gridDim.x < rows) fetch(row + gridDim.x);   // lands under the MFMAs
+
+    // wave: output pixels ow = 32 * wave + (lane & 31) (>= 112: dropped), channels 0..63; lanes
+    // 32..63 take the odd reduction row of each k-step
+    floatx16_t acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
+    const float* xa = X + owc;
+    const float* wb = Ws + hh * 64 + l31;
+#pragma unroll
+    for (int s = 0; s < KR / 2; ++s) {
+      const float a = xa[hh ? kx_of(2 * s + 1) : kx_of(2 * s)];
+      const float b0 = wb[2 * s * 64], b1 = wb[2 * s * 64 + 32];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+    }
+
+    // epilogue: y rows (pixels) and this wave's BatchNorm partial (no cross-wave exchange)
+    const long prow = (long)row * SW;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int px = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (px < SW) {
+        y[(prow + px) * 64 + l31] = acc0[r];
+        y[(prow + px) * 64 + 32 + l31] = acc1[r];
+        s0 += acc0[r];
+        s1 += acc1[r];
+      }
+    }
+    const float m0 = (s0 + __shfl_xor(s0, 32, 64)) / cnt;
+    const float m1 = (s1 + __shfl_xor(s1, 32, 64)) / cnt;
+    float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int px = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (px < SW) {
+        const float d0 = acc0[r] - m0, d1 = acc1[r] - m1;
+        q0 = fmaf(d0, d0, q0);
+        q1 = fmaf(d1, d1, q1);
+      }
+    }
+    q0 += __shfl_xor(q0, 32, 64);
+    q1 += __shfl_xor(q1, 32, 64);
+    float4* st = stats + ((long)row * 4 + wave) * 64;
+    if (hh == 0) st[l31] = make_float4((float)cnt, m0, q0, 0.f);
+    else st[32 + l31] = make_float4((float)cnt, m1, q1, 0.f);
+  }
+}
+
+}  // namespace
+
+// tmr_conv2d_fwd_bnstats for the stem geometry (gemm_conv.hip routes it here): x NHWC4 fp32
+// (n, h, w, 4) with the 4th channel ignored, w KRSC (64, 7, 7, 4) fp32, stride 2, pad 3, output
+// width 112; one BatchNorm partial row per output row and wave (4 * n * ho rows of 64).
+int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const float* w_krsc,
+                         float* y, void* stats, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && ho > 0 && (w + 6 - 7) / 2 + 1 == SW && 2 * XHALF >= w + 6,
+                "tmr_stem_fwd_bnstats: unsupported geometry %dx%d", h, w);
+  TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)w_krsc) & 15) == 0,
+                "tmr_stem_fwd_bnstats: x / w must be 16-B aligned");
+  // persistent: two workgroups per CU (LDS), each over a strided sequence of output rows (the
+  // weights are staged once per workgroup)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int rows = n * ho;
+  const int grid = rows < 2 * cus ? rows : 2 * cus;
+  hipLaunchKernelGGL(stem_fwd_k, dim3(grid), dim3(256), 0, stream, x, w_krsc, y,
+                     (float4*)stats, h, w, ho, rows);
+  TMR_CHECK_LAUNCH("stem_fwd");
+  return 0;
+}
