@@ -704,3 +704,29 @@ def test_stem_direct_fwd_bnstats(dev, monkeypatch):
         mean, inv, _, _ = ops.bn_finalize(st_, np_, ones, zeros, rm, rv, 0.1, 1e-5)
         assert rel_err(mean, yd.mean(0)) < 1e-6
         assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
+
+
+@pytest.mark.gpu
+def test_stem_direct_wgrad(dev, monkeypatch):
+    """The fp32 stem's weight gradient as a direct convolution (stem.hip: per-workgroup partial
+    slabs over the 147 real (tap, channel) pairs, summed by the engine's tap reduction) against
+    float64, with beta accumulation, and against the implicit-GEMM engine (TMR_STEM_DIRECT=0).
+    Six frames: 672 output rows over the 512 persistent workgroups."""
+    n = 6
+    g = torch.Generator().manual_seed(13)
+    x = torch.relu(torch.randn(n, 3, 224, 224, generator=g)) + 0.5
+    dy = torch.randn(n, 64, 112, 112, generator=g)
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    dyn = dy.to(dev).permute(0, 2, 3, 1).contiguous()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (64, 3, 7, 7), dy.double(), stride=2, padding=3)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    dw = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3)
+    prev = torch.randn(64, 3, 7, 7, generator=g).to(dev)
+    acc = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, out=prev.clone(), beta=0.5)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    dw0 = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3)
+    torch.cuda.synchronize()
+    assert tuple(dw.shape) == (64, 3, 7, 7)
+    # fp32 sums of 75,264 products per weight (random-sign dy): ~1e-6 of the largest weight
+    assert rel_err(dw, ref) < 4e-6 and rel_err(dw0, ref) < 4e-6
+    assert rel_err(acc, ref + 0.5 * prev.double().cpu()) < 4e-6

@@ -299,10 +299,14 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
 }
 
 // The fp32 7x7/2 stem with BatchNorm statistics runs as a direct convolution over its 147 real
-// (tap, channel) pairs (stem.hip): a partial row per output row and wave.  TMR_STEM_DIRECT=0: the
+// (tap, channel) pairs (stem.hip): a partial row per output row and wave; its weight gradient too
+// (partial slabs per workgroup, reduced by wgrad_reduce_taps_kernel).  TMR_STEM_DIRECT=0: the
 // implicit-GEMM engine (A/B, tests).
 int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const float* w_krsc,
                          float* y, void* stats, hipStream_t stream);
+int tmr_stem_wgrad_slabs(int n, int h, int w, int ho, const float* x, const float* dy, float* ws,
+                         size_t ws_bytes, int* nslabs, hipStream_t stream);
+constexpr long kStemSlabs = 512, kStemSlab = 64 * 49 * 4;   // stem.hip's grid and slab
 static bool stem_direct(const tmr_conv_desc* d) {
   return env_int("TMR_STEM_DIRECT", 1) != 0 && d->math == TMR_MATH_F32 && d->io == 0 &&
          ngroups(d) == 1 && d->c == 4 && d->k == 64 && d->r == 7 && d->s == 7 && d->stride == 2 &&
@@ -654,7 +658,10 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
   long slab;
   const tmr_conv_desc c = chunk_desc(&g, frames_per_launch(&g));   // the largest chunk
   wgrad_plan(&c, &sp, &kc, &slab);
-  return (size_t)sp * slab * sizeof(float);
+  size_t bytes = (size_t)sp * slab * sizeof(float);
+  if (stem_direct(d) && bytes < (size_t)kStemSlabs * kStemSlab * sizeof(float))
+    bytes = (size_t)kStemSlabs * kStemSlab * sizeof(float);
+  return bytes;
 }
 
 static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* dy,
@@ -704,6 +711,15 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_wgrad: stored input channels %d must be a power of two >= 4", d->c);
   TMR_CHECK_ARG(c_real >= 1 && c_real <= d->c, "tmr_conv2d_wgrad: bad c_real %d", c_real);
+  if (!pro && c_real == 3 && stem_direct(d)) {
+    int ns = 0;
+    const int rc = tmr_stem_wgrad_slabs(d->n, d->h, d->w, d->ho, x, dy, ws, ws_bytes, &ns, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, 1), dim3(256), 0, stream, ws, ns,
+                       kStemSlab, dw_oihw, 49, 4, 3, beta);
+    TMR_CHECK_LAUNCH("wgrad_reduce_taps_kernel");
+    return 0;
+  }
   int sp, kc;
   long slab;
   wgrad_plan(d, &sp, &kc, &slab);

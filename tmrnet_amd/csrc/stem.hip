@@ -26,6 +26,7 @@ constexpr int SW = 112;          // output width
 constexpr int XH = 7;            // input rows per output row
 constexpr int XHALF = 116;       // padded columns / 2 (230 used)
 constexpr int KR = 148;          // 147 real reduction rows + 1 zero row (k-steps of 2)
+constexpr int GRID = 512;        // persistent workgroups (two per CU) = the wgrad's partial slabs
 
 typedef float floatx16_t __attribute__((ext_vector_type(16)));
 
@@ -145,6 +146,116 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_k(const float* __restrict__ x
   }
 }
 
+// Weight gradient: dW[co][k] = sum over output pixels p of dy[p][co] * X[p][k] (k the 147 real
+// (tap, channel) pairs).  Persistent workgroups over output rows as in the forward (patch double
+// buffer); wave w takes pixel pairs w, w + 4, ... of a
+// row (14 k-steps of 2 pixels): A = dy (32 channels x 2 pixels, straight from HBM, each element
+// read once), B = the patch (2 pixels x 32 reduction rows from LDS), 2 x 5 accumulator tiles of
+// 32x32 (64 channels x 160 reduction rows).  At the end the four waves add their tiles in LDS and
+// the workgroup writes one partial slab in the engine's wgrad layout ((co * 49 + tap) * 4 + c),
+// which wgrad_reduce_taps_kernel sums in a fixed order (deterministic).
+__global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__ x,
+                                                       const float* __restrict__ dy,
+                                                       float* __restrict__ slabs, int h, int wd,
+                                                       int ho, int rows) {
+  constexpr int XS = XH * 3 * 2 * XHALF;
+  __shared__ float Xs[2 * XS];   // 2 x 19.5 KB; at the end the 64 x 147 partial
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l31 = lane & 31, hh = lane >> 5;
+  constexpr int NP = XH * 2 * XHALF, PPT = (NP + 255) / 256;
+  float4 pv[PPT];
+  auto fetch = [&](int row) {
+    const int oh = row % ho, n = row / ho;
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int i = tid + 256 * q;
+      const int kh = i / (2 * XHALF), col = i % (2 * XHALF);
+      const int ih = 2 * oh - 3 + kh, iw = col - 3;
+      pv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NP && ih >= 0 && ih < h && iw >= 0 && iw < wd)
+        pv[q] = reinterpret_cast<const float4*>(x)[((long)n * h + ih) * wd + iw];
+    }
+  };
+  int kxl[5];   // this lane's reduction row k = 32 * t + (lane & 31) in the patch image
+#pragma unroll
+  for (int t = 0; t < 5; ++t) kxl[t] = kx_of(32 * t + l31);
+  floatx16_t acc[2][5];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
+
+  // the patch goes global -> registers -> LDS at the top of each row (no registers to carry it
+  // under the MFMAs: the 160 accumulators fill the budget); the two workgroups of a CU overlap
+  // one's loads with the other's MFMAs
+  for (int row = blockIdx.x, buf = 0; row < rows; row += gridDim.x, buf ^= 1) {
+    fetch(row);
+    float* X = Xs + buf * XS;
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int i = tid + 256 * q;
+      if (i < NP) {
+        const int kh = i / (2 * XHALF), col = i % (2 * XHALF);
+        const int base = (kh * 3) * 2 * XHALF + (col & 1) * XHALF + (col >> 1);
+        X[base] = pv[q].x;
+        X[base + 2 * XHALF] = pv[q].y;
+        X[base + 4 * XHALF] = pv[q].z;
+      }
+    }
+    __syncthreads();   // the patch visible (the other buffer was last read two rows ago)
+    // this wave's dy: pixels p = 2 * (wave + 4 * j) + (lane >> 5), channels (lane & 31) + 32 m
+    const float* dyr = dy + ((long)row * SW + 2 * wave + hh) * 64 + l31;
+    float a[14][2];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      a[j][0] = dyr[8 * j * 64];
+      a[j][1] = dyr[8 * j * 64 + 32];
+    }
+    const float* xb = X + 2 * wave + hh;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      float b[5];
+#pragma unroll
+      for (int t = 0; t < 5; ++t) b[t] = xb[kxl[t] + 8 * j];
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][0], b[t], acc[0][t], 0, 0, 0);
+        acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][1], b[t], acc[1][t], 0, 0, 0);
+      }
+    }
+  }
+
+  // the four waves' tiles summed in LDS (fixed order), then one partial slab per workgroup
+  float* red = Xs;   // 64 x 147 floats <= 2 * XS
+  __syncthreads();
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const int k = 32 * t + l31;
+          if (k < 147) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int co = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              float& dst = red[co * 147 + k];
+              dst = w == 0 ? acc[m][t][r] : dst + acc[m][t][r];
+            }
+          }
+        }
+    }
+    __syncthreads();
+  }
+  float* slab = slabs + (long)blockIdx.x * (64 * 49 * 4);
+  for (int i = tid; i < 64 * 147; i += 256) {
+    const int co = i / 147, k = i - co * 147;
+    slab[(co * 49 + k / 3) * 4 + k % 3] = red[i];
+  }
+}
+
 }  // namespace
 
 // tmr_conv2d_fwd_bnstats for the stem geometry (gemm_conv.hip routes it here): x NHWC4 fp32
@@ -158,13 +269,28 @@ int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const floa
                 "tmr_stem_fwd_bnstats: x / w must be 16-B aligned");
   // persistent: two workgroups per CU (LDS), each over a strided sequence of output rows (the
   // weights are staged once per workgroup)
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int rows = n * ho;
-  const int grid = rows < 2 * cus ? rows : 2 * cus;
+  const int grid = rows < GRID ? rows : GRID;
   hipLaunchKernelGGL(stem_fwd_k, dim3(grid), dim3(256), 0, stream, x, w_krsc, y,
                      (float4*)stats, h, w, ho, rows);
   TMR_CHECK_LAUNCH("stem_fwd");
+  return 0;
+}
+
+// Stem weight gradient (gemm_conv.hip routes the fp32 stem here): partial slabs of the engine's
+// wgrad layout (64 x 49 x 4 floats, channel 3 not written) into ws, one per workgroup; *nslabs
+// = their number (the caller reduces them).
+int tmr_stem_wgrad_slabs(int n, int h, int w, int ho, const float* x, const float* dy, float* ws,
+                         size_t ws_bytes, int* nslabs, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && ho > 0 && (w + 6 - 7) / 2 + 1 == SW && 2 * XHALF >= w + 6,
+                "tmr_stem_wgrad: unsupported geometry %dx%d", h, w);
+  TMR_CHECK_ARG(((uintptr_t)x & 15) == 0, "tmr_stem_wgrad: x must be 16-B aligned");
+  const int rows = n * ho;
+  const int grid = rows < GRID ? rows : GRID;
+  TMR_CHECK_ARG(ws && ws_bytes >= (size_t)grid * 64 * 49 * 4 * sizeof(float),
+                "tmr_stem_wgrad: workspace too small (%zu)", ws_bytes);
+  hipLaunchKernelGGL(stem_wgrad_k, dim3(grid), dim3(256), 0, stream, x, dy, ws, h, w, ho, rows);
+  TMR_CHECK_LAUNCH("stem_wgrad");
+  *nslabs = grid;
   return 0;
 }
