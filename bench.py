@@ -231,8 +231,10 @@ def main():
             a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
         peak = MFMA_F32_PEAK_TF if args.precision == "fp32" else MFMA_BF16_PEAK_TF
         roof = {"bound": "mfma",
-                "kernel": "gemm16_kernel (LDS-DMA implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA)"
-                          % ("f32" if args.precision == "fp32" else "bf16 operands, f32 acc"),
+                "kernel": ("gemm16_kernel (LDS-DMA implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA)%s"
+                           % ("f32" if args.precision == "fp32" else "bf16 operands, f32 acc",
+                              " + stem_fwd_k / stem_wgrad_k (direct fp32 7x7 stem)"
+                              if args.precision == "fp32" else "")),
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
                 # HBM bytes per conv call (PMC, per step / calls per step), same unit as achieved
@@ -337,8 +339,11 @@ def load_traffic(model, precision, seq, lfb):
         d = json.load(f)
     fams = d.get("families", {})
     # the conv family: gemm_kernel / tmrg::gemm_kernel (register-staged), tmrg::gemm16_kernel
-    # (LDS-DMA engine) and the split-K weight-gradient reductions
-    conv = [k for k in fams if any(t in k for t in ("gemm_kernel", "gemm16_kernel", "wgrad_reduce"))]
+    # (LDS-DMA engine), the direct fp32 stem (stem_fwd_k / stem_wgrad_k, round 3) and the split-K
+    # weight-gradient reductions
+    conv = [k for k in fams
+            if any(t in k for t in ("gemm_kernel", "gemm16_kernel", "wgrad_reduce", "stem_fwd_k",
+                                    "stem_wgrad_k"))]
     if not conv:
         return None
     per_step = sum(fams[k]["hbm_bytes_per_step"] for k in conv)

@@ -306,6 +306,24 @@ int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n, int h, 
                          const float* save_mean, const float* save_invstd, const float* gamma,
                          void* dy, float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
                          int out_bf16, hipStream_t stream);
+/* The fp32 stem's backward without its output gradient in HBM (round 3; autograd of share.conv1 /
+ * bn1 / relu / maxpool, train_only_non-local_pretrained.py:204-214, run by loss.backward() :724):
+ * tmr_bn_bwd_maxpool_coefs is tmr_bn_bwd_maxpool up to the BN-backward coefficients coef[3][c]
+ * (dy = A*g + B*y + C, g the maxpool-gathered, ReLU-masked gradient) and dgamma / dbeta, with no
+ * dy pass; tmr_conv2d_wgrad_stem_bnbwd is the stem conv's weight gradient with that dy evaluated
+ * per output row in LDS from (pooled gradient dyp (n, ho_p, wo_p, 64), argmax, y, scale, shift,
+ * coef) -- the direct stem geometry only (x NHWC4 fp32 (n, h, w <= 226, 4), 64 filters 7x7/2,
+ * pad 3, 112 output columns); ws from tmr_conv2d_wgrad_ws_bytes. */
+int tmr_bn_bwd_maxpool_coefs(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho,
+                             int wo, const float* y, const float* scale, const float* shift,
+                             const float* save_mean, const float* save_invstd, const float* gamma,
+                             float* coef, float* dgamma, float* dbeta, int c, void* ws,
+                             size_t ws_bytes, hipStream_t stream);
+int tmr_conv2d_wgrad_stem_bnbwd(const tmr_conv_desc* d, const float* x, const float* y,
+                                const float* scale, const float* shift, const float* coef,
+                                const float* dyp, const uint8_t* argmax, int ho_p, int wo_p,
+                                float* dw_oihw, float beta, float* ws, size_t ws_bytes,
+                                hipStream_t stream);
 int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, int r, int s, int cpad,
                               int out_bf16, hipStream_t stream);
 /* bf16 operands of the LDS-DMA conv engine (every operand of a bf16-math conv stored bf16):

@@ -730,3 +730,34 @@ def test_stem_direct_wgrad(dev, monkeypatch):
     # fp32 sums of 75,264 products per weight (random-sign dy): ~1e-6 of the largest weight
     assert rel_err(dw, ref) < 4e-6 and rel_err(dw0, ref) < 4e-6
     assert rel_err(acc, ref + 0.5 * prev.double().cpu()) < 4e-6
+
+
+@pytest.mark.gpu
+def test_stem_wgrad_bnbwd_fused(dev, monkeypatch):
+    """The fp32 stem backward without its output gradient in HBM: BN-backward coefficients from
+    the pooled side (tmr_bn_bwd_maxpool_coefs), then the direct stem wgrad evaluating dy per row
+    in LDS (tmr_conv2d_wgrad_stem_bnbwd) -- the two-pass form's arithmetic per element and the same
+    MFMA order, so dW, dgamma and dbeta are bit-identical to bn_bwd_maxpool + the direct wgrad;
+    dW against float64 of the two-pass dy.  Six frames (workgroups run a second row)."""
+    n, c = 6, 64
+    g = torch.Generator().manual_seed(14)
+    x = torch.relu(torch.randn(n, 3, 224, 224, generator=g)) + 0.5
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    y = torch.randn(n, 112, 112, c, generator=g).to(dev)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
+    beta = torch.randn(c, generator=g).to(dev)
+    rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
+    mean, inv, scale, shift = ops.bn_fwd_train(y.view(-1, c), gamma, beta, rm, rv, 0.1, 1e-5)
+    p, am = ops.maxpool_fwd_bn(y, scale, shift)
+    dp = torch.randn(p.shape, generator=g).to(dev)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    dy, dg, db = ops.bn_bwd_maxpool(dp, am, y, scale, shift, mean, inv, gamma)
+    dw_ref = ops.conv_wgrad(x4, dy, 7, 7, 2, 3, c_real=3)
+    coef, dg2, db2 = ops.bn_bwd_maxpool_coefs(dp, am, y, scale, shift, mean, inv, gamma)
+    dw = ops.conv_wgrad_stem_bnbwd(x4, y, scale, shift, coef, dp, am, 7, 7, 2, 3)
+    torch.cuda.synchronize()
+    assert torch.equal(dg2, dg) and torch.equal(db2, db)
+    assert torch.equal(dw, dw_ref)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (64, 3, 7, 7),
+                                      dy.double().cpu().permute(0, 3, 1, 2), stride=2, padding=3)
+    assert rel_err(dw, ref) < 4e-6

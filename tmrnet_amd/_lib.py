@@ -66,6 +66,8 @@ SIGNATURES = {
     "tmr_bn_bwd_parts_x": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, I, P],
     "tmr_bn_bwd_x": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, I, P],
     "tmr_bn_bwd_maxpool_x": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, I, P],
+    "tmr_bn_bwd_maxpool_coefs": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
+    "tmr_conv2d_wgrad_stem_bnbwd": [DP, P, P, P, P, P, P, P, I, I, P, F, P, SZ, P],
     "tmr_weight_oihw_to_krsc_x": [P, P, I, I, I, I, I, I, P],
     "tmr_weight_oihw_to_crsk_x": [P, P, I, I, I, I, I, P],
     "tmr_bn_apply_dual": [P, P, P, P, P, P, I, I, I, P],

@@ -1100,12 +1100,43 @@ TMR_API int tmr_bn_bwd_maxpool(const float* dyp, const uint8_t* argmax, int n, i
                               save_invstd, gamma, dy, dgamma, dbeta, c, ws, ws_bytes, 0, stream);
 }
 
+static int bn_bwd_maxpool_impl(const float* dyp, const uint8_t* argmax, int n, int h, int w,
+                               int ho, int wo, const float* y, const float* scale,
+                               const float* shift, const float* save_mean,
+                               const float* save_invstd, const float* gamma, void* dyv,
+                               float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                               int out_bf16, float* coef_out, hipStream_t stream);
+
 TMR_API int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n, int h, int w,
                                  int ho, int wo, const float* y, const float* scale,
                                  const float* shift, const float* save_mean,
                                  const float* save_invstd, const float* gamma, void* dyv,
                                  float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
                                  int out_bf16, hipStream_t stream) {
+  TMR_CHECK_ARG(dyv, "tmr_bn_bwd_maxpool: null dy");
+  return bn_bwd_maxpool_impl(dyp, argmax, n, h, w, ho, wo, y, scale, shift, save_mean,
+                             save_invstd, gamma, dyv, dgamma, dbeta, c, ws, ws_bytes, out_bf16,
+                             nullptr, stream);
+}
+
+TMR_API int tmr_bn_bwd_maxpool_coefs(const float* dyp, const uint8_t* argmax, int n, int h, int w,
+                                     int ho, int wo, const float* y, const float* scale,
+                                     const float* shift, const float* save_mean,
+                                     const float* save_invstd, const float* gamma, float* coef,
+                                     float* dgamma, float* dbeta, int c, void* ws,
+                                     size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(coef, "tmr_bn_bwd_maxpool_coefs: null coef");
+  return bn_bwd_maxpool_impl(dyp, argmax, n, h, w, ho, wo, y, scale, shift, save_mean,
+                             save_invstd, gamma, nullptr, dgamma, dbeta, c, ws, ws_bytes, 0, coef,
+                             stream);
+}
+
+static int bn_bwd_maxpool_impl(const float* dyp, const uint8_t* argmax, int n, int h, int w,
+                               int ho, int wo, const float* y, const float* scale,
+                               const float* shift, const float* save_mean,
+                               const float* save_invstd, const float* gamma, void* dyv,
+                               float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
+                               int out_bf16, float* coef_out, hipStream_t stream) {
   const long rows_l = (long)n * h * w;
   TMR_CHECK_ARG(c % 4 == 0 && c >= 4 && rows_l > 0 && rows_l < 0x7fffffffL,
                 "tmr_bn_bwd_maxpool: bad shape n=%d h=%d w=%d c=%d", n, h, w, c);
@@ -1121,7 +1152,7 @@ TMR_API int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n,
   const int prows = n * ho * wo;
   Plan p = make_plan(prows, c);
   double* part = (double*)ws;
-  float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
+  float* coef = coef_out ? coef_out : (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
   hipLaunchKernelGGL(stem_bwd_partial_pooled<float>, dim3(p.nrb, p.cblocks), dim3(NT), 0, stream, pg, h, w,
                      y, scale, shift, save_mean, prows, c, p.rpb, p.cthreads,
                      make_fastdiv((uint32_t)(ho * wo)), make_fastdiv((uint32_t)wo), part);
@@ -1129,6 +1160,7 @@ TMR_API int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n,
   hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");
+  if (!dyv) return 0;   // coefficients only: the stem's direct wgrad applies them on load
   const long n4 = rows_l * c / 4;
   if (out_bf16)
     hipLaunchKernelGGL(stem_bwd_apply<__bf16>, dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg, y, scale,

@@ -306,12 +306,19 @@ int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const floa
                          float* y, void* stats, hipStream_t stream);
 int tmr_stem_wgrad_slabs(int n, int h, int w, int ho, const float* x, const float* dy, float* ws,
                          size_t ws_bytes, int* nslabs, hipStream_t stream);
+int tmr_stem_wgrad_bnbwd_slabs(int n, int h, int w, int ho, const float* x, const float* y,
+                               const float* scale, const float* shift, const float* coef,
+                               const float* dyp, const uint8_t* argmax, int hp, int wp, float* ws,
+                               size_t ws_bytes, int* nslabs, hipStream_t stream);
 constexpr long kStemSlabs = 512, kStemSlab = 64 * 49 * 4;   // stem.hip's grid and slab
-static bool stem_direct(const tmr_conv_desc* d) {
-  return env_int("TMR_STEM_DIRECT", 1) != 0 && d->math == TMR_MATH_F32 && d->io == 0 &&
+static bool stem_geometry(const tmr_conv_desc* d) {
+  return d->math == TMR_MATH_F32 && d->io == 0 &&
          ngroups(d) == 1 && d->c == 4 && d->k == 64 && d->r == 7 && d->s == 7 && d->stride == 2 &&
          d->pad == 3 && d->pad_w == 3 && d->wo == 112 && d->w <= 226 && xld_of(d) == 4 &&
          yld_of(d) == 64;
+}
+static bool stem_direct(const tmr_conv_desc* d) {
+  return env_int("TMR_STEM_DIRECT", 1) != 0 && stem_geometry(d);
 }
 
 TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
@@ -659,7 +666,7 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
   const tmr_conv_desc c = chunk_desc(&g, frames_per_launch(&g));   // the largest chunk
   wgrad_plan(&c, &sp, &kc, &slab);
   size_t bytes = (size_t)sp * slab * sizeof(float);
-  if (stem_direct(d) && bytes < (size_t)kStemSlabs * kStemSlab * sizeof(float))
+  if (stem_geometry(d) && bytes < (size_t)kStemSlabs * kStemSlab * sizeof(float))
     bytes = (size_t)kStemSlabs * kStemSlab * sizeof(float);
   return bytes;
 }
@@ -701,6 +708,23 @@ TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const f
                              f0 == 0 ? beta : 1.f, ws, ws_bytes, stream, pro ? &pc : nullptr);
     if (rc) return rc;
   }
+  return 0;
+}
+
+TMR_API int tmr_conv2d_wgrad_stem_bnbwd(const tmr_conv_desc* d, const float* x, const float* y,
+                                        const float* scale, const float* shift, const float* coef,
+                                        const float* dyp, const uint8_t* argmax, int ho_p,
+                                        int wo_p, float* dw_oihw, float beta, float* ws,
+                                        size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(d && stem_geometry(d) && ngroups(d) == 1,
+                "tmr_conv2d_wgrad_stem_bnbwd: not the fp32 7x7/2 stem geometry");
+  int ns = 0;
+  const int rc = tmr_stem_wgrad_bnbwd_slabs(d->n, d->h, d->w, d->ho, x, y, scale, shift, coef,
+                                            dyp, argmax, ho_p, wo_p, ws, ws_bytes, &ns, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, 1), dim3(256), 0, stream, ws, ns,
+                     kStemSlab, dw_oihw, 49, 4, 3, beta);
+  TMR_CHECK_LAUNCH("wgrad_reduce_taps_kernel");
   return 0;
 }
 

@@ -330,6 +330,44 @@ def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma, bf16=False):
     return dy, dgamma, dbeta
 
 
+def bn_bwd_maxpool_coefs(dyp, am, y, scale, shift, mean, inv, gamma):
+    """The fp32 stem's BN backward up to its coefficients (dy = A*g + B*y + C, g the maxpool-
+    gathered ReLU-masked gradient), no dy pass: -> (coef [3][c], dgamma, dbeta) for
+    conv_wgrad_stem_bnbwd."""
+    n, h, w, c = y.shape
+    _, ho, wo, _ = dyp.shape
+    ws, nb = _bn_ws(n * h * w, c, y.device)
+    coef = _empty((3, c), y)
+    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
+    call("tmr_bn_bwd_maxpool_coefs", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma,
+         coef, dgamma, dbeta, c, ws, ctypes.c_size_t(nb), stream_ptr())
+    return coef, dgamma, dbeta
+
+
+def conv_wgrad_stem_bnbwd(x, y, scale, shift, coef, dyp, am, r, s, stride, pad, out=None,
+                          beta=0.0):
+    """Weight gradient of the fp32 7x7/2 stem with its output gradient evaluated on the fly from
+    the BN backward (stem.hip FUSED; dy never written): x NHWC4 fp32, y the stem's conv output
+    (n, 112, 112, 64), (dyp, am) the maxpool's pooled gradient and argmax -> dW (64, 3, r, s)."""
+    n, h, w, c = x.shape
+    k = y.shape[3]
+    d = conv_desc(n, h, w, c, k, r, s, stride, pad, None, math="fp32", io=0)
+    d.x_ld = _nhwc_ld(x, "x")
+    d.y_ld = _nhwc_ld(y, "y")
+    assert (d.ho, d.wo) == tuple(y.shape[1:3])
+    if out is None:
+        out = _empty((k, 3, r, s), x)
+    ws_bytes = query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d))
+    ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
+    with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * 3, (n, h, w, c, k, r, stride),
+               4 * n * h * w * c + 4 * n * d.ho * d.wo * k + 5 * dyp.numel()
+               + 4 * k * r * s * 3):
+        call("tmr_conv2d_wgrad_stem_bnbwd", ctypes.byref(d), x, y, scale, shift, coef, dyp, am,
+             int(dyp.shape[1]), int(dyp.shape[2]), out, float(beta), ws,
+             ctypes.c_size_t(ws.numel() * 4), stream_ptr())
+    return out
+
+
 def bn_bwd_coefs(parts, nparts, mean, inv, gamma, rows):
     """BN backward coefficients from conv_dgrad_bnbwd partials -> (coef [3][c], dgamma, dbeta);
     the consumers apply dy = A*g + B*y + C on load (dpro=(y, coef))."""

@@ -152,6 +152,22 @@ def _dma32(math):
 # bf16 activations: the stem input as NHWC8 bf16 (TMR_BF16_STEM8=0: the NHWC4 fp32 input on the
 # register-staged engine, A/B measurements)
 STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
+# fp32 stem backward, TMR_STEM_FUSED=1: the stem conv's weight gradient evaluates its output
+# gradient per row in LDS from the BN backward's inputs (tmr_conv2d_wgrad_stem_bnbwd), so that
+# gradient (2 GB at C2) is never written or read.  Off by default: measured slower than the two
+# passes (4.06 ms vs 1.78 + 1.34 ms at C2, profiles/r3/bench_r5q/)
+STEM_FUSED = (os.environ.get("TMR_STEM_FUSED", "0") == "1"
+              and os.environ.get("TMR_STEM_DIRECT", "1") != "0")
+
+
+def _stem_fused(rec, pool):
+    """The fp32 7x7/2 stem over NHWC4 input at the direct kernel's geometry (112 columns)."""
+    x, y, conv = rec["x"], rec["y"], rec["conv"]
+    return (STEM_FUSED and rec["math"] == "fp32" and rec.get("xpro") is None
+            and rec.get("groups", 1) == 1 and x.dtype == torch.float32 and x.shape[-1] == 4
+            and x.shape[2] <= 226 and y.dtype == torch.float32 and tuple(y.shape[2:]) == (112, 64)
+            and tuple(conv.weight.shape) == (64, 3, 7, 7) and rec["stride"] == 2
+            and rec["pad"] == 3 and pool[0].dtype == torch.float32)
 
 
 def _full16(math):
@@ -273,6 +289,19 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     dy_given = dy is not None
     if dy_given:
         dres = None
+    elif pool is not None and not need_dx and _stem_fused(rec, pool):
+        # the fp32 stem: BN-backward coefficients, then the weight gradient with dy evaluated
+        # on load (neither dz nor dy is written)
+        coef, dg, db = ops.bn_bwd_maxpool_coefs(pool[0], pool[1], rec["y"], rec["scale"],
+                                                rec["shift"], rec["mean"], rec["inv"],
+                                                bn.weight.detach())
+        grads[bn.weight] = dg
+        grads[bn.bias] = db
+        _, _, r, s = conv.weight.shape
+        grads[conv.weight] = ops.conv_wgrad_stem_bnbwd(rec["x"], rec["y"], rec["scale"],
+                                                       rec["shift"], coef, pool[0], pool[1], r, s,
+                                                       rec["stride"], rec["pad"])
+        return None, None, None
     elif pool is not None:
         # the stem: maxpool backward + ReLU mask + BN backward without writing dz
         dy, dg, db = ops.bn_bwd_maxpool(pool[0], pool[1], rec["y"], rec["scale"], rec["shift"],
