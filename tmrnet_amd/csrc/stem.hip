@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_k(const float* __restrict__ x
 
 // Weight gradient: dW[co][k] = sum over output pixels p of dy[p][co] * X[p][k] (k the 147 real
 // (tap, channel) pairs).  Persistent workgroups over output rows as in the forward (patch double
-// buffer); wave w takes pixel pairs w, w + 4, ... of a
+// buffer, the next row's patch in registers under the MFMAs); wave w takes pixel pairs w, w + 4, ... of a
 // row (14 k-steps of 2 pixels): A = dy (32 channels x 2 pixels, straight from HBM, each element
 // read once), B = the patch (2 pixels x 32 reduction rows from LDS), 2 x 5 accumulator tiles of
 // 32x32 (64 channels x 160 reduction rows).  At the end the four waves add their tiles in LDS and
@@ -214,11 +214,11 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
 
-  // the patch goes global -> registers -> LDS at the top of each row (no registers to carry it
-  // under the MFMAs: the 160 accumulators fill the budget); the two workgroups of a CU overlap
-  // one's loads with the other's MFMAs
+  // HBM form: the next row's patch is fetched into registers under this row's MFMAs.  FUSED: the
+  // patch goes global -> registers -> LDS after each row's dy phase (the gather leaves no
+  // registers to carry it); the two workgroups of a CU overlap one's loads with the other's MFMAs
+  if (!FUSED && (int)blockIdx.x < rows) fetch(blockIdx.x);
   for (int row = blockIdx.x, buf = 0; row < rows; row += gridDim.x, buf ^= 1) {
-    if (!FUSED) fetch(row);
     if (FUSED) {
       __syncthreads();   // the previous row's MFMAs are done reading Ds (and Cf is written)
       const int oh = row % ho, nn = row / ho;
@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__
         a[j][0] = dyr[8 * j * 64];
         a[j][1] = dyr[8 * j * 64 + 32];
       }
+      if (row + (int)gridDim.x < rows) fetch(row + gridDim.x);
 #pragma unroll
       for (int j = 0; j < 14; ++j) {
         float b[5];
