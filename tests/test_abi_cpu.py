@@ -93,3 +93,20 @@ def test_argument_errors_raise_with_message(built):
     # a good query after a failure is not poisoned by the old message
     assert _lib.query("tmr_bn_ws_bytes", 1024, 64) > 0
     assert _lib.query("tmr_lstm_ws_bytes", 64, 10, 2048, 512) > 0
+
+
+def test_stem_entry_points_host_checks(built):
+    """The direct stem's host-side contract (no GPU work): the wgrad workspace query covers the
+    direct kernel's 512 partial slabs at the stem geometry (with or without TMR_STEM_DIRECT), and
+    the fused stem entries refuse other geometries / null operands before any launch."""
+    import ctypes
+    from tmrnet_amd import _lib, ops
+    d = ops.conv_desc(640, 224, 224, 4, 64, 7, 7, 2, 3)
+    assert _lib.query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d)) >= 512 * 64 * 49 * 4 * 4
+    d3 = ops.conv_desc(8, 56, 56, 64, 64, 3, 3, 1, 1)
+    with pytest.raises(RuntimeError, match="not the fp32 7x7/2 stem geometry"):
+        _lib.call("tmr_conv2d_wgrad_stem_bnbwd", ctypes.byref(d3), *([None] * 7), 28, 28, None,
+                  0.0, None, 0, None)
+    with pytest.raises(RuntimeError, match="null coef"):
+        _lib.call("tmr_bn_bwd_maxpool_coefs", None, None, 2, 112, 112, 56, 56, *([None] * 6), None,
+                  None, None, 64, None, 0, None)
