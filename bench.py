@@ -141,6 +141,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    ranks_seen = check_ranks(dist, world, dev)
 
     import tmrnet_amd
     from tmrnet_amd import ops, LFBRows
@@ -208,6 +209,10 @@ def main():
     # the committed PMC passes profile the default geometry (64 clips x 10 frames, L=40)
     traffic = (load_traffic(args.model, args.precision, args.seq, args.lfb)
                if args.clips == 64 else None)
+    stale = bool(traffic and traffic.get("stale"))
+    if stale:
+        traffic_src = traffic
+        traffic = None
     if not args.no_roofline:
         ops.PROF = []
         torch.cuda.synchronize()
@@ -239,7 +244,10 @@ def main():
                 "frac": round(achieved / peak, 4),
                 # HBM bytes per conv call (PMC, per step / calls per step), same unit as achieved
                 "traffic": int(traffic["hbm_bytes_per_step"] / len(recs)) if traffic else None,
-                "traffic_source": traffic.get("source") if traffic else None,
+                "traffic_source": (traffic or (traffic_src if stale else {})).get("source"),
+                # the committed PMC record was collected on a different build of libtmr.so
+                "traffic_stale": stale,
+                "build_sha": lib_sha(),
                 # SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) over the conv
                 # launches of the same committed PMC record
                 "mfma_busy_frac": traffic.get("mfma_busy_frac") if traffic else None,
@@ -267,6 +275,7 @@ def main():
     hbm = {"model_bytes_per_frame": act_bytes,
            "model_frac": round(fps / world * act_bytes / (HBM_PEAK_GBS * 1e9), 4),
            "pmc_bytes_per_step": traffic["all_kernels_bytes_per_step"] if traffic else None,
+           "pmc_stale": stale,
            "pmc_frac": (round(traffic["all_kernels_bytes_per_step"] / (ms * 1e-3)
                               / (HBM_PEAK_GBS * 1e9), 4) if traffic else None),
            "peak_gbs": HBM_PEAK_GBS}
@@ -297,6 +306,7 @@ def main():
                                  "resnet_lstm (train_non-local_mutiConv_resnest)"),
                        "global_batch": B * world, "clips_per_gpu": B, "seq_len": T, "lfb_len": L,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world,
+                       "ranks_seen": ranks_seen,
                        "input_transform": ("reference train transform (use_flip=1) on device"
                                            if aug is not None else "crop+normalize")},
             "loss_last": loss_v,
@@ -315,6 +325,29 @@ def workload_name(args):
         return ("C5-style: TMRNet ResNet50+LSTM+NLBlock train step, seq %d, LFB %d, %s convs"
                 % (args.seq, args.lfb, args.precision))
     return "C2/C3: TMRNet ResNet50+LSTM+NLBlock train step"
+
+
+def check_ranks(dist, world, dev):
+    """What the communicator actually saw (train_only_non-local_pretrained.py:628 replaces
+    DataParallel): world size, backend and one all-reduce SUM of ones, which must equal N.
+    A bench line is never printed for fewer ranks than --gpus."""
+    if dist is None:
+        return {"world_size": 1, "backend": None, "allreduce_ones": 1}
+    backend = dist.get_backend()
+    t = torch.ones(1, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t)
+    seen = {"world_size": dist.get_world_size(), "backend": backend,
+            "allreduce_ones": int(round(t.item()))}
+    if seen["world_size"] != world or seen["allreduce_ones"] != world:
+        raise SystemExit("bench: communicator saw %s, expected %d ranks" % (seen, world))
+    return seen
+
+
+def lib_sha():
+    """Build stamp of the library this run loaded (scripts/pmc_summary.lib_sha)."""
+    import hashlib
+    with open(os.path.join(ROOT, "tmrnet_amd", "libtmr.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def load_traffic(model, precision, seq, lfb):
@@ -346,6 +379,10 @@ def load_traffic(model, precision, seq, lfb):
                                     "stem_wgrad_k"))]
     if not conv:
         return None
+    if d.get("build_sha") != lib_sha():
+        # collected on another build: the bytes and MFMA-busy cycles describe other kernels
+        return {"stale": True, "source": os.path.relpath(files[-1], ROOT),
+                "record_build_sha": d.get("build_sha")}
     per_step = sum(fams[k]["hbm_bytes_per_step"] for k in conv)
     busy = sum(fams[k].get("mfma_busy_cycles", 0.0) for k in conv)
     gui = sum(fams[k].get("gui_active_cycles", 0.0) for k in conv)

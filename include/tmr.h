@@ -521,7 +521,9 @@ int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr, float m
 /* Multi-tensor SGD: every (param, grad, momentum buffer) of every param group in ONE launch
  * (optimizer.step() of :725 over the groups of :646-655).  table: DEVICE array of ntensors
  * entries; entry t covers workgroups [block_begin_t, block_begin_{t+1}), i.e. block_begin is the
- * prefix sum of ceil(n / tmr_sgd_chunk()) and nblocks the total. */
+ * prefix sum of ceil(n / tmr_sgd_chunk()) and nblocks the total.  status: the device health
+ * word (tmrnet_amd/health.py) or NULL; when it is non-zero at launch time (a device-side failure
+ * earlier in this step, e.g. a persistent LSTM that gave up a grid barrier) no weight changes. */
 typedef struct tmr_sgd_tensor {
   float* p;
   const float* g;
@@ -533,11 +535,11 @@ typedef struct tmr_sgd_tensor {
 } tmr_sgd_tensor;
 int64_t tmr_sgd_chunk(void);
 int tmr_sgd_step_multi(const tmr_sgd_tensor* table, int ntensors, int64_t nblocks,
-                       hipStream_t stream);
+                       const int32_t* status, hipStream_t stream);
 /* Multi-tensor torch.optim.Adam step (the -o 1 optimizer, train_only_non-local_pretrained.py:644-645,
  * code/models.py:63-68; amsgrad off): same table scheme as tmr_sgd_step_multi (chunks of
  * tmr_sgd_chunk()), per tensor the moments m / v and the host-computed step_size = lr / (1 -
- * beta1^step), bc2_sqrt = sqrt(1 - beta2^step). */
+ * beta1^step), bc2_sqrt = sqrt(1 - beta2^step); status as for tmr_sgd_step_multi. */
 typedef struct tmr_adam_tensor {
   float* p;
   const float* g;
@@ -549,7 +551,7 @@ typedef struct tmr_adam_tensor {
   int32_t maximize, reserved;
 } tmr_adam_tensor;
 int tmr_adam_step_multi(const tmr_adam_tensor* table, int ntensors, int64_t nblocks,
-                        hipStream_t stream);
+                        const int32_t* status, hipStream_t stream);
 /* LFB row table of get_long_feature (train_only_non-local_pretrained.py:293-311):
  * rows[b][k] = index of the first valid start >= max(start_b - k - 1, 0) in the sorted
  * valid-start list (== the reference's dict walk, incl. own-row fallback and

@@ -42,11 +42,22 @@ def read_pass(d, counter, optional=False, sub=None):
     return per, {k: len(v) for k, v in launches.items()}
 
 
+def lib_sha(path):
+    """First 16 hex digits of the sha256 of the built library (the build stamp)."""
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--steps", type=int, default=2, help="train steps covered by the passes")
+    ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "tmrnet_amd", "libtmr.so"),
+        help="the library the passes ran (its sha256 stamps the record; bench.py load_traffic "
+             "drops a record whose stamp differs from the library it runs)")
     args = ap.parse_args()
     fetch, nf = read_pass(args.dir, "FETCH_SIZE")
     write, nw = read_pass(args.dir, "WRITE_SIZE")
@@ -66,7 +77,7 @@ def main():
             d["mfma_busy_frac"] = round(busy[fam] / (gui[fam] / 8.0 * 1024.0), 4)
             d["mfma_busy_cycles"] = busy[fam]
             d["gui_active_cycles"] = gui[fam]
-    out = {"model": args.model, "steps": args.steps,
+    out = {"model": args.model, "steps": args.steps, "build_sha": lib_sha(args.lib),
            "what": "bench.py --steps 1 --warmup 1 (2 train steps + setup), rocprofv3 --pmc "
                    "FETCH_SIZE / WRITE_SIZE in separate passes, kernel-trace only",
            "correction": "read = 2 x FETCH_SIZE(KiB) x 1024 (gfx950 wide-read halving); "

@@ -3,6 +3,8 @@
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/${PROF_NAME:-prof}
 mkdir -p "$OUT"
+# build stamp: the sha256 of the library these kernel stats come from (bench.py build_sha)
+python3 -c "import sys; sys.path.insert(0, '$R/scripts'); import pmc_summary as p; print(p.lib_sha('$R/tmrnet_amd/libtmr.so'))" > "$OUT/build_sha.txt"
 cd /tmp && export TMPDIR=/tmp
 export TMR_EXIT_MAPS="$OUT/exit_maps.txt"
 # the LSTM's per-step path under the profiler (see scripts/pmc.sh: the cooperative launch makes the

@@ -1,6 +1,9 @@
 # one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
 set -o pipefail
-O=gpurun_out/r5u; mkdir -p $O
-PROF_NAME=r5u/rocprof_c5 STEPS=3 BENCH_ARGS="--precision bf16 --seq 30 --lfb 300" bash scripts/profile.sh > $O/prof_c5.txt 2>&1 && \
-PROF_NAME=r5u/rocprof_c4 STEPS=8 BENCH_ARGS="--model resnest50 --precision bf16" bash scripts/profile.sh > $O/prof_c4.txt 2>&1
-echo "main rc=$?"
+O=gpurun_out/r4c; mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread \
+  tests/test_modules_gpu.py tests/test_compat_gpu.py tests/test_ddp_gpu.py tests/test_bf16_vs_fp32_gpu.py > $O/pytest.txt 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -8 $O/pytest.txt
+mv gpurun_out/bf16_vs_fp32_*.json $O/
+exit $rc

@@ -39,6 +39,8 @@ def test_bench_two_ranks_one_gpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4
     assert d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    # what the communicator saw: two ranks, an all-reduce of ones = 2 (bench.check_ranks)
+    assert d["config"]["ranks_seen"] == {"world_size": 2, "backend": "gloo", "allreduce_ones": 2}
     assert d["loss_last"] == d["loss_last"]       # finite
 
 

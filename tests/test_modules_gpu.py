@@ -93,26 +93,45 @@ def test_lstm_giveup_is_loud(dev, monkeypatch):
     import tmrnet_amd
     from tmrnet_amd import health
     health.reset()
+    try:
+        _giveup_steps(dev, monkeypatch)
+    finally:
+        health.reset()      # never leave a set health word to the tests that follow
+
+
+def _giveup_steps(dev, monkeypatch):
+    import tmrnet_amd
+    from tmrnet_amd import health
     monkeypatch.setenv("TMR_LSTM_PERSIST", "1")
     monkeypatch.setenv("TMR_LSTM_SPIN_LIMIT", "1")
     torch.manual_seed(5)
     m = tmrnet_amd.LSTM(2048, 512).to(dev)
     opt = tmrnet_amd.SGD(m.parameters(), lr=1e-3, momentum=0.9)
     x = torch.randn(64, 10, 2048, device=dev)
+    w0 = [p.detach().clone() for p in m.parameters()]
     y, _ = m(x)
     y.sum().backward()
     opt.step()                      # schedules the status copy of this step
     torch.cuda.synchronize()
+    # the failed step's update was skipped on the device (the kernel reads the health word)
+    assert all(torch.equal(p, q) for p, q in zip(m.parameters(), w0))
     with pytest.raises(RuntimeError, match="gave up a grid barrier"):
         opt.step()                  # ... and raises on it one step later, without a sync
     with pytest.raises(RuntimeError, match="gave up a grid barrier"):
         health.check(sync=True)
+    health.reset()
+    # inference (no grad): the forward itself waits for the launch and raises at once
+    with torch.no_grad(), pytest.raises(RuntimeError, match="gave up a grid barrier"):
+        m(x)
     health.reset()
     monkeypatch.delenv("TMR_LSTM_SPIN_LIMIT")
     y, _ = m(x)                     # default limit: no give-up, nothing raised
     y.sum().backward()
     opt.step()
     health.check(sync=True)
+    assert not all(torch.equal(p, q) for p, q in zip(m.parameters(), w0))
+    with torch.no_grad():
+        m(x)
 
 
 @pytest.mark.parametrize("B,L,rows", [(64, 300, True), (3, 40, False), (2, 1, False),

@@ -87,7 +87,7 @@ SIGNATURES = {
     "tmr_avgpool_fwd_a16": [P, P, I, I, I, P],
     "tmr_cast_f32_bf16": [P, P, ctypes.c_long, P],
     "tmr_nhwc4_to_bf16x8": [P, P, ctypes.c_long, P],
-    "tmr_adam_step_multi": [P, I, ctypes.c_int64, P],
+    "tmr_adam_step_multi": [P, I, ctypes.c_int64, P, P],
     "tmr_resize_ksize": [I, I],
     "tmr_resize_coeffs": [I, I, P, P, I],
     "tmr_resize_tmp_bytes": [I, I, I, I, I],
@@ -141,7 +141,7 @@ SIGNATURES = {
     "tmr_softmax_max": [P, I, I, P, P, P, P],
     "tmr_ce_sum": [P, P, P, I, I, F, P, P, P, P],
     "tmr_sgd_chunk": [],
-    "tmr_sgd_step_multi": [P, I, ctypes.c_int64, P],
+    "tmr_sgd_step_multi": [P, I, ctypes.c_int64, P, P],
     "tmr_sgd_step": [P, P, P, L, F, F, F, F, I, I, P],
     "tmr_lfb_index": [P, I, P, I, I, P, P],
     "tmr_lfb_gather": [P, P, P, L, I, P],

@@ -375,7 +375,11 @@ TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
   const size_t need = (size_t)np * d->k * sizeof(float4);
   TMR_CHECK_ARG(stats && stats_bytes >= need, "tmr_conv2d_fwd_bnstats: stats buffer too small (%zu < %zu)",
                 stats_bytes, need);
-  if (!pro && stem_direct(d))
+  // the parts query (above) sized `stats` for the direct stem's row layout: an operand prologue
+  // would route the stem to the engine, which writes a different number of partial rows
+  TMR_CHECK_ARG(!(pro && stem_direct(d)),
+                "tmr_conv2d_fwd_bnstats: the 7x7 stem takes no operand prologue");
+  if (stem_direct(d))
     return tmr_stem_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, y, stats, stream);
   if (ngroups(d) == 1) return fwd_bnstats_impl(d, x, w_krsc, y, (float4*)stats, d->k, pro, stream);
   TMR_CHECK_ARG(!pro, "tmr_conv2d_fwd_bnstats: operand prologues take no groups");

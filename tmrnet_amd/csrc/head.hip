@@ -296,7 +296,10 @@ __global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, float*
 // SGD_CHUNK elements of the tensor whose [block_begin, next block_begin) range holds b (binary
 // search over the small table, read through the scalar cache).
 constexpr int SGD_CHUNK = 8192;
-__global__ __launch_bounds__(256) void sgd_multi_k(const tmr_sgd_tensor* __restrict__ tab, int nt) {
+__global__ __launch_bounds__(256) void sgd_multi_k(const tmr_sgd_tensor* __restrict__ tab, int nt,
+                                                   const int32_t* __restrict__ status) {
+  // a device-side failure of this step (health word) leaves the weights untouched
+  if (status && *status) return;
   const long b = blockIdx.x;
   int lo = 0, hi = nt - 1;
   while (lo < hi) {
@@ -323,7 +326,9 @@ __global__ __launch_bounds__(256) void sgd_multi_k(const tmr_sgd_tensor* __restr
 // Per element the arithmetic of torch's _multi_tensor_adam: lerp of m toward the gradient
 // (weight 1 - beta1 < 0.5 branch), v = v * beta2 + (1 - beta2) * d * d, denom = sqrt(v) /
 // sqrt(bc2) + eps, p -= step_size * m / denom (step_size = lr / bc1 from the host, in double).
-__global__ __launch_bounds__(256) void adam_multi_k(const tmr_adam_tensor* __restrict__ tab, int nt) {
+__global__ __launch_bounds__(256) void adam_multi_k(const tmr_adam_tensor* __restrict__ tab, int nt,
+                                                    const int32_t* __restrict__ status) {
+  if (status && *status) return;
   const long b = blockIdx.x;
   int lo = 0, hi = nt - 1;
   while (lo < hi) {
@@ -472,21 +477,23 @@ TMR_API int tmr_sgd_step(float* p, const float* g, float* buf, long n, float lr,
 TMR_API int64_t tmr_sgd_chunk(void) { return SGD_CHUNK; }
 
 TMR_API int tmr_adam_step_multi(const tmr_adam_tensor* table, int ntensors, int64_t nblocks,
-                                hipStream_t stream) {
+                                const int32_t* status, hipStream_t stream) {
   if (ntensors == 0 || nblocks == 0) return 0;
   TMR_CHECK_ARG(table && ntensors > 0 && nblocks > 0 && nblocks < (1L << 31),
                 "tmr_adam_step_multi: bad table (%d tensors, %ld blocks)", ntensors, (long)nblocks);
-  hipLaunchKernelGGL(adam_multi_k, dim3((unsigned)nblocks), dim3(256), 0, stream, table, ntensors);
+  hipLaunchKernelGGL(adam_multi_k, dim3((unsigned)nblocks), dim3(256), 0, stream, table, ntensors,
+                     status);
   TMR_CHECK_LAUNCH("adam_step_multi");
   return 0;
 }
 
 TMR_API int tmr_sgd_step_multi(const tmr_sgd_tensor* table, int ntensors, int64_t nblocks,
-                               hipStream_t stream) {
+                               const int32_t* status, hipStream_t stream) {
   if (ntensors == 0 || nblocks == 0) return 0;
   TMR_CHECK_ARG(table && ntensors > 0 && nblocks > 0 && nblocks < (1L << 31),
                 "tmr_sgd_step_multi: bad table (%d tensors, %ld blocks)", ntensors, (long)nblocks);
-  hipLaunchKernelGGL(sgd_multi_k, dim3((unsigned)nblocks), dim3(256), 0, stream, table, ntensors);
+  hipLaunchKernelGGL(sgd_multi_k, dim3((unsigned)nblocks), dim3(256), 0, stream, table, ntensors,
+                     status);
   TMR_CHECK_LAUNCH("sgd_step_multi");
   return 0;
 }

@@ -146,6 +146,18 @@ class DecodeJob:
         assert n == self.shape[0] - 1
         return self.pool._view(self.slot, self.shape)
 
+    def to(self, device):
+        """result() copied to `device` asynchronously (the slot is pinned memory).  The copy's
+        completion event is kept by the pool: the slot is not handed to the workers again, nor
+        unregistered, before that copy has run."""
+        host = self.result()
+        out = host.to(device, non_blocking=True)
+        if out.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(out.device))
+            self.pool._pending[self.slot] = ev
+        return out
+
 
 class DecodePool:
     """pil_loader (:96-99) in `workers` processes (the reference's DataLoader workers, :682-688)
@@ -160,7 +172,15 @@ class DecodePool:
         self.workers, self.slots, self.chunk = max(1, workers), max(1, slots), max(1, chunk)
         self._pool = mp.get_context("spawn").Pool(self.workers)
         self._seg = [None] * self.slots   # (SharedMemory, nbytes, tensor view or None)
+        self._pending = [None] * self.slots   # event after the last async copy out of the slot
         self._next = 0
+
+    def _drain(self, slot):
+        """Wait for the last asynchronous copy out of `slot` (DecodeJob.to) to finish."""
+        ev = self._pending[slot]
+        if ev is not None:
+            ev.synchronize()
+            self._pending[slot] = None
 
     def _segment(self, slot, nbytes):
         cur = self._seg[slot]
@@ -182,6 +202,7 @@ class DecodePool:
         cur = self._seg[slot]
         if cur is None:
             return
+        self._drain(slot)       # no DMA may still read the mapping we unregister
         shm, _, registered = cur
         self._seg[slot] = None
         if registered:
@@ -206,6 +227,7 @@ class DecodePool:
         nbytes = int(np.prod(shape))
         slot = self._next
         self._next = (self._next + 1) % self.slots
+        self._drain(slot)       # the workers overwrite the slot: its last copy must have run
         shm = self._segment(slot, nbytes)
         np.ndarray(shape, dtype=np.uint8, buffer=shm.buf[:nbytes])[0] = first
         asyncs = [self._pool.apply_async(_w_decode, (shm.name, nbytes, shape, i,
@@ -245,8 +267,12 @@ def _buf_addr(shm):
 def load_frames(paths, device="cuda", size=RESIZE, workers=8, pool=None):
     """Files -> decoded (host, PIL; threads, or the processes of `pool`, a DecodePool) -> HBM ->
     resized on the device: (F, 250, 250, 3) uint8."""
-    host = pool.decode(paths) if pool is not None else decode_frames(paths, workers=workers)
-    dev = host.to(device, non_blocking=True)
-    if tuple(host.shape[1:3]) == tuple(size):
+    if pool is not None:
+        job = pool.submit(paths)
+        dev = job.to(device)          # the pool tracks this copy before reusing the slot
+    else:
+        host = decode_frames(paths, workers=workers)
+        dev = host.to(device, non_blocking=True)
+    if tuple(dev.shape[1:3]) == tuple(size):
         return dev
     return resize_frames(dev, size)

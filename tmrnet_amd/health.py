@@ -2,6 +2,9 @@
 (today: a persistent LSTM launch that gave up a grid barrier, include/tmr.h tmr_lstm_status_or)
 are OR-ed into one int32 per device, stream-ordered and without a host sync.
 
+The fused optimizer kernels (optim.SGD / Adam, tmr_sgd_step_multi / tmr_adam_step_multi) read
+the word on the device and skip the update when it is non-zero, so a failed step never changes
+the weights.  An inference forward (lstm.LSTM under no_grad) waits and checks at once.
 `check()` is called once per optimizer step (optim.SGD / Adam .step()).  It never stalls the
 stream: it starts an asynchronous copy of the word into pinned host memory and raises on the value
 of the PREVIOUS step's copy once that copy has landed (so a failure surfaces at most one step

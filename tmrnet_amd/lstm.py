@@ -17,7 +17,7 @@ import math
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import health, ops
 
 
 class LSTMFn(torch.autograd.Function):
@@ -81,4 +81,8 @@ class LSTM(nn.Module):
             raise NotImplementedError("initial state hx is not supported (reference passes none)")
         y, hn, cn = LSTMFn.apply(x, self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0,
                                  self.bias_hh_l0)
+        if not torch.is_grad_enabled():
+            # inference (eval loops run under no_grad): no optimizer step will read the health
+            # word, so wait for the recurrence and raise now rather than return invalid outputs
+            health.check(sync=True, device=x.device)
         return y, (hn, cn)

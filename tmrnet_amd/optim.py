@@ -86,7 +86,9 @@ class SGD(torch.optim.Optimizer):
             self._table_key = key
             self.table_uploads += 1
         self._keep = keep        # contiguous grad copies stay alive until the next step
-        call("tmr_sgd_step_multi", self._table_dev, len(entries), int(nblk.sum()), stream_ptr(dev))
+        # the kernel reads the device health word and skips the update when this step failed
+        call("tmr_sgd_step_multi", self._table_dev, len(entries), int(nblk.sum()),
+             health.status_word(dev), stream_ptr(dev))
         return loss
 
 
@@ -158,7 +160,8 @@ class Adam(torch.optim.Optimizer):
         host = torch.frombuffer(bytearray(tab.tobytes()), dtype=torch.uint8).pin_memory()
         self._table_dev = host.to(dev, non_blocking=True)
         self._keep = keep
-        call("tmr_adam_step_multi", self._table_dev, len(entries), int(nblk.sum()), stream_ptr(dev))
+        call("tmr_adam_step_multi", self._table_dev, len(entries), int(nblk.sum()),
+             health.status_word(dev), stream_ptr(dev))
         return loss
 
 
