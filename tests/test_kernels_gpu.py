@@ -554,13 +554,14 @@ def test_stem_bwd_maxpool_fused(dev):
     assert rel_err(dg, dg_ref) < 1e-5 and rel_err(db, db_ref) < 1e-5
 
 
-def test_bn_fold_bit_identical(dev):
+@pytest.mark.parametrize("engine", ["lds_dma", "register_staged"])
+def test_bn_fold_bit_identical(dev, engine):
     """Train step with the BatchNorm folded into the conv loaders (tmr_conv_prologue: BN+ReLU of
     units 1-2 on the X operand, the BN backward on every dY operand) against the explicit passes
     (tmr_bn_apply / tmr_bn_bwd_parts / tmr_bn_bwd): same operand values by construction, same
     GEMM arithmetic -> logits, every gradient and the running statistics bit-identical.  Both
-    on the register-staged engine (the LDS-DMA engine has no prologues; TMR_GEMM32=0 keeps the
-    explicit side's fp32 convs off it too, read per launch)."""
+    sides on the fp32 LDS-DMA engine (prologues applied in LDS, gemm16_kernel PRO), or both on
+    the register-staged engine (TMR_GEMM32=0, read per launch)."""
     import os
     import tmrnet_amd
     from tmrnet_amd import trunk
@@ -573,8 +574,9 @@ def test_bn_fold_bit_identical(dev):
     res = {}
     saved = trunk.FOLD_BN
     saved_dma, saved_env = trunk.DMA32, os.environ.get("TMR_GEMM32")
-    trunk.DMA32 = False
-    os.environ["TMR_GEMM32"] = "0"
+    if engine == "register_staged":
+        trunk.DMA32 = False
+        os.environ["TMR_GEMM32"] = "0"
     try:
         for fold in (True, False):
             trunk.FOLD_BN = fold

@@ -430,7 +430,17 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // WGRAD (reduction-major images [32 k-rows][R floats]): fragment element t of k-step s is
 // k = 8s + 2t + hh, one ds_read_b32 each; odd k-rows have their chunks XOR 8 (columns ^ 32), so
 // the two lane halves (rows k, k + 1) read disjoint bank halves.
-template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0>
+//
+// PRO (fp32 form only; GemmArgs::pro): operand prologues -- the BatchNorm that produced an
+// operand applied in LDS, so its output is never written to HBM.  Bit 1, the X operand (FWD A,
+// WGRAD B): x' = relu(fmaf(x, scale[c], shift[c])) (bn_apply_k's arithmetic), 0 where the
+// gather is out of range (the zero padding belongs to the post-ReLU tensor).  Bit 2, the dY
+// operand (DGRAD A, WGRAD A): dy' = fmaf(A[c], g, fmaf(B[c], y, C[c])) (bn_bwd_apply's), with y
+// brought into an LDS scratch image by a second LDS-DMA at g's offsets, 0 out of range.  Each
+// lane transforms the 16-B pieces it issued, after its own LDS-DMA has landed (vmcnt) and
+// before the barrier that publishes the k-tile, so no extra barrier; the coefficient tables
+// are staged in LDS once per workgroup.
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && BM * BN <= 128 * 128) ? 4 : 2))
 void gemm16_kernel(const GemmArgs a) {
   constexpr uint32_t ES = F32 ? 4u : 2u;   // element bytes
@@ -450,7 +460,18 @@ void gemm16_kernel(const GemmArgs a) {
   using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
   constexpr int EPI = WM * BN * 2 * 4;
   constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+  static_assert(PRO == 0 || F32, "operand prologues: fp32 form only");
+  static_assert(!(PRO & 1) || MODE != MODE_DGRAD, "X prologue: FWD / WGRAD views");
+  static_assert(!(PRO & 2) || MODE != MODE_FWD, "dY prologue: DGRAD / WGRAD views");
+  // prologue regions after the stages / epilogue buffer: dY's y image (one stage: each lane reads
+  // back only the pieces it issued), dY coefficients A|B|C, X scale|shift
+  constexpr int YIMG = (PRO & 2) ? ABYTES : 0;
+  constexpr int DCOEF = (PRO & 2) ? 3 * PRO_DMAX * 4 : 0;
+  constexpr int XCOEF = (PRO & 1) ? 2 * PRO_XMAX * 4 : 0;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM + YIMG + DCOEF + XCOEF];
+  unsigned char* const ysm = smem + SMEM;
+  float* const dcoef = reinterpret_cast<float*>(smem + SMEM + YIMG);
+  float* const xcoef = reinterpret_cast<float*>(smem + SMEM + YIMG + DCOEF);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -552,6 +573,12 @@ void gemm16_kernel(const GemmArgs a) {
     }
   }
 
+  // prologue pieces of the k-tile in flight: in range, first channel of the 4 (A: X or dY,
+  // B: WGRAD's X); set by stage(), consumed by transform() of the same tile
+  bool pokA[PRO ? NIA : 1], pokB[PRO ? NIB : 1];
+  int pcA[PRO ? NIA : 1];
+  const __amdgpu_buffer_rsrc_t rY = make_rsrc((PRO & 2) ? a.pd_y : a.A, a.Abytes);
+
   // ---------------- stage one k-tile into LDS buffer `buf` ----------------
   auto stage = [&](int kt, int buf) {
     const int kb = kbeg + kt * BK;
@@ -585,6 +612,11 @@ void gemm16_kernel(const GemmArgs a) {
                         (unsigned)xs < (unsigned)a.Ws;
         const uint32_t off = apix[q] + (uint32_t)((dy * a.Ws + dx) * a.lds + c) * ES;
         glds16(rA, As + 1024 * (wave + NW * q), ok ? off : OOB);
+        if constexpr (PRO != 0) {
+          pokA[q] = ok;
+          pcA[q] = c;
+          if constexpr ((PRO & 2) != 0) glds16(rY, ysm + 1024 * (wave + NW * q), ok ? off : OOB);
+        }
       }
       if constexpr (MODE == MODE_FWD) {
         // B[j][k] = W[co][tap][c]: k-contiguous rows of the KRSC weights
@@ -628,7 +660,13 @@ void gemm16_kernel(const GemmArgs a) {
       for (int q = 0; q < NIA; ++q) {
         const int m = kb + akr[q];
         const bool ok = acok[q] && m < kend;
-        glds16(rA, As + 1024 * (wave + NW * q), ok ? (uint32_t)m * (uint32_t)a.ldb * ES + aco[q] : OOB);
+        const uint32_t off = (uint32_t)m * (uint32_t)a.ldb * ES + aco[q];
+        glds16(rA, As + 1024 * (wave + NW * q), ok ? off : OOB);
+        if constexpr ((PRO & 2) != 0) {
+          pokA[q] = ok;
+          pcA[q] = (int)(aco[q] / ES);
+          glds16(rY, ysm + 1024 * (wave + NW * q), ok ? off : OOB);
+        }
       }
       // WGRAD B[k=m][j=(tap,c)] = X[src(m, tap)][c]
 #pragma unroll
@@ -644,6 +682,57 @@ void gemm16_kernel(const GemmArgs a) {
                         (unsigned)xs < (unsigned)a.Ws;
         const uint32_t off = (uint32_t)(((int)n * a.Hs + ys) * a.Ws + xs) * (uint32_t)a.lds * ES + bco[q];
         glds16(rB, Bs + 1024 * (wave + NW * q), ok ? off : OOB);
+        if constexpr ((PRO & 1) != 0) pokB[q] = ok;
+      }
+    }
+  };
+
+  // ---------------- operand prologues on this lane's landed pieces of buffer `buf` ----------------
+  auto transform = [&](int buf) {
+    unsigned char* As = smem + buf * STAGE;
+    unsigned char* Bs = As + ABYTES;
+    if constexpr ((PRO & 2) != 0) {   // dY = A operand (DGRAD, WGRAD)
+#pragma unroll
+      for (int q = 0; q < NIA; ++q) {
+        float4* p = reinterpret_cast<float4*>(As + 1024 * (wave + NW * q) + 16 * lane);
+        const float4 g = *p;
+        const float4 yv = *reinterpret_cast<const float4*>(ysm + 1024 * (wave + NW * q) + 16 * lane);
+        const int c = pcA[q];
+        const float4 A4 = *reinterpret_cast<const float4*>(dcoef + c);
+        const float4 B4 = *reinterpret_cast<const float4*>(dcoef + PRO_DMAX + c);
+        const float4 C4 = *reinterpret_cast<const float4*>(dcoef + 2 * PRO_DMAX + c);
+        float4 o;
+        o.x = fmaf(A4.x, g.x, fmaf(B4.x, yv.x, C4.x));
+        o.y = fmaf(A4.y, g.y, fmaf(B4.y, yv.y, C4.y));
+        o.z = fmaf(A4.z, g.z, fmaf(B4.z, yv.z, C4.z));
+        o.w = fmaf(A4.w, g.w, fmaf(B4.w, yv.w, C4.w));
+        *p = pokA[q] ? o : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if constexpr ((PRO & 1) != 0) {   // X = A operand (FWD) or B operand (WGRAD)
+      constexpr int NX = MODE == MODE_FWD ? NIA : NIB;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        unsigned char* img = MODE == MODE_FWD ? As : Bs;
+        float4* p = reinterpret_cast<float4*>(img + 1024 * (wave + NW * q) + 16 * lane);
+        const float4 v = *p;
+        int c;
+        bool ok;
+        if constexpr (MODE == MODE_FWD) {
+          c = pcA[q];
+          ok = pokA[q];
+        } else {
+          c = (int)(bco[q] / ES);
+          ok = pokB[q];
+        }
+        const float4 sc = *reinterpret_cast<const float4*>(xcoef + c);
+        const float4 sh = *reinterpret_cast<const float4*>(xcoef + PRO_XMAX + c);
+        float4 o;
+        o.x = fmaxf(fmaf(v.x, sc.x, sh.x), 0.f);
+        o.y = fmaxf(fmaf(v.y, sc.y, sh.y), 0.f);
+        o.z = fmaxf(fmaf(v.z, sc.z, sh.z), 0.f);
+        o.w = fmaxf(fmaf(v.w, sc.w, sh.w), 0.f);
+        *p = ok ? o : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   };
@@ -758,6 +847,25 @@ void gemm16_kernel(const GemmArgs a) {
     }
   };
 
+  if constexpr (PRO != 0) {
+    // coefficient tables -> LDS (published by the barrier below, before any transform)
+    if constexpr ((PRO & 2) != 0) {
+      const int cd = MODE == MODE_WGRAD ? a.ldb : a.lds;
+      for (int i = tid; i < cd; i += 64 * NW) {
+        dcoef[i] = a.pd_a[i];
+        dcoef[PRO_DMAX + i] = a.pd_b[i];
+        dcoef[2 * PRO_DMAX + i] = a.pd_c[i];
+      }
+    }
+    if constexpr ((PRO & 1) != 0) {
+      for (int i = tid; i < a.lds; i += 64 * NW) {
+        xcoef[i] = a.px_scale[i];
+        xcoef[PRO_XMAX + i] = a.px_shift[i];
+      }
+    }
+    __syncthreads();
+  }
+
   // ---------------- main loop: two LDS stages ----------------
   // Iteration kt: wait for this wave's pieces of tile kt, barrier (every wave's pieces landed;
   // every wave finished reading the other buffer in iteration kt-1), issue tile kt+1 into the
@@ -766,6 +874,7 @@ void gemm16_kernel(const GemmArgs a) {
     stage(0, 0);
     for (int kt = 0; kt < ntiles; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (PRO != 0) transform(kt & 1);
       __syncthreads();
       if (kt + 1 < ntiles) stage(kt + 1, (kt + 1) & 1);
       compute(kt & 1);
@@ -777,6 +886,7 @@ void gemm16_kernel(const GemmArgs a) {
     stage(0, 0);
     for (int kt = 0; kt < ntiles; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (PRO != 0) transform(kt & 1);
       __syncthreads();
       const int buf = kt & 1;
       Frag a0[TM], b0[TN], a1[TM], b1[TN];
@@ -807,15 +917,37 @@ void gemm16_kernel(const GemmArgs a) {
                                                  split);
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int F32>
+template <int MODE, int BM, int BN, int WM, int WN, int F32, int PRO = 0>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
-  if (tapv)
+  if constexpr (PRO != 0) {   // one tap per k-tile (pro32_ok)
+    hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, PRO>), grid, blk, 0, st, a);
+  } else if (tapv) {
     hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, F32>), grid, blk, 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32>), grid, blk, 0, st, a);
+  }
   TMR_CHECK_LAUNCH(F32 ? "gemm16_kernel (fp32)" : "gemm16_kernel");
   return 0;
+}
+
+template <int MODE, int F32, int PRO>
+int launch16_switch(const GemmArgs& a, int cfg, bool tapv, dim3 grid, hipStream_t st) {
+  switch (cfg) {
+    case 1: return launch16_cfg<MODE, 256, 128, 4, 2, F32, PRO>(a, tapv, grid, st);
+    case 2: return launch16_cfg<MODE, 128, 128, 2, 2, F32, PRO>(a, tapv, grid, st);
+    case 3: return launch16_cfg<MODE, 256, 64, 4, 1, F32, PRO>(a, tapv, grid, st);
+    case 4: return launch16_cfg<MODE, 64, 256, 1, 4, F32, PRO>(a, tapv, grid, st);
+    case 7: return launch16_cfg<MODE, 128, 128, 4, 2, F32, PRO>(a, tapv, grid, st);
+    case 5: return launch16_cfg<MODE, 64, 64, 2, 2, F32, PRO>(a, tapv, grid, st);
+    default: break;
+  }
+  if constexpr ((PRO & 2) == 0) {   // 256x256: no room for the dY prologue's LDS (pick_cfg16)
+    if (cfg == 0) return launch16_cfg<MODE, 256, 256, 2, 4, F32, PRO>(a, tapv, grid, st);
+    if (cfg == 6) return launch16_cfg<MODE, 256, 256, 4, 4, F32, PRO>(a, tapv, grid, st);
+  }
+  TMR_CHECK_ARG(false, "gemm16: no tile config %d for prologue %d", cfg, PRO);
+  return 1;
 }
 
 template <int MODE, int F32>
@@ -829,8 +961,10 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                                                 ((uintptr_t)a.C & 15) == 0)
                                              : a.ldb % 4 == 0)),
                 "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
-  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32);
+  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32, a.pro);
   const Cfg16 c = kCfgs16[cfg];
+  TMR_CHECK_ARG(!a.pro || (f32 && pro32_ok(a, MODE)),
+                "gemm (LDS-DMA path): operand prologue %d not supported here (view %d)", a.pro, MODE);
   // ReLU-mask bits are read by the LDS-staged BN-backward epilogue only (every dgrad tile but
   // 256x256, whose wave row-blocks do not fit the staging buffer)
   TMR_CHECK_ARG(a.bn_part == nullptr || a.bn_mask != 3 ||
@@ -849,16 +983,19 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   const int bk = f32 ? 32 : 64;
   const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
-  switch (cfg) {
-    case 0: return launch16_cfg<MODE, 256, 256, 2, 4, F32>(a, tapv, grid, st);
-    case 1: return launch16_cfg<MODE, 256, 128, 4, 2, F32>(a, tapv, grid, st);
-    case 2: return launch16_cfg<MODE, 128, 128, 2, 2, F32>(a, tapv, grid, st);
-    case 3: return launch16_cfg<MODE, 256, 64, 4, 1, F32>(a, tapv, grid, st);
-    case 4: return launch16_cfg<MODE, 64, 256, 1, 4, F32>(a, tapv, grid, st);
-    case 6: return launch16_cfg<MODE, 256, 256, 4, 4, F32>(a, tapv, grid, st);
-    case 7: return launch16_cfg<MODE, 128, 128, 4, 2, F32>(a, tapv, grid, st);
-    default: return launch16_cfg<MODE, 64, 64, 2, 2, F32>(a, tapv, grid, st);
+  if constexpr (F32 != 0) {
+    // prologue variants (fp32 only): FWD X, DGRAD dY, WGRAD dY / dY + X
+    if (a.pro) {
+      if constexpr (MODE == MODE_FWD) return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
+      if constexpr (MODE == MODE_DGRAD) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
+      if constexpr (MODE == MODE_WGRAD) {
+        if (a.pro == 2) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
+        if (a.pro == 3) return launch16_switch<MODE, F32, 3>(a, cfg, tapv, grid, st);
+        return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
+      }
+    }
   }
+  return launch16_switch<MODE, F32, 0>(a, cfg, tapv, grid, st);
 }
 
 template <int MODE, int F32>

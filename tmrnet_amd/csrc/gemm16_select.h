@@ -18,10 +18,28 @@ constexpr Cfg16 kCfgs16[] = {{256, 256}, {256, 128}, {128, 128}, {256, 64}, {64,
 // fp32 form (GemmArgs::dma32, set by the conv entry points): FWD with every operand fp32 and
 // 16-B aligned, 4-channel pieces; DGRAD whenever the weights come transposed (wt: the engine is
 // the only reader of that layout, so eligibility is checked again by launch_gemm16_t).
+// Operand prologues on the fp32 engine (GemmArgs::pro; gemm16_kernel PRO): the per-channel
+// coefficient tables are staged in LDS, so their channel counts are bounded
+constexpr int PRO_XMAX = 512;    // X-operand channels (the inputs of conv2 / conv3: planes <= 512)
+constexpr int PRO_DMAX = 2048;   // dY-operand channels (conv outputs <= 2048)
+inline bool pro32_ok(const GemmArgs& a, int mode) {
+  if (!a.pro) return true;
+  // one tap per 32-float k-tile (the transform takes the piece's channel from the tile's tap)
+  if (mode != MODE_WGRAD && a.ntaps != 1 && a.log2C < 5) return false;
+  if ((a.pro & 1) && (mode == MODE_DGRAD || a.lds > PRO_XMAX || a.lds % 4)) return false;
+  if (a.pro & 2) {
+    if (mode == MODE_FWD || ((uintptr_t)a.pd_y & 15)) return false;
+    const int cd = mode == MODE_WGRAD ? a.ldb : a.lds;
+    if (cd > PRO_DMAX || cd % 4) return false;
+  }
+  return true;
+}
+
 inline bool use32(const GemmArgs& a, int mode) {
   // A/B switch for the forward view, read per launch (tests flip it in-process)
   const bool on = env_int("TMR_GEMM32", 1) != 0;
-  if (a.prec != TMR_MATH_F32 || a.sab || a.pro) return false;
+  if (a.prec != TMR_MATH_F32 || a.sab) return false;
+  if (!pro32_ok(a, mode)) return false;
   if (mode == MODE_DGRAD) return a.wt != 0;
   if (!on || !a.dma32) return false;
   if ((((uintptr_t)a.A | (uintptr_t)a.B) & 15) != 0) return false;
@@ -56,7 +74,16 @@ inline long cfg16_tiles(long M, long N, int c) {
 // wgrads with 64 output channels want 64-wide tiles, the big-FLOP wgrads (>= 100 GFLOP: 3x3,
 // strided downsample) 256x256 as 16 waves, the rest 128x128 as 8 waves; the N = 128 forwards and
 // the >= 512-column dgrads 128x128 as 8 waves.
-inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false) {
+inline int pick_cfg16_base(long M, long N, long K, int mode, bool f32);
+// pro: the launch's operand prologues -- a dY prologue (bit 2) stages y and 24 KB of coefficients
+// in LDS besides the two k-tile stages, which a 256x256 tile (128 KB of stages) cannot fit: its
+// 8-wave 128x128 form instead
+inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false, int pro = 0) {
+  const int cfg = pick_cfg16_base(M, N, K, mode, f32);
+  if ((pro & 2) && kCfgs16[cfg].bm == 256 && kCfgs16[cfg].bn == 256) return 7;
+  return cfg;
+}
+inline int pick_cfg16_base(long M, long N, long K, int mode, bool f32) {
   static const int forced = env_int("TMR_GEMM16_CFG", -1);   // experiments only
   if (forced >= 0 && forced < (int)(sizeof(kCfgs16) / sizeof(kCfgs16[0]))) return forced;
   int cfg;
@@ -102,11 +129,11 @@ inline int pick_cfg16(long M, long N, long K, int mode, bool f32 = false) {
 // rows / columns of the output tile the launch for `a` will use (host planning: BN-partial rows,
 // wgrad split counts)
 inline int gemm_tile_bm(const GemmArgs& a, int mode) {
-  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32)].bm
+  return use16(a, mode) ? kCfgs16[pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32, a.pro)].bm
                         : kCfgs[pick_cfg(a.M, a.N, a.K, mode)].bm;
 }
 inline long gemm_tiles(const GemmArgs& a, int mode) {
-  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32))
+  return use16(a, mode) ? cfg16_tiles(a.M, a.N, pick_cfg16(a.M, a.N, a.K, mode, a.prec == TMR_MATH_F32, a.pro))
                         : cfg_tiles(a.M, a.N, pick_cfg(a.M, a.N, a.K, mode));
 }
 

@@ -82,9 +82,14 @@ def _bn_momentum(bn):
 # backward writes dy: the conv's dgrad and wgrad read the masked gradient g and y through a
 # dY-operand prologue with per-channel coefficients.  Bit-identical to the explicit passes
 # (tests/test_kernels_gpu.py::test_bn_fold_bit_identical), but measured slower on MI355X: the
-# prologue costs the MFMA-bound fp32 GEMMs more (wgrad +21 ms, dgrad +12 ms, fwd +6 ms per step,
-# profiles/r2/convbench_fold/) than the HBM-bound passes it removes (~17 ms) -- C2 210 vs 181
-# ms/step.  Kept for the bf16 path and for A/B measurements.
+# prologue costs the MFMA-bound fp32 GEMMs more than the HBM-bound passes it removes (~17 ms).
+# Register-staged engine (round 2): wgrad +21 ms, dgrad +12 ms, fwd +6 ms per step, C2 210 vs 181
+# ms/step (profiles/r2/convbench_fold/).  LDS-DMA engine (round 4, gemm16_kernel PRO: each lane
+# transforms its landed pieces in LDS before the barrier that publishes the k-tile): fwd +3.0,
+# wgrad +12.7, dgrad +21.0 ms per step, C2 193.3 vs 173.9 ms/step, 3312 vs 3680 frames/s, same
+# box (profiles/r4/fold_ab/): the transform sits between the LDS-DMA landing and the barrier with
+# every MFMA idle, and on the narrow tiles (256x64: 8 pieces per lane per k-tile) it triples the
+# LDS traffic; the dgrads also read y next to g (twice the A-operand bytes).  Off by default.
 FOLD_BN = os.environ.get("TMR_FOLD_BN", "0") == "1"
 
 # bf16 math (configs C4/C5): the tensors consumed only as conv operands -- the KRSC weights, the
@@ -146,7 +151,8 @@ BITS16 = os.environ.get("TMR_RELU_BITS16", "0") == "1"
 
 
 def _dma32(math):
-    return math == "fp32" and DMA32 and not FOLD_BN
+    # (FOLD_BN too: the fp32 LDS-DMA engine applies the operand prologues in LDS, gemm16_kernel PRO)
+    return math == "fp32" and DMA32
 
 
 # bf16 activations: the stem input as NHWC8 bf16 (TMR_BF16_STEM8=0: the NHWC4 fp32 input on the
