@@ -80,9 +80,11 @@ typedef struct tmr_conv_desc {
 #define TMR_IO_BN_BF16 32  /* tmr_conv2d_dgrad_bnbwd: the y / z of the fused BN backward are bf16 */
 #define TMR_IO_G16 128     /* tmr_conv2d_dgrad_bnbwd, bf16 math on the LDS-DMA engine: dx -- the
                               ReLU-masked BN-output gradient g -- is written as bf16 (RNE) and the
-                              partials describe the rounded values; beta 0, c a multiple of 8
-                              (the non-residual units of the bf16 train step; tmr_bn_bwd_parts_g16
-                              reads it) */
+                              partials describe the rounded values; c a multiple of 8 (the
+                              non-residual units of the bf16 train step; tmr_bn_bwd_parts_g16
+                              reads it).  With beta: the old dx is bf16 in place, or any fp32 /
+                              bf16 tensor given to tmr_conv2d_dgrad_bnbwd_acc (the residual
+                              stream's gradient of the bf16 train step) */
 #define TMR_IO_WT_BF16 8   /* dgrad only: w is the transposed bf16 weight copy Wt[Cin][R][S][Cout]
                               (tmr_weight_oihw_to_crsk_x), read K-contiguous by the LDS-DMA engine */
 #define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the one io bit fp32 math takes): w is the
@@ -157,6 +159,17 @@ int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy, const fl
                                const float* scale, const float* shift, const float* mean,
                                int mask, void* parts, size_t parts_bytes,
                                const tmr_conv_prologue* pro, hipStream_t stream);
+/* tmr_conv2d_dgrad_bnbwd with the beta operand read from dx_old (fp32, or bf16 when old_bf16)
+ * instead of dx, and dx written as bf16 (TMR_IO_G16, bf16 math on the LDS-DMA engine): the
+ * Bottleneck's conv1 dgrad adding into the residual stream's gradient -- the sum of the identity
+ * branch and conv1 branch gradients of the block input (train_only_non-local_pretrained.py:210-213,
+ * torchvision Bottleneck `out += identity`), masked by the previous block's ReLU and rounded to
+ * bf16 once.  beta != 0, dx_old 16-B aligned; dx_old may equal dx (bf16 in place). */
+int tmr_conv2d_dgrad_bnbwd_acc(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                               void* dx, float beta, const void* dx_old, int old_bf16,
+                               const float* y, const float* z, const float* scale,
+                               const float* shift, const float* mean, int mask, void* parts,
+                               size_t parts_bytes, hipStream_t stream);
 int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy, float* dw_oihw,
                          int c_real, float beta, float* ws, size_t ws_bytes,
                          const tmr_conv_prologue* pro, hipStream_t stream);
@@ -385,6 +398,12 @@ int tmr_bn_bwd_parts_g16(const void* g, const void* y, const void* parts, int np
                          const float* save_mean, const float* save_invstd, const float* gamma,
                          void* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
                          size_t ws_bytes, hipStream_t stream);
+/* BatchNorm2d backward (no ReLU) of the downsample branch's BN when its output gradient is the
+ * bf16 residual-stream gradient (train_only_non-local_pretrained.py:210-213, the Bottleneck
+ * `downsample` Sequential): dz, y, dy bf16, c a multiple of 8, 16-B aligned; ws as tmr_bn_ws_bytes */
+int tmr_bn_bwd_g16(const void* dz, const void* y, const float* save_mean,
+                   const float* save_invstd, const float* gamma, void* dy, float* dgamma,
+                   float* dbeta, int rows, int c, void* ws, size_t ws_bytes, hipStream_t stream);
 int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho,
                            int wo, const void* y, const float* scale, const float* shift,
                            const float* save_mean, const float* save_invstd, const float* gamma,

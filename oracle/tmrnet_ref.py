@@ -151,6 +151,10 @@ class Bottleneck(nn.Module):
         out = self.relu(out + identity)
         if getattr(self, "round_out", False) and self.training:   # emulate_bf16_convs(activations)
             out = _RoundFn.apply(out)
+        if getattr(self, "round_res_grad", False) and self.training:
+            # trunk.R16: the gradient of this block output (the residual stream's), masked by the
+            # ReLU, is stored bf16 -- mask * round(g) == round(mask * g)
+            out = _GradRoundFn.apply(out)
         return out
 
 
@@ -362,15 +366,20 @@ class Bf16Conv2d(nn.Conv2d):
         return y
 
 
-def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=None):
+def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=None, res_grads=None):
     """Switch every trunk Conv2d of `module` to bf16-operand math (class swap, so deepcopy
     and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay.
     activations=True: in train mode the conv outputs and the Bottleneck outputs are rounded to
     bf16 as well (the bf16-activation contract of the train step; ResNeSt-50 also stores the
     split attention's relu(bn0) input and output and the avd pool output as bf16).
     grads (default: activations): the ResNet-50 Bottleneck's relu(bn1) / relu(bn2) gradients are
-    rounded to bf16 in the backward (trunk.G16: the fused dgrad stores them bf16)."""
+    rounded to bf16 in the backward (trunk.G16: the fused dgrad stores them bf16), and so is the
+    gradient of every Bottleneck output but the last (trunk.R16: the residual stream's gradient,
+    written by the next block's conv1 dgrad; the last block's comes from the avgpool in fp32).
+    res_grads (default: grads) switches the second part alone."""
     grads = activations if grads is None else grads
+    res_grads = grads if res_grads is None else res_grads
+    blocks = [m for m in module.modules() if isinstance(m, Bottleneck)]
     for name, m in module.named_modules():
         if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
             m.__class__ = Bf16Conv2d
@@ -379,6 +388,7 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
             m.round_out = activations
             if isinstance(m, Bottleneck):
                 m.round_grad = grads
+                m.round_res_grad = res_grads and m is not blocks[-1]
     return module
 
 

@@ -472,6 +472,72 @@ def test_gemm16_dgrad_g16(dev, case):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("case", [
+    # n, h, w, cin(dx channels), cout(dy channels), old dtype
+    (3, 14, 14, 256, 64, "bf16"),      # a Bottleneck conv1 dgrad adding into the bf16 stream
+    (2, 12, 12, 512, 128, "fp32"),     # ... reading the fp32 stream (downsample dgrad / last block)
+])
+@pytest.mark.parametrize("mask", [1, 3])
+def test_gemm16_dgrad_residual_g16(dev, case, mask):
+    """The bf16 residual-stream gradient (trunk.R16, tmr_conv2d_dgrad_bnbwd_acc / TMR_IO_G16 with
+    beta): the conv1 dgrad adds into the old gradient (bf16 in place, or fp32 from another tensor),
+    masks by the previous block's ReLU (z, or its bits) and stores bf16 -- exactly the RNE rounding
+    of the fp32 path's result on the same old values; partials those of the rounded values."""
+    n, h, w, cin, cout, odt = case
+    g = torch.Generator().manual_seed(23)
+    dy = _r(torch.randn(n, h, w, cout, generator=g)).to(dev).to(torch.bfloat16)
+    wt = (torch.randn(cout, cin, 1, 1, generator=g) / np.sqrt(cout)).to(dev)
+    wct = ops.weight_to_crsk(wt)
+    y = torch.randn(n, h, w, cin, generator=g).to(dev).to(torch.bfloat16)
+    ye = y.float()
+    mean = ye.view(-1, cin).mean(0)
+    zf = torch.relu(ye + torch.randn(n, h, w, cin, generator=g).to(dev) * 0.5)
+    z = zf.to(torch.bfloat16)
+    zm = z
+    if mask == 3:
+        from tests.test_kernels_gpu import _pack_bits
+        zm = _pack_bits((z.float() > 0).cpu()).to(dev)
+    old = torch.randn(n, h, w, cin, generator=g).to(dev)
+    if odt == "bf16":
+        old = old.to(torch.bfloat16)
+    old32 = old.float().clone()
+    kw = dict(z=zm, math="bf16", wt=True, beta=1.0)
+    d32, p32, n32 = ops.conv_dgrad_bnbwd(dy, wct, (h, w), 1, 0, y, mean, mask, out=old32, **kw)
+    if odt == "bf16":
+        o16 = old.clone()
+        d16, p16, n16 = ops.conv_dgrad_bnbwd(dy, wct, (h, w), 1, 0, y, mean, mask, out=o16,
+                                             g16=True, **kw)
+        assert d16.data_ptr() == o16.data_ptr()
+    else:
+        d16, p16, n16 = ops.conv_dgrad_bnbwd(dy, wct, (h, w), 1, 0, y, mean, mask, g16=True,
+                                             old=old, **kw)
+    torch.cuda.synchronize()
+    assert d16.dtype == torch.bfloat16 and n16 == n32
+    assert torch.equal(d16, d32.to(torch.bfloat16))
+    gd = d16.double().view(-1, cin)
+    want = torch.stack([gd.sum(0), (gd * (ye.double().view(-1, cin) - mean.double())).sum(0)], -1)
+    got = p16[:n16].double().sum(0)
+    assert (got - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
+
+
+def test_bn_bwd_bf16_dz(dev):
+    """The downsample branch's BN backward with the bf16 residual-stream gradient as dz
+    (tmr_bn_bwd_g16): bit-identical to the fp32-dz path on the same values."""
+    g = torch.Generator().manual_seed(29)
+    rows, c = 3 * 14 * 14, 256
+    y = torch.randn(3, 14, 14, c, generator=g).to(dev).to(torch.bfloat16)
+    dz = torch.randn(3, 14, 14, c, generator=g).to(dev).to(torch.bfloat16)
+    ye = y.float().view(rows, c)
+    mean = ye.mean(0)
+    inv = 1.0 / (ye.var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
+    a = ops.bn_bwd(dz, y, None, mean, inv, gamma, False)
+    b = ops.bn_bwd(dz.float(), y, None, mean, inv, gamma, False)
+    torch.cuda.synchronize()
+    assert a[0].dtype == torch.bfloat16 and a[1] is None
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+
+
 def test_stem_nhwc8_bf16_input(dev):
     """The bf16 step's stem input (tmr_nhwc4_to_bf16x8): bit-exact bf16 (RNE) of the NHWC4 fp32
     pixels with channels 3-7 zero; the 7x7/2 stem on it (bf16 LDS-DMA engine, forward and

@@ -60,6 +60,7 @@ SIGNATURES = {
     "tmr_conv2d_fwd_bnstats_pro": [DP, P, P, P, P, SZ, PP, P],
     "tmr_conv2d_dgrad_pro": [DP, P, P, P, F, PP, P],
     "tmr_conv2d_dgrad_bnbwd_pro": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, PP, P],
+    "tmr_conv2d_dgrad_bnbwd_acc": [DP, P, P, P, F, P, I, P, P, P, P, P, I, P, SZ, P],
     "tmr_conv2d_wgrad_pro": [DP, P, P, P, I, F, P, SZ, PP, P],
     "tmr_bn_bwd_coefs": [P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_apply_x": [P, P, P, P, P, I, I, I, I, P],
@@ -82,6 +83,7 @@ SIGNATURES = {
     "tmr_bn_bwd_a16": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_a16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_g16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_bwd_g16": [P, P, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_maxpool_a16": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
     "tmr_maxpool2d_fwd_bn_a16": [P, P, P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd_a16": [P, P, I, I, I, P],

@@ -9,6 +9,7 @@
 // float4 loads/stores along channels, grid sized to fill 256 CUs.
 #include "common.h"
 #include "tmr.h"
+#include <type_traits>
 
 namespace {
 
@@ -335,8 +336,10 @@ __device__ __forceinline__ float4 affine4(float4 v, float4 sc, float4 sf) {
 
 // WB: write the masked gradient back over dz (dres aliasing dz: the identity branch of a
 // residual block takes the masked gradient in place, and the apply pass needs no mask)
-template <int MASK, bool WB = false, typename TY = float>
-__global__ __launch_bounds__(NT) void bn_bwd_partial(float* dz, const TY* __restrict__ y,
+// TG: element type of dz (bf16: the bf16 residual-stream gradient of the bf16-activation step,
+// tmr_bn_bwd_g16; no write-back)
+template <int MASK, bool WB = false, typename TY = float, typename TG = float>
+__global__ __launch_bounds__(NT) void bn_bwd_partial(TG* dz, const TY* __restrict__ y,
                                                      const TY* __restrict__ z,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift,
@@ -356,11 +359,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(float* dz, const TY* __rest
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
   for (int r = r0 + tr; r < r1; r += rthreads) {
     const long o = (long)r * c + ch;
-    float4 g = *reinterpret_cast<const float4*>(dz + o);
+    float4 g = ld4(dz, o >> 2);
     const float4 v = ld4(y, o >> 2);
     if (MASK == 1) g = relu_mask4(g, ld4(z, o >> 2));
     if (MASK == 2) g = relu_mask4(g, affine4(v, sc, sf));
-    if (WB) *reinterpret_cast<float4*>(dz + o) = g;
+    if constexpr (WB) {
+      static_assert(std::is_same<TG, float>::value, "bn_bwd_partial: write-back of an fp32 dz only");
+      *reinterpret_cast<float4*>(dz + o) = g;
+    }
     s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
     q.x = fmaf(g.x, v.x - mu.x, q.x); q.y = fmaf(g.y, v.y - mu.y, q.y);
     q.z = fmaf(g.z, v.z - mu.z, q.z); q.w = fmaf(g.w, v.w - mu.w, q.w);
@@ -1361,6 +1367,34 @@ TMR_API int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const 
   }
 #undef TMR_BN_APPLY16
   TMR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+// BatchNorm backward of a unit without ReLU (the downsample branch's BN) whose output gradient is
+// the bf16 residual-stream gradient of the bf16-activation step (trunk.R16): dz, y, dy bf16
+TMR_API int tmr_bn_bwd_g16(const void* dz, const void* y, const float* save_mean,
+                           const float* save_invstd, const float* gamma, void* dy, float* dgamma,
+                           float* dbeta, int rows, int c, void* ws, size_t ws_bytes,
+                           hipStream_t stream) {
+  TMR_CHECK_ARG(c % 8 == 0 && c >= 8 && rows > 0, "tmr_bn_bwd_g16: bad shape rows=%d c=%d", rows, c);
+  TMR_CHECK_ARG((((uintptr_t)dz | (uintptr_t)y | (uintptr_t)dy) & 15) == 0,
+                "tmr_bn_bwd_g16: dz / y / dy must be 16-B aligned");
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd_g16: workspace too small");
+  Plan p = make_plan(rows, c);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + (size_t)p.nrb * c * 2 * sizeof(double));
+  const __bf16 *gb = (const __bf16*)dz, *yb = (const __bf16*)y;
+  hipLaunchKernelGGL((bn_bwd_partial<0, false, __bf16, const __bf16>), dim3(p.nrb, p.cblocks), dim3(NT),
+                     0, stream, gb, yb, nullptr, nullptr, nullptr, save_mean, rows, c, p.rpb,
+                     p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_bwd_partial_g16");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  const long n8 = (long)rows * c / 8;
+  hipLaunchKernelGGL(bn_bwd_apply8_a16<__bf16>, dim3(ew_blocks(n8)), dim3(NT), 0, stream, gb, yb,
+                     coef, (__bf16*)dy, n8, c / 8);
+  TMR_CHECK_LAUNCH("bn_bwd_apply_g16");
   return 0;
 }
 

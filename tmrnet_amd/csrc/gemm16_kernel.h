@@ -72,6 +72,33 @@ __device__ __forceinline__ void store_g8(const GemmArgs& a, long off, const floa
   }
 }
 
+// the 8 old-dx values of the fused BN-backward epilogue's beta at element offset `off` (fp32, or
+// bf16 when GemmArgs::cold16), raw: (c0, c1) = 32 B of fp32, or c0 = 16 B of bf16
+__device__ __forceinline__ void load_old8(const GemmArgs& a, long off, uint4& c0, uint4& c1) {
+  const void* base = a.Cold ? a.Cold : (const void*)a.C;
+  if (a.cold16) {
+    c0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(base) + off);
+  } else {
+    c0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + off);
+    c1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + off + 4);
+  }
+}
+__device__ __forceinline__ void unpack_old8(const GemmArgs& a, const uint4& c0, const uint4& c1,
+                                            float (&old)[8]) {
+  if (a.cold16) {
+    const uint32_t u[4] = {c0.x, c0.y, c0.z, c0.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      old[2 * e] = __uint_as_float(u[e] << 16);
+      old[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+    }
+  } else {
+    const uint32_t u[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) old[e] = __uint_as_float(u[e]);
+  }
+}
+
 #ifndef TMR_EPI_DEPTH
 #define TMR_EPI_DEPTH 3
 #endif
@@ -133,10 +160,7 @@ struct LdsBnbwd {
       }
     }
     if (a.bn_mask == 3) x.bits = reinterpret_cast<const uint32_t*>(a.bn_z)[off >> 5];
-    if (a.beta != 0.f) {
-      x.c0 = *reinterpret_cast<const uint4*>(a.C + off);
-      x.c1 = *reinterpret_cast<const uint4*>(a.C + off + 4);
-    }
+    if (a.beta != 0.f) load_old8(a, off, x.c0, x.c1);
   }
 
   __device__ __forceinline__ static void prefetch(const GemmArgs& a, int m0, int n0, In (&pf)[D]) {
@@ -226,9 +250,7 @@ struct LdsBnbwd {
             for (int e = 0; e < 8; ++e) zv[e] = 0.f;
           }
           if (has_beta) {
-            const uint32_t cu[8] = {x.c0.x, x.c0.y, x.c0.z, x.c0.w, x.c1.x, x.c1.y, x.c1.z, x.c1.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) old[e] = __uint_as_float(cu[e]);
+            unpack_old8(a, x.c0, x.c1, old);
           } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) old[e] = 0.f;
@@ -375,10 +397,9 @@ __device__ __forceinline__ void epilogue_lds_bnbwd(const GemmArgs& a, floatx16 (
           for (int e = 0; e < 8; ++e) zv[e] = 0.f;
         }
         if (has_beta) {
-          const float4 c0 = *reinterpret_cast<const float4*>(a.C + off);
-          const float4 c1 = *reinterpret_cast<const float4*>(a.C + off + 4);
-          old[0] = c0.x; old[1] = c0.y; old[2] = c0.z; old[3] = c0.w;
-          old[4] = c1.x; old[5] = c1.y; old[6] = c1.z; old[7] = c1.w;
+          uint4 c0, c1;
+          load_old8(a, off, c0, c1);
+          unpack_old8(a, c0, c1, old);
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) old[e] = 0.f;
@@ -971,11 +992,16 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                     (MODE == MODE_DGRAD && !(c.bm == 256 && c.bn == 256)),
                 "gemm: ReLU-mask bits (mask 3) need the LDS-DMA dgrad's LDS-staged epilogue (tile %dx%d)",
                 c.bm, c.bn);
-  TMR_CHECK_ARG(!a.g16 || (MODE == MODE_DGRAD && a.bn_part != nullptr && a.beta == 0.f &&
+  TMR_CHECK_ARG(!a.g16 || (MODE == MODE_DGRAD && a.bn_part != nullptr &&
                            !(c.bm == 256 && c.bn == 256) && ((uintptr_t)a.C & 15) == 0 &&
                            a.ldc % 8 == 0),
                 "gemm: a bf16 BN-backward gradient (TMR_IO_G16) needs the fused LDS-staged dgrad "
-                "epilogue, beta 0, 16-B aligned rows (tile %dx%d)", c.bm, c.bn);
+                "epilogue, 16-B aligned rows (tile %dx%d)", c.bm, c.bn);
+  TMR_CHECK_ARG((!a.Cold && !a.cold16) ||
+                    (MODE == MODE_DGRAD && a.bn_part != nullptr && !(c.bm == 256 && c.bn == 256) &&
+                     ((uintptr_t)(a.Cold ? a.Cold : a.C) & 15) == 0),
+                "gemm: a separate / bf16 old dx needs the fused LDS-staged dgrad epilogue (tile %dx%d)",
+                c.bm, c.bn);
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   // a k-tile (64 bf16 / 32 fp32) spans several taps when the channels per tap are fewer (or not

@@ -403,6 +403,8 @@ struct BnBwdFuse {
   long nparts;
   bool count_only;
   int part_ld;   // columns per partial row (the total channels of a grouped dgrad)
+  const void* old;   // the beta operand when it is not dx itself (nullptr: dx)
+  int old16;         // the beta operand is bf16
 };
 
 static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
@@ -469,6 +471,8 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
         }
         a.bn_part = fz->part;
         a.part_ld = fz->part_ld;
+        a.Cold = fz->old;
+        a.cold16 = fz->old16;
         fz->part += nmt * fz->part_ld;
         fz->nparts += nmt;
       }
@@ -502,6 +506,7 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
     fc_.z = fz->mask == 3 ? (const float*)((const uint32_t*)fz->z + f0 * px_frame / 32)
                           : adv(fz->z, f0 * px_frame, esz_bn(d));
     fc_.nparts = 0;
+    if (fz->old) fc_.old = adv(fz->old, f0 * x_frame(d), fz->old16 ? 2 : 4);
     tmr_conv_prologue pc{};
     if (pro) pc = chunk_pro(pro, d, f0);
     int rc = conv_dgrad_impl(&c, adv(dy, f0 * y_frame(d), esz_dy(d)), w_krsc,
@@ -537,6 +542,12 @@ TMR_API int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, cons
                                     parts_bytes, nullptr, stream);
 }
 
+static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                             float* dx, float beta, const void* dx_old, int old_bf16,
+                             const float* y, const float* z, const float* scale,
+                             const float* shift, const float* mean, int mask, void* parts,
+                             size_t parts_bytes, const tmr_conv_prologue* pro, hipStream_t stream);
+
 TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
                                        const float* w_krsc, float* dx, float beta, const float* y,
                                        const float* z, const float* scale, const float* shift,
@@ -544,15 +555,41 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
                                        size_t parts_bytes, const tmr_conv_prologue* pro,
                                        hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd: null descriptor");
+  // in place: a bf16 gradient (TMR_IO_G16) accumulates into its own bf16 values
+  return dgrad_bnbwd_entry(d, dy, w_krsc, dx, beta, nullptr, (d->io & TMR_IO_G16) ? 1 : 0, y, z,
+                           scale, shift, mean, mask, parts, parts_bytes, pro, stream);
+}
+
+TMR_API int tmr_conv2d_dgrad_bnbwd_acc(const tmr_conv_desc* d, const float* dy,
+                                       const float* w_krsc, void* dx, float beta,
+                                       const void* dx_old, int old_bf16, const float* y,
+                                       const float* z, const float* scale, const float* shift,
+                                       const float* mean, int mask, void* parts,
+                                       size_t parts_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd_acc: null descriptor");
+  TMR_CHECK_ARG(beta != 0.f && dx_old && ((uintptr_t)dx_old & 15) == 0 &&
+                    (d->io & TMR_IO_G16) && (d->io & TMR_IO_WT_BF16),
+                "tmr_conv2d_dgrad_bnbwd_acc: needs beta != 0, a 16-B aligned old dx and a bf16 "
+                "output (TMR_IO_G16) on the bf16 LDS-DMA engine (TMR_IO_WT_BF16)");
+  return dgrad_bnbwd_entry(d, dy, w_krsc, (float*)dx, beta, dx_old, old_bf16 ? 1 : 0, y, z, scale,
+                           shift, mean, mask, parts, parts_bytes, nullptr, stream);
+}
+
+static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                             float* dx, float beta, const void* dx_old, int old_bf16,
+                             const float* y, const float* z, const float* scale,
+                             const float* shift, const float* mean, int mask, void* parts,
+                             size_t parts_bytes, const tmr_conv_prologue* pro, hipStream_t stream) {
   TMR_CHECK_ARG(xld_of(d) == d->c, "tmr_conv2d_dgrad_bnbwd: dx must be dense (x_ld == c)");
   TMR_CHECK_ARG(ngroups(d) == 1 || (mask != 3 && !pro),
                 "tmr_conv2d_dgrad_bnbwd: a grouped dgrad takes no ReLU-mask bits / prologue");
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
   TMR_CHECK_ARG(!(d->io & TMR_IO_G16) ||
-                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) && beta == 0.f &&
+                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) &&
                      ngroups(d) == 1 && !pro && d->c % 8 == 0),
                 "tmr_conv2d_dgrad_bnbwd: a bf16 gradient (TMR_IO_G16) needs bf16 math on the LDS-DMA "
-                "engine (TMR_IO_WT_BF16), beta 0, no groups / prologue, c a multiple of 8");
+                "engine (TMR_IO_WT_BF16), no groups / prologue, c a multiple of 8");
+  TMR_CHECK_ARG(!dx_old || ngroups(d) == 1, "tmr_conv2d_dgrad_bnbwd: a separate old dx takes no groups");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
                 "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
   TMR_CHECK_ARG(mask != 3 || ((d->io & (TMR_IO_WT_F32 | TMR_IO_WT_BF16)) &&
@@ -583,6 +620,8 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
   fz.y = y; fz.z = z; fz.sc = scale; fz.sh = shift; fz.mean = mean; fz.mask = mask;
   fz.part = (float2*)parts;
   fz.part_ld = d->c;
+  fz.old = dx_old;
+  fz.old16 = beta != 0.f ? old_bf16 : 0;
   return dgrad_bnbwd_run(d, dy, w_krsc, dx, beta, &fz, stream, pro);
 }
 

@@ -123,6 +123,11 @@ struct GemmArgs {
   // gradient g -- is stored as bf16 (RNE) and the partials describe the rounded values; no beta
   // (TMR_IO_G16)
   int g16;
+  // the fused BN-backward DGRAD's beta operand (the old dx), when it is not C itself: the bf16
+  // residual-gradient step (trunk.R16) reads an fp32 gradient and stores the sum as bf16 elsewhere.
+  // cold16: the old dx is bf16 (element offsets as C's).  Cold == nullptr: C.
+  const void* Cold;
+  int cold16;
 };
 
 __device__ __forceinline__ float bf16_rne(float v) { return (float)(__bf16)v; }

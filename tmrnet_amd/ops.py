@@ -263,11 +263,19 @@ def conv_dgrad(dy, w_krsc, in_hw, stride, pad, out=None, beta=0.0, pad_w=None, m
 
 def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scale=None,
                      shift=None, out=None, beta=0.0, math="fp32", dpro=None, wt=False, groups=1,
-                     g16=False):
+                     g16=False, old=None):
     """conv_dgrad whose epilogue masks dx by the previous unit's ReLU (mask 1: z > 0, 2:
     y*scale+shift > 0) and emits that unit's BN-backward partials -> (dx_masked, parts, nparts).
     wt: as conv_dgrad.  y / z may be bf16 (the bf16-activation step, TMR_IO_BN_BF16).
-    g16: dx_masked stored bf16, the partials those of the rounded values (TMR_IO_G16)."""
+    g16: dx_masked stored bf16, the partials those of the rounded values (TMR_IO_G16); with beta
+    the old dx is `out` itself (bf16, in place) or `old` (fp32 or bf16; tmr_conv2d_dgrad_bnbwd_acc,
+    a new bf16 dx is returned)."""
+    if old is not None:
+        if not (g16 and beta != 0.0 and out is None and dpro is None and groups == 1):
+            raise RuntimeError("conv_dgrad_bnbwd: a separate old dx needs g16, beta, no out / "
+                               "prologue / groups")
+        if old.dtype not in (f32, BF16) or not old.is_contiguous():
+            raise RuntimeError("conv_dgrad_bnbwd: old dx must be a contiguous fp32 / bf16 tensor")
     _req_op(w_krsc, "w"); _req_op(y, "y"); _req(mean, "mean")
     if mask == 3:   # z = ReLU-mask bits of dx's shape (bn_apply_bits)
         if z is None or z.dtype != torch.int32 or z.numel() * 32 < y.numel():
@@ -288,6 +296,8 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     if tuple(y.shape) != tuple(out.shape) or (z is not None and mask != 3
                                               and tuple(z.shape) != tuple(out.shape)):
         raise RuntimeError("conv_dgrad_bnbwd: y/z must have dx's shape %s" % (tuple(out.shape),))
+    if old is not None and tuple(old.shape) != tuple(out.shape):
+        raise RuntimeError("conv_dgrad_bnbwd: old dx must have dx's shape %s" % (tuple(out.shape),))
     d.x_ld = _nhwc_ld(out, "dx")
     d.y_ld = _nhwc_ld(dy, "dy")
     nparts = query("tmr_conv2d_dgrad_bnbwd_parts", ctypes.byref(d))
@@ -296,11 +306,17 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     parts = torch.empty((max(nparts, 1), c, 2), dtype=f32, device=dy.device)
     with _prof("conv_dgrad" + _SUFFIX[math], 2.0 * n * ho * wo * k * r * s * c / groups, (n, h, w, c, k, r, stride),
                _esz(dy) * n * ho * wo * k * (2 if dpro is not None else 1) + _esz(w_krsc) * w_krsc.numel()
-               + (2 if g16 else 4) * n * h * w * c * (2 if beta else 1)
+               + (2 if g16 else 4) * n * h * w * c
+               + ((old.element_size() if old is not None else (2 if g16 else 4)) * n * h * w * c
+                  if beta else 0)
                + y.element_size() * n * h * w * c * (2 if z is not None and mask != 3 else 1)
                + (n * h * w * c // 8 if mask == 3 else 0)):
         pro = _prologue(None, dpro)
-        if pro is None:
+        if old is not None:
+            call("tmr_conv2d_dgrad_bnbwd_acc", ctypes.byref(d), dy, w_krsc, out, float(beta), old,
+                 int(old.dtype == BF16), y, z, scale, shift, mean, int(mask), parts,
+                 ctypes.c_size_t(parts.numel() * 4), stream_ptr())
+        elif pro is None:
             call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z,
                  scale, shift, mean, int(mask), parts, ctypes.c_size_t(parts.numel() * 4),
                  stream_ptr())
@@ -701,6 +717,15 @@ def bn_bwd(dz, y, z, mean, inv, gamma, relu, want_dres=False, dres_out=None, sca
     c = y.shape[-1]
     rows = y.numel() // c
     ws, nb = _bn_ws(rows, c, y.device)
+    if y.dtype == BF16 and dz.dtype == BF16:
+        # the bf16 residual-stream gradient into a BN without ReLU (the downsample branch)
+        if relu or want_dres:
+            raise RuntimeError("bn_bwd: a bf16 dz takes no ReLU mask / identity gradient")
+        dy = torch.empty_like(y)
+        dgamma = _empty((c,), mean); dbeta = _empty((c,), mean)
+        call("tmr_bn_bwd_g16", dz, y, mean, inv, gamma, dy, dgamma, dbeta, rows, c, ws,
+             ctypes.c_size_t(nb), stream_ptr())
+        return dy, None, dgamma, dbeta
     if y.dtype == BF16:   # bf16 activations: y, z bf16; dz, dres fp32; dy bf16
         dy = torch.empty_like(y)
         dres = None

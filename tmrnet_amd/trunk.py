@@ -142,6 +142,16 @@ DS_FIRST = os.environ.get("TMR_DS_FIRST", "1") != "0"
 # contract (oracle.emulate_bf16_convs(grads=True)) rounds the gradient at those two points.
 G16 = os.environ.get("TMR_G16", "1") != "0"
 
+# bf16-activation step (ResNet-50 trunk): the residual stream's gradient -- the masked gradient of
+# every Bottleneck's sum bn3(y3) + identity but the last block's -- is stored bf16 too
+# (TMR_BF16_RESGRAD=0: fp32).  Each block's conv1 dgrad adds its part to the identity branch's
+# gradient (read bf16, or fp32 from the downsample dgrad / the last block), masks it by the previous
+# block's ReLU and rounds once (tmr_conv2d_dgrad_bnbwd_acc); the BN backward of bn3 and of the
+# downsample BN read it bf16 (tmr_bn_bwd_parts_g16, tmr_bn_bwd_g16).  12-14 -> 6-7 B per element on
+# the residual dgrads' epilogue.  The contract (oracle.emulate_bf16_convs(grads=True)) rounds the
+# gradient of every block output but the last.
+R16 = os.environ.get("TMR_BF16_RESGRAD", "1") != "0"
+
 # the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
 BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
 # ... and for the bf16-activation step (TMR_RELU_BITS16=1).  Off: the bf16 dgrads re-read the 2-byte
@@ -274,7 +284,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
 
 
 def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need_dx=True,
-                 dres_inplace=False, parts=None, fuse_prev=None, pool=None, dy=None, g16=False):
+                 dres_inplace=False, parts=None, fuse_prev=None, pool=None, dy=None, g16=False,
+                 r16=False):
     """BN backward, wgrad, dgrad (optionally accumulated into dx_out) of one conv+BN unit.
 
     parts: dz was produced by a fused dgrad (conv_dgrad_bnbwd): it is already ReLU-masked and
@@ -288,7 +299,9 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     dy: the conv's output gradient computed by the caller (ResNeSt's split-attention backward
     writes the grouped conv's dy with bn0's backward folded in): only wgrad and dgrad run here.
     g16: the fused dgrad may store fuse_prev's masked gradient as bf16 (TMR_IO_G16) when that unit
-    has no residual and the dgrad runs on the bf16 LDS-DMA engine (the bf16-activation step)."""
+    has no residual and the dgrad runs on the bf16 LDS-DMA engine (the bf16-activation step).
+    r16: the same for fuse_prev a block output (R16): the dgrad adds into dx_out (bf16 in place,
+    or fp32 read and a new bf16 tensor returned)."""
     conv, bn = rec["conv"], rec["bn"]
     dpro = None    # (y, coef): dy = A*g + B*y + C evaluated by the consumer convs' loaders
     s16 = _store16(rec["math"])   # dy feeds only this conv's dgrad / wgrad
@@ -355,14 +368,18 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
             zm = p["z"]
             if mask == 1 and wt and p.get("zbits") is not None:
                 mask, zm = 3, p["zbits"]   # the ReLU mask as bits (fp32 LDS-DMA dgrad)
-            gb = (g16 and G16 and mask == 2 and dx_out is None and dx_beta == 0.0 and wt and
-                  grp == 1 and dpro is None and p["y"].dtype == torch.bfloat16 and
-                  p["y"].shape[-1] % 8 == 0)
+            bf8 = (wt and grp == 1 and dpro is None and p["y"].dtype == torch.bfloat16 and
+                   p["y"].shape[-1] % 8 == 0)
+            gb = (g16 and G16 and mask == 2 and dx_out is None and dx_beta == 0.0 and bf8)
+            rb = (r16 and R16 and mask in (1, 3) and dx_out is not None and dx_beta == 1.0 and bf8)
+            old = None
+            if rb and dx_out.dtype != torch.bfloat16:   # fp32 old dx -> a new bf16 dx
+                old, dx_out = dx_out, None
             dx, pp, npp = ops.conv_dgrad_bnbwd(dy, wdg, hw, rec["stride"], rec["pad"],
                                                p["y"], p["mean"], mask, z=zm,
                                                scale=p["scale"], shift=p["shift"], out=dx_out,
                                                beta=dx_beta, math=rec["math"], dpro=dpro,
-                                               wt=wt, groups=grp, g16=gb)
+                                               wt=wt, groups=grp, g16=gb or rb, old=old)
             fused = (pp, npp)
         else:
             dx = ops.conv_dgrad(dy, wdg, hw, rec["stride"], rec["pad"], out=dx_out,
@@ -465,15 +482,15 @@ class TrunkFn(torch.autograd.Function):
                 # the strided downsample dgrad writes dx (its tap-less parity classes as zeros),
                 # the stride-1 conv1 dgrad accumulates into it with the fused BN backward
                 dx, _, _ = _conv_bn_bwd(rd, dres, grads)
-                _, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dx, dx_beta=1.0,
-                                             fuse_prev=prev3)
+                dx, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dx, dx_beta=1.0,
+                                              fuse_prev=prev3, r16=True)
             elif has_ds:
                 dx, _, _ = _conv_bn_bwd(r1, dz1, grads, parts=fz1)
                 _, _, pending = _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0,
                                              fuse_prev=prev3)
             else:
                 dx, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dres, dx_beta=1.0,
-                                              fuse_prev=prev3)
+                                              fuse_prev=prev3, r16=True)
             del dz1, brec, dres
             g = dx
             if ready is not None:   # this block's parameter grads are final: start their exchange
