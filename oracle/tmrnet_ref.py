@@ -256,7 +256,10 @@ class BottleneckS(nn.Module):
         out = self.bn3(self.conv3(out))
         res = self.downsample(x) if self.downsample is not None else x
         out = self.relu(out + res)
-        return _RoundFn.apply(out) if rnd else out
+        out = _RoundFn.apply(out) if rnd else out
+        if getattr(self, "round_res_grad", False) and self.training:   # trunk.R16, as Bottleneck
+            out = _GradRoundFn.apply(out)
+        return out
 
 
 def _make_layer_s(inplanes, planes, blocks, stride):
@@ -374,12 +377,13 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
     split attention's relu(bn0) input and output and the avd pool output as bf16).
     grads (default: activations): the ResNet-50 Bottleneck's relu(bn1) / relu(bn2) gradients are
     rounded to bf16 in the backward (trunk.G16: the fused dgrad stores them bf16), and so is the
-    gradient of every Bottleneck output but the last (trunk.R16: the residual stream's gradient,
-    written by the next block's conv1 dgrad; the last block's comes from the avgpool in fp32).
+    gradient of every Bottleneck (ResNeSt: BottleneckS) output but the last (trunk.R16: the
+    residual stream's gradient, written by the next block's conv1 dgrad; the last block's comes
+    from the avgpool in fp32).
     res_grads (default: grads) switches the second part alone."""
     grads = activations if grads is None else grads
     res_grads = grads if res_grads is None else res_grads
-    blocks = [m for m in module.modules() if isinstance(m, Bottleneck)]
+    blocks = [m for m in module.modules() if isinstance(m, (Bottleneck, BottleneckS))]
     for name, m in module.named_modules():
         if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
             m.__class__ = Bf16Conv2d
@@ -388,6 +392,7 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
             m.round_out = activations
             if isinstance(m, Bottleneck):
                 m.round_grad = grads
+            if isinstance(m, (Bottleneck, BottleneckS)):
                 m.round_res_grad = res_grads and m is not blocks[-1]
     return module
 

@@ -56,6 +56,11 @@ def main():
     ap.add_argument("--wt32", action="store_true",
                     help="fp32 dgrad on the LDS-DMA engine (transposed fp32 weights, "
                          "TMR_IO_WT_F32), as the fp32 train step")
+    ap.add_argument("--y16", action="store_true",
+                    help="forward with the fused statistics writing y as bf16 (the bf16-activation "
+                         "step, GemmArgs::c16)")
+    ap.add_argument("--only", default=None,
+                    help="comma list of cin:cout:r:h filters, e.g. 64:256:1:56")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
     args = ap.parse_args()
@@ -64,8 +69,13 @@ def main():
     kinds = args.kinds.split(",")
     res = []
     tot = {k: [0.0, 0.0] for k in kinds}
+    only = None
+    if args.only:
+        only = [tuple(int(v) for v in f.split(":")) for f in args.only.split(",")]
     for shp, cnt in shapes.items():
         n, h, w, cin, cout, r, st, pad = shp
+        if only is not None and (cin, cout, r, h) not in only:
+            continue
         cs = 4 if cin == 3 else cin
         x = torch.randn(n, h, w, cs, device=dev)
         wk = torch.randn(cout, r, r, cs, device=dev)
@@ -97,8 +107,8 @@ def main():
                 continue
             mt = args.math
             fn = {"fwd": (lambda: ops.conv_fwd_bnstats(x, wk, st, pad, c_real=cin, xpro=xpro,
-                                                       math=mt))
-                  if (args.stats or xpro is not None)
+                                                       math=mt, y16=args.y16))
+                  if (args.stats or xpro is not None or args.y16)
                   else (lambda: ops.conv_fwd(x, wk, st, pad, out=y, math=mt)),
                   "dgrad": (lambda: ops.conv_dgrad_bnbwd(dy, wdg, (h, w), st, pad, yb, meanb, 1,
                                                          z=zb, out=dx, beta=args.dgrad_beta,

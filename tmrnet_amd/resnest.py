@@ -357,12 +357,12 @@ class ResNeStTrunkFn(torch.autograd.Function):
                 if "pool" in rec:
                     k, st = rec["pool"]
                     dxr = ops.avgpool2d_bwd(dxr, rec["in_hw"], k, st, 0, False)
-                _, _, pending = _conv_bn_bwd(rec["r1"], dz1, grads, parts=fz1, dx_out=dxr,
-                                             dx_beta=1.0, fuse_prev=prev3)
-                dx = dxr
+                # (trunk.R16: the sum is returned as a new bf16 tensor when dxr is fp32)
+                dx, _, pending = _conv_bn_bwd(rec["r1"], dz1, grads, parts=fz1, dx_out=dxr,
+                                              dx_beta=1.0, fuse_prev=prev3, r16=True)
             else:
                 dx, _, pending = _conv_bn_bwd(rec["r1"], dz1, grads, parts=fz1, dx_out=dres,
-                                              dx_beta=1.0, fuse_prev=prev3)
+                                              dx_beta=1.0, fuse_prev=prev3, r16=True)
             del dz1, dres, rec
             g = dx
             if ready is not None:   # this block's parameter grads are final: start their exchange

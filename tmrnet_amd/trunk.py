@@ -142,8 +142,9 @@ DS_FIRST = os.environ.get("TMR_DS_FIRST", "1") != "0"
 # contract (oracle.emulate_bf16_convs(grads=True)) rounds the gradient at those two points.
 G16 = os.environ.get("TMR_G16", "1") != "0"
 
-# bf16-activation step (ResNet-50 trunk): the residual stream's gradient -- the masked gradient of
-# every Bottleneck's sum bn3(y3) + identity but the last block's -- is stored bf16 too
+# bf16-activation step (ResNet-50 and ResNeSt-50 trunks): the residual stream's gradient -- the
+# masked gradient of every Bottleneck's sum bn3(y3) + identity but the last block's -- is stored
+# bf16 too
 # (TMR_BF16_RESGRAD=0: fp32).  Each block's conv1 dgrad adds its part to the identity branch's
 # gradient (read bf16, or fp32 from the downsample dgrad / the last block), masks it by the previous
 # block's ReLU and rounds once (tmr_conv2d_dgrad_bnbwd_acc); the BN backward of bn3 and of the
