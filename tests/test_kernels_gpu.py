@@ -708,6 +708,72 @@ def test_stem_direct_fwd_bnstats(dev, monkeypatch):
         assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
 
 
+def test_stem16_direct_fwd_bnstats(dev, monkeypatch):
+    """The bf16-activation step's 7x7/2 stem as a direct convolution (stem16.hip: the NHWC4 fp32
+    input rounded to bf16 in LDS, 147 real of 176 reduction rows on v_mfma_f32_32x32x16_bf16, y
+    stored bf16, BatchNorm partials merged per workgroup) against float64 of the bf16-rounded
+    operands (y within one bf16 rounding: the fp32 accumulation order decides ties), its
+    statistics against float64 statistics of its own stored y, and the LDS-DMA engine on the
+    NHWC8 copy (TMR_STEM_DIRECT=0) within one bf16 ulp.  Sixteen frames: 1792 output rows over the
+    768 persistent workgroups, each a contiguous range of 2-3 rows (the input-row ring reused across
+    a range, ranges crossing frame boundaries, statistics merged over a range)."""
+    n = 16
+    g = torch.Generator().manual_seed(14)
+    x = torch.relu(torch.randn(n, 3, 224, 224, generator=g)) + 0.5
+    wt = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    wk4 = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=4, bf16=True)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    y, stats, nparts = ops.conv_fwd_bnstats(x4, wk4, 2, 3, c_real=3, math="bf16", y16=True)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    x8 = ops.nhwc4_to_bf16x8(x4)
+    wk8 = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=8, bf16=True)
+    y0, _, _ = ops.conv_fwd_bnstats(x8, wk8, 2, 3, c_real=3, math="bf16", y16=True)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.bfloat16 and tuple(y.shape) == (n, 112, 112, 64)
+    assert nparts == 4 * 768
+    ref = F.conv2d(x.to(torch.bfloat16).double(), wt.to(torch.bfloat16).double(), stride=2,
+                   padding=3).permute(0, 2, 3, 1)
+    yf = y.double().cpu()
+    # one bf16 ulp of the exact value, plus the fp32 accumulation's absolute error (a result
+    # that cancels to ~1e-6 of the row's magnitude rounds at a finer ulp than that error)
+    ulp = 2.0 ** (torch.floor(torch.log2(ref.abs().clamp_min(1e-30))) - 7)
+    floor = 1e-6 * ref.abs().max().item()
+    assert ((yf - ref).abs() <= ulp * 1.0001 + floor).all()
+    assert ((yf - y0.double().cpu()).abs() <= 2 * ulp * 1.0001 + 2 * floor).all()
+    yd = yf.reshape(-1, 64)
+    ones, zeros = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    rm, rv = zeros.clone(), ones.clone()
+    mean, inv, _, _ = ops.bn_finalize(stats, nparts, ones, zeros, rm, rv, 0.1, 1e-5)
+    assert rel_err(mean, yd.mean(0)) < 1e-6
+    assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
+
+
+def test_stem16_direct_wgrad(dev, monkeypatch):
+    """The bf16 stem's weight gradient as a direct convolution (stem16.hip: per-row im2col and
+    transposed dy in LDS, bf16 MFMA, per-workgroup slabs summed by the tap reduction) against
+    float64 of the bf16 operands, with beta accumulation, and against the engine
+    (TMR_STEM_DIRECT=0).  Sixteen frames: 1792 output rows over the 768 persistent workgroups
+    (contiguous ranges of 2-3 rows: the input-row ring reused, ranges crossing frames)."""
+    n = 16
+    g = torch.Generator().manual_seed(15)
+    x = torch.relu(torch.randn(n, 3, 224, 224, generator=g)) + 0.5
+    dy = torch.randn(n, 64, 112, 112, generator=g).to(torch.bfloat16)
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    dyn = dy.to(dev).permute(0, 2, 3, 1).contiguous()
+    ref = torch.nn.grad.conv2d_weight(x.to(torch.bfloat16).double(), (64, 3, 7, 7), dy.double(),
+                                      stride=2, padding=3)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    dw = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, math="bf16")
+    prev = torch.randn(64, 3, 7, 7, generator=g).to(dev)
+    acc = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, math="bf16", out=prev.clone(), beta=0.5)
+    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    dw0 = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, math="bf16")
+    torch.cuda.synchronize()
+    assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
+    assert rel_err(acc, 0.5 * prev.double().cpu() + ref) < 2e-6
+
+
 @pytest.mark.gpu
 def test_stem_direct_wgrad(dev, monkeypatch):
     """The fp32 stem's weight gradient as a direct convolution (stem.hip: per-workgroup partial

@@ -311,6 +311,7 @@ int tmr_stem_wgrad_bnbwd_slabs(int n, int h, int w, int ho, const float* x, cons
                                const float* dyp, const uint8_t* argmax, int hp, int wp, float* ws,
                                size_t ws_bytes, int* nslabs, hipStream_t stream);
 constexpr long kStemSlabs = 512, kStemSlab = 64 * 49 * 4;   // stem.hip's grid and slab
+constexpr long kStem16Slabs = 768;                            // stem16.hip's grid
 static bool stem_geometry(const tmr_conv_desc* d) {
   return d->math == TMR_MATH_F32 && d->io == 0 &&
          ngroups(d) == 1 && d->c == 4 && d->k == 64 && d->r == 7 && d->s == 7 && d->stride == 2 &&
@@ -320,6 +321,32 @@ static bool stem_geometry(const tmr_conv_desc* d) {
 static bool stem_direct(const tmr_conv_desc* d) {
   return env_int("TMR_STEM_DIRECT", 1) != 0 && stem_geometry(d);
 }
+// the bf16-activation step's stem (stem16.hip): bf16 math on the NHWC4 fp32 input, bf16 KRSC
+// weights (4 or 8 channels per tap), y bf16 with the statistics of the rounded values
+int tmr_stem16_stats_parts(int n, int ho);
+int tmr_stem16_fwd_bnstats(int n, int h, int w, int ho, const float* x, const void* w_krsc, int cp,
+                           void* y, void* stats, hipStream_t stream);
+static bool stem16_geometry(const tmr_conv_desc* d) {
+  return d->math == TMR_MATH_BF16 && d->io == (TMR_IO_W_BF16 | TMR_IO_Y_BF16) &&
+         ngroups(d) == 1 && d->c == 4 && d->k == 64 && d->r == 7 && d->s == 7 && d->stride == 2 &&
+         d->pad == 3 && d->pad_w == 3 && d->wo == 112 && d->w <= 224 && xld_of(d) == 4 &&
+         yld_of(d) == 64 && (d->h + 6 - 7) / 2 + 1 == d->ho;
+}
+static bool stem16_direct(const tmr_conv_desc* d) {
+  return env_int("TMR_STEM_DIRECT", 1) != 0 && stem16_geometry(d);
+}
+// its weight gradient (bf16 dy, the NHWC4 fp32 input)
+int tmr_stem16_wgrad_slabs(int n, int h, int w, int ho, const float* x, const void* dy, int dy32,
+                           float* ws, size_t ws_bytes, int* nslabs, hipStream_t stream);
+// (dy bf16 or fp32: both storages of the bf16-math step take this kernel, so they stay
+// bit-identical)
+static bool stem16_wgrad_geometry(const tmr_conv_desc* d) {
+  return d->math == TMR_MATH_BF16 && (d->io == TMR_IO_DY_BF16 || d->io == 0) && ngroups(d) == 1 &&
+         d->c == 4 &&
+         d->k == 64 && d->r == 7 && d->s == 7 && d->stride == 2 && d->pad == 3 && d->pad_w == 3 &&
+         d->wo == 112 && d->w <= 224 && xld_of(d) == 4 && yld_of(d) == 64 &&
+         (d->h + 6 - 7) / 2 + 1 == d->ho;
+}
 
 TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
   if (!d || d->n <= 0) {
@@ -327,6 +354,7 @@ TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
     return -1;
   }
   if (stem_direct(d)) return 4 * d->n * d->ho;
+  if (stem16_direct(d)) return tmr_stem16_stats_parts(d->n, d->ho);
   tmr_conv_desc g = *d;
   if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
   const int fc = frames_per_launch(&g);
@@ -377,10 +405,12 @@ TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
                 stats_bytes, need);
   // the parts query (above) sized `stats` for the direct stem's row layout: an operand prologue
   // would route the stem to the engine, which writes a different number of partial rows
-  TMR_CHECK_ARG(!(pro && stem_direct(d)),
+  TMR_CHECK_ARG(!(pro && (stem_direct(d) || stem16_direct(d))),
                 "tmr_conv2d_fwd_bnstats: the 7x7 stem takes no operand prologue");
   if (stem_direct(d))
     return tmr_stem_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, y, stats, stream);
+  if (stem16_direct(d))
+    return tmr_stem16_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, 4, y, stats, stream);
   if (ngroups(d) == 1) return fwd_bnstats_impl(d, x, w_krsc, y, (float4*)stats, d->k, pro, stream);
   TMR_CHECK_ARG(!pro, "tmr_conv2d_fwd_bnstats: operand prologues take no groups");
   tmr_conv_desc g;
@@ -711,6 +741,8 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
   size_t bytes = (size_t)sp * slab * sizeof(float);
   if (stem_geometry(d) && bytes < (size_t)kStemSlabs * kStemSlab * sizeof(float))
     bytes = (size_t)kStemSlabs * kStemSlab * sizeof(float);
+  if (stem16_wgrad_geometry(d) && bytes < (size_t)kStem16Slabs * kStemSlab * sizeof(float))
+    bytes = (size_t)kStem16Slabs * kStemSlab * sizeof(float);
   return bytes;
 }
 
@@ -778,9 +810,14 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_wgrad: stored input channels %d must be a power of two >= 4", d->c);
   TMR_CHECK_ARG(c_real >= 1 && c_real <= d->c, "tmr_conv2d_wgrad: bad c_real %d", c_real);
-  if (!pro && c_real == 3 && stem_direct(d)) {
+  const bool s16 = !pro && c_real == 3 && env_int("TMR_STEM_DIRECT", 1) != 0 &&
+                   stem16_wgrad_geometry(d);
+  if (s16 || (!pro && c_real == 3 && stem_direct(d))) {
     int ns = 0;
-    const int rc = tmr_stem_wgrad_slabs(d->n, d->h, d->w, d->ho, x, dy, ws, ws_bytes, &ns, stream);
+    const int rc = s16 ? tmr_stem16_wgrad_slabs(d->n, d->h, d->w, d->ho, x, dy,
+                                                (d->io & TMR_IO_DY_BF16) ? 0 : 1, ws, ws_bytes,
+                                                &ns, stream)
+                       : tmr_stem_wgrad_slabs(d->n, d->h, d->w, d->ho, x, dy, ws, ws_bytes, &ns, stream);
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, 1), dim3(256), 0, stream, ws, ns,
                        kStemSlab, dw_oihw, 49, 4, 3, beta);

@@ -169,6 +169,9 @@ def _dma32(math):
 # bf16 activations: the stem input as NHWC8 bf16 (TMR_BF16_STEM8=0: the NHWC4 fp32 input on the
 # register-staged engine, A/B measurements)
 STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
+# ... unless the direct bf16 stem takes the NHWC4 fp32 input itself (stem16.hip, round 4: 147 of
+# 176 multiplies useful instead of 147 of 392, no NHWC8 copy; TMR_STEM_DIRECT=0 turns it off)
+STEM16 = os.environ.get("TMR_STEM_DIRECT", "1") != "0"
 # fp32 stem backward, TMR_STEM_FUSED=1: the stem conv's weight gradient evaluates its output
 # gradient per row in LDS from the BN backward's inputs (tmr_conv2d_wgrad_stem_bnbwd), so that
 # gradient (2 GB at C2) is never written or read.  Off by default: measured slower than the two
@@ -404,7 +407,7 @@ class TrunkFn(torch.autograd.Function):
         if training:
             # bf16 activations: the stem reads an NHWC8 bf16 copy of its input (8-channel
             # pieces: the LDS-DMA engine; exact, the bf16 math rounds x anyway)
-            xs = ops.nhwc4_to_bf16x8(x4) if (a16 and STEM8) else x4
+            xs = ops.nhwc4_to_bf16x8(x4) if (a16 and STEM8 and not STEM16) else x4
             # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
             # mask from y, so the stem's BN output is never needed)
             y0, sc0, sh0 = _conv_bn(xs, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
