@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 5
+#define TMR_ABI_VERSION 6
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
@@ -119,7 +119,7 @@ int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krs
  * column sums (sum g, sum g*(y - mean)) as float2 [tmr_conv2d_dgrad_bnbwd_parts(d)][c], finished
  * by tmr_bn_bwd_parts.  Removes the separate statistics pass over (dz, y[, z]) of tmr_bn_bwd.
  * dx, y, z dense NHWC (x_ld == c).  mask 3: z is the ReLU mask as bits (tmr_bn_apply_bits /
- * _bits_a16; the LDS-DMA dgrad with transposed weights, TMR_IO_WT_F32 or TMR_IO_WT_BF16, and
+ * tmr_bn_apply2_bits; the LDS-DMA dgrad with transposed weights, TMR_IO_WT_F32 or TMR_IO_WT_BF16, and
  * h*w*c a multiple of 32). */
 int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d);
 int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
@@ -130,35 +130,6 @@ size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d);
 /* dw_oihw[k, c_real, r, s] = beta*dw + sum_m dy[m,k] * im2col(x)[m,(r,s,c)] */
 int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float* dy, float* dw_oihw,
                      int c_real, float beta, float* ws, size_t ws_bytes, hipStream_t stream);
-/* Operand prologues: the BatchNorm around a conv applied while its operands are loaded, so the
- * tensors it would produce are never written to HBM.
- *   x_scale/x_shift: the X operand (forward input, wgrad input) is read as
- *     relu(x * x_scale[c] + x_shift[c]), and as 0 at the zero padding -- the train-mode
- *     BatchNorm + ReLU of the Bottleneck unit that produced x (torchvision Bottleneck bn1/bn2 +
- *     relu, train_only_non-local_pretrained.py:210-213), whose output z = relu(bn(y)) then never
- *     exists: the consumer conv reads y.  Identical values to tmr_bn_apply(y, ..., relu = 1).
- *   dy_y/dy_coef: the dY operand (dgrad and wgrad output gradient) is read as
- *     A[k]*g + B[k]*y + C[k] (fmaf(A, g, fmaf(B, y, C))), g = the ReLU-masked gradient at this
- *     conv's BatchNorm output, y = this conv's pre-BN output, coef = [3][k] from
- *     tmr_bn_bwd_coefs(_dense) -- the BatchNorm backward, whose dy then never exists.  Identical
- *     values to the apply pass of tmr_bn_bwd_parts.
- * Either half may be NULL; dense NHWC operands only (x_ld == c, y_ld == k). */
-typedef struct tmr_conv_prologue {
-  const float* x_scale;
-  const float* x_shift;
-  const float* dy_y;
-  const float* dy_coef;
-} tmr_conv_prologue;
-int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x, const float* w_krsc,
-                               float* y, void* stats, size_t stats_bytes,
-                               const tmr_conv_prologue* pro, hipStream_t stream);
-int tmr_conv2d_dgrad_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
-                         float beta, const tmr_conv_prologue* pro, hipStream_t stream);
-int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
-                               float* dx, float beta, const float* y, const float* z,
-                               const float* scale, const float* shift, const float* mean,
-                               int mask, void* parts, size_t parts_bytes,
-                               const tmr_conv_prologue* pro, hipStream_t stream);
 /* tmr_conv2d_dgrad_bnbwd with the beta operand read from dx_old (fp32, or bf16 when old_bf16)
  * instead of dx, and dx written as bf16 (TMR_IO_G16, bf16 math on the LDS-DMA engine): the
  * Bottleneck's conv1 dgrad adding into the residual stream's gradient -- the sum of the identity
@@ -170,9 +141,6 @@ int tmr_conv2d_dgrad_bnbwd_acc(const tmr_conv_desc* d, const float* dy, const fl
                                const float* y, const float* z, const float* scale,
                                const float* shift, const float* mean, int mask, void* parts,
                                size_t parts_bytes, hipStream_t stream);
-int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy, float* dw_oihw,
-                         int c_real, float beta, float* ws, size_t ws_bytes,
-                         const tmr_conv_prologue* pro, hipStream_t stream);
 /* C[M][N] = beta*C + A[M][K] * B[N][K]^T (+bias) */
 int tmr_gemm_nt(int M, int N, int K, const float* A, int lda, const float* B, int ldb,
                 const float* bias, float* C, int ldc, float beta, hipStream_t stream);
@@ -281,20 +249,6 @@ int tmr_bn_bwd_parts(const float* g, const float* y, const void* parts, int npar
                      const float* save_mean, const float* save_invstd, const float* gamma,
                      float* dy, float* dgamma, float* dbeta, int rows, int c, void* ws,
                      size_t ws_bytes, hipStream_t stream);
-/* BatchNorm backward as per-channel coefficients, for a dY-operand prologue (the apply pass is
- * folded into the consumer convs): coef = [3][c] with dy = fmaf(A, g, fmaf(B, y, C));
- * dgamma / dbeta as tmr_bn_bwd.  From the fused-dgrad partials (g already masked; ws >=
- * tmr_bn_parts_ws_bytes(nparts, c)), or from g itself (one reduction pass over g and y, the ReLU
- * mask -- z > 0 or y*scale+shift > 0 -- applied to g IN PLACE when relu; ws >=
- * tmr_bn_ws_bytes(rows, c)). */
-int tmr_bn_bwd_coefs(const void* parts, int nparts, const float* save_mean,
-                     const float* save_invstd, const float* gamma, float* coef, float* dgamma,
-                     float* dbeta, int rows, int c, void* ws, size_t ws_bytes,
-                     hipStream_t stream);
-int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, const float* scale,
-                           const float* shift, const float* save_mean, const float* save_invstd,
-                           const float* gamma, float* coef, float* dgamma, float* dbeta, int rows,
-                           int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream);
 int tmr_bn_bwd(const float* dz, const float* y, const float* z, const float* scale,
                const float* shift, const float* save_mean, const float* save_invstd,
                const float* gamma, float* dy, float* dres, float* dgamma, float* dbeta, int rows,
@@ -319,24 +273,6 @@ int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n, int h, 
                          const float* save_mean, const float* save_invstd, const float* gamma,
                          void* dy, float* dgamma, float* dbeta, int c, void* ws, size_t ws_bytes,
                          int out_bf16, hipStream_t stream);
-/* The fp32 stem's backward without its output gradient in HBM (round 3; autograd of share.conv1 /
- * bn1 / relu / maxpool, train_only_non-local_pretrained.py:204-214, run by loss.backward() :724):
- * tmr_bn_bwd_maxpool_coefs is tmr_bn_bwd_maxpool up to the BN-backward coefficients coef[3][c]
- * (dy = A*g + B*y + C, g the maxpool-gathered, ReLU-masked gradient) and dgamma / dbeta, with no
- * dy pass; tmr_conv2d_wgrad_stem_bnbwd is the stem conv's weight gradient with that dy evaluated
- * per output row in LDS from (pooled gradient dyp (n, ho_p, wo_p, 64), argmax, y, scale, shift,
- * coef) -- the direct stem geometry only (x NHWC4 fp32 (n, h, w <= 226, 4), 64 filters 7x7/2,
- * pad 3, 112 output columns); ws from tmr_conv2d_wgrad_ws_bytes. */
-int tmr_bn_bwd_maxpool_coefs(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho,
-                             int wo, const float* y, const float* scale, const float* shift,
-                             const float* save_mean, const float* save_invstd, const float* gamma,
-                             float* coef, float* dgamma, float* dbeta, int c, void* ws,
-                             size_t ws_bytes, hipStream_t stream);
-int tmr_conv2d_wgrad_stem_bnbwd(const tmr_conv_desc* d, const float* x, const float* y,
-                                const float* scale, const float* shift, const float* coef,
-                                const float* dyp, const uint8_t* argmax, int ho_p, int wo_p,
-                                float* dw_oihw, float beta, float* ws, size_t ws_bytes,
-                                hipStream_t stream);
 int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, int r, int s, int cpad,
                               int out_bf16, hipStream_t stream);
 /* bf16 operands of the LDS-DMA conv engine (every operand of a bf16-math conv stored bf16):
@@ -375,15 +311,6 @@ int tmr_bn_apply_a16(const void* y, const float* scale, const float* shift, cons
 int tmr_bn_apply2_a16(const void* y, const float* scale, const float* shift, const void* yr,
                       const float* rscale, const float* rshift, void* z, int rows, int c, int relu,
                       hipStream_t stream);
-/* tmr_bn_apply_bits / tmr_bn_apply2_bits for bf16 activations: z bf16 and its ReLU mask as bits
- * (taken from the rounded z, so mask 3 equals the mask-1 test z > 0) for the residual-gradient
- * dgrads of the bf16 LDS-DMA engine (TMR_IO_WT_BF16, mask 3) */
-int tmr_bn_apply_bits_a16(const void* y, const float* scale, const float* shift,
-                          const void* residual, void* z, uint32_t* bits, int rows, int c,
-                          hipStream_t stream);
-int tmr_bn_apply2_bits_a16(const void* y, const float* scale, const float* shift, const void* yr,
-                           const float* rscale, const float* rshift, void* z, uint32_t* bits,
-                           int rows, int c, hipStream_t stream);
 int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const float* scale,
                    const float* shift, const float* save_mean, const float* save_invstd,
                    const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta, int rows,

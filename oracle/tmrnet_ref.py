@@ -148,7 +148,7 @@ class Bottleneck(nn.Module):
         out = self.bn3(self.conv3(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        out = self.relu(out + identity)
+        out = _act(self, out + identity)
         if getattr(self, "round_out", False) and self.training:   # emulate_bf16_convs(activations)
             out = _RoundFn.apply(out)
         if getattr(self, "round_res_grad", False) and self.training:
@@ -156,6 +156,18 @@ class Bottleneck(nn.Module):
             # ReLU, is stored bf16 -- mask * round(g) == round(mask * g)
             out = _GradRoundFn.apply(out)
         return out
+
+
+def _act(blk, v):
+    """The block output ReLU; with `blk.forced_act` set (a 0/1 tensor of v's shape, test
+    instrumentation) the given active set instead -- v * act, the ReLU's value and gradient on
+    that set.  The geometry tests force the HIP step's own last-block active set on both oracles,
+    as they do for the head ReLU (tests/test_geometry_gpu.py)."""
+    act = getattr(blk, "forced_act", None)
+    if act is None:
+        return blk.relu(v)
+    blk.pre_act = v.detach()   # (the tests count the elements the forced set moves)
+    return v * act.to(v.dtype)
 
 
 def make_layer(inplanes, planes, blocks, stride):
@@ -255,7 +267,7 @@ class BottleneckS(nn.Module):
                 out = _RoundFn.apply(out)
         out = self.bn3(self.conv3(out))
         res = self.downsample(x) if self.downsample is not None else x
-        out = self.relu(out + res)
+        out = _act(self, out + res)
         out = _RoundFn.apply(out) if rnd else out
         if getattr(self, "round_res_grad", False) and self.training:   # trunk.R16, as Bottleneck
             out = _GradRoundFn.apply(out)

@@ -10,8 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "tmrnet_amd", "libtmr.so")
 
 
-def header_symbols():
-    src = open(os.path.join(ROOT, "include", "tmr.h")).read()
+def header_symbols(name="tmr.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(tmr_[a-z0-9_]+)\s*\(", src)))
 
@@ -33,12 +33,24 @@ def test_library_exports_every_declared_symbol(built):
 def test_python_binding_covers_header(built):
     from tmrnet_amd import _lib
     assert sorted(_lib.SIGNATURES) == header_symbols()
+    assert sorted(_lib.PROLOGUE_SIGNATURES) == header_symbols("tmr_prologue.h")
+
+
+def test_retired_prologues_absent_from_default_library(built):
+    """The operand prologues (include/tmr_prologue.h, measured slower) are an A/B build only:
+    the product library exports none of their entry points and the binding reports them absent."""
+    from tmrnet_amd import _lib
+    out = subprocess.check_output(["nm", "-D", "--defined-only", built]).decode()
+    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    assert not set(header_symbols("tmr_prologue.h")) & exported
+    if os.path.abspath(_lib.LIB_PATH) == os.path.abspath(built):
+        assert not _lib.has_prologues()
 
 
 def test_library_loads_and_reports_version(built):
     from tmrnet_amd import _lib
     h = _lib.lib()
-    assert h.tmr_abi_version() == 5
+    assert h.tmr_abi_version() == 6
     assert isinstance(h.tmr_last_error(), bytes)
 
 
@@ -103,10 +115,6 @@ def test_stem_entry_points_host_checks(built):
     from tmrnet_amd import _lib, ops
     d = ops.conv_desc(640, 224, 224, 4, 64, 7, 7, 2, 3)
     assert _lib.query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d)) >= 512 * 64 * 49 * 4 * 4
-    d3 = ops.conv_desc(8, 56, 56, 64, 64, 3, 3, 1, 1)
-    with pytest.raises(RuntimeError, match="not the fp32 7x7/2 stem geometry"):
-        _lib.call("tmr_conv2d_wgrad_stem_bnbwd", ctypes.byref(d3), *([None] * 7), 28, 28, None,
-                  0.0, None, 0, None)
-    with pytest.raises(RuntimeError, match="null coef"):
-        _lib.call("tmr_bn_bwd_maxpool_coefs", None, None, 2, 112, 112, 56, 56, *([None] * 6), None,
-                  None, None, 64, None, 0, None)
+    # the bf16 stem's (stem16.hip) slabs: 768 persistent workgroups
+    d16 = ops.conv_desc(640, 224, 224, 4, 64, 7, 7, 2, 3, math="bf16", io=ops.IO_DY)
+    assert _lib.query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d16)) >= 768 * 64 * 49 * 4 * 4

@@ -57,18 +57,11 @@ SIGNATURES = {
     "tmr_conv2d_dgrad_bnbwd": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, P],
     "tmr_conv2d_wgrad_ws_bytes": [DP],
     "tmr_conv2d_wgrad": [DP, P, P, P, I, F, P, SZ, P],
-    "tmr_conv2d_fwd_bnstats_pro": [DP, P, P, P, P, SZ, PP, P],
-    "tmr_conv2d_dgrad_pro": [DP, P, P, P, F, PP, P],
-    "tmr_conv2d_dgrad_bnbwd_pro": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, PP, P],
     "tmr_conv2d_dgrad_bnbwd_acc": [DP, P, P, P, F, P, I, P, P, P, P, P, I, P, SZ, P],
-    "tmr_conv2d_wgrad_pro": [DP, P, P, P, I, F, P, SZ, PP, P],
-    "tmr_bn_bwd_coefs": [P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_apply_x": [P, P, P, P, P, I, I, I, I, P],
     "tmr_bn_bwd_parts_x": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, I, P],
     "tmr_bn_bwd_x": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, I, P],
     "tmr_bn_bwd_maxpool_x": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, I, P],
-    "tmr_bn_bwd_maxpool_coefs": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
-    "tmr_conv2d_wgrad_stem_bnbwd": [DP, P, P, P, P, P, P, P, I, I, P, F, P, SZ, P],
     "tmr_weight_oihw_to_krsc_x": [P, P, I, I, I, I, I, I, P],
     "tmr_weight_oihw_to_crsk_x": [P, P, I, I, I, I, I, P],
     "tmr_bn_apply_dual": [P, P, P, P, P, P, I, I, I, P],
@@ -78,8 +71,6 @@ SIGNATURES = {
     "tmr_maxpool2d_fwd_bn_x": [P, P, P, P, P, I, I, I, I, I, I, I, P],
     "tmr_bn_apply_a16": [P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2_a16": [P, P, P, P, P, P, P, I, I, I, P],
-    "tmr_bn_apply_bits_a16": [P, P, P, P, P, P, I, I, P],
-    "tmr_bn_apply2_bits_a16": [P, P, P, P, P, P, P, P, I, I, P],
     "tmr_bn_bwd_a16": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_a16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_g16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
@@ -94,7 +85,6 @@ SIGNATURES = {
     "tmr_resize_coeffs": [I, I, P, P, I],
     "tmr_resize_tmp_bytes": [I, I, I, I, I],
     "tmr_resize_u8": [P, I, I, I, P, SZ, P, I, I, P, P, I, P, P, I, I, I, P],
-    "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_gemm_nt": [I, I, I, P, I, P, I, P, P, I, F, P],
     "tmr_gemm_nn": [I, I, I, P, I, P, I, P, I, F, P],
     "tmr_gemm_tn": [I, I, I, P, I, P, I, P, I, F, P],
@@ -177,6 +167,16 @@ SIGNATURES = {
     "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],
     "tmr_lstm_cell_bwd": [P, I, P, P, P, P, P, P, I, P, I, I, P],
 }
+# include/tmr_prologue.h: the retired operand-prologue experiment, bound only when the loaded
+# library is the A/B build (`make PROLOGUES=1` -> libtmr_pro.so)
+PROLOGUE_SIGNATURES = {
+    "tmr_conv2d_fwd_bnstats_pro": [DP, P, P, P, P, SZ, PP, P],
+    "tmr_conv2d_dgrad_pro": [DP, P, P, P, F, PP, P],
+    "tmr_conv2d_dgrad_bnbwd_pro": [DP, P, P, P, F, P, P, P, P, P, I, P, SZ, PP, P],
+    "tmr_conv2d_wgrad_pro": [DP, P, P, P, I, F, P, SZ, PP, P],
+    "tmr_bn_bwd_coefs": [P, I, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
+}
 _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,
     "tmr_clear_error": None,
@@ -210,8 +210,18 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        for name, args in PROLOGUE_SIGNATURES.items():
+            if hasattr(h, name):
+                fn = getattr(h, name)
+                fn.argtypes = args
+                fn.restype = ctypes.c_int
         _lib = h
     return _lib
+
+
+def has_prologues():
+    """True when the loaded library is the operand-prologue A/B build (include/tmr_prologue.h)."""
+    return all(hasattr(lib(), n) for n in PROLOGUE_SIGNATURES)
 
 
 def exported_symbols():

@@ -979,40 +979,6 @@ TMR_API int tmr_bn_apply2_bits(const float* y, const float* scale, const float* 
   return 0;
 }
 
-TMR_API int tmr_bn_apply_bits_a16(const void* y, const float* scale, const float* shift,
-                                  const void* residual, void* z, uint32_t* bits, int rows, int c,
-                                  hipStream_t stream) {
-  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && z && bits,
-                "tmr_bn_apply_bits_a16: null operand or channels %d not a multiple of 4", c);
-  const long n4 = (long)rows * c / 4;
-  if (n4 == 0) return 0;
-  const __bf16* yb = (const __bf16*)y;
-  if (residual)
-    hipLaunchKernelGGL((bn_apply_bits_k<true, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, yb,
-                       scale, shift, (const __bf16*)residual, nullptr, nullptr, nullptr, (__bf16*)z,
-                       bits, n4, c / 4);
-  else
-    hipLaunchKernelGGL((bn_apply_bits_k<false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, yb,
-                       scale, shift, nullptr, nullptr, nullptr, nullptr, (__bf16*)z, bits, n4, c / 4);
-  TMR_CHECK_LAUNCH("bn_apply_bits_a16");
-  return 0;
-}
-
-TMR_API int tmr_bn_apply2_bits_a16(const void* y, const float* scale, const float* shift,
-                                   const void* yr, const float* rscale, const float* rshift,
-                                   void* z, uint32_t* bits, int rows, int c, hipStream_t stream) {
-  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && yr && rscale && rshift && z && bits,
-                "tmr_bn_apply2_bits_a16: null operand or channels %d not a multiple of 4", c);
-  TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_bits_a16: the branch input must not alias z");
-  const long n4 = (long)rows * c / 4;
-  if (n4 == 0) return 0;
-  hipLaunchKernelGGL((bn_apply_bits_k<false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream,
-                     (const __bf16*)y, scale, shift, nullptr, (const __bf16*)yr, rscale, rshift,
-                     (__bf16*)z, bits, n4, c / 4);
-  TMR_CHECK_LAUNCH("bn_apply2_bits_a16");
-  return 0;
-}
-
 TMR_API int tmr_bn_apply_dual(const float* y, const float* scale, const float* shift,
                               const float* residual, float* z, void* z16, int rows, int c, int relu,
                               hipStream_t stream) {
@@ -1125,18 +1091,6 @@ TMR_API int tmr_bn_bwd_maxpool_x(const float* dyp, const uint8_t* argmax, int n,
                              nullptr, stream);
 }
 
-TMR_API int tmr_bn_bwd_maxpool_coefs(const float* dyp, const uint8_t* argmax, int n, int h, int w,
-                                     int ho, int wo, const float* y, const float* scale,
-                                     const float* shift, const float* save_mean,
-                                     const float* save_invstd, const float* gamma, float* coef,
-                                     float* dgamma, float* dbeta, int c, void* ws,
-                                     size_t ws_bytes, hipStream_t stream) {
-  TMR_CHECK_ARG(coef, "tmr_bn_bwd_maxpool_coefs: null coef");
-  return bn_bwd_maxpool_impl(dyp, argmax, n, h, w, ho, wo, y, scale, shift, save_mean,
-                             save_invstd, gamma, nullptr, dgamma, dbeta, c, ws, ws_bytes, 0, coef,
-                             stream);
-}
-
 static int bn_bwd_maxpool_impl(const float* dyp, const uint8_t* argmax, int n, int h, int w,
                                int ho, int wo, const float* y, const float* scale,
                                const float* shift, const float* save_mean,
@@ -1216,6 +1170,7 @@ TMR_API int tmr_bn_bwd_parts_x(const float* g, const float* y, const void* parts
   return 0;
 }
 
+#if TMR_PROLOGUES   // include/tmr_prologue.h: the retired operand-prologue A/B build
 // ---- BatchNorm backward as per-channel coefficients (the apply folded into the consumer GEMMs) --
 // dy = fmaf(A[c], g, fmaf(B[c], y, C[c])) -- the arithmetic of bn_bwd_apply -- is evaluated by
 // the dgrad / wgrad operand loaders (tmr_conv_prologue.dy_coef = coef [3][c]), so dy is never
@@ -1270,6 +1225,7 @@ TMR_API int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, con
   TMR_CHECK_LAUNCH("bn_bwd_final");
   return 0;
 }
+#endif
 
 // ---- bf16-activation forms (TMR_MATH_BF16 train step, include/tmr.h "_a16"): y, z and the
 // residual are bf16 tensors (the conv outputs rounded by their epilogue, the BN outputs rounded

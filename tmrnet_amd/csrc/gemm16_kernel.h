@@ -1009,8 +1009,9 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   const int bk = f32 ? 32 : 64;
   const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
+#if TMR_PROLOGUES
   if constexpr (F32 != 0) {
-    // prologue variants (fp32 only): FWD X, DGRAD dY, WGRAD dY / dY + X
+    // prologue variants (fp32 only, A/B build): FWD X, DGRAD dY, WGRAD dY / dY + X
     if (a.pro) {
       if constexpr (MODE == MODE_FWD) return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
       if constexpr (MODE == MODE_DGRAD) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
@@ -1021,6 +1022,7 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
       }
     }
   }
+#endif
   return launch16_switch<MODE, F32, 0>(a, cfg, tapv, grid, st);
 }
 

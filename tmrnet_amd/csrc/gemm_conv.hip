@@ -5,6 +5,22 @@
 
 using namespace tmrg;
 
+// the prologue forms behind the plain entry points (pro = nullptr); exported as the
+// include/tmr_prologue.h entry points in the A/B build only (TMR_PROLOGUES, end of file)
+static int conv_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x, const float* w_krsc,
+                                float* y, void* stats, size_t stats_bytes,
+                                const tmr_conv_prologue* pro, hipStream_t stream);
+static int conv_dgrad_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc, float* dx,
+                          float beta, const tmr_conv_prologue* pro, hipStream_t stream);
+static int conv_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                                float* dx, float beta, const float* y, const float* z,
+                                const float* scale, const float* shift, const float* mean,
+                                int mask, void* parts, size_t parts_bytes,
+                                const tmr_conv_prologue* pro, hipStream_t stream);
+static int conv_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy,
+                          float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
+                          const tmr_conv_prologue* pro, hipStream_t stream);
+
 namespace {
 
 // sum over the split slabs in split order, loads issued 8 at a time (the adds stay in order, so
@@ -130,6 +146,9 @@ void set_grid(GemmArgs& a, int n, int hg, int wg) {
 int set_prologue(GemmArgs& a, const tmr_conv_prologue* pro, const tmr_conv_desc* d, bool x_ok,
                  bool dy_ok, long y_off) {
   if (!pro) return 0;
+#if !TMR_PROLOGUES
+  TMR_CHECK_ARG(false, "tmr_conv2d: operand prologues exist in the A/B build only (TMR_PROLOGUES)");
+#endif
   if (pro->x_scale || pro->x_shift) {
     TMR_CHECK_ARG(x_ok, "tmr_conv2d: an X-operand prologue applies to the forward and wgrad views");
     TMR_CHECK_ARG(pro->x_scale && pro->x_shift, "tmr_conv2d: X prologue needs scale and shift");
@@ -302,14 +321,11 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
 // (tap, channel) pairs (stem.hip): a partial row per output row and wave; its weight gradient too
 // (partial slabs per workgroup, reduced by wgrad_reduce_taps_kernel).  TMR_STEM_DIRECT=0: the
 // implicit-GEMM engine (A/B, tests).
+int tmr_stem_stats_parts(int n, int ho);
 int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const float* w_krsc,
                          float* y, void* stats, hipStream_t stream);
 int tmr_stem_wgrad_slabs(int n, int h, int w, int ho, const float* x, const float* dy, float* ws,
                          size_t ws_bytes, int* nslabs, hipStream_t stream);
-int tmr_stem_wgrad_bnbwd_slabs(int n, int h, int w, int ho, const float* x, const float* y,
-                               const float* scale, const float* shift, const float* coef,
-                               const float* dyp, const uint8_t* argmax, int hp, int wp, float* ws,
-                               size_t ws_bytes, int* nslabs, hipStream_t stream);
 constexpr long kStemSlabs = 512, kStemSlab = 64 * 49 * 4;   // stem.hip's grid and slab
 constexpr long kStem16Slabs = 768;                            // stem16.hip's grid
 static bool stem_geometry(const tmr_conv_desc* d) {
@@ -353,7 +369,7 @@ TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
     tmr_set_error("tmr_conv2d_fwd_stats_parts: null or empty descriptor");
     return -1;
   }
-  if (stem_direct(d)) return 4 * d->n * d->ho;
+  if (stem_direct(d)) return tmr_stem_stats_parts(d->n, d->ho);
   if (stem16_direct(d)) return tmr_stem16_stats_parts(d->n, d->ho);
   tmr_conv_desc g = *d;
   if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
@@ -368,7 +384,7 @@ TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
 
 TMR_API int tmr_conv2d_fwd_bnstats(const tmr_conv_desc* d, const float* x, const float* w_krsc,
                                    float* y, void* stats, size_t stats_bytes, hipStream_t stream) {
-  return tmr_conv2d_fwd_bnstats_pro(d, x, w_krsc, y, stats, stats_bytes, nullptr, stream);
+  return conv_fwd_bnstats_pro(d, x, w_krsc, y, stats, stats_bytes, nullptr, stream);
 }
 
 // stats: partial rows of part_ld columns (this launch's k columns at the pointer)
@@ -392,10 +408,10 @@ static int fwd_bnstats_impl(const tmr_conv_desc* d, const float* x, const float*
   return 0;
 }
 
-TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
-                                       const float* w_krsc, float* y, void* stats,
-                                       size_t stats_bytes, const tmr_conv_prologue* pro,
-                                       hipStream_t stream) {
+static int conv_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
+                                const float* w_krsc, float* y, void* stats,
+                                size_t stats_bytes, const tmr_conv_prologue* pro,
+                                hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd_bnstats: null descriptor");
   TMR_CHECK_ARG(yld_of(d) == d->k, "tmr_conv2d_fwd_bnstats: output must be dense (y_ld == k)");
   const int np = tmr_conv2d_fwd_stats_parts(d);
@@ -568,7 +584,7 @@ TMR_API int tmr_conv2d_dgrad_bnbwd(const tmr_conv_desc* d, const float* dy, cons
                                    float* dx, float beta, const float* y, const float* z,
                                    const float* scale, const float* shift, const float* mean,
                                    int mask, void* parts, size_t parts_bytes, hipStream_t stream) {
-  return tmr_conv2d_dgrad_bnbwd_pro(d, dy, w_krsc, dx, beta, y, z, scale, shift, mean, mask, parts,
+  return conv_dgrad_bnbwd_pro(d, dy, w_krsc, dx, beta, y, z, scale, shift, mean, mask, parts,
                                     parts_bytes, nullptr, stream);
 }
 
@@ -578,12 +594,12 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
                              const float* shift, const float* mean, int mask, void* parts,
                              size_t parts_bytes, const tmr_conv_prologue* pro, hipStream_t stream);
 
-TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
-                                       const float* w_krsc, float* dx, float beta, const float* y,
-                                       const float* z, const float* scale, const float* shift,
-                                       const float* mean, int mask, void* parts,
-                                       size_t parts_bytes, const tmr_conv_prologue* pro,
-                                       hipStream_t stream) {
+static int conv_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
+                                const float* w_krsc, float* dx, float beta, const float* y,
+                                const float* z, const float* scale, const float* shift,
+                                const float* mean, int mask, void* parts,
+                                size_t parts_bytes, const tmr_conv_prologue* pro,
+                                hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd: null descriptor");
   // in place: a bf16 gradient (TMR_IO_G16) accumulates into its own bf16 values
   return dgrad_bnbwd_entry(d, dy, w_krsc, dx, beta, nullptr, (d->io & TMR_IO_G16) ? 1 : 0, y, z,
@@ -657,19 +673,19 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
 
 TMR_API int tmr_conv2d_dgrad(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
                              float* dx, float beta, hipStream_t stream) {
-  return tmr_conv2d_dgrad_pro(d, dy, w_krsc, dx, beta, nullptr, stream);
+  return conv_dgrad_pro(d, dy, w_krsc, dx, beta, nullptr, stream);
 }
 
-TMR_API int tmr_conv2d_dgrad_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
-                                 float* dx, float beta, const tmr_conv_prologue* pro,
-                                 hipStream_t stream) {
+static int conv_dgrad_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                          float* dx, float beta, const tmr_conv_prologue* pro,
+                          hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_dgrad: null descriptor");
   if (ngroups(d) > 1) {
     TMR_CHECK_ARG(!pro, "tmr_conv2d_dgrad: operand prologues take no groups");
     tmr_conv_desc g;
     if (group_split(d, g)) return 1;
     for (int i = 0; i < d->groups; ++i) {
-      const int rc = tmr_conv2d_dgrad_pro(&g, adv(dy, (long)i * g.k, esz_dy(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
+      const int rc = conv_dgrad_pro(&g, adv(dy, (long)i * g.k, esz_dy(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
                                           dx + (long)i * g.c, beta, nullptr, stream);
       if (rc) return rc;
     }
@@ -754,20 +770,20 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
 TMR_API int tmr_conv2d_wgrad(const tmr_conv_desc* d, const float* x, const float* dy,
                              float* dw_oihw, int c_real, float beta, float* ws, size_t ws_bytes,
                              hipStream_t stream) {
-  return tmr_conv2d_wgrad_pro(d, x, dy, dw_oihw, c_real, beta, ws, ws_bytes, nullptr, stream);
+  return conv_wgrad_pro(d, x, dy, dw_oihw, c_real, beta, ws, ws_bytes, nullptr, stream);
 }
 
-TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy,
-                                 float* dw_oihw, int c_real, float beta, float* ws,
-                                 size_t ws_bytes, const tmr_conv_prologue* pro,
-                                 hipStream_t stream) {
+static int conv_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy,
+                          float* dw_oihw, int c_real, float beta, float* ws,
+                          size_t ws_bytes, const tmr_conv_prologue* pro,
+                          hipStream_t stream) {
   TMR_CHECK_ARG(d, "tmr_conv2d_wgrad: null descriptor");
   if (ngroups(d) > 1) {   // c_real = real input channels per group; dw (k, c_real, r, s)
     TMR_CHECK_ARG(!pro, "tmr_conv2d_wgrad: operand prologues take no groups");
     tmr_conv_desc g;
     if (group_split(d, g)) return 1;
     for (int i = 0; i < d->groups; ++i) {
-      const int rc = tmr_conv2d_wgrad_pro(&g, adv(x, (long)i * g.c, esz_x(d)), adv(dy, (long)i * g.k, esz_dy(d)),
+      const int rc = conv_wgrad_pro(&g, adv(x, (long)i * g.c, esz_x(d)), adv(dy, (long)i * g.k, esz_dy(d)),
                                           dw_oihw + (long)i * g.k * c_real * g.r * g.s, c_real,
                                           beta, ws, ws_bytes, nullptr, stream);
       if (rc) return rc;
@@ -783,23 +799,6 @@ TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const f
                              f0 == 0 ? beta : 1.f, ws, ws_bytes, stream, pro ? &pc : nullptr);
     if (rc) return rc;
   }
-  return 0;
-}
-
-TMR_API int tmr_conv2d_wgrad_stem_bnbwd(const tmr_conv_desc* d, const float* x, const float* y,
-                                        const float* scale, const float* shift, const float* coef,
-                                        const float* dyp, const uint8_t* argmax, int ho_p,
-                                        int wo_p, float* dw_oihw, float beta, float* ws,
-                                        size_t ws_bytes, hipStream_t stream) {
-  TMR_CHECK_ARG(d && stem_geometry(d) && ngroups(d) == 1,
-                "tmr_conv2d_wgrad_stem_bnbwd: not the fp32 7x7/2 stem geometry");
-  int ns = 0;
-  const int rc = tmr_stem_wgrad_bnbwd_slabs(d->n, d->h, d->w, d->ho, x, y, scale, shift, coef,
-                                            dyp, argmax, ho_p, wo_p, ws, ws_bytes, &ns, stream);
-  if (rc) return rc;
-  hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, 1), dim3(256), 0, stream, ws, ns,
-                     kStemSlab, dw_oihw, 49, 4, 3, beta);
-  TMR_CHECK_LAUNCH("wgrad_reduce_taps_kernel");
   return 0;
 }
 
@@ -918,3 +917,35 @@ TMR_API int tmr_gemm_tn(int M, int N, int K, const float* A, int lda, const floa
             N % 4 == 0;
   return launch_gemm<MODE_WGRAD>(a, al, 1, stream);
 }
+
+#if TMR_PROLOGUES
+TMR_API int tmr_conv2d_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
+                                       const float* w_krsc, float* y, void* stats,
+                                       size_t stats_bytes, const tmr_conv_prologue* pro,
+                                       hipStream_t stream) {
+  return conv_fwd_bnstats_pro(d, x, w_krsc, y, stats, stats_bytes, pro, stream);
+}
+
+TMR_API int tmr_conv2d_dgrad_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                                 float* dx, float beta, const tmr_conv_prologue* pro,
+                                 hipStream_t stream) {
+  return conv_dgrad_pro(d, dy, w_krsc, dx, beta, pro, stream);
+}
+
+TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
+                                       const float* w_krsc, float* dx, float beta, const float* y,
+                                       const float* z, const float* scale, const float* shift,
+                                       const float* mean, int mask, void* parts,
+                                       size_t parts_bytes, const tmr_conv_prologue* pro,
+                                       hipStream_t stream) {
+  return conv_dgrad_bnbwd_pro(d, dy, w_krsc, dx, beta, y, z, scale, shift, mean, mask, parts,
+                              parts_bytes, pro, stream);
+}
+
+TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy,
+                                 float* dw_oihw, int c_real, float beta, float* ws,
+                                 size_t ws_bytes, const tmr_conv_prologue* pro,
+                                 hipStream_t stream) {
+  return conv_wgrad_pro(d, x, dy, dw_oihw, c_real, beta, ws, ws_bytes, pro, stream);
+}
+#endif

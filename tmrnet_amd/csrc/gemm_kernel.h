@@ -25,7 +25,7 @@
 // k-tile).  LDS tiles are k-major ([16][BM+pad]) so each MFMA operand read is a
 // conflict-free ds_read_b32 of 32 consecutive floats per half-wave.
 #include "common.h"
-#include "tmr.h"
+#include "tmr_prologue.h"
 #include <stdlib.h>
 
 namespace tmrg {
@@ -1274,7 +1274,8 @@ int launch_cfg(const GemmArgs& a, int var, dim3 grid, hipStream_t st) {
       return 0;
     }
   }
-  if (a.pro) {   // operand prologues (var == 0, checked by launch_gemm_t)
+#if TMR_PROLOGUES
+  if (a.pro) {   // operand prologues (var == 0, checked by launch_gemm_t; A/B build only)
     if constexpr (MODE == MODE_FWD) {
       hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 0, PREC, 1>), grid, blk, 0, st, a);
     } else if constexpr (MODE == MODE_DGRAD) {
@@ -1290,6 +1291,7 @@ int launch_cfg(const GemmArgs& a, int var, dim3 grid, hipStream_t st) {
     TMR_CHECK_LAUNCH("gemm_kernel");
     return 0;
   }
+#endif
   if (var == 2)
     hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, BKT, 2, PREC>), grid, blk, 0, st, a);
   else if (MODE == MODE_FWD && var == 1)

@@ -15,8 +15,9 @@
 //   * weights k-major: W[k][co], k = (kh * 7 + kw) * 3 + c (148 rows, the last 0);
 //   * v_mfma_f32_32x32x2_f32, each wave 32 output pixels x 64 channels, 74 k-steps;
 //   * epilogue: y (NHWC, 64 channels) and each wave's BatchNorm partial (n, mean, M2) per channel
-//     over its 32 (last wave: 16) pixels -- the conv epilogue's statistics format, combined by
-//     tmr_bn_finalize -- with no cross-wave exchange, so a row needs a single barrier.
+//     over its 32 (last wave: 16) pixels, merged over the workgroup's rows (Chan, in double) --
+//     the conv epilogue's statistics format, combined by tmr_bn_finalize -- with no cross-wave
+//     exchange, so a row needs a single barrier.
 #include "common.h"
 #include "tmr.h"
 
@@ -89,6 +90,9 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_k(const float* __restrict__ x
   const int ow = 32 * wave + l31;
   const int owc = ow < SW ? ow : SW - 1;   // clamped read (rows >= 112 are dropped)
   const int cnt = wave == 3 ? SW - 96 : 32;   // this wave's valid output pixels
+  // running BatchNorm statistics of this wave's pixels over the workgroup's rows (Chan, double,
+  // fixed row order): one partial row per wave of the grid (not one per output row)
+  double rn = 0.0, rm0 = 0.0, rq0 = 0.0, rm1 = 0.0, rq1 = 0.0;
   int row = blockIdx.x, buf = 0;
   if (row < rows) fetch(row);
   for (; row < rows; row += gridDim.x, buf ^= 1) {
@@ -140,9 +144,18 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_k(const float* __restrict__ x
     }
     q0 += __shfl_xor(q0, 32, 64);
     q1 += __shfl_xor(q1, 32, 64);
-    float4* st = stats + ((long)row * 4 + wave) * 64;
-    if (hh == 0) st[l31] = make_float4((float)cnt, m0, q0, 0.f);
-    else st[32 + l31] = make_float4((float)cnt, m1, q1, 0.f);
+    const double nb = (double)cnt, na = rn, nt = na + nb;
+    const double d0 = (double)m0 - rm0, d1 = (double)m1 - rm1;
+    rm0 += d0 * nb / nt;
+    rm1 += d1 * nb / nt;
+    rq0 += (double)q0 + d0 * d0 * na * nb / nt;
+    rq1 += (double)q1 + d1 * d1 * na * nb / nt;
+    rn = nt;
+  }
+  if ((int)blockIdx.x < rows) {
+    float4* st = stats + ((long)blockIdx.x * 4 + wave) * 64;
+    if (hh == 0) st[l31] = make_float4((float)rn, (float)rm0, (float)rq0, 0.f);
+    else st[32 + l31] = make_float4((float)rn, (float)rm1, (float)rq1, 0.f);
   }
 }
 
@@ -154,35 +167,12 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_k(const float* __restrict__ x
 // 32x32 (64 channels x 160 reduction rows).  At the end the four waves add their tiles in LDS and
 // the workgroup writes one partial slab in the engine's wgrad layout ((co * 49 + tap) * 4 + c),
 // which wgrad_reduce_taps_kernel sums in a fixed order (deterministic).
-// FUSED: dy is not read from HBM but evaluated per output row into LDS from the stem's BN
-// backward inputs -- g = the MaxPool2d(3, 2, 1) gradient gathered at the pixel (pooled gradient
-// and argmax), masked by ReLU(y * scale + shift) > 0; dy = A g + B y + C (coef[3][64]) -- the
-// arithmetic of stem_bwd_apply (bn.hip), so dy and the weight gradient are bit-identical to the
-// two-pass form.
-struct StemBwd {
-  const float* y;
-  const float* scale;
-  const float* shift;
-  const float* coef;
-  const float* dyp;
-  const uchar4* am;
-  int hp, wp;   // pooled height / width
-};
-
-template <bool FUSED>
 __global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__ x,
                                                        const float* __restrict__ dy,
                                                        float* __restrict__ slabs, int h, int wd,
-                                                       int ho, int rows, StemBwd sb) {
+                                                       int ho, int rows) {
   constexpr int XS = XH * 3 * 2 * XHALF;
   __shared__ float Xs[2 * XS];   // 2 x 19.5 KB; at the end the 64 x 147 partial
-  __shared__ float Ds[FUSED ? SW * 64 : 1];   // FUSED: this row's dy (28 KB)
-  __shared__ float4 Cf[FUSED ? 5 * 16 : 1];    // FUSED: scale, shift, A, B, C per channel quad
-  if (FUSED && threadIdx.x < 5 * 16) {
-    const int f = threadIdx.x >> 4, q = threadIdx.x & 15;
-    const float* src = f == 0 ? sb.scale : f == 1 ? sb.shift : sb.coef + (f - 2) * 64;
-    Cf[threadIdx.x] = reinterpret_cast<const float4*>(src)[q];
-  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l31 = lane & 31, hh = lane >> 5;
   constexpr int NP = XH * 2 * XHALF, PPT = (NP + 255) / 256;
@@ -214,61 +204,9 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
 
-  // HBM form: the next row's patch is fetched into registers under this row's MFMAs.  FUSED: the
-  // patch goes global -> registers -> LDS after each row's dy phase (the gather leaves no
-  // registers to carry it); the two workgroups of a CU overlap one's loads with the other's MFMAs
-  if (!FUSED && (int)blockIdx.x < rows) fetch(blockIdx.x);
+  // the next row's patch is fetched into registers under this row's MFMAs
+  if ((int)blockIdx.x < rows) fetch(blockIdx.x);
   for (int row = blockIdx.x, buf = 0; row < rows; row += gridDim.x, buf ^= 1) {
-    if (FUSED) {
-      __syncthreads();   // the previous row's MFMAs are done reading Ds (and Cf is written)
-      const int oh = row % ho, nn = row / ho;
-      const int cq = tid & 15;   // the same channel quad for every pixel of this thread
-      // this frame's pooled gradient / argmax (32-bit offsets below); the windows containing
-      // output row oh: pooled rows oy0..oy1
-      const long fb = (long)nn * sb.hp * sb.wp * 16 + cq;
-      const float4* dp = reinterpret_cast<const float4*>(sb.dyp) + fb;
-      const uchar4* ap = sb.am + fb;
-      const float4* yr = reinterpret_cast<const float4*>(sb.y) + (long)row * SW * 16 + cq;
-      const int oy0 = oh >> 1, oy1 = min((oh + 1) >> 1, sb.hp - 1);
-#pragma unroll 1
-      for (int q = 0; q < SW * 16 / 256; ++q) {
-        const int px = (tid >> 4) + 16 * q;
-        const float4 v = yr[px * 16];
-        // maxpool_grad4 (common.h) with the frame offset hoisted: the same windows, in the same
-        // order, so the same sums
-        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int ox0 = px >> 1, ox1 = min((px + 1) >> 1, sb.wp - 1);
-#pragma unroll 1
-        for (int oy = oy0; oy <= oy1; ++oy) {
-#pragma unroll 1
-          for (int ox = ox0; ox <= ox1; ++ox) {
-            const int o = (oy * sb.wp + ox) * 16;
-            const unsigned char id = (unsigned char)((oh - (oy * 2 - 1)) * 3 + (px - (ox * 2 - 1)));
-            const uchar4 a = ap[o];
-            const float4 d = dp[o];
-            if (a.x == id) g.x += d.x;
-            if (a.y == id) g.y += d.y;
-            if (a.z == id) g.z += d.z;
-            if (a.w == id) g.w += d.w;
-          }
-        }
-        // ReLU mask of the BN output, then dy = A g + B y + C (stem_bwd_apply's order); the
-        // per-channel factors from LDS, so nothing is held across the MFMAs
-        const float4 sc = Cf[cq], sf = Cf[16 + cq];
-        g.x = fmaf(v.x, sc.x, sf.x) > 0.f ? g.x : 0.f;
-        g.y = fmaf(v.y, sc.y, sf.y) > 0.f ? g.y : 0.f;
-        g.z = fmaf(v.z, sc.z, sf.z) > 0.f ? g.z : 0.f;
-        g.w = fmaf(v.w, sc.w, sf.w) > 0.f ? g.w : 0.f;
-        const float4 A = Cf[32 + cq], B = Cf[48 + cq], C = Cf[64 + cq];
-        float4 o;
-        o.x = fmaf(A.x, g.x, fmaf(B.x, v.x, C.x));
-        o.y = fmaf(A.y, g.y, fmaf(B.y, v.y, C.y));
-        o.z = fmaf(A.z, g.z, fmaf(B.z, v.z, C.z));
-        o.w = fmaf(A.w, g.w, fmaf(B.w, v.w, C.w));
-        reinterpret_cast<float4*>(Ds)[px * 16 + cq] = o;
-      }
-      fetch(row);
-    }
     float* X = Xs + buf * XS;
     int tt = tid;
     asm volatile("" : "+v"(tt));
@@ -285,25 +223,9 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__
     }
     __syncthreads();   // the patch visible (the other buffer was last read two rows ago)
     // this wave's dy: pixels p = 2 * (wave + 4 * j) + (lane >> 5), channels (lane & 31) + 32 m
-    const float* dyr = FUSED ? Ds + (2 * wave + hh) * 64 + l31
-                             : dy + ((long)row * SW + 2 * wave + hh) * 64 + l31;
+    const float* dyr = dy + ((long)row * SW + 2 * wave + hh) * 64 + l31;
     const float* xb = X + 2 * wave + hh;
-    if constexpr (FUSED) {
-      // A from this row's dy in LDS, one k-step at a time (few registers next to the 160
-      // accumulators)
-#pragma unroll 2
-      for (int j = 0; j < 14; ++j) {
-        float b[5];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) b[t] = xb[kxl[t] + 8 * j];
-        const float a0 = dyr[8 * j * 64], a1 = dyr[8 * j * 64 + 32];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) {
-          acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b[t], acc[0][t], 0, 0, 0);
-          acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b[t], acc[1][t], 0, 0, 0);
-        }
-      }
-    } else {
+    {
       // A straight from HBM: all of the row's loads issued up front
       float a[14][2];
 #pragma unroll
@@ -359,7 +281,12 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_k(const float* __restrict__
 
 // tmr_conv2d_fwd_bnstats for the stem geometry (gemm_conv.hip routes it here): x NHWC4 fp32
 // (n, h, w, 4) with the 4th channel ignored, w KRSC (64, 7, 7, 4) fp32, stride 2, pad 3, output
-// width 112; one BatchNorm partial row per output row and wave (4 * n * ho rows of 64).
+// width 112; one BatchNorm partial row per wave of the grid (tmr_stem_stats_parts rows of 64).
+int tmr_stem_stats_parts(int n, int ho) {
+  const int rows = n * ho;
+  return 4 * (rows < GRID ? rows : GRID);
+}
+
 int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const float* w_krsc,
                          float* y, void* stats, hipStream_t stream) {
   TMR_CHECK_ARG(n > 0 && ho > 0 && (w + 6 - 7) / 2 + 1 == SW && 2 * XHALF >= w + 6,
@@ -388,35 +315,8 @@ int tmr_stem_wgrad_slabs(int n, int h, int w, int ho, const float* x, const floa
   const int grid = rows < GRID ? rows : GRID;
   TMR_CHECK_ARG(ws && ws_bytes >= (size_t)grid * 64 * 49 * 4 * sizeof(float),
                 "tmr_stem_wgrad: workspace too small (%zu)", ws_bytes);
-  hipLaunchKernelGGL(stem_wgrad_k<false>, dim3(grid), dim3(256), 0, stream, x, dy, ws, h, w, ho,
-                     rows, StemBwd{});
+  hipLaunchKernelGGL(stem_wgrad_k, dim3(grid), dim3(256), 0, stream, x, dy, ws, h, w, ho, rows);
   TMR_CHECK_LAUNCH("stem_wgrad");
-  *nslabs = grid;
-  return 0;
-}
-
-// The same with dy evaluated in LDS from the stem's BN-backward inputs (FUSED above): y (n, ho,
-// 112, 64) fp32, scale / shift (64), coef [3][64], pooled gradient dyp and argmax (n, hp, wp, 64).
-int tmr_stem_wgrad_bnbwd_slabs(int n, int h, int w, int ho, const float* x, const float* y,
-                               const float* scale, const float* shift, const float* coef,
-                               const float* dyp, const uint8_t* argmax, int hp, int wp, float* ws,
-                               size_t ws_bytes, int* nslabs, hipStream_t stream) {
-  TMR_CHECK_ARG(n > 0 && ho > 0 && (w + 6 - 7) / 2 + 1 == SW && 2 * XHALF >= w + 6,
-                "tmr_stem_wgrad_bnbwd: unsupported geometry %dx%d", h, w);
-  TMR_CHECK_ARG(hp == (ho + 2 - 3) / 2 + 1 && wp == (SW + 2 - 3) / 2 + 1,
-                "tmr_stem_wgrad_bnbwd: pooled %dx%d is not MaxPool2d(3,2,1) of %dx%d", hp, wp, ho,
-                SW);
-  TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)y | (uintptr_t)scale | (uintptr_t)shift |
-                  (uintptr_t)coef | (uintptr_t)dyp) & 15) == 0 && ((uintptr_t)argmax & 3) == 0,
-                "tmr_stem_wgrad_bnbwd: operands must be 16-B aligned (argmax 4-B)");
-  const int rows = n * ho;
-  const int grid = rows < GRID ? rows : GRID;
-  TMR_CHECK_ARG(ws && ws_bytes >= (size_t)grid * 64 * 49 * 4 * sizeof(float),
-                "tmr_stem_wgrad_bnbwd: workspace too small (%zu)", ws_bytes);
-  StemBwd sb{y, scale, shift, coef, dyp, (const uchar4*)argmax, hp, wp};
-  hipLaunchKernelGGL(stem_wgrad_k<true>, dim3(grid), dim3(256), 0, stream, x, nullptr, ws, h, w,
-                     ho, rows, sb);
-  TMR_CHECK_LAUNCH("stem_wgrad_bnbwd");
   *nslabs = grid;
   return 0;
 }

@@ -7,7 +7,7 @@ anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 """
 import torch
 
-from ._lib import call, query, stream_ptr, ConvDesc, ConvPrologue
+from ._lib import call, query, stream_ptr, has_prologues, ConvDesc, ConvPrologue
 from . import health
 import ctypes
 
@@ -177,11 +177,18 @@ def conv_fwd_fused(x, w_krsc, stride, pad, scale, shift, residual=None, relu=Tru
     return out
 
 
+def _need_prologues():
+    if not has_prologues():
+        raise RuntimeError("operand prologues (TMR_FOLD_BN=1) are a retired A/B experiment: build "
+                           "`make PROLOGUES=1` and set TMR_LIB_PATH=tmrnet_amd/libtmr_pro.so")
+
+
 def _prologue(xpro=None, dpro=None):
     """tmr_conv_prologue from (scale, shift) of the X operand's producer BN+ReLU and/or (y, coef)
     of this conv's BN backward; None when neither is given."""
     if xpro is None and dpro is None:
         return None
+    _need_prologues()
     p = ConvPrologue()
     if xpro is not None:
         p.x_scale, p.x_shift = _req(xpro[0], "x_scale").data_ptr(), _req(xpro[1], "x_shift").data_ptr()
@@ -346,47 +353,10 @@ def bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma, bf16=False):
     return dy, dgamma, dbeta
 
 
-def bn_bwd_maxpool_coefs(dyp, am, y, scale, shift, mean, inv, gamma):
-    """The fp32 stem's BN backward up to its coefficients (dy = A*g + B*y + C, g the maxpool-
-    gathered ReLU-masked gradient), no dy pass: -> (coef [3][c], dgamma, dbeta) for
-    conv_wgrad_stem_bnbwd."""
-    n, h, w, c = y.shape
-    _, ho, wo, _ = dyp.shape
-    ws, nb = _bn_ws(n * h * w, c, y.device)
-    coef = _empty((3, c), y)
-    dgamma = _empty((c,), y); dbeta = _empty((c,), y)
-    call("tmr_bn_bwd_maxpool_coefs", dyp, am, n, h, w, ho, wo, y, scale, shift, mean, inv, gamma,
-         coef, dgamma, dbeta, c, ws, ctypes.c_size_t(nb), stream_ptr())
-    return coef, dgamma, dbeta
-
-
-def conv_wgrad_stem_bnbwd(x, y, scale, shift, coef, dyp, am, r, s, stride, pad, out=None,
-                          beta=0.0):
-    """Weight gradient of the fp32 7x7/2 stem with its output gradient evaluated on the fly from
-    the BN backward (stem.hip FUSED; dy never written): x NHWC4 fp32, y the stem's conv output
-    (n, 112, 112, 64), (dyp, am) the maxpool's pooled gradient and argmax -> dW (64, 3, r, s)."""
-    n, h, w, c = x.shape
-    k = y.shape[3]
-    d = conv_desc(n, h, w, c, k, r, s, stride, pad, None, math="fp32", io=0)
-    d.x_ld = _nhwc_ld(x, "x")
-    d.y_ld = _nhwc_ld(y, "y")
-    assert (d.ho, d.wo) == tuple(y.shape[1:3])
-    if out is None:
-        out = _empty((k, 3, r, s), x)
-    ws_bytes = query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d))
-    ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=f32, device=x.device)
-    with _prof("conv_wgrad", 2.0 * n * d.ho * d.wo * k * r * s * 3, (n, h, w, c, k, r, stride),
-               4 * n * h * w * c + 4 * n * d.ho * d.wo * k + 5 * dyp.numel()
-               + 4 * k * r * s * 3):
-        call("tmr_conv2d_wgrad_stem_bnbwd", ctypes.byref(d), x, y, scale, shift, coef, dyp, am,
-             int(dyp.shape[1]), int(dyp.shape[2]), out, float(beta), ws,
-             ctypes.c_size_t(ws.numel() * 4), stream_ptr())
-    return out
-
-
 def bn_bwd_coefs(parts, nparts, mean, inv, gamma, rows):
     """BN backward coefficients from conv_dgrad_bnbwd partials -> (coef [3][c], dgamma, dbeta);
     the consumers apply dy = A*g + B*y + C on load (dpro=(y, coef))."""
+    _need_prologues()
     c = mean.shape[0]
     coef = _empty((3, c), mean)
     dgamma = _empty((c,), mean); dbeta = _empty((c,), mean)
@@ -401,6 +371,7 @@ def bn_bwd_coefs_dense(g, y, z, scale, shift, mean, inv, gamma, relu):
     """BN backward coefficients from the output gradient g itself (one reduction pass over g and
     y); with relu, g is masked IN PLACE (z > 0, or y*scale+shift > 0 when z is None).
     -> (coef [3][c], dgamma, dbeta)."""
+    _need_prologues()
     c = y.shape[-1]
     rows = y.numel() // c
     _req(g, "g"); _req(y, "y")
@@ -647,33 +618,25 @@ def relu_bits_empty(like):
 
 def bn_apply_bits(y, scale, shift, residual=None):
     """Block output with ReLU: z = relu(y*scale + shift (+ residual)) and its ReLU mask as bits
-    (tmr_bn_apply_bits, or _bits_a16 for bf16 activations: y, residual and z bf16) -> (z, bits),
-    for the mask-3 residual-gradient dgrads."""
-    _req(y, "y", y.dtype)
+    (tmr_bn_apply_bits; fp32) -> (z, bits), for the mask-3 residual-gradient dgrads."""
+    _req(y, "y")
     c = y.shape[-1]
     z = torch.empty_like(y)
     bits = relu_bits_empty(y)
-    if y.dtype == BF16:
-        if residual is not None and residual.dtype != BF16:
-            raise RuntimeError("bn_apply_bits: a bf16 y takes a bf16 residual")
-        call("tmr_bn_apply_bits_a16", y, scale, shift, residual, z, bits, y.numel() // c, c,
-             stream_ptr())
-    else:
-        call("tmr_bn_apply_bits", y, scale, shift, residual, z, bits, y.numel() // c, c,
-             stream_ptr())
+    call("tmr_bn_apply_bits", y, scale, shift, residual, z, bits, y.numel() // c, c, stream_ptr())
     return z, bits
 
 
 def bn_apply2_bits(y, scale, shift, yr, rscale, rshift):
-    """bn_apply2 with ReLU plus the ReLU mask as bits -> (z, bits); fp32, or bf16 y / yr / z."""
-    _req(y, "y", y.dtype); _req(yr, "yr", y.dtype)
+    """bn_apply2 with ReLU plus the ReLU mask as bits -> (z, bits); fp32."""
+    _req(y, "y"); _req(yr, "yr")
     if yr.shape != y.shape:
         raise RuntimeError("bn_apply2_bits: branch shape %s != %s" % (tuple(yr.shape), tuple(y.shape)))
     c = y.shape[-1]
     z = torch.empty_like(y)
     bits = relu_bits_empty(y)
-    name = "tmr_bn_apply2_bits_a16" if y.dtype == BF16 else "tmr_bn_apply2_bits"
-    call(name, y, scale, shift, yr, rscale, rshift, z, bits, y.numel() // c, c, stream_ptr())
+    call("tmr_bn_apply2_bits", y, scale, shift, yr, rscale, rshift, z, bits, y.numel() // c, c,
+         stream_ptr())
     return z, bits
 
 

@@ -89,7 +89,10 @@ def _bn_momentum(bn):
 # wgrad +12.7, dgrad +21.0 ms per step, C2 193.3 vs 173.9 ms/step, 3312 vs 3680 frames/s, same
 # box (profiles/r4/fold_ab/): the transform sits between the LDS-DMA landing and the barrier with
 # every MFMA idle, and on the narrow tiles (256x64: 8 pieces per lane per k-tile) it triples the
-# LDS traffic; the dgrads also read y next to g (twice the A-operand bytes).  Off by default.
+# LDS traffic; the dgrads also read y next to g (twice the A-operand bytes).  Retired to an A/B
+# build: the prologue entry points (include/tmr_prologue.h) exist only in `make PROLOGUES=1`'s
+# tmrnet_amd/libtmr_pro.so (run with TMR_LIB_PATH pointing at it); the default library rejects
+# TMR_FOLD_BN=1 at the first conv.
 FOLD_BN = os.environ.get("TMR_FOLD_BN", "0") == "1"
 
 # bf16 math (configs C4/C5): the tensors consumed only as conv operands -- the KRSC weights, the
@@ -153,12 +156,11 @@ G16 = os.environ.get("TMR_G16", "1") != "0"
 # gradient of every block output but the last.
 R16 = os.environ.get("TMR_BF16_RESGRAD", "1") != "0"
 
-# the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
+# the fp32 block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z).
+# The bf16-activation step re-reads its 2-byte z instead: bits measured slower there (C5 dgrads
+# 58.8 vs 56.6 ms/step, C4 23.1 vs 22.2; profiles/r3/bench_r4i/ -- one dword load per row shared
+# by 8 threads), and that variant was removed in round 4.
 BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
-# ... and for the bf16-activation step (TMR_RELU_BITS16=1).  Off: the bf16 dgrads re-read the 2-byte
-# z, measured faster than the bits (C5 dgrads 56.6 vs 58.8 ms/step, C4 22.2 vs 23.1;
-# profiles/r3/bench_r4i/) -- the bits cost one dword load per row shared by 8 threads
-BITS16 = os.environ.get("TMR_RELU_BITS16", "0") == "1"
 
 
 def _dma32(math):
@@ -172,24 +174,6 @@ STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
 # ... unless the direct bf16 stem takes the NHWC4 fp32 input itself (stem16.hip, round 4: 147 of
 # 176 multiplies useful instead of 147 of 392, no NHWC8 copy; TMR_STEM_DIRECT=0 turns it off)
 STEM16 = os.environ.get("TMR_STEM_DIRECT", "1") != "0"
-# fp32 stem backward, TMR_STEM_FUSED=1: the stem conv's weight gradient evaluates its output
-# gradient per row in LDS from the BN backward's inputs (tmr_conv2d_wgrad_stem_bnbwd), so that
-# gradient (2 GB at C2) is never written or read.  Off by default: measured slower than the two
-# passes (4.06 ms vs 1.78 + 1.34 ms at C2, profiles/r3/bench_r5q/)
-STEM_FUSED = (os.environ.get("TMR_STEM_FUSED", "0") == "1"
-              and os.environ.get("TMR_STEM_DIRECT", "1") != "0")
-
-
-def _stem_fused(rec, pool):
-    """The fp32 7x7/2 stem over NHWC4 input at the direct kernel's geometry (112 columns)."""
-    x, y, conv = rec["x"], rec["y"], rec["conv"]
-    return (STEM_FUSED and rec["math"] == "fp32" and rec.get("xpro") is None
-            and rec.get("groups", 1) == 1 and x.dtype == torch.float32 and x.shape[-1] == 4
-            and x.shape[2] <= 226 and y.dtype == torch.float32 and tuple(y.shape[2:]) == (112, 64)
-            and tuple(conv.weight.shape) == (64, 3, 7, 7) and rec["stride"] == 2
-            and rec["pad"] == 3 and pool[0].dtype == torch.float32)
-
-
 def _full16(math):
     return _store16(math) and FULL16 and not FOLD_BN
 
@@ -246,11 +230,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     # fp32 block outputs on the LDS-DMA path also record their ReLU mask as bits: the dgrad that
     # produces their gradient reads 1 bit instead of z's 4 bytes (mask 3)
     zbits = None
-    # (bf16 activations too: the bits of the rounded z, tmr_bn_apply_bits_a16)
-    bits = (recs is not None and relu and not dual and
-            ((_dma32(math) and y.dtype == torch.float32) or
-             (_act16(math) and y.dtype == torch.bfloat16 and BITS16))
-            and (residual is not None or branch is not None) and BITS)
+    bits = (recs is not None and relu and not dual and _dma32(math) and
+            y.dtype == torch.float32 and (residual is not None or branch is not None) and BITS)
     if defer:
         z = None
     elif branch is not None and bits:
@@ -312,19 +293,6 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
     dy_given = dy is not None
     if dy_given:
         dres = None
-    elif pool is not None and not need_dx and _stem_fused(rec, pool):
-        # the fp32 stem: BN-backward coefficients, then the weight gradient with dy evaluated
-        # on load (neither dz nor dy is written)
-        coef, dg, db = ops.bn_bwd_maxpool_coefs(pool[0], pool[1], rec["y"], rec["scale"],
-                                                rec["shift"], rec["mean"], rec["inv"],
-                                                bn.weight.detach())
-        grads[bn.weight] = dg
-        grads[bn.bias] = db
-        _, _, r, s = conv.weight.shape
-        grads[conv.weight] = ops.conv_wgrad_stem_bnbwd(rec["x"], rec["y"], rec["scale"],
-                                                       rec["shift"], coef, pool[0], pool[1], r, s,
-                                                       rec["stride"], rec["pad"])
-        return None, None, None
     elif pool is not None:
         # the stem: maxpool backward + ReLU mask + BN backward without writing dz
         dy, dg, db = ops.bn_bwd_maxpool(pool[0], pool[1], rec["y"], rec["scale"], rec["shift"],
