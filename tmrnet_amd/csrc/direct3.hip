@@ -1,0 +1,553 @@
+// Direct 3x3 / stride-1 convolutions of the narrow 112x112 layers of the bf16-activation train step:
+// ResNeSt-50's deep stem (the third-party resnest50() called at
+// train_non-local_mutiConv_resnest.py:210; conv1 = 3x3/2 3 -> 32, BN, ReLU, 3x3 32 -> 32, BN, ReLU,
+// 3x3 32 -> 64) -- its two stride-1 convs, all operands bf16 (TMR_IO_*_BF16), fp32 accumulation.
+//
+// On the implicit-GEMM engine these run at 140-340 TF: 32-64 output channels leave most of a
+// 256x64 tile's columns or k-tiles idle, and every input pixel is gathered 9 times through L2.  Here
+// a persistent workgroup computes whole output rows (112 pixels x COUT channels) from a ring of the
+// 3 input rows it needs in LDS, each fetched from HBM once (one new row per output row, prefetched
+// into registers a row ahead):
+//   * forward (d3_k MODE 0): v_mfma_f32_16x16x32_bf16, the 112 pixels as 7 m-tiles of 16, one k-step
+//     per (tap, 32 channels); the weights stay in registers (72 VGPRs per wave); y rounded to bf16,
+//     staged in LDS and stored as 16-B pieces; BatchNorm partials (n, mean, M2) of the stored values
+//     per wave and channel, merged over the workgroup's rows (Chan, double, fixed order);
+//   * dgrad (MODE 1): the same kernel over dy with the transposed weights (CRSK) tap-flipped -- the
+//     dgrad of a stride-1 pad-1 3x3 conv is that conv -- and the fused BatchNorm backward of the
+//     unit that produced the conv input in its epilogue (tmr_conv2d_dgrad_bnbwd's contract: ReLU
+//     mask from z (1) or from y * scale + shift (2), beta * old dx, partial sums sum(g) and
+//     sum(g * (y - mean)) per channel, one partial row per workgroup);
+//   * weight gradient (d3w_k): per output row dW[co][tap][ci] += dy^T x over the row's pixels (K =
+//     112 padded to 128), both operands as stored ([pixel][channel]) and read transposed by
+//     ds_read_b64_tr_b16; per-workgroup slabs in the engine's wgrad layout, summed in a fixed order
+//     by wgrad_reduce_taps_kernel (deterministic).
+// LDS pixel rows are padded to 2 C + 32 bytes: conflict-free for the b128 row reads and for the
+// transposed reads with the odd 16-lane groups taking their upper 4 rows first
+// (scripts/probe/lds_banks.py).
+#include "common.h"
+#include "tmr.h"
+
+namespace {
+
+constexpr int DW = 112;   // output (= input) width
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned short bfb(float v) {
+  return __builtin_bit_cast(unsigned short, (__bf16)v);
+}
+__device__ __forceinline__ float bff(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+template <int C>
+struct Px {
+  static constexpr int PS = 2 * C + 32;       // LDS bytes per pixel row
+  static constexpr int CPP = C / 8;           // 16-B chunks per pixel
+  static constexpr int PIECES = DW * CPP;     // 16-B pieces of a 112-pixel row
+  static constexpr int PPT = (PIECES + 255) / 256;
+};
+
+// One 112-pixel row of an NHWC bf16 tensor (global row index g) <-> registers <-> an LDS image of
+// pixel rows (pixel p at byte (p + off) * PS).
+template <int C>
+struct RowIO {
+  using P = Px<C>;
+  __device__ static void fetch(const uint4* __restrict__ t, int g, bool valid, uint4 (&v)[P::PPT]) {
+    int tt = threadIdx.x;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int q = 0; q < P::PPT; ++q) {
+      const int i = tt + 256 * q;
+      v[q] = (valid && i < P::PIECES) ? t[(long)g * P::PIECES + i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __device__ static void put(unsigned char* img, int off, const uint4 (&v)[P::PPT]) {
+    int tt = threadIdx.x;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int q = 0; q < P::PPT; ++q) {
+      const int i = tt + 256 * q;
+      if (i < P::PIECES)
+        *reinterpret_cast<uint4*>(img + (i / P::CPP + off) * P::PS + (i % P::CPP) * 16) = v[q];
+    }
+  }
+};
+
+// workgroups per CU (the grid is that many per CU: persistent): three where the registers allow
+constexpr int d3_minb(int cin, int cout, int mode) { return (cin == 32 && cout == 32 && mode == 0) ? 3 : 2; }
+
+// MODE 0: forward, y bf16 + BatchNorm partial statistics.  MODE 1: dgrad (x = dy, w = the CRSK copy,
+// taps flipped) with the fused BatchNorm backward; out = dx fp32.
+template <int CIN, int COUT, int MODE>
+__global__ __launch_bounds__(256, d3_minb(CIN, COUT, MODE))
+void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __restrict__ out,
+          float4* __restrict__ stats, const uint4* __restrict__ by, const uint4* __restrict__ bz,
+          const float* __restrict__ bsc, const float* __restrict__ bsh,
+          const float* __restrict__ bmu, int mask, float beta, float2* __restrict__ part, int h,
+          int rows) {
+  using PI = Px<CIN>;
+  constexpr int KPT = CIN / 32, KS = 9 * KPT;
+  constexpr int NT = COUT / 16, NPW = 18 / KS, WN = NT / NPW, WM = 4 / WN;
+  constexpr int MPW = (7 + WM - 1) / WM;
+  static_assert(NPW * KS == 18 && NT % NPW == 0 && WN * WM == 4, "wave split");
+  constexpr int SLOT = 114 * PI::PS;   // pixel columns x = -1 .. 112
+  constexpr int OST = MODE == 0 ? DW * COUT * 2 : DW * (COUT + 4) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char ring[3 * SLOT];
+  __shared__ __attribute__((aligned(16))) unsigned char ost[OST];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int c16 = lane & 15, kg = lane >> 4;
+
+  for (int i = tid; i < 3 * SLOT / 16; i += 256)
+    reinterpret_cast<uint4*>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);   // incl. the padding columns
+
+  // this wave's weights for its NPW n-tiles, all k-steps: B[k = (tap, ci)][co], lane (kg, c16)
+  bf16x8_t bw[NPW][KS];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int co = 16 * (wn * NPW + j) + c16;
+      const int tap = s / KPT, tp = MODE == 1 ? 8 - tap : tap;
+      const int ci = 32 * (s % KPT) + 8 * kg;
+      bw[j][s] = *reinterpret_cast<const bf16x8_t*>(wk + ((long)co * 9 + tp) * CIN + ci);
+    }
+
+  const int r0 = (int)((long)blockIdx.x * rows / gridDim.x);
+  const int r1 = (int)((long)(blockIdx.x + 1) * rows / gridDim.x);
+  const int nvalid = min(MPW, 7 - wm * MPW);   // this wave's m-tiles (uniform)
+
+  // forward statistics: running (n, mean, M2) of this wave's pixels per channel (lanes kg share)
+  double rn = 0.0, rm[NPW], rq[NPW];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) { rm[j] = 0.0; rq[j] = 0.0; }
+  // dgrad: the thread's 8 channels (fixed: 256 is a multiple of COUT / 8) and its partial sums
+  constexpr int CG = COUT / 8, ITEMS = DW * CG, IPT = (ITEMS + 255) / 256;
+  const int cg = tid % CG;
+  float esc[8], esh[8], emu[8];
+  double ds[8], dq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    esc[e] = (MODE == 1 && mask == 2) ? bsc[8 * cg + e] : 0.f;
+    esh[e] = (MODE == 1 && mask == 2) ? bsh[8 * cg + e] : (mask == 0 ? 1.f : 0.f);
+    emu[e] = MODE == 1 ? bmu[8 * cg + e] : 0.f;
+    ds[e] = 0.0;
+    dq[e] = 0.0;
+  }
+
+  uint4 setA[PI::PPT], setB[PI::PPT];
+  auto first = [&](int row) { return row == r0 || row % h == 0; };
+  auto slot = [&](int g) { return ring + ((g + 3) % 3) * SLOT; };   // g >= -1
+
+  auto step = [&](int row, uint4 (&cur)[PI::PPT], uint4 (&nxt)[PI::PPT]) {
+    const int oh = row % h;
+    __syncthreads();   // the previous row's MFMAs / staged output are done
+    if (first(row)) {
+#pragma unroll 1
+      for (int d = -1; d <= 1; ++d) {
+        RowIO<CIN>::fetch(x, row + d, oh + d >= 0 && oh + d < h, cur);
+        RowIO<CIN>::put(slot(row + d), 1, cur);
+      }
+    } else {
+      RowIO<CIN>::put(slot(row + 1), 1, cur);   // (zeros past the frame's last row)
+    }
+    __syncthreads();
+    // the next row's new input row lands under this row's MFMAs
+    if (row + 1 < r1 && !first(row + 1)) RowIO<CIN>::fetch(x, row + 2, oh + 2 < h, nxt);
+    // dgrad epilogue operands of this row (y, z, old dx), issued before the MFMAs
+    uint4 yv[IPT], zv[IPT];
+    float4 ov[IPT][2];
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int q = 0; q < IPT; ++q) {
+        const int it = tid + 256 * q;
+        const bool ok = it < ITEMS;
+        const long e8 = (long)row * ITEMS + (ok ? it : 0);
+        yv[q] = ok ? by[e8] : make_uint4(0u, 0u, 0u, 0u);
+        zv[q] = (ok && mask == 1) ? bz[e8] : make_uint4(0u, 0u, 0u, 0u);
+        if (beta != 0.f && ok) {
+          ov[q][0] = reinterpret_cast<const float4*>(out)[2 * e8];
+          ov[q][1] = reinterpret_cast<const float4*>(out)[2 * e8 + 1];
+        } else {
+          ov[q][0] = ov[q][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+
+    f32x4_t acc[MPW][NPW];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i)
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const unsigned char* rb[3] = {slot(row - 1), slot(row), slot(row + 1)};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int tap = s / KPT, dy = tap / 3, dx = tap % 3;   // input row row - 1 + dy, column + dx - 1
+      const unsigned char* p = rb[dy] + (dx + c16) * PI::PS + (64 * (s % KPT) + 16 * kg);
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        if (i < nvalid) {
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(p + 16 * (wm * MPW + i) * PI::PS);
+#pragma unroll
+          for (int j = 0; j < NPW; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[j][s], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+
+    if constexpr (MODE == 0) {
+      // rounded values -> the staged tile + this wave's statistics (count 16 * nvalid per channel)
+      unsigned short* ys = reinterpret_cast<unsigned short*>(ost);
+      float sm[NPW];
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) sm[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        if (i < nvalid) {
+#pragma unroll
+          for (int j = 0; j < NPW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int px = 16 * (wm * MPW + i) + 4 * kg + r, co = 16 * (wn * NPW + j) + c16;
+              const unsigned short u = bfb(acc[i][j][r]);
+              acc[i][j][r] = bff(u);
+              ys[px * COUT + co] = u;
+              sm[j] += acc[i][j][r];
+            }
+        }
+      }
+      const float cnt = 16.f * nvalid;
+      float mj[NPW], qj[NPW];
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) {
+        float t = sm[j] + __shfl_xor(sm[j], 16, 64);
+        t += __shfl_xor(t, 32, 64);
+        mj[j] = t / cnt;
+        qj[j] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        if (i < nvalid) {
+#pragma unroll
+          for (int j = 0; j < NPW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float d = acc[i][j][r] - mj[j];
+              qj[j] = fmaf(d, d, qj[j]);
+            }
+        }
+      }
+      const double nb = (double)cnt, na = rn, nt = na + nb;
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) {
+        float t = qj[j] + __shfl_xor(qj[j], 16, 64);
+        t += __shfl_xor(t, 32, 64);
+        const double dd = (double)mj[j] - rm[j];
+        rm[j] += dd * nb / nt;
+        rq[j] += (double)t + dd * dd * na * nb / nt;
+      }
+      rn = nt;
+      __syncthreads();   // the tile staged
+      constexpr int YP = DW * COUT * 2 / 16;
+      uint4* yr = reinterpret_cast<uint4*>(out) + (long)row * YP;
+      for (int i = tid; i < YP; i += 256) yr[i] = reinterpret_cast<const uint4*>(ost)[i];
+    } else {
+      // fp32 dx tile -> LDS (rows of COUT + 4 floats), then 8 channels per thread
+      float* gs = reinterpret_cast<float*>(ost);
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        if (i < nvalid) {
+#pragma unroll
+          for (int j = 0; j < NPW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int px = 16 * (wm * MPW + i) + 4 * kg + r, co = 16 * (wn * NPW + j) + c16;
+              gs[px * (COUT + 4) + co] = acc[i][j][r];
+            }
+        }
+      }
+      __syncthreads();
+      float rs[8], rqq[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { rs[e] = 0.f; rqq[e] = 0.f; }
+#pragma unroll
+      for (int q = 0; q < IPT; ++q) {
+        const int it = tid + 256 * q;
+        if (it < ITEMS) {
+          const int px = it / CG;
+          const float4 a0 = *reinterpret_cast<const float4*>(gs + px * (COUT + 4) + 8 * cg);
+          const float4 a1 = *reinterpret_cast<const float4*>(gs + px * (COUT + 4) + 8 * cg + 4);
+          const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          const float ol[8] = {ov[q][0].x, ov[q][0].y, ov[q][0].z, ov[q][0].w,
+                               ov[q][1].x, ov[q][1].y, ov[q][1].z, ov[q][1].w};
+          const uint32_t yu[4] = {yv[q].x, yv[q].y, yv[q].z, yv[q].w};
+          const uint32_t zu[4] = {zv[q].x, zv[q].y, zv[q].z, zv[q].w};
+          float g[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float yy = (e & 1) ? __uint_as_float(yu[e >> 1] & 0xffff0000u) : bff(yu[e >> 1] & 0xffffu);
+            const float zz = (e & 1) ? __uint_as_float(zu[e >> 1] & 0xffff0000u) : bff(zu[e >> 1] & 0xffffu);
+            float t = fmaf(beta, ol[e], av[e]);
+            const bool keep = zz + fmaf(yy, esc[e], esh[e]) > 0.f;   // the engine's mask test
+            t = keep ? t : 0.f;
+            g[e] = t;
+            rs[e] += t;
+            rqq[e] = fmaf(t, yy - emu[e], rqq[e]);
+          }
+          float4* o = reinterpret_cast<float4*>(out) + 2 * ((long)row * ITEMS + it);
+          o[0] = make_float4(g[0], g[1], g[2], g[3]);
+          o[1] = make_float4(g[4], g[5], g[6], g[7]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ds[e] += (double)rs[e];
+        dq[e] += (double)rqq[e];
+      }
+    }
+  };
+  for (int row = r0; row < r1; row += 2) {
+    step(row, setA, setB);
+    if (row + 1 < r1) step(row + 1, setB, setA);
+  }
+
+  if constexpr (MODE == 0) {
+    if (kg == 0) {
+#pragma unroll
+      for (int j = 0; j < NPW; ++j)
+        stats[((long)blockIdx.x * WM + wm) * COUT + 16 * (wn * NPW + j) + c16] =
+            make_float4((float)rn, (float)rm[j], (float)rq[j], 0.f);
+    }
+  } else {
+    // the workgroup's partial row: per channel, the threads with this channel group (lanes
+    // l = cg mod CG of each wave, then the four waves) summed in a fixed order
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      for (int m = CG; m < 64; m <<= 1) {
+        ds[e] += __shfl_xor(ds[e], m, 64);
+        dq[e] += __shfl_xor(dq[e], m, 64);
+      }
+    }
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(ost);   // [4 waves][COUT][2]
+    if (lane < CG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * COUT + 8 * lane + e) * 2] = ds[e];
+        red[(wave * COUT + 8 * lane + e) * 2 + 1] = dq[e];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < COUT; c += 256) {
+      double t0 = 0.0, t1 = 0.0;
+      for (int w = 0; w < 4; ++w) {
+        t0 += red[(w * COUT + c) * 2];
+        t1 += red[(w * COUT + c) * 2 + 1];
+      }
+      part[(long)blockIdx.x * COUT + c] = make_float2((float)t0, (float)t1);
+    }
+  }
+}
+
+// Weight gradient dW[co][tap][ci] = sum over output pixels p of dy[p][co] * x[p + off(tap)][ci]:
+// per output row, A = the dy row (co x 128 pixels, pixels >= 112 zero), B = the input row of the
+// tap's kernel row shifted by its column offset (128 pixels x ci), both [pixel][channel] images read
+// by ds_read_b64_tr_b16.  Wave split: COUT 64 -> wave w owns co tile w (both ci tiles, 9 taps);
+// COUT 32 -> (co tile w & 1, ci tile w >> 1).
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256, 2)
+void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __restrict__ slabs,
+           int h, int rows) {
+  using PI = Px<CIN>;
+  using PO = Px<COUT>;
+  constexpr int XR = 130;   // ring slot rows: pixel columns x = -1 .. 128
+  constexpr int XSLOT = XR * PI::PS;
+  constexpr int MTW = COUT == 64 ? 1 : 1, NTW = COUT == 64 ? 2 : 1;   // tiles per wave
+  static_assert(COUT == 64 || COUT == 32, "d3w_k: 32 or 64 output channels");
+  static_assert(CIN == 32, "d3w_k: 32 input channels");
+  __shared__ __attribute__((aligned(16))) unsigned char ring[3 * XSLOT];
+  __shared__ __attribute__((aligned(16))) unsigned char dimg[128 * PO::PS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int tq = li >> 2, tp = li & 3;
+  const int mt = COUT == 64 ? wave : (wave & 1);
+  const int nt0 = COUT == 64 ? 0 : (wave >> 1);
+  for (int i = tid; i < 3 * XSLOT / 16; i += 256)
+    reinterpret_cast<uint4*>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < 128 * PO::PS / 16; i += 256)
+    reinterpret_cast<uint4*>(dimg)[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  f32x4_t acc[9][NTW];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[t][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  (void)MTW;
+
+  const int r0 = (int)((long)blockIdx.x * rows / gridDim.x);
+  const int r1 = (int)((long)(blockIdx.x + 1) * rows / gridDim.x);
+  auto first = [&](int row) { return row == r0 || row % h == 0; };
+  auto slot = [&](int gg) { return ring + ((gg + 3) % 3) * XSLOT; };
+
+  // transposed fragment: 8 consecutive pixel rows pr .. pr + 7 (this lane's group's), columns
+  // cb .. cb + 15 -> element j = row pr + j of column cb + li; the odd groups read their upper 4
+  // rows first (conflict-free pairing), swapped back here
+  auto frag = [&](const unsigned char* img, int stride, int pr, int cb) -> bf16x8_t {
+    const int hi = g & 1;
+    const unsigned char* p = img + (pr + tq) * stride + (cb + 4 * tp) * 2;
+    const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(p + 4 * hi * stride));
+    const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(p + 4 * (hi ^ 1) * stride));
+    const s16x4_t lo = hi ? v1 : v0, up = hi ? v0 : v1;
+    const s16x8_t w = __builtin_shufflevector(lo, up, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, w);
+  };
+
+  uint4 xA[PI::PPT], xB[PI::PPT], dA[PO::PPT], dB[PO::PPT];
+  if (r0 < r1) RowIO<COUT>::fetch(dy, r0, true, dA);
+  auto step = [&](int row, uint4 (&xc)[PI::PPT], uint4 (&xn)[PI::PPT], uint4 (&dc)[PO::PPT],
+                  uint4 (&dn)[PO::PPT]) {
+    const int oh = row % h;
+    __syncthreads();   // the previous row's fragments are read
+    if (first(row)) {
+#pragma unroll 1
+      for (int d = -1; d <= 1; ++d) {
+        RowIO<CIN>::fetch(x, row + d, oh + d >= 0 && oh + d < h, xc);
+        RowIO<CIN>::put(slot(row + d), 1, xc);
+      }
+    } else {
+      RowIO<CIN>::put(slot(row + 1), 1, xc);
+    }
+    RowIO<COUT>::put(dimg, 0, dc);
+    __syncthreads();
+    if (row + 1 < r1) {
+      if (!first(row + 1)) RowIO<CIN>::fetch(x, row + 2, oh + 2 < h, xn);
+      RowIO<COUT>::fetch(dy, row + 1, true, dn);
+    }
+    const unsigned char* rb[3] = {slot(row - 1), slot(row), slot(row + 1)};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {   // pixels 32 s .. 32 s + 31
+      const int pr = 32 * s + 8 * g;
+      const bf16x8_t a = frag(dimg, PO::PS, pr, 16 * mt);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t % 3;   // x pixel p + kx - 1 = image row p + kx
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const bf16x8_t b = frag(rb[ky], PI::PS, pr + kx, 16 * (nt0 + j));
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+  for (int row = r0; row < r1; row += 2) {
+    step(row, xA, xB, dA, dB);
+    if (row + 1 < r1) step(row + 1, xB, xA, dB, dA);
+  }
+  // this wave's tiles -> the workgroup's slab, layout (co * 9 + tap) * CIN + ci
+  float* slab = slabs + (long)blockIdx.x * (COUT * 9 * CIN);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * mt + 4 * g + r, ci = 16 * (nt0 + j) + li;
+        slab[((long)co * 9 + t) * CIN + ci] = acc[t][j][r];
+      }
+}
+
+constexpr int kGridW = 2 * 256;
+
+int grid_of(int rows, int cin, int cout, int mode) {
+  const int g = d3_minb(cin, cout, mode) * 256;
+  return rows < g ? rows : g;
+}
+
+}  // namespace
+
+// ---- host entries (gemm_conv.hip routes the deep stem's geometry here) ----
+
+int tmr_d3_stats_parts(int n, int h, int cin, int cout) {
+  const int wm = cout == 64 ? 2 : 4;   // d3_k<32, COUT, 0>: WM
+  return grid_of(n * h, cin, cout, 0) * wm;
+}
+
+int tmr_d3_dgrad_parts(int n, int h, int cin_conv, int cout_conv) {
+  return grid_of(n * h, cout_conv, cin_conv, 1);   // the dgrad kernel runs over dy
+}
+
+size_t tmr_d3_wgrad_ws_bytes(int n, int h, int cin, int cout) {
+  const int rows = n * h;
+  return (size_t)(rows < kGridW ? rows : kGridW) * cout * 9 * cin * sizeof(float);
+}
+
+int tmr_d3_fwd_bnstats(int n, int h, int cin, int cout, const void* x, const void* w_krsc, void* y,
+                       void* stats, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && cin == 32 && (cout == 32 || cout == 64),
+                "tmr_d3_fwd: unsupported shape (%d -> %d)", cin, cout);
+  TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)y | (uintptr_t)w_krsc) & 15) == 0,
+                "tmr_d3_fwd: x / y / w must be 16-B aligned");
+  const int rows = n * h, grid = grid_of(rows, cin, cout, 0);
+  if (cout == 64)
+    hipLaunchKernelGGL((d3_k<32, 64, 0>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
+                       (const __bf16*)w_krsc, y, (float4*)stats, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0, 0.f, nullptr, h, rows);
+  else
+    hipLaunchKernelGGL((d3_k<32, 32, 0>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
+                       (const __bf16*)w_krsc, y, (float4*)stats, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0, 0.f, nullptr, h, rows);
+  TMR_CHECK_LAUNCH("d3_fwd");
+  return 0;
+}
+
+// dgrad of the conv cin_conv -> cout_conv: dy (rows, 112, cout_conv) bf16, w_crsk (cin_conv, 3, 3,
+// cout_conv) bf16, dx (rows, 112, cin_conv) fp32 (read when beta != 0); the BatchNorm backward of
+// the unit that produced the conv input: y / z bf16 like dx, mask 0 / 1 / 2
+int tmr_d3_dgrad_bnbwd(int n, int h, int cin_conv, int cout_conv, const void* dy,
+                       const void* w_crsk, float* dx, float beta, const void* y, const void* z,
+                       const float* scale, const float* shift, const float* mean, int mask,
+                       void* parts, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && cin_conv == 32 && (cout_conv == 32 || cout_conv == 64),
+                "tmr_d3_dgrad: unsupported shape (%d -> %d)", cin_conv, cout_conv);
+  TMR_CHECK_ARG((((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w_crsk | (uintptr_t)y |
+                  (uintptr_t)z) & 15) == 0,
+                "tmr_d3_dgrad: operands must be 16-B aligned");
+  TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift),
+                "tmr_d3_dgrad: mask %d operands", mask);
+  const int rows = n * h, grid = grid_of(rows, cout_conv, cin_conv, 1);
+  if (cout_conv == 64)
+    hipLaunchKernelGGL((d3_k<64, 32, 1>), dim3(grid), dim3(256), 0, stream, (const uint4*)dy,
+                       (const __bf16*)w_crsk, (void*)dx, nullptr, (const uint4*)y,
+                       (const uint4*)z, scale, shift, mean, mask, beta, (float2*)parts, h, rows);
+  else
+    hipLaunchKernelGGL((d3_k<32, 32, 1>), dim3(grid), dim3(256), 0, stream, (const uint4*)dy,
+                       (const __bf16*)w_crsk, (void*)dx, nullptr, (const uint4*)y,
+                       (const uint4*)z, scale, shift, mean, mask, beta, (float2*)parts, h, rows);
+  TMR_CHECK_LAUNCH("d3_dgrad");
+  return 0;
+}
+
+int tmr_d3_wgrad_slabs(int n, int h, int cin, int cout, const void* x, const void* dy, float* ws,
+                       size_t ws_bytes, int* nslabs, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && cin == 32 && (cout == 32 || cout == 64),
+                "tmr_d3_wgrad: unsupported shape (%d -> %d)", cin, cout);
+  TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)dy) & 15) == 0, "tmr_d3_wgrad: x / dy must be 16-B aligned");
+  const int rows = n * h, grid = rows < kGridW ? rows : kGridW;
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_d3_wgrad_ws_bytes(n, h, cin, cout),
+                "tmr_d3_wgrad: workspace too small (%zu)", ws_bytes);
+  if (cout == 64)
+    hipLaunchKernelGGL((d3w_k<32, 64>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
+                       (const uint4*)dy, ws, h, rows);
+  else
+    hipLaunchKernelGGL((d3w_k<32, 32>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
+                       (const uint4*)dy, ws, h, rows);
+  TMR_CHECK_LAUNCH("d3_wgrad");
+  *nslabs = grid;
+  return 0;
+}
