@@ -147,3 +147,53 @@ def test_direct3_small_frames(dev, monkeypatch):
         rw = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (64, 32, 3, 3),
                                          dy.permute(0, 3, 1, 2).double(), padding=1)
         assert rel_err(dw, rw) < 2e-6
+
+
+def test_direct3_stem_fwd_bnstats(dev, monkeypatch):
+    """The deep stem's first conv (3x3/2, 3 -> 32) from the NHWC4 fp32 frames, 3 channels packed
+    per column: within one bf16 ulp of float64 of the bf16-rounded operands, within two of the
+    LDS-DMA engine on the NHWC8 copy; BatchNorm statistics of the stored values."""
+    g = torch.Generator().manual_seed(80)
+    x = torch.relu(torch.randn(N, 3, 224, 224, generator=g)) + 0.25
+    w = torch.randn(32, 3, 3, 3, generator=g) / np.sqrt(27)
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    wk4 = ops.weight_to_krsc(w.to(dev).contiguous(), cpad=4, bf16=True)
+    monkeypatch.setenv("TMR_DIRECT3", "1")
+    y, stats, nparts = ops.conv_fwd_bnstats(x4, wk4, 2, 1, c_real=3, math="bf16", y16=True)
+    monkeypatch.setenv("TMR_DIRECT3", "0")
+    x8 = ops.nhwc4_to_bf16x8(x4)
+    wk8 = ops.weight_to_krsc(w.to(dev).contiguous(), cpad=8, bf16=True)
+    y0, _, _ = ops.conv_fwd_bnstats(x8, wk8, 2, 1, c_real=3, math="bf16", y16=True)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.bfloat16 and tuple(y.shape) == (N, 112, 112, 32)
+    assert nparts == 4 * 768
+    ref = F.conv2d(_bf(x).double(), _bf(w).double(), stride=2, padding=1).permute(0, 2, 3, 1)
+    yf = y.double().cpu()
+    assert _ulp_bound(yf, ref)
+    assert _ulp_bound(yf, y0.double().cpu(), 2.0)
+    yd = yf.reshape(-1, 32)
+    ones, zeros = torch.ones(32, device=dev), torch.zeros(32, device=dev)
+    mean, inv, _, _ = ops.bn_finalize(stats, nparts, ones, zeros, zeros.clone(), ones.clone(), 0.1, 1e-5)
+    assert rel_err(mean, yd.mean(0)) < 1e-6
+    assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
+
+
+def test_direct3_stem_wgrad(dev, monkeypatch):
+    """Its weight gradient (per input row im2col columns transposed in LDS, dy by transposed reads):
+    against float64 of the bf16 operands, with beta accumulation, and against the engine."""
+    g = torch.Generator().manual_seed(81)
+    x = torch.relu(torch.randn(N, 3, 224, 224, generator=g)) + 0.25
+    dy = _bf(torch.randn(N, 112, 112, 32, generator=g))
+    x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
+    ref = torch.nn.grad.conv2d_weight(_bf(x).double(), (32, 3, 3, 3),
+                                      dy.permute(0, 3, 1, 2).double(), stride=2, padding=1)
+    monkeypatch.setenv("TMR_DIRECT3", "1")
+    dw = ops.conv_wgrad(x4, dy.to(dev), 3, 3, 2, 1, c_real=3, math="bf16")
+    prev = torch.randn(32, 3, 3, 3, generator=g).to(dev)
+    acc = ops.conv_wgrad(x4, dy.to(dev), 3, 3, 2, 1, c_real=3, math="bf16", out=prev.clone(),
+                         beta=0.5)
+    monkeypatch.setenv("TMR_DIRECT3", "0")
+    dw0 = ops.conv_wgrad(x4, dy.to(dev), 3, 3, 2, 1, c_real=3, math="bf16")
+    torch.cuda.synchronize()
+    assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
+    assert rel_err(acc, 0.5 * prev.double().cpu() + ref) < 2e-6

@@ -462,6 +462,284 @@ void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __r
       }
 }
 
+// ---- the deep stem's first conv: 3x3 / stride 2 / pad 1, 3 -> 32 channels, 224 -> 112 ----
+// From the NHWC4 fp32 input (rounded to bf16 when published; the 4th channel ignored), packed per
+// input row as 3 channels per column (columns x = -1 .. 226): the 3 taps x 3 channels of one
+// kernel row at output column ow are the 9 consecutive values from element 6 ow.  The reduction
+// runs over 4 kernel rows of 16 (9 real: 27 of 64 multiplies, the 4th row zero weights) -- two
+// k-steps of v_mfma_f32_16x16x32_bf16, each lane's 8 values four ds_read_b32 at 12 ow + 16 h bytes.
+// Input rows 2 oh - 1 .. 2 oh + 1 in a ring of 3 (slot (r + 3) % 3; consecutive output rows share
+// one), the 2 new rows of the next output row prefetched into registers.
+constexpr int SXR = 688;   // packed row: 229 columns x 3 channels = 687, padded
+constexpr int SW2 = 224;   // input width
+
+struct StemRows {
+  const float4* x;
+  int hin;
+  // rows r, r + 1 of the frame starting at global input row g0 (r + k < hin), two float4 per thread
+  __device__ void fetch2(long g0, int r, float4 (&v)[2]) const {
+    int tt = threadIdx.x;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = tt + 256 * q, k = i / SW2, col = i % SW2;
+      v[q] = (r + k >= 0 && r + k < hin) ? x[(g0 + r + k) * SW2 + col] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+};
+
+__device__ __forceinline__ void put_px3(unsigned short* row, int col, float4 v) {
+  unsigned short* d = row + (col + 1) * 3;
+  d[0] = bfb(v.x); d[1] = bfb(v.y); d[2] = bfb(v.z);
+}
+
+__global__ __launch_bounds__(256, 3)
+void d3s_k(const float4* __restrict__ x, const __bf16* __restrict__ wk, __bf16* __restrict__ y,
+           float4* __restrict__ stats, int hin, int ho, int rows) {
+  constexpr int COUT = 32, MPW = 2;
+  __shared__ __attribute__((aligned(16))) unsigned short ring[3 * SXR];
+  __shared__ __attribute__((aligned(16))) unsigned short ys[DW * COUT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, kg = lane >> 4;
+  for (int i = tid; i < 3 * SXR / 2; i += 256) reinterpret_cast<uint32_t*>(ring)[i] = 0u;
+  // weights: B[k = 32 s + 8 kg + e][co]: chunk m = 4 s + kg = (kernel row m / 2, half m % 2),
+  // k' = 8 (m % 2) + e = 3 kw + c (< 9), KRSC (32, 3, 3, 4) bf16
+  bf16x8_t bw[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int m = 4 * s + kg, kh = m >> 1, co = 16 * j + c16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int kk = 8 * (m & 1) + e, kw = kk / 3, c = kk % 3;
+        bw[j][s][e] = (kh < 3 && kk < 9) ? wk[((co * 3 + kh) * 3 + kw) * 4 + c] : (__bf16)0.f;
+      }
+    }
+  const int r0 = (int)((long)blockIdx.x * rows / gridDim.x);
+  const int r1 = (int)((long)(blockIdx.x + 1) * rows / gridDim.x);
+  const int nvalid = min(MPW, 7 - wave * MPW);
+  double rn = 0.0, rm[2] = {0.0, 0.0}, rq[2] = {0.0, 0.0};
+  StemRows feed{x, hin};
+  auto first = [&](int row) { return row == r0 || row % ho == 0; };
+  auto slot = [&](int r) { return ring + ((r + 3) % 3) * SXR; };
+  float4 setA[2], setB[2];
+  auto step = [&](int row, float4 (&cur)[2], float4 (&nxt)[2]) {
+    const int oh = row % ho;
+    const long g0 = (long)(row / ho) * hin;   // the frame's first input row
+    __syncthreads();
+    // publish rows r .. r + nr - 1 of a two-row register set (nr = 1: row r + 1 would overwrite
+    // the slot of row r - 2, which the ring of 3 still holds as 2 oh - 1)
+    auto put2 = [&](int r, const float4 (&v)[2], int nr) {
+      int tt = threadIdx.x;
+      asm volatile("" : "+v"(tt));
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = tt + 256 * q, k = i / SW2, col = i % SW2;
+        if (k < nr) put_px3(slot(r + k), col, v[q]);
+      }
+    };
+    if (first(row)) {
+      feed.fetch2(g0, 2 * oh - 1, cur);
+      put2(2 * oh - 1, cur, 2);
+      feed.fetch2(g0, 2 * oh + 1, cur);
+      put2(2 * oh + 1, cur, 1);
+    } else {
+      put2(2 * oh, cur, 2);
+    }
+    __syncthreads();
+    if (row + 1 < r1 && !first(row + 1)) feed.fetch2(g0, 2 * oh + 2, nxt);
+    f32x4_t acc[MPW][2];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i) acc[i][0] = acc[i][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int m = 4 * s + kg, kh = min(m >> 1, 2);   // (kernel row 3: zero weights)
+      const unsigned short* rp = slot(2 * oh - 1 + kh) + 8 * (m & 1);
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        if (i < nvalid) {
+          const int ow = 16 * (wave * MPW + i) + c16;
+          const uint32_t* pa = reinterpret_cast<const uint32_t*>(rp + 6 * ow);
+          uint4 av;
+          av.x = pa[0]; av.y = pa[1]; av.z = pa[2]; av.w = pa[3];
+          const bf16x8_t a = __builtin_bit_cast(bf16x8_t, av);
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][s], acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][s], acc[i][1], 0, 0, 0);
+        }
+      }
+    }
+    float sm[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MPW; ++i) {
+      if (i < nvalid) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int px = 16 * (wave * MPW + i) + 4 * kg + r, co = 16 * j + c16;
+            const unsigned short u = bfb(acc[i][j][r]);
+            acc[i][j][r] = bff(u);
+            ys[px * COUT + co] = u;
+            sm[j] += acc[i][j][r];
+          }
+      }
+    }
+    const float cnt = 16.f * nvalid;
+    float mj[2], qj[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float t = sm[j] + __shfl_xor(sm[j], 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      mj[j] = t / cnt;
+    }
+#pragma unroll
+    for (int i = 0; i < MPW; ++i) {
+      if (i < nvalid) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = acc[i][j][r] - mj[j];
+            qj[j] = fmaf(d, d, qj[j]);
+          }
+      }
+    }
+    const double nb = (double)cnt, na = rn, nt = na + nb;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float t = qj[j] + __shfl_xor(qj[j], 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      const double dd = (double)mj[j] - rm[j];
+      rm[j] += dd * nb / nt;
+      rq[j] += (double)t + dd * dd * na * nb / nt;
+    }
+    rn = nt;
+    __syncthreads();
+    uint4* yr = reinterpret_cast<uint4*>(y) + (long)row * (DW * COUT / 8);
+    for (int i = tid; i < DW * COUT / 8; i += 256) yr[i] = reinterpret_cast<const uint4*>(ys)[i];
+  };
+  for (int row = r0; row < r1; row += 2) {
+    step(row, setA, setB);
+    if (row + 1 < r1) step(row + 1, setB, setA);
+  }
+  if (kg == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      stats[((long)blockIdx.x * 4 + wave) * COUT + 16 * j + c16] =
+          make_float4((float)rn, (float)rm[j], (float)rq[j], 0.f);
+  }
+}
+
+// Its weight gradient: dW[co][kh][kw][c] = sum over output pixels of dy[p][co] * x[2 oh - 1 + kh]
+// [2 ow - 1 + kw][c].  Per output row: A = the dy row (co x 128 pixels) by transposed reads as in
+// d3w_k; B = per input row its im2col columns transposed, XI[slot][kw * 3 + c][p] (input column
+// col = 2 p - 1 + kw; built from each pixel's 3 values into the 1-2 kernel columns of its parity),
+// so a B fragment (8 consecutive pixels of one column k' = 9 kh + 3 kw + c) is one ds_read_b128.
+// Wave w: co tile w & 1, k' tile w >> 1 (k' 0..31, 27 real).
+constexpr int XPL = 136;   // pixels per XI row (128 + 8 pad: 272-B rows)
+
+__global__ __launch_bounds__(256, 2)
+void d3sw_k(const float4* __restrict__ x, const uint4* __restrict__ dy, float* __restrict__ slabs,
+            int hin, int ho, int rows) {
+  using PO = Px<32>;
+  __shared__ __attribute__((aligned(16))) unsigned short xi[3 * 9 * XPL + XPL];   // + a zero row
+  __shared__ __attribute__((aligned(16))) unsigned char dimg[128 * PO::PS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, tq = li >> 2, tp = li & 3;
+  const int mt = wave & 1, nt = wave >> 1;
+  for (int i = tid; i < (3 * 9 * XPL + XPL) / 2; i += 256) reinterpret_cast<uint32_t*>(xi)[i] = 0u;
+  for (int i = tid; i < 128 * PO::PS / 16; i += 256)
+    reinterpret_cast<uint4*>(dimg)[i] = make_uint4(0u, 0u, 0u, 0u);
+  unsigned short* const zrow = xi + 3 * 9 * XPL;
+  const int r0 = (int)((long)blockIdx.x * rows / gridDim.x);
+  const int r1 = (int)((long)(blockIdx.x + 1) * rows / gridDim.x);
+  StemRows feed{x, hin};
+  auto first = [&](int row) { return row == r0 || row % ho == 0; };
+  auto xslot = [&](int r) { return xi + ((r + 3) % 3) * 9 * XPL; };
+  // input pixel (row r, column col) -> its im2col columns: p = (col + 1 - kw) / 2 when even
+  auto put2 = [&](int r, const float4 (&v)[2], int nr) {   // (nr: as d3s_k)
+    int tt = threadIdx.x;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = tt + 256 * q, k = i / SW2, col = i % SW2;
+      if (k >= nr) continue;
+      unsigned short* blk = xslot(r + k);
+      const unsigned short u[3] = {bfb(v[q].x), bfb(v[q].y), bfb(v[q].z)};
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int t = col + 1 - kw;
+        if ((t & 1) == 0 && t >= 0 && t < 2 * DW) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) blk[(kw * 3 + c) * XPL + (t >> 1)] = u[c];
+        }
+      }
+    }
+  };
+  auto frag_a = [&](int pr) -> bf16x8_t {   // as d3w_k's transposed fragment (dy image)
+    const int hi = g & 1;
+    const unsigned char* p = dimg + (pr + tq) * PO::PS + (16 * mt + 4 * tp) * 2;
+    const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(p + 4 * hi * PO::PS));
+    const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(p + 4 * (hi ^ 1) * PO::PS));
+    const s16x4_t lo = hi ? v1 : v0, up = hi ? v0 : v1;
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, up, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float4 xA[2], xB[2];
+  uint4 dA[PO::PPT], dB[PO::PPT];
+  if (r0 < r1) RowIO<32>::fetch(dy, r0, true, dA);
+  auto step = [&](int row, float4 (&xc)[2], float4 (&xn)[2], uint4 (&dc)[PO::PPT],
+                  uint4 (&dn)[PO::PPT]) {
+    const int oh = row % ho;
+    const long g0 = (long)(row / ho) * hin;
+    __syncthreads();
+    // (rows outside the frame are fetched as zeros and published like any other: every im2col
+    // entry a real pixel can write is overwritten, the rest stays zero from the start)
+    if (first(row)) {
+      feed.fetch2(g0, 2 * oh - 1, xc);
+      put2(2 * oh - 1, xc, 2);
+      feed.fetch2(g0, 2 * oh + 1, xc);
+      put2(2 * oh + 1, xc, 1);
+    } else {
+      put2(2 * oh, xc, 2);
+    }
+    RowIO<32>::put(dimg, 0, dc);
+    __syncthreads();
+    if (row + 1 < r1) {
+      if (!first(row + 1)) feed.fetch2(g0, 2 * oh + 2, xn);
+      RowIO<32>::fetch(dy, row + 1, true, dn);
+    }
+    // B column k' = 16 nt + li: kernel row k' / 9, im2col column k' % 9 (k' >= 27: zero row)
+    const int kk = 16 * nt + li;
+    const unsigned short* pb = kk < 27 ? xslot(2 * oh - 1 + kk / 9) + (kk % 9) * XPL : zrow;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int pr = 32 * s + 8 * g;
+      const bf16x8_t a = frag_a(pr);
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(pb + pr);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
+  };
+  for (int row = r0; row < r1; row += 2) {
+    step(row, xA, xB, dA, dB);
+    if (row + 1 < r1) step(row + 1, xB, xA, dB, dA);
+  }
+  // slab layout of the engine's 4-channel stem wgrad: (co * 9 + tap) * 4 + c
+  float* slab = slabs + (long)blockIdx.x * (32 * 9 * 4);
+  const int kk = 16 * nt + li;
+  if (kk < 27) {
+    const int kh = kk / 9, kw = (kk % 9) / 3, c = kk % 3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 16 * mt + 4 * g + r;
+      slab[(co * 9 + kh * 3 + kw) * 4 + c] = acc[r];
+    }
+  }
+}
+
 constexpr int kGridW = 2 * 256;
 
 int grid_of(int rows, int cin, int cout, int mode) {
@@ -548,6 +826,41 @@ int tmr_d3_wgrad_slabs(int n, int h, int cin, int cout, const void* x, const voi
     hipLaunchKernelGGL((d3w_k<32, 32>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
                        (const uint4*)dy, ws, h, rows);
   TMR_CHECK_LAUNCH("d3_wgrad");
+  *nslabs = grid;
+  return 0;
+}
+
+// the deep stem's first conv (3x3/2, 3 -> 32 on the NHWC4 fp32 input): stats partial rows
+int tmr_d3s_stats_parts(int n, int ho) {
+  const int rows = n * ho;
+  return 4 * (rows < 3 * 256 ? rows : 3 * 256);
+}
+
+int tmr_d3s_fwd_bnstats(int n, int h, const float* x, const void* w_krsc, void* y, void* stats,
+                        hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && h % 2 == 0, "tmr_d3s_fwd: unsupported height %d", h);
+  TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)y) & 15) == 0, "tmr_d3s_fwd: x / y must be 16-B aligned");
+  const int ho = h / 2, rows = n * ho, grid = rows < 3 * 256 ? rows : 3 * 256;
+  hipLaunchKernelGGL(d3s_k, dim3(grid), dim3(256), 0, stream, (const float4*)x,
+                     (const __bf16*)w_krsc, (__bf16*)y, (float4*)stats, h, ho, rows);
+  TMR_CHECK_LAUNCH("d3s_fwd");
+  return 0;
+}
+
+size_t tmr_d3s_wgrad_ws_bytes(int n, int ho) {
+  const int rows = n * ho;
+  return (size_t)(rows < kGridW ? rows : kGridW) * 32 * 9 * 4 * sizeof(float);
+}
+
+int tmr_d3s_wgrad_slabs(int n, int h, const float* x, const void* dy, float* ws, size_t ws_bytes,
+                        int* nslabs, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && h % 2 == 0, "tmr_d3s_wgrad: unsupported height %d", h);
+  TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)dy) & 15) == 0, "tmr_d3s_wgrad: x / dy must be 16-B aligned");
+  const int ho = h / 2, rows = n * ho, grid = rows < kGridW ? rows : kGridW;
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_d3s_wgrad_ws_bytes(n, ho), "tmr_d3s_wgrad: workspace too small");
+  hipLaunchKernelGGL(d3sw_k, dim3(grid), dim3(256), 0, stream, (const float4*)x, (const uint4*)dy,
+                     ws, h, ho, rows);
+  TMR_CHECK_LAUNCH("d3s_wgrad");
   *nslabs = grid;
   return 0;
 }

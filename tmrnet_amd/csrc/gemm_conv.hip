@@ -384,6 +384,23 @@ static bool d3_shape(const tmr_conv_desc* d) {
          d->wo == 112 && d->ho == d->h && d->c == 32 && (d->k == 32 || d->k == 64) &&
          xld_of(d) == d->c && yld_of(d) == d->k && d->max_frames == 0;
 }
+// ... and the deep stem's first conv, 3x3/2 3 -> 32, on the NHWC4 fp32 input (bf16 math)
+int tmr_d3s_stats_parts(int n, int ho);
+int tmr_d3s_fwd_bnstats(int n, int h, const float* x, const void* w_krsc, void* y, void* stats,
+                        hipStream_t stream);
+size_t tmr_d3s_wgrad_ws_bytes(int n, int ho);
+int tmr_d3s_wgrad_slabs(int n, int h, const float* x, const void* dy, float* ws, size_t ws_bytes,
+                        int* nslabs, hipStream_t stream);
+static bool d3s_shape(const tmr_conv_desc* d) {
+  return env_int("TMR_DIRECT3", 1) != 0 && d->math == TMR_MATH_BF16 && ngroups(d) == 1 &&
+         d->c == 4 && d->k == 32 && d->r == 3 && d->s == 3 && d->stride == 2 && d->pad == 1 &&
+         d->pad_w == 1 && d->w == 224 && d->wo == 112 && d->h % 2 == 0 && d->ho == d->h / 2 &&
+         xld_of(d) == 4 && yld_of(d) == 32 && d->max_frames == 0;
+}
+static bool d3s_fwd(const tmr_conv_desc* d) {
+  return d3s_shape(d) && d->io == (TMR_IO_W_BF16 | TMR_IO_Y_BF16);
+}
+static bool d3s_wgrad(const tmr_conv_desc* d) { return d3s_shape(d) && d->io == TMR_IO_DY_BF16; }
 static bool d3_fwd(const tmr_conv_desc* d) {
   return d3_shape(d) && d->io == (TMR_IO_X_BF16 | TMR_IO_W_BF16 | TMR_IO_Y_BF16);
 }
@@ -402,6 +419,7 @@ TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
   if (stem_direct(d)) return tmr_stem_stats_parts(d->n, d->ho);
   if (stem16_direct(d)) return tmr_stem16_stats_parts(d->n, d->ho);
   if (d3_fwd(d)) return tmr_d3_stats_parts(d->n, d->h, d->c, d->k);
+  if (d3s_fwd(d)) return tmr_d3s_stats_parts(d->n, d->ho);
   tmr_conv_desc g = *d;
   if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
   const int fc = frames_per_launch(&g);
@@ -452,13 +470,14 @@ static int conv_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
                 stats_bytes, need);
   // the parts query (above) sized `stats` for the direct stem's row layout: an operand prologue
   // would route the stem to the engine, which writes a different number of partial rows
-  TMR_CHECK_ARG(!(pro && (stem_direct(d) || stem16_direct(d) || d3_fwd(d))),
+  TMR_CHECK_ARG(!(pro && (stem_direct(d) || stem16_direct(d) || d3_fwd(d) || d3s_fwd(d))),
                 "tmr_conv2d_fwd_bnstats: the 7x7 stem takes no operand prologue");
   if (stem_direct(d))
     return tmr_stem_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, y, stats, stream);
   if (stem16_direct(d))
     return tmr_stem16_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, 4, y, stats, stream);
   if (!pro && d3_fwd(d)) return tmr_d3_fwd_bnstats(d->n, d->h, d->c, d->k, x, w_krsc, y, stats, stream);
+  if (!pro && d3s_fwd(d)) return tmr_d3s_fwd_bnstats(d->n, d->h, x, w_krsc, y, stats, stream);
   if (ngroups(d) == 1) return fwd_bnstats_impl(d, x, w_krsc, y, (float4*)stats, d->k, pro, stream);
   TMR_CHECK_ARG(!pro, "tmr_conv2d_fwd_bnstats: operand prologues take no groups");
   tmr_conv_desc g;
@@ -799,6 +818,8 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
     bytes = (size_t)kStem16Slabs * kStemSlab * sizeof(float);
   if (d3_wgrad(d) && bytes < tmr_d3_wgrad_ws_bytes(d->n, d->h, d->c, d->k))
     bytes = tmr_d3_wgrad_ws_bytes(d->n, d->h, d->c, d->k);
+  if (d3s_wgrad(d) && bytes < tmr_d3s_wgrad_ws_bytes(d->n, d->ho))
+    bytes = tmr_d3s_wgrad_ws_bytes(d->n, d->ho);
   return bytes;
 }
 
@@ -860,6 +881,15 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, 1), dim3(256), 0, stream, ws, ns,
                        kStemSlab, dw_oihw, 49, 4, 3, beta);
+    TMR_CHECK_LAUNCH("wgrad_reduce_taps_kernel");
+    return 0;
+  }
+  if (!pro && c_real == 3 && d3s_wgrad(d)) {
+    int ns = 0;
+    const int rc = tmr_d3s_wgrad_slabs(d->n, d->h, x, dy, ws, ws_bytes, &ns, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, 1), dim3(256), 0, stream, ws, ns,
+                       (long)32 * 9 * 4, dw_oihw, 9, 4, 3, beta);
     TMR_CHECK_LAUNCH("wgrad_reduce_taps_kernel");
     return 0;
   }

@@ -62,6 +62,8 @@ def _bn_train_or_eval(y, bn, training):
 FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
 # the 4-channel stem input as NHWC8 bf16 on the bf16 operand path (trunk.STEM8's switch)
 STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
+# the deep stem's convs as direct kernels (direct3.hip; read again by the library per launch)
+DIRECT3 = os.environ.get("TMR_DIRECT3", "1") != "0"
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -281,8 +283,10 @@ class ResNeStTrunkFn(torch.autograd.Function):
         nbt = []
         stem = []
         c = share.conv1
-        # the stem input: NHWC8 bf16 under bf16 activations (the LDS-DMA engine's 8-channel pieces)
-        xs = ops.nhwc4_to_bf16x8(x4) if a16 else x4
+        # the stem input: under bf16 activations the NHWC4 fp32 frames themselves for the direct
+        # 3x3/2 stem conv (direct3.hip: rounded to bf16 as it is staged), or an NHWC8 bf16 copy
+        # for the LDS-DMA engine (TMR_DIRECT3=0: its 8-channel pieces)
+        xs = ops.nhwc4_to_bf16x8(x4) if (a16 and not DIRECT3) else x4
         z = _conv_bn(xs, c[0], c[1], 2, 1, True, True, recs=stem, math=mt, nbt=nbt)
         z = _conv_bn(z, c[3], c[4], 1, 1, True, True, recs=stem, math=mt, nbt=nbt)
         # share.bn1 + relu applied inside the maxpool (its backward recomputes the mask from y)
