@@ -311,6 +311,15 @@ int tmr_bn_apply_a16(const void* y, const float* scale, const float* shift, cons
 int tmr_bn_apply2_a16(const void* y, const float* scale, const float* shift, const void* yr,
                       const float* rscale, const float* rshift, void* z, int rows, int c, int relu,
                       hipStream_t stream);
+/* tmr_bn_apply_bits / tmr_bn_apply2_bits for bf16 activations: z bf16 and its ReLU mask as bits
+ * (taken from the rounded z, so mask 3 equals the mask-1 test z > 0) for the residual-gradient
+ * dgrads of the bf16 LDS-DMA engine (TMR_IO_WT_BF16, mask 3) */
+int tmr_bn_apply_bits_a16(const void* y, const float* scale, const float* shift,
+                          const void* residual, void* z, uint32_t* bits, int rows, int c,
+                          hipStream_t stream);
+int tmr_bn_apply2_bits_a16(const void* y, const float* scale, const float* shift, const void* yr,
+                           const float* rscale, const float* rshift, void* z, uint32_t* bits,
+                           int rows, int c, hipStream_t stream);
 int tmr_bn_bwd_a16(const float* dz, const void* y, const void* z, const float* scale,
                    const float* shift, const float* save_mean, const float* save_invstd,
                    const float* gamma, void* dy, float* dres, float* dgamma, float* dbeta, int rows,

@@ -643,6 +643,46 @@ def test_bn_apply_relu_bits(dev, rows, c):
                              z=ops.relu_bits_empty(torch.empty(1, 4, 4, 64, device=dev)))
 
 
+@pytest.mark.parametrize("rows,c", [(1000, 256), (77, 64), (3, 8)])
+def test_bn_apply_relu_bits_bf16(dev, rows, c):
+    """The bf16-activation forms (tmr_bn_apply_bits_a16 / _apply2_bits_a16): z bit-identical to
+    bn_apply / bn_apply2 on bf16 tensors, bits exactly (z > 0) of the stored bf16 z -- the test
+    the mask-1 dgrads apply to z -- and the bf16 LDS-DMA dgrad with mask 3 bit-identical to
+    mask 1 on the same z."""
+    g = torch.Generator().manual_seed(rows * 3 + c)
+    b16 = torch.bfloat16
+    y = torch.randn(rows, c, generator=g).to(dev).to(b16)
+    res = torch.randn(rows, c, generator=g).to(dev).to(b16)
+    yr = torch.randn(rows, c, generator=g).to(dev).to(b16)
+    sc, sh = (torch.rand(c, generator=g) + 0.5).to(dev), torch.randn(c, generator=g).to(dev)
+    rs, rf = (torch.rand(c, generator=g) + 0.5).to(dev), torch.randn(c, generator=g).to(dev)
+    for resid in (res, None):
+        z, bits = ops.bn_apply_bits(y, sc, sh, resid)
+        zr = ops.bn_apply(y, sc, sh, resid, True)
+        torch.cuda.synchronize()
+        assert z.dtype == b16 and torch.equal(z, zr)
+        assert torch.equal(bits.cpu(), _pack_bits((zr > 0).cpu()))
+    z2, bits2 = ops.bn_apply2_bits(y, sc, sh, yr, rs, rf)
+    z2r = ops.bn_apply2(y, sc, sh, yr, rs, rf, True)
+    torch.cuda.synchronize()
+    assert torch.equal(z2, z2r) and torch.equal(bits2.cpu(), _pack_bits((z2r > 0).cpu()))
+    if rows == 1000:   # a residual-gradient 1x1 dgrad over these rows as (10, 10, 10) pixels
+        n, hw = 10, 10
+        yv, zv, bv = y.view(n, hw, hw, c), z2.view(n, hw, hw, c), bits2
+        k = 64
+        dy = torch.randn(n, hw, hw, k, generator=g).to(dev).to(b16)
+        w = torch.randn(k, c, 1, 1, generator=g).to(dev) / c ** 0.5
+        wt = ops.weight_to_crsk(w)
+        mu = torch.randn(c, generator=g).to(dev) * 0.1
+        old = torch.randn(n, hw, hw, c, generator=g).to(dev)
+        d1, p1, n1 = ops.conv_dgrad_bnbwd(dy, wt, (hw, hw), 1, 0, yv, mu, 1, z=zv,
+                                          out=old.clone(), beta=1.0, math="bf16", wt=True)
+        d3, p3, n3 = ops.conv_dgrad_bnbwd(dy, wt, (hw, hw), 1, 0, yv, mu, 3, z=bv,
+                                          out=old.clone(), beta=1.0, math="bf16", wt=True)
+        torch.cuda.synchronize()
+        assert n1 == n3 and torch.equal(d1, d3) and torch.equal(p1[:n1], p3[:n3])
+
+
 def test_stem_direct_fwd_bnstats(dev, monkeypatch):
     """The fp32 7x7/2 stem with BatchNorm statistics as a direct convolution over its 147 real
     (tap, channel) pairs (stem.hip, the train step's 224x224 geometry) against float64: the

@@ -71,6 +71,8 @@ SIGNATURES = {
     "tmr_maxpool2d_fwd_bn_x": [P, P, P, P, P, I, I, I, I, I, I, I, P],
     "tmr_bn_apply_a16": [P, P, P, P, P, I, I, I, P],
     "tmr_bn_apply2_a16": [P, P, P, P, P, P, P, I, I, I, P],
+    "tmr_bn_apply_bits_a16": [P, P, P, P, P, P, I, I, P],
+    "tmr_bn_apply2_bits_a16": [P, P, P, P, P, P, P, P, I, I, P],
     "tmr_bn_bwd_a16": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_a16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_g16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],

@@ -979,6 +979,40 @@ TMR_API int tmr_bn_apply2_bits(const float* y, const float* scale, const float* 
   return 0;
 }
 
+TMR_API int tmr_bn_apply_bits_a16(const void* y, const float* scale, const float* shift,
+                                  const void* residual, void* z, uint32_t* bits, int rows, int c,
+                                  hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && z && bits,
+                "tmr_bn_apply_bits_a16: null operand or channels %d not a multiple of 4", c);
+  const long n4 = (long)rows * c / 4;
+  if (n4 == 0) return 0;
+  const __bf16* yb = (const __bf16*)y;
+  if (residual)
+    hipLaunchKernelGGL((bn_apply_bits_k<true, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, yb,
+                       scale, shift, (const __bf16*)residual, nullptr, nullptr, nullptr, (__bf16*)z,
+                       bits, n4, c / 4);
+  else
+    hipLaunchKernelGGL((bn_apply_bits_k<false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, yb,
+                       scale, shift, nullptr, nullptr, nullptr, nullptr, (__bf16*)z, bits, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply_bits_a16");
+  return 0;
+}
+
+TMR_API int tmr_bn_apply2_bits_a16(const void* y, const float* scale, const float* shift,
+                                   const void* yr, const float* rscale, const float* rshift,
+                                   void* z, uint32_t* bits, int rows, int c, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 4 == 0 && y && scale && shift && yr && rscale && rshift && z && bits,
+                "tmr_bn_apply2_bits_a16: null operand or channels %d not a multiple of 4", c);
+  TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_bits_a16: the branch input must not alias z");
+  const long n4 = (long)rows * c / 4;
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL((bn_apply_bits_k<false, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream,
+                     (const __bf16*)y, scale, shift, nullptr, (const __bf16*)yr, rscale, rshift,
+                     (__bf16*)z, bits, n4, c / 4);
+  TMR_CHECK_LAUNCH("bn_apply2_bits_a16");
+  return 0;
+}
+
 TMR_API int tmr_bn_apply_dual(const float* y, const float* scale, const float* shift,
                               const float* residual, float* z, void* z16, int rows, int c, int relu,
                               hipStream_t stream) {

@@ -618,25 +618,33 @@ def relu_bits_empty(like):
 
 def bn_apply_bits(y, scale, shift, residual=None):
     """Block output with ReLU: z = relu(y*scale + shift (+ residual)) and its ReLU mask as bits
-    (tmr_bn_apply_bits; fp32) -> (z, bits), for the mask-3 residual-gradient dgrads."""
-    _req(y, "y")
+    (tmr_bn_apply_bits, or _bits_a16 for bf16 activations: y, residual and z bf16) -> (z, bits),
+    for the mask-3 residual-gradient dgrads."""
+    _req(y, "y", y.dtype)
     c = y.shape[-1]
     z = torch.empty_like(y)
     bits = relu_bits_empty(y)
-    call("tmr_bn_apply_bits", y, scale, shift, residual, z, bits, y.numel() // c, c, stream_ptr())
+    if y.dtype == BF16:
+        if residual is not None and residual.dtype != BF16:
+            raise RuntimeError("bn_apply_bits: a bf16 y takes a bf16 residual")
+        call("tmr_bn_apply_bits_a16", y, scale, shift, residual, z, bits, y.numel() // c, c,
+             stream_ptr())
+    else:
+        call("tmr_bn_apply_bits", y, scale, shift, residual, z, bits, y.numel() // c, c,
+             stream_ptr())
     return z, bits
 
 
 def bn_apply2_bits(y, scale, shift, yr, rscale, rshift):
-    """bn_apply2 with ReLU plus the ReLU mask as bits -> (z, bits); fp32."""
-    _req(y, "y"); _req(yr, "yr")
+    """bn_apply2 with ReLU plus the ReLU mask as bits -> (z, bits); fp32, or bf16 y / yr / z."""
+    _req(y, "y", y.dtype); _req(yr, "yr", y.dtype)
     if yr.shape != y.shape:
         raise RuntimeError("bn_apply2_bits: branch shape %s != %s" % (tuple(yr.shape), tuple(y.shape)))
     c = y.shape[-1]
     z = torch.empty_like(y)
     bits = relu_bits_empty(y)
-    call("tmr_bn_apply2_bits", y, scale, shift, yr, rscale, rshift, z, bits, y.numel() // c, c,
-         stream_ptr())
+    name = "tmr_bn_apply2_bits_a16" if y.dtype == BF16 else "tmr_bn_apply2_bits"
+    call(name, y, scale, shift, yr, rscale, rshift, z, bits, y.numel() // c, c, stream_ptr())
     return z, bits
 
 

@@ -156,11 +156,13 @@ G16 = os.environ.get("TMR_G16", "1") != "0"
 # gradient of every block output but the last.
 R16 = os.environ.get("TMR_BF16_RESGRAD", "1") != "0"
 
-# the fp32 block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z).
-# The bf16-activation step re-reads its 2-byte z instead: bits measured slower there (C5 dgrads
-# 58.8 vs 56.6 ms/step, C4 23.1 vs 22.2; profiles/r3/bench_r4i/ -- one dword load per row shared
-# by 8 threads), and that variant was removed in round 4.
+# the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
 BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
+# ... and for the bf16-activation step (TMR_RELU_BITS16): under the round-3 fp32 residual gradient
+# the bits measured no faster than re-reading the 2-byte z (C5 dgrads 56.6 vs 58.8 ms/step,
+# profiles/r3/bench_r4i/); under the bf16 residual gradient (R16) z is a quarter of the residual
+# dgrads' epilogue bytes (round-4 A/B: profiles/r4/bits16_ab/)
+BITS16 = os.environ.get("TMR_RELU_BITS16", "0") == "1"
 
 
 def _dma32(math):
@@ -230,8 +232,11 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     # fp32 block outputs on the LDS-DMA path also record their ReLU mask as bits: the dgrad that
     # produces their gradient reads 1 bit instead of z's 4 bytes (mask 3)
     zbits = None
-    bits = (recs is not None and relu and not dual and _dma32(math) and
-            y.dtype == torch.float32 and (residual is not None or branch is not None) and BITS)
+    # (bf16 activations too: the bits of the rounded z, tmr_bn_apply_bits_a16)
+    bits = (recs is not None and relu and not dual and
+            ((_dma32(math) and y.dtype == torch.float32) or
+             (_act16(math) and y.dtype == torch.bfloat16 and BITS16))
+            and (residual is not None or branch is not None) and BITS)
     if defer:
         z = None
     elif branch is not None and bits:
