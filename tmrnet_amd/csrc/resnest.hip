@@ -479,6 +479,71 @@ __global__ __launch_bounds__(NT) void splat_bwd_apply_bn_k(
   }
 }
 
+// The bf16 form with 8 channels of both radix halves per thread (C a multiple of 8, 256 / (C/8)
+// whole): the channel octet is fixed per thread (the grid is a multiple of C/8 threads), so the
+// per-channel coefficients stay in registers, dout is read once for both halves (it was read per
+// half), att / dgap once per frame, every access 16 B.  The same arithmetic per element as
+// splat_bwd_apply_bn_k (dgap/hw rounded once per channel, as there per element).
+__global__ __launch_bounds__(NT) void splat_bwd_apply_bn8_k(
+    const float* __restrict__ dout, const __bf16* __restrict__ y, const float* __restrict__ sc,
+    const float* __restrict__ sh, const float* __restrict__ mean, const float* __restrict__ att,
+    const float* __restrict__ dgap, const float* __restrict__ coef, __bf16* __restrict__ dy,
+    uint32_t npix, int C, FastDiv dhw) {
+  const int c8 = C / 8;
+  const uint32_t t = blockIdx.x * NT + threadIdx.x;
+  const int q = (int)(t % (uint32_t)c8);
+  const uint32_t pstride = gridDim.x * NT / c8;
+  const float ihw = 1.0f / (float)dhw.d;
+  float s[2][8], h[2][8], mu[2][8], k0[2][8], k1[2][8], k2[2][8];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = r * C + 8 * q + e;
+      s[r][e] = sc[j]; h[r][e] = sh[j]; mu[r][e] = mean[j];
+      k0[r][e] = coef[j]; k1[r][e] = coef[2 * C + j]; k2[r][e] = coef[4 * C + j];
+    }
+  float a[2][8], dg[8];
+  uint32_t cur = 0xffffffffu;
+  for (uint32_t p = t / c8; p < npix; p += pstride) {
+    const uint32_t nn = fdiv(p, dhw);
+    if (nn != cur) {
+      cur = nn;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[0][e] = att[(long)nn * 2 * C + 8 * q + e];
+        a[1][e] = att[(long)nn * 2 * C + C + 8 * q + e];
+        dg[e] = dgap[(long)nn * C + 8 * q + e] * ihw;
+      }
+    }
+    const float4* gp = reinterpret_cast<const float4*>(dout + (long)p * C + 8 * q);
+    const float4 g0 = gp[0], g1 = gp[1];
+    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const long off = (long)p * 2 * C + r * C + 8 * q;   // elements
+      const uint4 yw = *reinterpret_cast<const uint4*>(y + off);
+      const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        float v[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int e = 2 * e2 + b;
+          const float yv = b ? __uint_as_float(yu[e2] & 0xffff0000u) : __uint_as_float(yu[e2] << 16);
+          const float gg = fmaf(yv, s[r][e], h[r][e]) > 0.f ? fmaf(a[r][e], gv[e], dg[e]) : 0.f;
+          v[b] = k0[r][e] * (gg - k1[r][e] - (yv - mu[r][e]) * k2[r][e]);
+        }
+        typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+        const b2 pr = {(__bf16)v[0], (__bf16)v[1]};
+        o[e2] = __builtin_bit_cast(uint32_t, pr);
+      }
+      *reinterpret_cast<uint4*>(dy + off) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 // AvgPool2d of bf16 activations (avd layer, avg_down): fp32 sums of the bf16 inputs, output rounded
 // IT: index type (uint32_t when the element groups fit 31 bits: 64-bit divisions cost
 // ~100 instructions per element; tmr_avgpool2d_* pick it)
@@ -706,7 +771,16 @@ TMR_API int tmr_splat_bwd_apply_bn(const float* dout, const void* y, const float
   TMR_CHECK_ARG(total < (1L << 31), "tmr_splat_bwd_apply_bn: %ld element groups exceed 2^31", total);
   const int nb = blocks_for(total);
   const FastDiv dj4 = make_fastdiv((uint32_t)(2 * c / 4)), dhw = make_fastdiv((uint32_t)hw);
-  if (act16)
+  const char* w8 = getenv("TMR_SPLAT8");   // A/B switch (0: the 4-wide form), read per call
+  const bool wide = !(w8 && w8[0] == '0');
+  if (act16 && wide && c % 8 == 0 && NT % (c / 8) == 0 &&
+      ((((uintptr_t)dout) | ((uintptr_t)y) | ((uintptr_t)dy)) & 15) == 0) {
+    const long npix = (long)n * hw;
+    const int nb8 = blocks_for(npix * (c / 8));   // (a multiple of c/8 threads: NT % (c/8) == 0)
+    hipLaunchKernelGGL(splat_bwd_apply_bn8_k, dim3(nb8), dim3(NT), 0, stream, dout,
+                       (const __bf16*)y, scale, shift, mean, att, dgap, coef, (__bf16*)dy,
+                       (uint32_t)npix, c, dhw);
+  } else if (act16)
     hipLaunchKernelGGL(splat_bwd_apply_bn_k<__bf16>, dim3(nb), dim3(NT), 0, stream, dout,
                        (const __bf16*)y, scale, shift, mean, att, dgap, coef, (__bf16*)dy,
                        (uint32_t)total, dj4, dhw);
