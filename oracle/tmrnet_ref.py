@@ -260,6 +260,9 @@ class BottleneckS(nn.Module):
     def forward(self, x):
         rnd = getattr(self, "round_out", False) and self.training   # emulate_bf16_convs(activations)
         out = self.relu(self.bn1(self.conv1(x)))
+        if getattr(self, "round_grad", False) and self.training:
+            # resnest.py: the grouped conv's fused dgrad stores relu(bn1)'s gradient bf16 (G16)
+            out = _GradRoundFn.apply(out)
         out = self.conv2(out)
         if self.avd:
             out = self.avd_layer(out)
@@ -387,8 +390,9 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
     activations=True: in train mode the conv outputs and the Bottleneck outputs are rounded to
     bf16 as well (the bf16-activation contract of the train step; ResNeSt-50 also stores the
     split attention's relu(bn0) input and output and the avd pool output as bf16).
-    grads (default: activations): the ResNet-50 Bottleneck's relu(bn1) / relu(bn2) gradients are
-    rounded to bf16 in the backward (trunk.G16: the fused dgrad stores them bf16), and so is the
+    grads (default: activations): the ResNet-50 Bottleneck's relu(bn1) / relu(bn2) gradients (the
+    ResNeSt BottleneckS's relu(bn1), round 4) are rounded to bf16 in the backward (trunk.G16: the
+    fused dgrad stores them bf16), and so is the
     gradient of every Bottleneck (ResNeSt: BottleneckS) output but the last (trunk.R16: the
     residual stream's gradient, written by the next block's conv1 dgrad; the last block's comes
     from the avgpool in fp32).
@@ -402,7 +406,7 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
             m.round_out = activations
         elif isinstance(m, (Bottleneck, BottleneckS, SplAtConv2d)):
             m.round_out = activations
-            if isinstance(m, Bottleneck):
+            if isinstance(m, (Bottleneck, BottleneckS)):
                 m.round_grad = grads
             if isinstance(m, (Bottleneck, BottleneckS)):
                 m.round_res_grad = res_grads and m is not blocks[-1]

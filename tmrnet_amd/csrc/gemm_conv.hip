@@ -683,10 +683,10 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
                 "tmr_conv2d_dgrad_bnbwd: a grouped dgrad takes no ReLU-mask bits / prologue");
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
   TMR_CHECK_ARG(!(d->io & TMR_IO_G16) ||
-                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) &&
-                     ngroups(d) == 1 && !pro && d->c % 8 == 0),
+                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) && !pro &&
+                     (d->c / ngroups(d)) % 8 == 0),
                 "tmr_conv2d_dgrad_bnbwd: a bf16 gradient (TMR_IO_G16) needs bf16 math on the LDS-DMA "
-                "engine (TMR_IO_WT_BF16), no groups / prologue, c a multiple of 8");
+                "engine (TMR_IO_WT_BF16), no prologue, channels per group a multiple of 8");
   TMR_CHECK_ARG(!dx_old || ngroups(d) == 1, "tmr_conv2d_dgrad_bnbwd: a separate old dx takes no groups");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
                 "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
@@ -714,7 +714,7 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
       fz.part = (float2*)parts + o;
       fz.part_ld = d->c;
       const int rc = dgrad_bnbwd_run(&g, adv(dy, (long)i * g.k, esz_dy(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
-                                     dx + o, beta, &fz, stream);
+                                     adv(dx, o, esz_dx(d)), beta, &fz, stream);
       if (rc) return rc;
     }
     return 0;

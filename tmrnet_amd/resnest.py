@@ -354,7 +354,8 @@ class ResNeStTrunkFn(torch.autograd.Function):
             r2 = rec["r2"]
             dy2 = _splat_bwd(blk.conv2, rec["spl"], r2, dout, grads)
             del dout
-            dz1, _, fz1 = _conv_bn_bwd(r2, None, grads, dy=dy2, fuse_prev=rec["r1"])
+            # (relu(bn1)'s gradient stored bf16 by the grouped dgrad: trunk.G16, round 4)
+            dz1, _, fz1 = _conv_bn_bwd(r2, None, grads, dy=dy2, fuse_prev=rec["r1"], g16=True)
             del dy2
             if rec["rd"] is not None:
                 dxr, _, _ = _conv_bn_bwd(rec["rd"], dres, grads)

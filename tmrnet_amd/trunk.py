@@ -345,10 +345,13 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
             zm = p["z"]
             if mask == 1 and wt and p.get("zbits") is not None:
                 mask, zm = 3, p["zbits"]   # the ReLU mask as bits (fp32 LDS-DMA dgrad)
-            bf8 = (wt and grp == 1 and dpro is None and p["y"].dtype == torch.bfloat16 and
-                   p["y"].shape[-1] % 8 == 0)
+            bf8 = (wt and dpro is None and p["y"].dtype == torch.bfloat16 and
+                   (p["y"].shape[-1] // grp) % 8 == 0)
+            # (a grouped dgrad -- ResNeSt's radix-2 conv -- stores its per-group channel slices bf16
+            # too; the residual accumulation stays ungrouped)
             gb = (g16 and G16 and mask == 2 and dx_out is None and dx_beta == 0.0 and bf8)
-            rb = (r16 and R16 and mask in (1, 3) and dx_out is not None and dx_beta == 1.0 and bf8)
+            rb = (r16 and R16 and mask in (1, 3) and dx_out is not None and dx_beta == 1.0 and bf8
+                  and grp == 1)
             old = None
             if rb and dx_out.dtype != torch.bfloat16:   # fp32 old dx -> a new bf16 dx
                 old, dx_out = dx_out, None
