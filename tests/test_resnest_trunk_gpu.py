@@ -158,10 +158,10 @@ def test_split_attention_bn_on_load(dev, n, h, w, C, bf16):
 
 
 @pytest.mark.parametrize("n,h,w,C", [(6, 56, 56, 64), (8, 7, 7, 512), (5, 5, 3, 32)])
-def test_split_attention_apply8_bit_identical(dev, monkeypatch, n, h, w, C):
-    """The 8-channel bf16 backward apply (splat_bwd_apply_bn8_k: both radix halves per thread,
-    coefficients in registers) against the 4-wide form (TMR_SPLAT8=0): the same arithmetic per
-    element, so dy bit-identical."""
+def test_split_attention_8wide_bit_identical(dev, monkeypatch, n, h, w, C):
+    """The 8-channel bf16 combine and backward apply (splat_combine_bn8_k, splat_bwd_apply_bn8_k:
+    both radix halves per thread, coefficients in registers) against the 4-wide forms
+    (TMR_SPLAT8=0): the same arithmetic per element, so out and dy bit-identical."""
     from tmrnet_amd.resnest import SplAtConv2d, _splat_fwd, _splat_bwd
     torch.manual_seed(3 * C + h)
     md = SplAtConv2d(C, C).to(dev).train()
@@ -171,11 +171,13 @@ def test_split_attention_apply8_bit_identical(dev, monkeypatch, n, h, w, C):
     mean, inv, sc, sh = ops.bn_fwd_train(y.float().view(-1, 2 * C), bn0.weight.detach(),
                                          bn0.bias.detach(), bn0.running_mean, bn0.running_var,
                                          bn0.momentum, bn0.eps)
-    out, spl = _splat_fwd(md, y, sc, sh, [])
     r2 = {"y": y, "scale": sc, "shift": sh, "mean": mean, "inv": inv}
-    dys = []
+    outs, dys = [], []
     for flag in ("1", "0"):
         monkeypatch.setenv("TMR_SPLAT8", flag)
+        out, spl = _splat_fwd(md, y, sc, sh, [])
+        outs.append(out)
         dys.append(_splat_bwd(md, spl, r2, gy, {}))
     torch.cuda.synchronize()
+    assert outs[0].dtype == torch.bfloat16 and torch.equal(outs[0], outs[1])
     assert dys[0].dtype == torch.bfloat16 and torch.equal(dys[0], dys[1])

@@ -326,6 +326,63 @@ __global__ __launch_bounds__(NT) void splat_combine_bn_k(const T* __restrict__ y
   }
 }
 
+// The bf16 form with 8 channels per thread (splat_bwd_apply_bn8_k's layout: the octet fixed per
+// thread, both radix halves' BN coefficients in registers, att once per frame, 16-B accesses); the
+// same arithmetic per element as splat_combine_bn_k.
+__global__ __launch_bounds__(NT) void splat_combine_bn8_k(const __bf16* __restrict__ y,
+                                                          const float* __restrict__ sc,
+                                                          const float* __restrict__ sh,
+                                                          const float* __restrict__ att,
+                                                          __bf16* __restrict__ out, uint32_t npix,
+                                                          int C, FastDiv dhw) {
+  const int c8 = C / 8;
+  const uint32_t t = blockIdx.x * NT + threadIdx.x;
+  const int q = (int)(t % (uint32_t)c8);
+  const uint32_t pstride = gridDim.x * NT / c8;
+  float s[2][8], h[2][8];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s[r][e] = sc[r * C + 8 * q + e];
+      h[r][e] = sh[r * C + 8 * q + e];
+    }
+  float a[2][8];
+  uint32_t cur = 0xffffffffu;
+  for (uint32_t p = t / c8; p < npix; p += pstride) {
+    const uint32_t nn = fdiv(p, dhw);
+    if (nn != cur) {
+      cur = nn;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[0][e] = att[(long)nn * 2 * C + 8 * q + e];
+        a[1][e] = att[(long)nn * 2 * C + C + 8 * q + e];
+      }
+    }
+    const uint4 w0 = *reinterpret_cast<const uint4*>(y + (long)p * 2 * C + 8 * q);
+    const uint4 w1 = *reinterpret_cast<const uint4*>(y + (long)p * 2 * C + C + 8 * q);
+    const uint32_t u0[4] = {w0.x, w0.y, w0.z, w0.w}, u1[4] = {w1.x, w1.y, w1.z, w1.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      float v[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int e = 2 * e2 + b;
+        const float y0 = b ? __uint_as_float(u0[e2] & 0xffff0000u) : __uint_as_float(u0[e2] << 16);
+        const float y1 = b ? __uint_as_float(u1[e2] & 0xffff0000u) : __uint_as_float(u1[e2] << 16);
+        const float x0 = Act<__bf16>::rnd(fmaxf(fmaf(y0, s[0][e], h[0][e]), 0.f));
+        const float x1 = Act<__bf16>::rnd(fmaxf(fmaf(y1, s[1][e], h[1][e]), 0.f));
+        v[b] = fmaf(a[1][e], x1, a[0][e] * x0);
+      }
+      typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+      const b2 pr = {(__bf16)v[0], (__bf16)v[1]};
+      o[e2] = __builtin_bit_cast(uint32_t, pr);
+    }
+    *reinterpret_cast<uint4*>(out + (long)p * C + 8 * q) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // Backward reduction pass, per (frame, channel): for each radix r (x_r recomputed, m_r its ReLU
 // mask, d_r = y_r - mean_r)
 //   P_r = sum dout*x_r        -> dzl = softmax backward over the radix pair (weighted-sum -> att)
@@ -723,7 +780,13 @@ TMR_API int tmr_splat_combine_bn(const void* y, const float* scale, const float*
   TMR_CHECK_ARG(total < (1L << 31), "tmr_splat_combine_bn: %ld element groups exceed 2^31", total);
   const int nb = blocks_for(total);
   const FastDiv dc4 = make_fastdiv((uint32_t)(c / 4)), dhw = make_fastdiv((uint32_t)hw);
-  if (act16)
+  const char* w8 = getenv("TMR_SPLAT8");   // A/B switch (0: the 4-wide form), read per call
+  if (act16 && !(w8 && w8[0] == '0') && c % 8 == 0 && NT % (c / 8) == 0 &&
+      ((((uintptr_t)y) | ((uintptr_t)out)) & 15) == 0) {
+    const long npix = (long)n * hw;
+    hipLaunchKernelGGL(splat_combine_bn8_k, dim3(blocks_for(npix * (c / 8))), dim3(NT), 0, stream,
+                       (const __bf16*)y, scale, shift, att, (__bf16*)out, (uint32_t)npix, c, dhw);
+  } else if (act16)
     hipLaunchKernelGGL(splat_combine_bn_k<__bf16>, dim3(nb), dim3(NT), 0, stream, (const __bf16*)y,
                        scale, shift, att, (__bf16*)out, (uint32_t)total, dc4, dhw);
   else
