@@ -2,7 +2,7 @@
 set -o pipefail
 O=gpurun_out/r4s; mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 400 python -u -m pytest -m gpu -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "bits" tests/test_resnest_trunk_gpu.py tests/test_resnest_gpu.py tests/test_geometry_gpu.py -k "bits or c4 or resnest or split or grouped" > $O/pytest.txt 2>&1
+timeout -k 10 400 python -u -m pytest -m gpu -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "bits" tests/test_resnest_trunk_gpu.py tests/test_resnest_gpu.py tests/test_geometry_gpu.py -k "bits or c4 or resnest or split or grouped or attention" > $O/pytest.txt 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "FAIL|ERROR|passed|failed" $O/pytest.txt | tail -8
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for rep in 1 2; do for b in 0 1; do

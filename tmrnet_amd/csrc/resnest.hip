@@ -265,13 +265,15 @@ __device__ __forceinline__ float4 bnrelu4(float4 y, float4 sc, float4 sh) {
 __device__ __forceinline__ float4 ld4f(const float* p, long i4) { return reinterpret_cast<const float4*>(p)[i4]; }
 
 // gap[n][c] = mean_hw (x0[n,hw,c] + x1[n,hw,c]) with x_r recomputed from y2 (splat_gap_k's block shape)
-template <typename T>
-__global__ __launch_bounds__(NT) void splat_gap_bn_k(const T* __restrict__ y, const float* __restrict__ sc,
+// (BT threads per block: the bf16 step launches 1024 -- one block per frame and channel chunk is
+// too few blocks at 256 threads to keep enough loads in flight)
+template <typename T, int BT = NT>
+__global__ __launch_bounds__(BT) void splat_gap_bn_k(const T* __restrict__ y, const float* __restrict__ sc,
                                                      const float* __restrict__ sh, float* __restrict__ gap,
                                                      int hw, int c4, int cols, int chunks) {
-  __shared__ Red4 lds[NT];
+  __shared__ Red4 lds[BT];
   const int nn = blockIdx.x / chunks, cq = (blockIdx.x % chunks) * cols + threadIdx.x % cols;
-  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = NT / cols;
+  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = BT / cols;
   const bool live = cq < c4;
   Red4 acc[1] = {{0.0, 0.0, 0.0, 0.0}};
   if (live) {
@@ -391,14 +393,14 @@ __global__ __launch_bounds__(NT) void splat_combine_bn8_k(const __bf16* __restri
 // backward; its BatchNorm sums over the frame are att_r*S1 + dgap/hw*S2 and att_r*S3 + dgap/hw*S4,
 // so one pass over (dout, y2) serves the attention and the BatchNorm backward.
 // sums: float [4][n][2C].
-template <typename T>
-__global__ __launch_bounds__(NT) void splat_bwd_reduce_bn_k(
+template <typename T, int BT = NT>
+__global__ __launch_bounds__(BT) void splat_bwd_reduce_bn_k(
     const float* __restrict__ dout, const T* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ mean, const float* __restrict__ att,
     float* __restrict__ dzl, float* __restrict__ sums, int n, int hw, int c4, int cols, int chunks) {
-  __shared__ Red4 lds[NT];
+  __shared__ Red4 lds[BT];
   const int nn = blockIdx.x / chunks, cq = (blockIdx.x % chunks) * cols + threadIdx.x % cols;
-  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = NT / cols;
+  const int col = threadIdx.x % cols, row = threadIdx.x / cols, rows = BT / cols;
   const bool live = cq < c4;
   Red4 acc[10];
 #pragma unroll
@@ -754,7 +756,12 @@ TMR_API int tmr_splat_gap_bn(const void* y, const float* scale, const float* shi
   TMR_CHECK_ARG(c % 4 == 0 && n > 0 && hw > 0, "tmr_splat_gap_bn: bad shape n %d hw %d c %d", n, hw, c);
   int cols, chunks;
   red_shape(c / 4, cols, chunks);
-  if (act16)
+  const char* wb = getenv("TMR_SPLAT_GAP_BT");   // A/B: threads per block (256: the old shape)
+  const int bt = wb ? atoi(wb) : 1024;
+  if (act16 && bt == 1024)
+    hipLaunchKernelGGL((splat_gap_bn_k<__bf16, 1024>), dim3(n * chunks), dim3(1024), 0, stream,
+                       (const __bf16*)y, scale, shift, gap, hw, c / 4, cols, chunks);
+  else if (act16)
     hipLaunchKernelGGL(splat_gap_bn_k<__bf16>, dim3(n * chunks), dim3(NT), 0, stream,
                        (const __bf16*)y, scale, shift, gap, hw, c / 4, cols, chunks);
   else
