@@ -223,6 +223,44 @@ __global__ __launch_bounds__(NT) void avgpool2d_bwd_k(const float* __restrict__ 
   }
 }
 
+// The same with the pixel / channel indices by magic-number division (the element-group count
+// fits 32 bits, checked on the host): the generic form's three 32-bit divisions per 4 elements
+// made it instruction-bound (~2 TB/s).  Same sums in the same order.
+__global__ __launch_bounds__(NT) void avgpool2d_bwd_fd_k(const float* __restrict__ dy,
+                                                         float* __restrict__ dx, uint32_t total,
+                                                         FastDiv dc4, FastDiv dw, FastDiv dh,
+                                                         int ho, int wo, int k, int s, int p,
+                                                         int incl) {
+  const uint32_t c4 = dc4.d, w = dw.d, h = dh.d;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const uint32_t t0 = fdiv(i, dc4);
+    const int cq = (int)(i - t0 * c4);
+    const uint32_t t1 = fdiv(t0, dw);
+    const int ix = (int)(t0 - t1 * w);
+    const uint32_t nn = fdiv(t1, dh);
+    const int iy = (int)(t1 - nn * h);
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int oy0 = max(0, (iy + p - k + s) / s), oy1 = min(ho - 1, (iy + p) / s);
+    const int ox0 = max(0, (ix + p - k + s) / s), ox1 = min(wo - 1, (ix + p) / s);
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      if (iy < oy * s - p || iy > oy * s - p + k - 1) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        if (ix < ox * s - p || ix > ox * s - p + k - 1) continue;
+        int cnt = k * k;
+        if (!incl) {
+          const int y0 = max(0, oy * s - p), y1 = min((int)h, oy * s - p + k);
+          const int x0 = max(0, ox * s - p), x1 = min((int)w, ox * s - p + k);
+          cnt = (y1 - y0) * (x1 - x0);
+        }
+        const float inv = 1.0f / (float)cnt;
+        const float4 d = reinterpret_cast<const float4*>(dy)[(((long)nn * ho + oy) * wo + ox) * c4 + cq];
+        g.x += d.x * inv; g.y += d.y * inv; g.z += d.z * inv; g.w += d.w * inv;
+      }
+    }
+    reinterpret_cast<float4*>(dx)[i] = g;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Split attention with bn0 + ReLU applied on load (the whole-trunk ResNeSt node, resnest.py).
 // The grouped conv's pre-BN output y2 [n][hw][2C] (bf16 under the bf16-activation contract, else
@@ -742,8 +780,10 @@ TMR_API int tmr_avgpool2d_bwd(const float* dy, float* dx, int n, int h, int w, i
                               hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_bwd: channels %d must be a multiple of 4", c);
   if ((long)n * h * w * c / 4 < (1L << 31))
-    hipLaunchKernelGGL(avgpool2d_bwd_k<uint32_t>, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
-                     dy, dx, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
+    hipLaunchKernelGGL(avgpool2d_bwd_fd_k, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
+                       dy, dx, (uint32_t)((long)n * h * w * c / 4), make_fastdiv((uint32_t)(c / 4)),
+                       make_fastdiv((uint32_t)w), make_fastdiv((uint32_t)h), ho, wo, k, s, p,
+                       count_include_pad);
   else
     hipLaunchKernelGGL(avgpool2d_bwd_k<long>, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
                      dy, dx, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
