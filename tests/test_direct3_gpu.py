@@ -197,3 +197,90 @@ def test_direct3_stem_wgrad(dev, monkeypatch):
     torch.cuda.synchronize()
     assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
     assert rel_err(acc, 0.5 * prev.double().cpu() + ref) < 2e-6
+
+
+W56 = 8   # frames of the 56x56 cases: 448 rows over 384-512 workgroups (ranges of 1-2 rows)
+
+
+def test_direct3_w56_fwd_bnstats(dev, monkeypatch):
+    """ResNet-50 layer1's 3x3 64 -> 64 conv at 56x56 (C5, bf16): 3.5 m-tiles of 16 pixels per row
+    (the last half empty: zeros, not counted in the statistics)."""
+    g = torch.Generator().manual_seed(90)
+    x = _bf(torch.relu(torch.randn(W56, 56, 56, 64, generator=g)))
+    w = _bf(torch.randn(64, 64, 3, 3, generator=g) / np.sqrt(576))
+    wk = ops.weight_to_krsc(w.float().to(dev).contiguous(), bf16=True)
+    monkeypatch.setenv("TMR_DIRECT3", "1")
+    y, stats, nparts = ops.conv_fwd_bnstats(x.to(dev), wk, 1, 1, math="bf16", y16=True)
+    monkeypatch.setenv("TMR_DIRECT3", "0")
+    y0, _, np0 = ops.conv_fwd_bnstats(x.to(dev), wk, 1, 1, math="bf16", y16=True)
+    torch.cuda.synchronize()
+    assert nparts == min(W56 * 56, 768) and np0 != nparts
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double(), padding=1).permute(0, 2, 3, 1)
+    yf = y.double().cpu()
+    assert _ulp_bound(yf, ref) and _ulp_bound(yf, y0.double().cpu(), 2.0)
+    yd = yf.reshape(-1, 64)
+    ones, zeros = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    mean, inv, _, _ = ops.bn_finalize(stats, nparts, ones, zeros, zeros.clone(), ones.clone(), 0.1, 1e-5)
+    assert rel_err(mean, yd.mean(0)) < 1e-6
+    assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
+
+
+@pytest.mark.parametrize("g16,mask,beta", [(True, 2, 0.0), (False, 2, 0.0), (False, 1, 0.0),
+                                           (False, 0, 1.0)])
+def test_direct3_w56_dgrad_bnbwd(dev, monkeypatch, g16, mask, beta):
+    """Its dgrad with the fused BatchNorm backward of bn1; g16: the masked gradient stored bf16
+    (TMR_IO_G16, the C5 step's contract) with the partial sums of the stored values."""
+    g = torch.Generator().manual_seed(91 + mask)
+    dy = _bf(torch.randn(W56, 56, 56, 64, generator=g))
+    w = _bf(torch.randn(64, 64, 3, 3, generator=g) / np.sqrt(576))
+    y = _bf(torch.randn(W56, 56, 56, 64, generator=g))
+    z = _bf(torch.relu(torch.randn(W56, 56, 56, 64, generator=g)))
+    scale = torch.rand(64, generator=g) + 0.5
+    shift = torch.randn(64, generator=g) * 0.3
+    mean = torch.randn(64, generator=g) * 0.1
+    old = torch.randn(W56, 56, 56, 64, generator=g)
+    wt = ops.weight_to_crsk(w.float().to(dev).contiguous())
+    outs = []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("TMR_DIRECT3", direct)
+        dx, parts, nparts = ops.conv_dgrad_bnbwd(
+            dy.to(dev), wt, (56, 56), 1, 1, y.to(dev), mean.to(dev), mask,
+            z=z.to(dev) if mask == 1 else None, scale=scale.to(dev), shift=shift.to(dev),
+            out=None if g16 else old.to(dev).clone(), beta=beta, math="bf16", wt=True, g16=g16)
+        outs.append((dx, parts[:nparts].double().sum(0).cpu(), nparts))
+    torch.cuda.synchronize()
+    ref = F.conv_transpose2d(dy.permute(0, 3, 1, 2).double(), w.double(), padding=1)
+    ref = ref.permute(0, 2, 3, 1) + beta * old.double()
+    yd = y.double()
+    keep = {0: torch.ones_like(yd, dtype=torch.bool), 1: z.double() > 0,
+            2: yd * scale.double() + shift.double() > 0}[mask]
+    ref = torch.where(keep, ref, torch.zeros_like(ref))
+    (dx, ps, npd), (dx0, ps0, _) = outs
+    assert npd == min(W56 * 56, 512)
+    if g16:
+        assert dx.dtype == torch.bfloat16
+        assert _ulp_bound(dx.double().cpu(), ref) and _ulp_bound(dx.double().cpu(), dx0.double().cpu(), 2.0)
+    else:
+        assert rel_err(dx, ref) < 2e-6 and rel_err(dx0, ref) < 2e-6
+    gd = dx.double().cpu().reshape(-1, 64)
+    assert rel_err(ps[:, 0], gd.sum(0)) < 1e-5
+    assert rel_err(ps[:, 1], (gd * (yd.reshape(-1, 64) - mean.double())).sum(0)) < 1e-5
+    assert rel_err(ps, ps0) < (2e-3 if g16 else 1e-5)
+
+
+def test_direct3_w56_wgrad(dev, monkeypatch):
+    """Its weight gradient: K = 56 pixels per row padded to 64, 36 accumulator tiles per wave."""
+    g = torch.Generator().manual_seed(93)
+    x = _bf(torch.relu(torch.randn(W56, 56, 56, 64, generator=g)))
+    dy = _bf(torch.randn(W56, 56, 56, 64, generator=g))
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (64, 64, 3, 3),
+                                      dy.permute(0, 3, 1, 2).double(), padding=1)
+    monkeypatch.setenv("TMR_DIRECT3", "1")
+    dw = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16")
+    prev = torch.randn(64, 64, 3, 3, generator=g).to(dev)
+    acc = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16", out=prev.clone(), beta=0.5)
+    monkeypatch.setenv("TMR_DIRECT3", "0")
+    dw0 = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16")
+    torch.cuda.synchronize()
+    assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
+    assert rel_err(acc, 0.5 * prev.double().cpu() + ref) < 2e-6

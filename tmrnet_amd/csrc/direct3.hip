@@ -41,19 +41,19 @@ __device__ __forceinline__ unsigned short bfb(float v) {
 }
 __device__ __forceinline__ float bff(uint32_t u16) { return __uint_as_float(u16 << 16); }
 
-template <int C>
+template <int C, int W = DW>
 struct Px {
   static constexpr int PS = 2 * C + 32;       // LDS bytes per pixel row
   static constexpr int CPP = C / 8;           // 16-B chunks per pixel
-  static constexpr int PIECES = DW * CPP;     // 16-B pieces of a 112-pixel row
+  static constexpr int PIECES = W * CPP;      // 16-B pieces of a W-pixel row
   static constexpr int PPT = (PIECES + 255) / 256;
 };
 
-// One 112-pixel row of an NHWC bf16 tensor (global row index g) <-> registers <-> an LDS image of
+// One W-pixel row of an NHWC bf16 tensor (global row index g) <-> registers <-> an LDS image of
 // pixel rows (pixel p at byte (p + off) * PS).
-template <int C>
+template <int C, int W = DW>
 struct RowIO {
-  using P = Px<C>;
+  using P = Px<C, W>;
   __device__ static void fetch(const uint4* __restrict__ t, int g, bool valid, uint4 (&v)[P::PPT]) {
     int tt = threadIdx.x;
     asm volatile("" : "+v"(tt));
@@ -76,24 +76,30 @@ struct RowIO {
 };
 
 // workgroups per CU (the grid is that many per CU: persistent): three where the registers allow
-constexpr int d3_minb(int cin, int cout, int mode) { return (cin == 32 && cout == 32 && mode == 0) ? 3 : 2; }
+constexpr int d3_minb(int cin, int cout, int mode) {
+  return (mode == 0 && cin == cout) ? 3 : 2;   // the forwards 32 -> 32 and 64 -> 64
+}
 
 // MODE 0: forward, y bf16 + BatchNorm partial statistics.  MODE 1: dgrad (x = dy, w = the CRSK copy,
 // taps flipped) with the fused BatchNorm backward; out = dx fp32.
-template <int CIN, int COUT, int MODE>
+// W: row width (112, or 56 with a half-empty last m-tile).  G16 (dgrad): dx -- the masked gradient
+// -- stored bf16 and the partial sums those of the rounded values (TMR_IO_G16), no beta.
+template <int CIN, int COUT, int MODE, int W = DW, int G16 = 0>
 __global__ __launch_bounds__(256, d3_minb(CIN, COUT, MODE))
 void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __restrict__ out,
           float4* __restrict__ stats, const uint4* __restrict__ by, const uint4* __restrict__ bz,
           const float* __restrict__ bsc, const float* __restrict__ bsh,
           const float* __restrict__ bmu, int mask, float beta, float2* __restrict__ part, int h,
           int rows) {
-  using PI = Px<CIN>;
+  using PI = Px<CIN, W>;
   constexpr int KPT = CIN / 32, KS = 9 * KPT;
   constexpr int NT = COUT / 16, NPW = 18 / KS, WN = NT / NPW, WM = 4 / WN;
-  constexpr int MPW = (7 + WM - 1) / WM;
+  constexpr int MT = (W + 15) / 16;   // m-tiles of 16 pixels
+  constexpr int MPW = (MT + WM - 1) / WM;
   static_assert(NPW * KS == 18 && NT % NPW == 0 && WN * WM == 4, "wave split");
-  constexpr int SLOT = 114 * PI::PS;   // pixel columns x = -1 .. 112
-  constexpr int OST = MODE == 0 ? DW * COUT * 2 : DW * (COUT + 4) * 4;
+  static_assert(!G16 || MODE == 1, "G16: dgrad only");
+  constexpr int SLOT = (16 * MT + 2) * PI::PS;   // pixel columns x = -1 .. 16 MT (zeros past W)
+  constexpr int OST = MODE == 0 ? W * COUT * 2 : W * (COUT + 4) * 4;
   __shared__ __attribute__((aligned(16))) unsigned char ring[3 * SLOT];
   __shared__ __attribute__((aligned(16))) unsigned char ost[OST];
 
@@ -118,14 +124,16 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
 
   const int r0 = (int)((long)blockIdx.x * rows / gridDim.x);
   const int r1 = (int)((long)(blockIdx.x + 1) * rows / gridDim.x);
-  const int nvalid = min(MPW, 7 - wm * MPW);   // this wave's m-tiles (uniform)
+  const int nvalid = min(MPW, MT - wm * MPW);   // this wave's m-tiles (uniform)
+  // this wave's output pixels (the last m-tile of a 56-pixel row holds 8)
+  const int npx = min(16 * (wm * MPW + nvalid), W) - 16 * wm * MPW;
 
   // forward statistics: running (n, mean, M2) of this wave's pixels per channel (lanes kg share)
   double rn = 0.0, rm[NPW], rq[NPW];
 #pragma unroll
   for (int j = 0; j < NPW; ++j) { rm[j] = 0.0; rq[j] = 0.0; }
   // dgrad: the thread's 8 channels (fixed: 256 is a multiple of COUT / 8) and its partial sums
-  constexpr int CG = COUT / 8, ITEMS = DW * CG, IPT = (ITEMS + 255) / 256;
+  constexpr int CG = COUT / 8, ITEMS = W * CG, IPT = (ITEMS + 255) / 256;
   const int cg = tid % CG;
   float esc[8], esh[8], emu[8];
   double ds[8], dq[8];
@@ -148,15 +156,15 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
     if (first(row)) {
 #pragma unroll 1
       for (int d = -1; d <= 1; ++d) {
-        RowIO<CIN>::fetch(x, row + d, oh + d >= 0 && oh + d < h, cur);
-        RowIO<CIN>::put(slot(row + d), 1, cur);
+        RowIO<CIN, W>::fetch(x, row + d, oh + d >= 0 && oh + d < h, cur);
+        RowIO<CIN, W>::put(slot(row + d), 1, cur);
       }
     } else {
-      RowIO<CIN>::put(slot(row + 1), 1, cur);   // (zeros past the frame's last row)
+      RowIO<CIN, W>::put(slot(row + 1), 1, cur);   // (zeros past the frame's last row)
     }
     __syncthreads();
     // the next row's new input row lands under this row's MFMAs
-    if (row + 1 < r1 && !first(row + 1)) RowIO<CIN>::fetch(x, row + 2, oh + 2 < h, nxt);
+    if (row + 1 < r1 && !first(row + 1)) RowIO<CIN, W>::fetch(x, row + 2, oh + 2 < h, nxt);
     // dgrad epilogue operands of this row (y, z, old dx), issued before the MFMAs
     uint4 yv[IPT], zv[IPT];
     float4 ov[IPT][2];
@@ -168,7 +176,7 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
         const long e8 = (long)row * ITEMS + (ok ? it : 0);
         yv[q] = ok ? by[e8] : make_uint4(0u, 0u, 0u, 0u);
         zv[q] = (ok && mask == 1) ? bz[e8] : make_uint4(0u, 0u, 0u, 0u);
-        if (beta != 0.f && ok) {
+        if (!G16 && beta != 0.f && ok) {
           ov[q][0] = reinterpret_cast<const float4*>(out)[2 * e8];
           ov[q][1] = reinterpret_cast<const float4*>(out)[2 * e8 + 1];
         } else {
@@ -213,13 +221,15 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
             for (int r = 0; r < 4; ++r) {
               const int px = 16 * (wm * MPW + i) + 4 * kg + r, co = 16 * (wn * NPW + j) + c16;
               const unsigned short u = bfb(acc[i][j][r]);
-              acc[i][j][r] = bff(u);
-              ys[px * COUT + co] = u;
-              sm[j] += acc[i][j][r];
+              acc[i][j][r] = bff(u);   // (pixels past W: exactly 0, not counted)
+              if (W % 16 == 0 || px < W) {
+                ys[px * COUT + co] = u;
+                sm[j] += acc[i][j][r];
+              }
             }
         }
       }
-      const float cnt = 16.f * nvalid;
+      const float cnt = (float)npx;
       float mj[NPW], qj[NPW];
 #pragma unroll
       for (int j = 0; j < NPW; ++j) {
@@ -236,7 +246,7 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float d = acc[i][j][r] - mj[j];
-              qj[j] = fmaf(d, d, qj[j]);
+              if (W % 16 == 0 || 16 * (wm * MPW + i) + 4 * kg + r < W) qj[j] = fmaf(d, d, qj[j]);
             }
         }
       }
@@ -251,7 +261,7 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
       }
       rn = nt;
       __syncthreads();   // the tile staged
-      constexpr int YP = DW * COUT * 2 / 16;
+      constexpr int YP = W * COUT * 2 / 16;
       uint4* yr = reinterpret_cast<uint4*>(out) + (long)row * YP;
       for (int i = tid; i < YP; i += 256) yr[i] = reinterpret_cast<const uint4*>(ost)[i];
     } else {
@@ -265,7 +275,7 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int px = 16 * (wm * MPW + i) + 4 * kg + r, co = 16 * (wn * NPW + j) + c16;
-              gs[px * (COUT + 4) + co] = acc[i][j][r];
+              if (W % 16 == 0 || px < W) gs[px * (COUT + 4) + co] = acc[i][j][r];
             }
         }
       }
@@ -293,13 +303,22 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
             float t = fmaf(beta, ol[e], av[e]);
             const bool keep = zz + fmaf(yy, esc[e], esh[e]) > 0.f;   // the engine's mask test
             t = keep ? t : 0.f;
+            if (G16) t = bff(bfb(t));   // the stored value, which the partial sums describe
             g[e] = t;
             rs[e] += t;
             rqq[e] = fmaf(t, yy - emu[e], rqq[e]);
           }
-          float4* o = reinterpret_cast<float4*>(out) + 2 * ((long)row * ITEMS + it);
-          o[0] = make_float4(g[0], g[1], g[2], g[3]);
-          o[1] = make_float4(g[4], g[5], g[6], g[7]);
+          if constexpr (G16) {
+            uint32_t pk[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2)
+              pk[e2] = (uint32_t)bfb(g[2 * e2]) | ((uint32_t)bfb(g[2 * e2 + 1]) << 16);
+            reinterpret_cast<uint4*>(out)[(long)row * ITEMS + it] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          } else {
+            float4* o = reinterpret_cast<float4*>(out) + 2 * ((long)row * ITEMS + it);
+            o[0] = make_float4(g[0], g[1], g[2], g[3]);
+            o[1] = make_float4(g[4], g[5], g[6], g[7]);
+          }
         }
       }
 #pragma unroll
@@ -357,19 +376,22 @@ void d3_k(const uint4* __restrict__ x, const __bf16* __restrict__ wk, void* __re
 // tap's kernel row shifted by its column offset (128 pixels x ci), both [pixel][channel] images read
 // by ds_read_b64_tr_b16.  Wave split: COUT 64 -> wave w owns co tile w (both ci tiles, 9 taps);
 // COUT 32 -> (co tile w & 1, ci tile w >> 1).
-template <int CIN, int COUT>
+template <int CIN, int COUT, int W = DW>
 __global__ __launch_bounds__(256, 2)
 void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __restrict__ slabs,
            int h, int rows) {
-  using PI = Px<CIN>;
-  using PO = Px<COUT>;
-  constexpr int XR = 130;   // ring slot rows: pixel columns x = -1 .. 128
+  using PI = Px<CIN, W>;
+  using PO = Px<COUT, W>;
+  constexpr int KP = 32 * ((W + 31) / 32);   // reduction pixels per row, zero-padded
+  constexpr int XR = KP + 2;                 // ring slot rows: pixel columns x = -1 .. KP
   constexpr int XSLOT = XR * PI::PS;
-  constexpr int MTW = COUT == 64 ? 1 : 1, NTW = COUT == 64 ? 2 : 1;   // tiles per wave
-  static_assert(COUT == 64 || COUT == 32, "d3w_k: 32 or 64 output channels");
-  static_assert(CIN == 32, "d3w_k: 32 input channels");
+  // tiles per wave: COUT 64 -> co tile w, all CIN / 16 ci tiles; COUT 32 (CIN 32) -> co tile w & 1,
+  // ci tile w >> 1
+  constexpr int NTW = COUT == 64 ? CIN / 16 : 1;
+  static_assert((COUT == 64 && (CIN == 32 || CIN == 64)) || (COUT == 32 && CIN == 32),
+                "d3w_k: (32 | 64) -> 64 or 32 -> 32 channels");
   __shared__ __attribute__((aligned(16))) unsigned char ring[3 * XSLOT];
-  __shared__ __attribute__((aligned(16))) unsigned char dimg[128 * PO::PS];
+  __shared__ __attribute__((aligned(16))) unsigned char dimg[KP * PO::PS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
@@ -378,7 +400,7 @@ void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __r
   const int nt0 = COUT == 64 ? 0 : (wave >> 1);
   for (int i = tid; i < 3 * XSLOT / 16; i += 256)
     reinterpret_cast<uint4*>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (int i = tid; i < 128 * PO::PS / 16; i += 256)
+  for (int i = tid; i < KP * PO::PS / 16; i += 256)
     reinterpret_cast<uint4*>(dimg)[i] = make_uint4(0u, 0u, 0u, 0u);
 
   f32x4_t acc[9][NTW];
@@ -386,7 +408,6 @@ void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __r
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[t][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  (void)MTW;
 
   const int r0 = (int)((long)blockIdx.x * rows / gridDim.x);
   const int r1 = (int)((long)(blockIdx.x + 1) * rows / gridDim.x);
@@ -409,7 +430,7 @@ void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __r
   };
 
   uint4 xA[PI::PPT], xB[PI::PPT], dA[PO::PPT], dB[PO::PPT];
-  if (r0 < r1) RowIO<COUT>::fetch(dy, r0, true, dA);
+  if (r0 < r1) RowIO<COUT, W>::fetch(dy, r0, true, dA);
   auto step = [&](int row, uint4 (&xc)[PI::PPT], uint4 (&xn)[PI::PPT], uint4 (&dc)[PO::PPT],
                   uint4 (&dn)[PO::PPT]) {
     const int oh = row % h;
@@ -417,21 +438,21 @@ void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __r
     if (first(row)) {
 #pragma unroll 1
       for (int d = -1; d <= 1; ++d) {
-        RowIO<CIN>::fetch(x, row + d, oh + d >= 0 && oh + d < h, xc);
-        RowIO<CIN>::put(slot(row + d), 1, xc);
+        RowIO<CIN, W>::fetch(x, row + d, oh + d >= 0 && oh + d < h, xc);
+        RowIO<CIN, W>::put(slot(row + d), 1, xc);
       }
     } else {
-      RowIO<CIN>::put(slot(row + 1), 1, xc);
+      RowIO<CIN, W>::put(slot(row + 1), 1, xc);
     }
-    RowIO<COUT>::put(dimg, 0, dc);
+    RowIO<COUT, W>::put(dimg, 0, dc);
     __syncthreads();
     if (row + 1 < r1) {
-      if (!first(row + 1)) RowIO<CIN>::fetch(x, row + 2, oh + 2 < h, xn);
-      RowIO<COUT>::fetch(dy, row + 1, true, dn);
+      if (!first(row + 1)) RowIO<CIN, W>::fetch(x, row + 2, oh + 2 < h, xn);
+      RowIO<COUT, W>::fetch(dy, row + 1, true, dn);
     }
     const unsigned char* rb[3] = {slot(row - 1), slot(row), slot(row + 1)};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {   // pixels 32 s .. 32 s + 31
+    for (int s = 0; s < KP / 32; ++s) {   // pixels 32 s .. 32 s + 31
       const int pr = 32 * s + 8 * g;
       const bf16x8_t a = frag(dimg, PO::PS, pr, 16 * mt);
 #pragma unroll
@@ -751,75 +772,90 @@ int grid_of(int rows, int cin, int cout, int mode) {
 
 // ---- host entries (gemm_conv.hip routes the deep stem's geometry here) ----
 
-int tmr_d3_stats_parts(int n, int h, int cin, int cout) {
-  const int wm = cout == 64 ? 2 : 4;   // d3_k<32, COUT, 0>: WM
+// supported (width, input, output channels) of the forward / wgrad; the dgrad takes the same convs
+static bool d3_ok(int w, int cin, int cout) {
+  return (w == 112 && cin == 32 && (cout == 32 || cout == 64)) ||
+         (w == 56 && cin == 64 && cout == 64);
+}
+
+int tmr_d3_stats_parts(int n, int h, int w, int cin, int cout) {
+  const int ks = 9 * cin / 32, npw = 18 / ks, wn = (cout / 16) / npw, wm = 4 / wn;   // d3_k's WM
   return grid_of(n * h, cin, cout, 0) * wm;
 }
 
-int tmr_d3_dgrad_parts(int n, int h, int cin_conv, int cout_conv) {
+int tmr_d3_dgrad_parts(int n, int h, int w, int cin_conv, int cout_conv) {
+  (void)w;
   return grid_of(n * h, cout_conv, cin_conv, 1);   // the dgrad kernel runs over dy
 }
 
-size_t tmr_d3_wgrad_ws_bytes(int n, int h, int cin, int cout) {
+size_t tmr_d3_wgrad_ws_bytes(int n, int h, int w, int cin, int cout) {
+  (void)w;
   const int rows = n * h;
   return (size_t)(rows < kGridW ? rows : kGridW) * cout * 9 * cin * sizeof(float);
 }
 
-int tmr_d3_fwd_bnstats(int n, int h, int cin, int cout, const void* x, const void* w_krsc, void* y,
-                       void* stats, hipStream_t stream) {
-  TMR_CHECK_ARG(n > 0 && h > 0 && cin == 32 && (cout == 32 || cout == 64),
-                "tmr_d3_fwd: unsupported shape (%d -> %d)", cin, cout);
+int tmr_d3_fwd_bnstats(int n, int h, int w, int cin, int cout, const void* x, const void* w_krsc,
+                       void* y, void* stats, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && d3_ok(w, cin, cout), "tmr_d3_fwd: unsupported shape (w %d, %d -> %d)",
+                w, cin, cout);
   TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)y | (uintptr_t)w_krsc) & 15) == 0,
                 "tmr_d3_fwd: x / y / w must be 16-B aligned");
   const int rows = n * h, grid = grid_of(rows, cin, cout, 0);
-  if (cout == 64)
-    hipLaunchKernelGGL((d3_k<32, 64, 0>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
-                       (const __bf16*)w_krsc, y, (float4*)stats, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, 0, 0.f, nullptr, h, rows);
-  else
-    hipLaunchKernelGGL((d3_k<32, 32, 0>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
-                       (const __bf16*)w_krsc, y, (float4*)stats, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, 0, 0.f, nullptr, h, rows);
+#define D3F(CI, CO, W)                                                                            \
+  hipLaunchKernelGGL((d3_k<CI, CO, 0, W>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,     \
+                     (const __bf16*)w_krsc, y, (float4*)stats, nullptr, nullptr, nullptr, nullptr, \
+                     nullptr, 0, 0.f, nullptr, h, rows)
+  if (w == 56) D3F(64, 64, 56);
+  else if (cout == 64) D3F(32, 64, 112);
+  else D3F(32, 32, 112);
+#undef D3F
   TMR_CHECK_LAUNCH("d3_fwd");
   return 0;
 }
 
-// dgrad of the conv cin_conv -> cout_conv: dy (rows, 112, cout_conv) bf16, w_crsk (cin_conv, 3, 3,
-// cout_conv) bf16, dx (rows, 112, cin_conv) fp32 (read when beta != 0); the BatchNorm backward of
-// the unit that produced the conv input: y / z bf16 like dx, mask 0 / 1 / 2
-int tmr_d3_dgrad_bnbwd(int n, int h, int cin_conv, int cout_conv, const void* dy,
-                       const void* w_crsk, float* dx, float beta, const void* y, const void* z,
-                       const float* scale, const float* shift, const float* mean, int mask,
-                       void* parts, hipStream_t stream) {
-  TMR_CHECK_ARG(n > 0 && h > 0 && cin_conv == 32 && (cout_conv == 32 || cout_conv == 64),
-                "tmr_d3_dgrad: unsupported shape (%d -> %d)", cin_conv, cout_conv);
+// dgrad of the conv cin_conv -> cout_conv: dy (rows, w, cout_conv) bf16, w_crsk (cin_conv, 3, 3,
+// cout_conv) bf16, dx (rows, w, cin_conv) fp32 (read when beta != 0), or bf16 when g16 (the masked
+// gradient rounded, no beta); the BatchNorm backward of the unit that produced the conv input:
+// y / z bf16 like dx, mask 0 / 1 / 2
+int tmr_d3_dgrad_bnbwd(int n, int h, int w, int cin_conv, int cout_conv, const void* dy,
+                       const void* w_crsk, void* dx, int g16, float beta, const void* y,
+                       const void* z, const float* scale, const float* shift, const float* mean,
+                       int mask, void* parts, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && d3_ok(w, cin_conv, cout_conv) && (!g16 || w == 56) &&
+                    !(g16 && beta != 0.f),
+                "tmr_d3_dgrad: unsupported shape (w %d, %d -> %d, g16 %d, beta %g)", w, cin_conv,
+                cout_conv, g16, beta);
   TMR_CHECK_ARG((((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)w_crsk | (uintptr_t)y |
                   (uintptr_t)z) & 15) == 0,
                 "tmr_d3_dgrad: operands must be 16-B aligned");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift),
                 "tmr_d3_dgrad: mask %d operands", mask);
   const int rows = n * h, grid = grid_of(rows, cout_conv, cin_conv, 1);
-  if (cout_conv == 64)
-    hipLaunchKernelGGL((d3_k<64, 32, 1>), dim3(grid), dim3(256), 0, stream, (const uint4*)dy,
-                       (const __bf16*)w_crsk, (void*)dx, nullptr, (const uint4*)y,
-                       (const uint4*)z, scale, shift, mean, mask, beta, (float2*)parts, h, rows);
-  else
-    hipLaunchKernelGGL((d3_k<32, 32, 1>), dim3(grid), dim3(256), 0, stream, (const uint4*)dy,
-                       (const __bf16*)w_crsk, (void*)dx, nullptr, (const uint4*)y,
-                       (const uint4*)z, scale, shift, mean, mask, beta, (float2*)parts, h, rows);
+#define D3D(CI, CO, W, G)                                                                         \
+  hipLaunchKernelGGL((d3_k<CI, CO, 1, W, G>), dim3(grid), dim3(256), 0, stream, (const uint4*)dy, \
+                     (const __bf16*)w_crsk, dx, nullptr, (const uint4*)y, (const uint4*)z, scale,  \
+                     shift, mean, mask, beta, (float2*)parts, h, rows)
+  if (w == 56 && g16) D3D(64, 64, 56, 1);
+  else if (w == 56) D3D(64, 64, 56, 0);
+  else if (cout_conv == 64) D3D(64, 32, 112, 0);
+  else D3D(32, 32, 112, 0);
+#undef D3D
   TMR_CHECK_LAUNCH("d3_dgrad");
   return 0;
 }
 
-int tmr_d3_wgrad_slabs(int n, int h, int cin, int cout, const void* x, const void* dy, float* ws,
-                       size_t ws_bytes, int* nslabs, hipStream_t stream) {
-  TMR_CHECK_ARG(n > 0 && h > 0 && cin == 32 && (cout == 32 || cout == 64),
-                "tmr_d3_wgrad: unsupported shape (%d -> %d)", cin, cout);
+int tmr_d3_wgrad_slabs(int n, int h, int w, int cin, int cout, const void* x, const void* dy,
+                       float* ws, size_t ws_bytes, int* nslabs, hipStream_t stream) {
+  TMR_CHECK_ARG(n > 0 && h > 0 && d3_ok(w, cin, cout), "tmr_d3_wgrad: unsupported shape (w %d, %d -> %d)",
+                w, cin, cout);
   TMR_CHECK_ARG((((uintptr_t)x | (uintptr_t)dy) & 15) == 0, "tmr_d3_wgrad: x / dy must be 16-B aligned");
   const int rows = n * h, grid = rows < kGridW ? rows : kGridW;
-  TMR_CHECK_ARG(ws && ws_bytes >= tmr_d3_wgrad_ws_bytes(n, h, cin, cout),
+  TMR_CHECK_ARG(ws && ws_bytes >= tmr_d3_wgrad_ws_bytes(n, h, w, cin, cout),
                 "tmr_d3_wgrad: workspace too small (%zu)", ws_bytes);
-  if (cout == 64)
+  if (w == 56)
+    hipLaunchKernelGGL((d3w_k<64, 64, 56>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
+                       (const uint4*)dy, ws, h, rows);
+  else if (cout == 64)
     hipLaunchKernelGGL((d3w_k<32, 64>), dim3(grid), dim3(256), 0, stream, (const uint4*)x,
                        (const uint4*)dy, ws, h, rows);
   else

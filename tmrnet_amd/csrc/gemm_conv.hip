@@ -367,22 +367,25 @@ static bool stem16_wgrad_geometry(const tmr_conv_desc* d) {
 // the narrow stride-1 3x3 convs of the bf16-activation step (ResNeSt-50's deep stem: 32 -> 32,
 // 32 -> 64 at 112x112) as direct convolutions over an LDS ring of input rows (direct3.hip); every
 // operand bf16 in HBM, dense NHWC.  TMR_DIRECT3=0: the implicit-GEMM engine (A/B, tests).
-int tmr_d3_stats_parts(int n, int h, int cin, int cout);
-int tmr_d3_dgrad_parts(int n, int h, int cin_conv, int cout_conv);
-size_t tmr_d3_wgrad_ws_bytes(int n, int h, int cin, int cout);
-int tmr_d3_fwd_bnstats(int n, int h, int cin, int cout, const void* x, const void* w_krsc, void* y,
-                       void* stats, hipStream_t stream);
-int tmr_d3_dgrad_bnbwd(int n, int h, int cin_conv, int cout_conv, const void* dy,
-                       const void* w_crsk, float* dx, float beta, const void* y, const void* z,
-                       const float* scale, const float* shift, const float* mean, int mask,
-                       void* parts, hipStream_t stream);
-int tmr_d3_wgrad_slabs(int n, int h, int cin, int cout, const void* x, const void* dy, float* ws,
-                       size_t ws_bytes, int* nslabs, hipStream_t stream);
+int tmr_d3_stats_parts(int n, int h, int w, int cin, int cout);
+int tmr_d3_dgrad_parts(int n, int h, int w, int cin_conv, int cout_conv);
+size_t tmr_d3_wgrad_ws_bytes(int n, int h, int w, int cin, int cout);
+int tmr_d3_fwd_bnstats(int n, int h, int w, int cin, int cout, const void* x, const void* w_krsc,
+                       void* y, void* stats, hipStream_t stream);
+int tmr_d3_dgrad_bnbwd(int n, int h, int w, int cin_conv, int cout_conv, const void* dy,
+                       const void* w_crsk, void* dx, int g16, float beta, const void* y,
+                       const void* z, const float* scale, const float* shift, const float* mean,
+                       int mask, void* parts, hipStream_t stream);
+int tmr_d3_wgrad_slabs(int n, int h, int w, int cin, int cout, const void* x, const void* dy,
+                       float* ws, size_t ws_bytes, int* nslabs, hipStream_t stream);
+// (round 4, C5: ResNet-50 layer1's 64 -> 64 3x3 convs at 56x56 too)
 static bool d3_shape(const tmr_conv_desc* d) {
+  const bool wc = (d->w == 112 && d->c == 32 && (d->k == 32 || d->k == 64)) ||
+                  (d->w == 56 && d->c == 64 && d->k == 64);
   return env_int("TMR_DIRECT3", 1) != 0 && d->math == TMR_MATH_BF16 && ngroups(d) == 1 &&
-         d->r == 3 && d->s == 3 && d->stride == 1 && d->pad == 1 && d->pad_w == 1 && d->w == 112 &&
-         d->wo == 112 && d->ho == d->h && d->c == 32 && (d->k == 32 || d->k == 64) &&
-         xld_of(d) == d->c && yld_of(d) == d->k && d->max_frames == 0;
+         d->r == 3 && d->s == 3 && d->stride == 1 && d->pad == 1 && d->pad_w == 1 && wc &&
+         d->wo == d->w && d->ho == d->h && xld_of(d) == d->c && yld_of(d) == d->k &&
+         d->max_frames == 0;
 }
 // ... and the deep stem's first conv, 3x3/2 3 -> 32, on the NHWC4 fp32 input (bf16 math)
 int tmr_d3s_stats_parts(int n, int ho);
@@ -405,7 +408,9 @@ static bool d3_fwd(const tmr_conv_desc* d) {
   return d3_shape(d) && d->io == (TMR_IO_X_BF16 | TMR_IO_W_BF16 | TMR_IO_Y_BF16);
 }
 static bool d3_dgrad(const tmr_conv_desc* d) {
-  return d3_shape(d) && d->io == (TMR_IO_DY_BF16 | TMR_IO_WT_BF16 | TMR_IO_BN_BF16);
+  const int io = d->io & ~TMR_IO_G16;   // (a bf16 masked gradient: the 56-wide convs)
+  return d3_shape(d) && io == (TMR_IO_DY_BF16 | TMR_IO_WT_BF16 | TMR_IO_BN_BF16) &&
+         (!(d->io & TMR_IO_G16) || d->w == 56);
 }
 static bool d3_wgrad(const tmr_conv_desc* d) {
   return d3_shape(d) && d->io == (TMR_IO_X_BF16 | TMR_IO_DY_BF16);
@@ -418,7 +423,7 @@ TMR_API int tmr_conv2d_fwd_stats_parts(const tmr_conv_desc* d) {
   }
   if (stem_direct(d)) return tmr_stem_stats_parts(d->n, d->ho);
   if (stem16_direct(d)) return tmr_stem16_stats_parts(d->n, d->ho);
-  if (d3_fwd(d)) return tmr_d3_stats_parts(d->n, d->h, d->c, d->k);
+  if (d3_fwd(d)) return tmr_d3_stats_parts(d->n, d->h, d->w, d->c, d->k);
   if (d3s_fwd(d)) return tmr_d3s_stats_parts(d->n, d->ho);
   tmr_conv_desc g = *d;
   if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
@@ -476,7 +481,8 @@ static int conv_fwd_bnstats_pro(const tmr_conv_desc* d, const float* x,
     return tmr_stem_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, y, stats, stream);
   if (stem16_direct(d))
     return tmr_stem16_fwd_bnstats(d->n, d->h, d->w, d->ho, x, w_krsc, 4, y, stats, stream);
-  if (!pro && d3_fwd(d)) return tmr_d3_fwd_bnstats(d->n, d->h, d->c, d->k, x, w_krsc, y, stats, stream);
+  if (!pro && d3_fwd(d))
+    return tmr_d3_fwd_bnstats(d->n, d->h, d->w, d->c, d->k, x, w_krsc, y, stats, stream);
   if (!pro && d3s_fwd(d)) return tmr_d3s_fwd_bnstats(d->n, d->h, x, w_krsc, y, stats, stream);
   if (ngroups(d) == 1) return fwd_bnstats_impl(d, x, w_krsc, y, (float4*)stats, d->k, pro, stream);
   TMR_CHECK_ARG(!pro, "tmr_conv2d_fwd_bnstats: operand prologues take no groups");
@@ -622,7 +628,7 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d) {
     tmr_set_error("tmr_conv2d_dgrad_bnbwd_parts: null or empty descriptor");
     return -1;
   }
-  if (d3_dgrad(d)) return tmr_d3_dgrad_parts(d->n, d->h, d->c, d->k);
+  if (d3_dgrad(d)) return tmr_d3_dgrad_parts(d->n, d->h, d->w, d->c, d->k);
   tmr_conv_desc g = *d;
   if (ngroups(d) > 1 && group_split(d, g)) return -1;   // every group has the same row tiling
   BnBwdFuse fz{};
@@ -697,10 +703,13 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
   const int np = tmr_conv2d_dgrad_bnbwd_parts(d);
   TMR_CHECK_ARG(np >= 0 && parts_bytes >= (size_t)np * d->c * sizeof(float2),
                 "tmr_conv2d_dgrad_bnbwd: parts buffer too small");
-  if (d3_dgrad(d)) {
-    TMR_CHECK_ARG(!pro && !dx_old, "tmr_conv2d_dgrad_bnbwd: the direct 3x3 dgrad takes no prologue / old dx");
-    return tmr_d3_dgrad_bnbwd(d->n, d->h, d->c, d->k, dy, w_krsc, dx, beta, y, z, scale, shift,
-                              mean, mask, parts, stream);
+  if (d3_dgrad(d)) {   // (the parts query above counted the direct kernel's rows)
+    TMR_CHECK_ARG(!pro && !dx_old && !((d->io & TMR_IO_G16) && beta != 0.f),
+                  "tmr_conv2d_dgrad_bnbwd: the direct 3x3 dgrad takes no prologue / old dx / "
+                  "accumulating bf16 gradient");
+    return tmr_d3_dgrad_bnbwd(d->n, d->h, d->w, d->c, d->k, dy, w_krsc, dx,
+                              (d->io & TMR_IO_G16) ? 1 : 0, beta, y, z, scale, shift, mean, mask,
+                              parts, stream);
   }
   if (ngroups(d) > 1) {
     tmr_conv_desc g;
@@ -816,8 +825,8 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
     bytes = (size_t)kStemSlabs * kStemSlab * sizeof(float);
   if (stem16_wgrad_geometry(d) && bytes < (size_t)kStem16Slabs * kStemSlab * sizeof(float))
     bytes = (size_t)kStem16Slabs * kStemSlab * sizeof(float);
-  if (d3_wgrad(d) && bytes < tmr_d3_wgrad_ws_bytes(d->n, d->h, d->c, d->k))
-    bytes = tmr_d3_wgrad_ws_bytes(d->n, d->h, d->c, d->k);
+  if (d3_wgrad(d) && bytes < tmr_d3_wgrad_ws_bytes(d->n, d->h, d->w, d->c, d->k))
+    bytes = tmr_d3_wgrad_ws_bytes(d->n, d->h, d->w, d->c, d->k);
   if (d3s_wgrad(d) && bytes < tmr_d3s_wgrad_ws_bytes(d->n, d->ho))
     bytes = tmr_d3s_wgrad_ws_bytes(d->n, d->ho);
   return bytes;
@@ -895,7 +904,7 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   }
   if (!pro && d3_wgrad(d)) {
     int ns = 0;
-    const int rc = tmr_d3_wgrad_slabs(d->n, d->h, d->c, d->k, x, dy, ws, ws_bytes, &ns, stream);
+    const int rc = tmr_d3_wgrad_slabs(d->n, d->h, d->w, d->c, d->k, x, dy, ws, ws_bytes, &ns, stream);
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3(d->k, cdiv(c_real, 64)), dim3(256), 0, stream,
                        ws, ns, (long)d->k * 9 * d->c, dw_oihw, 9, d->c, c_real, beta);
