@@ -173,12 +173,15 @@ def test_conv_bf16_all_resnet50_shapes(dev):
 
 
 @pytest.mark.parametrize("backbone,time_conv", [("resnet50", False)])
-def test_bf16_storage_bit_identical(dev, backbone, time_conv):
+def test_bf16_storage_bit_identical(dev, monkeypatch, backbone, time_conv):
     """bf16 storage of the conv-operand-only tensors (KRSC weights, non-residual BN+ReLU outputs,
     BatchNorm-backward outputs; tmr_conv_desc.io) against fp32 storage of the same bf16-math
     step: the convs round those operands to bf16 (RNE) either way, so the logits, every
-    gradient and the running statistics are bit-identical."""
+    gradient and the running statistics are bit-identical.  On the implicit-GEMM engine: the
+    direct 3x3 kernels (direct3.hip) take only all-bf16 operands, a different summation order
+    (tested against float64 and the engine in tests/test_direct3_gpu.py), so TMR_DIRECT3=0 here."""
     from tmrnet_amd import trunk
+    monkeypatch.setenv("TMR_DIRECT3", "0")
     B, T, L = 2, 5, 7
     frames, off, lt, labels = _inputs(B, T, L, seed=51)
     res = {}
