@@ -372,11 +372,13 @@ def load_traffic(model, precision, seq, lfb):
         d = json.load(f)
     fams = d.get("families", {})
     # the conv family: gemm_kernel / tmrg::gemm_kernel (register-staged), tmrg::gemm16_kernel
-    # (LDS-DMA engine), the direct fp32 stem (stem_fwd_k / stem_wgrad_k, round 3) and the split-K
-    # weight-gradient reductions
+    # (LDS-DMA engine), the direct stems (stem_fwd_k / stem_wgrad_k, round 3; stem16_*, round 4),
+    # the direct 3x3 kernels (d3_k, d3w_k, d3s_k, d3sw_k, round 4) and the split-K weight-gradient
+    # reductions
     conv = [k for k in fams
             if any(t in k for t in ("gemm_kernel", "gemm16_kernel", "wgrad_reduce", "stem_fwd_k",
-                                    "stem_wgrad_k"))]
+                                    "stem_wgrad_k", "stem16_fwd_k", "stem16_wgrad_k", "d3_k",
+                                    "d3w_k", "d3s_k", "d3sw_k"))]
     if not conv:
         return None
     if d.get("build_sha") != lib_sha():

@@ -451,18 +451,25 @@ void d3w_k(const uint4* __restrict__ x, const uint4* __restrict__ dy, float* __r
       RowIO<COUT, W>::fetch(dy, row + 1, true, dn);
     }
     const unsigned char* rb[3] = {slot(row - 1), slot(row), slot(row + 1)};
+    // B fragments read three (tap, ci tile) pairs ahead of their MFMA (7% on the 112-wide
+    // 32 -> 64 wgrad; the same LDS reads, fewer exposed latencies)
+    constexpr int Q = 9 * NTW, LA = 3;
+    auto ldB = [&](int pr, int q) -> bf16x8_t {
+      const int t = q / NTW, j = q % NTW, ky = t / 3, kx = t % 3;   // x pixel p + kx - 1 = row p + kx
+      return frag(rb[ky], PI::PS, pr + kx, 16 * (nt0 + j));
+    };
 #pragma unroll
     for (int s = 0; s < KP / 32; ++s) {   // pixels 32 s .. 32 s + 31
       const int pr = 32 * s + 8 * g;
       const bf16x8_t a = frag(dimg, PO::PS, pr, 16 * mt);
+      bf16x8_t bq[Q];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int ky = t / 3, kx = t % 3;   // x pixel p + kx - 1 = image row p + kx
+      for (int q = 0; q < LA; ++q) bq[q] = ldB(pr, q);
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const bf16x8_t b = frag(rb[ky], PI::PS, pr + kx, 16 * (nt0 + j));
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t][j], 0, 0, 0);
-        }
+      for (int q = 0; q < Q; ++q) {
+        if (q + LA < Q) bq[q + LA] = ldB(pr, q + LA);
+        acc[q / NTW][q % NTW] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[q], acc[q / NTW][q % NTW], 0, 0, 0);
       }
     }
   };
