@@ -1,11 +1,14 @@
 # one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
-# final-build PMC passes: C2 fp32, C4 bf16 (ResNeSt), C5 bf16 -> gpurun_out/r4f_pmc_*/pmc_traffic_*.json
+# final build: rocprofv3 kernel stats (C2, C4, C5) and the bench lines (traffic from profiles/r4/)
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-PROF_NAME=r4f_pmc_c2 MODEL=resnet50 PRECISION=fp32 SEQ=10 LFB=40 timeout -k 10 900 bash scripts/pmc.sh > gpurun_out/r4f_pmc_c2.log 2>&1 || { tail -5 gpurun_out/r4f_pmc_c2.log; exit 2; }
-echo c2 done
-PROF_NAME=r4f_pmc_c4 MODEL=resnest50 PRECISION=bf16 SEQ=10 LFB=40 timeout -k 10 900 bash scripts/pmc.sh > gpurun_out/r4f_pmc_c4.log 2>&1 || { tail -5 gpurun_out/r4f_pmc_c4.log; exit 3; }
-echo c4 done
-PROF_NAME=r4f_pmc_c5 MODEL=resnet50 PRECISION=bf16 SEQ=30 LFB=300 timeout -k 10 900 bash scripts/pmc.sh > gpurun_out/r4f_pmc_c5.log 2>&1 || { tail -5 gpurun_out/r4f_pmc_c5.log; exit 4; }
-echo c5 done
-ls gpurun_out/r4f_pmc_*/pmc_traffic_*.json
+O=gpurun_out/r4f; mkdir -p $O
+timeout -k 10 600 python bench.py > $O/bench_c2_default.json 2> $O/bench_c2_default.err || exit 2
+cat $O/bench_c2_default.json
+timeout -k 10 300 python bench.py --steps 20 --precision bf16 --model resnest50 --seq 10 --lfb 40 --no-cpu-baseline --conv-table > $O/bench_c4.json 2> $O/bench_c4.err || exit 3
+timeout -k 10 400 python bench.py --steps 20 --precision bf16 --seq 30 --lfb 300 --no-cpu-baseline --conv-table > $O/bench_c5.json 2> $O/bench_c5.err || exit 4
+for c in c4 c5; do python -c "import json;d=json.load(open('$O/bench_$c.json'));r=d['roofline'];print('$c', d['value'], d['ms_per_step'], r.get('traffic'), r.get('traffic_stale'), r.get('frac'))"; done
+PROF_NAME=r4f_prof_c2 STEPS=3 BENCH_ARGS="" bash scripts/profile.sh > $O/prof_c2.txt 2>&1 || exit 5
+PROF_NAME=r4f_prof_c4 STEPS=3 BENCH_ARGS="--precision bf16 --model resnest50 --seq 10 --lfb 40" bash scripts/profile.sh > $O/prof_c4.txt 2>&1 || exit 6
+PROF_NAME=r4f_prof_c5 STEPS=3 BENCH_ARGS="--precision bf16 --seq 30 --lfb 300" bash scripts/profile.sh > $O/prof_c5.txt 2>&1 || exit 7
+echo profiles done
