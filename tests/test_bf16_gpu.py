@@ -289,7 +289,7 @@ def _conv_ref16(x, wt, stride, pad):
     (5, 14, 14, 256, 256, 3, 1, 1, 0),   # 256x256 tiles
     (2, 6, 6, 512, 1024, 1, 2, 0, 0),    # strided 1x1 with empty parity classes in dgrad
 ])
-def test_gemm16_views(dev, case):
+def test_gemm16_views(dev, case, monkeypatch):
     """The bf16 LDS-DMA engine (every operand bf16 in HBM) on its three views against float64
     convolutions of the same bf16 operands: FWD / DGRAD / WGRAD, TAPV (k-tiles spanning taps),
     partial tiles, strided parity classes and channel-slice operands.  FWD and DGRAD also
@@ -314,6 +314,11 @@ def test_gemm16_views(dev, case):
     if not xoff:   # bf16 output (TMR_IO_Y_BF16): the rounded accumulators, BN partials of those
         yb, stb, npb = ops.conv_fwd_bnstats(x16, w16, st, pad, math="bf16", y16=True)
         assert yb.dtype == torch.bfloat16 and torch.equal(yb, y32.to(torch.bfloat16))
+        # the whole-line store form (default) and the 64-B pair form write the same bytes
+        monkeypatch.setenv("TMR_C16W", "0")
+        yp, stp, _ = ops.conv_fwd_bnstats(x16, w16, st, pad, math="bf16", y16=True)
+        monkeypatch.delenv("TMR_C16W")
+        assert torch.equal(yp.view(torch.int16), yb.view(torch.int16)) and torch.equal(stp, stb)
         c = yb.shape[-1]
         mean, inv, _, _ = ops.bn_finalize(stb, npb, torch.ones(c, device=dev),
                                           torch.zeros(c, device=dev), torch.zeros(c, device=dev),
@@ -337,6 +342,31 @@ def test_gemm16_views(dev, case):
     dw = ops.conv_wgrad(x16, dy16, r, r, st, pad, math="bf16")
     err = (dw.double().cpu() - wr.grad).abs().max().item() / wr.grad.abs().max().item()
     assert err < 1e-5, ("wgrad", err)
+
+
+@pytest.mark.parametrize("case", [
+    # n, h, w, cin, cout, stride: 1x1 forwards over the tile configs (256x256, 128x128, 256x64)
+    (5, 14, 14, 64, 256, 1), (2, 13, 9, 64, 128, 1), (3, 9, 9, 128, 64, 1),
+    (2, 9, 9, 64, 200, 1),     # N not a multiple of 64: a 32-column block with 8 valid columns
+    (3, 7, 7, 32, 96, 1),      # N = 96: a partial 64-column wave block
+    (2, 12, 12, 64, 512, 2),   # strided
+])
+def test_gemm16_y16_store_forms(dev, case, monkeypatch):
+    """bf16 y (TMR_IO_Y_BF16): the whole-line store form of epilogue_batched (default) writes the
+    same bytes as the 64-B pair form (TMR_C16W=0) and as the fp32 output rounded to bf16, with
+    the same BN partials, including ragged M and N."""
+    n, h, w, cin, cout, st = case
+    g = torch.Generator().manual_seed(5 + cin + cout)
+    wt = _r(torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5)
+    x16 = _r(torch.randn(n, h, w, cin, generator=g)).to(dev).to(torch.bfloat16)
+    w16 = ops.weight_to_krsc(wt.to(dev), bf16=True)
+    y32, st32, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16")
+    yb, stb, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
+    monkeypatch.setenv("TMR_C16W", "0")
+    yp, stp, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
+    monkeypatch.delenv("TMR_C16W")
+    assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
+    assert torch.equal(yp.view(torch.int16), yb.view(torch.int16)) and torch.equal(stp, stb)
 
 
 def test_bf16_full16_step(dev):

@@ -197,6 +197,11 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.sab = ((d->io & TMR_IO_X_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldc, d->k));
   a.c16 = (d->io & TMR_IO_Y_BF16) ? 1 : 0;
+  // (2: the whole-line store form of epilogue_batched; TMR_C16W=0 the 64-B pair form, A/B)
+  if (a.c16) {
+    const char* e = getenv("TMR_C16W");
+    if (!(e && e[0] == '0')) a.c16 = 2;
+  }
   a.dma32 = d->math == TMR_MATH_F32;
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;

@@ -477,6 +477,36 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
     const int col = col0 + 32 * j;
     scj[j] = (MODE == MODE_FWD && a.scale && col < a.N) ? a.scale[col] : 1.f;
   }
+  // bf16 output, TN even: whole 128-B lines per row.  The lane pair (2k, 2k+1) stores columns
+  // (2k, 2k+1) of accumulator column block 2jp (even lane) and of block 2jp + 1 (odd lane), both of
+  // the same row, so the 32 lanes of a half-wave write one row's 64 columns = 128 contiguous bytes
+  // (the pair form below writes 64-B halves of two rows).  Same values, same bytes.  a.c16 == 2
+  // selects it (host: TMR_C16W).
+  const bool c16w = c16 && TN % 2 == 0 && a.c16 == 2;
+  if (c16w) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r0 = 0; r0 < 16; r0 += ER) {
+#pragma unroll
+        for (int r = 0; r < ER; ++r) {
+          const uint32_t ro = row_off(i, r0 + r);
+#pragma unroll
+          for (int jp = 0; jp < TN / 2; ++jp) {
+            const float mine = odd ? acc[i][2 * jp + 1][r0 + r] : acc[i][2 * jp][r0 + r];
+            const float send = odd ? acc[i][2 * jp][r0 + r] : acc[i][2 * jp + 1][r0 + r];
+            const uint32_t got = swap1((uint32_t)bf16_bits(send));
+            const uint32_t mb = (uint32_t)bf16_bits(mine);
+            const uint32_t w = odd ? ((mb << 16) | got) : ((got << 16) | mb);
+            const int scol = odd ? col0 - 1 + 32 * (2 * jp + 1) : col0 + 64 * jp;
+            const uint32_t o = (ro >= OOB || scol >= a.N) ? OOB : (ro >> 1) + (uint32_t)scol * 2u;
+            __builtin_amdgcn_raw_buffer_store_b32(w, rC, o, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
