@@ -83,6 +83,73 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_k(const TX* __restrict__ x, TY
   }
 }
 
+// The bf16-activation form (bf16 pre-BN input, bf16 output), 8 channels per thread: 32-bit
+// magic-number index division instead of maxpool_fwd_k's 64-bit divides, the 9 window loads
+// (16 B each) issued before any is consumed, 16-B y and 8-B argmax stores.  Same BN+ReLU
+// arithmetic and scan order as maxpool_fwd_k: identical outputs.  total = n*ho*wo*c/8 < 2^31,
+// c / 8 a power of two (lc8 = log2), both checked on the host.
+__global__ __launch_bounds__(NT) void maxpool_fwd_bn8_a16(const __bf16* __restrict__ x,
+                                                         __bf16* __restrict__ y,
+                                                         uint2* __restrict__ am, int total, int h,
+                                                         int w, int lc8, FastDiv dHWo, FastDiv dWo,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift) {
+  const int c8 = 1 << lc8;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int cq = i & (c8 - 1);
+    const uint32_t p = (uint32_t)i >> lc8;
+    const uint32_t nn = fdiv(p, dHWo);
+    const uint32_t rem = p - nn * dHWo.d;
+    const int oy = (int)fdiv(rem, dWo), ox = (int)(rem - (uint32_t)oy * dWo.d);
+    uint4 u[9];
+    bool ok[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int iy = oy * 2 - 1 + k / 3, ix = ox * 2 - 1 + k % 3;
+      ok[k] = iy >= 0 && iy < h && ix >= 0 && ix < w;
+      const int src = ok[k] ? (((int)nn * h + iy) * w + ix) * c8 + cq : i;
+      u[k] = reinterpret_cast<const uint4*>(x)[src];
+    }
+    float sc[8], sf[8];
+    {
+      const float4 s0 = reinterpret_cast<const float4*>(scale)[2 * cq];
+      const float4 s1 = reinterpret_cast<const float4*>(scale)[2 * cq + 1];
+      const float4 f0 = reinterpret_cast<const float4*>(shift)[2 * cq];
+      const float4 f1 = reinterpret_cast<const float4*>(shift)[2 * cq + 1];
+      const float a[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float b[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = a[e]; sf[e] = b[e]; }
+    }
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0u; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (!ok[k]) continue;
+      const uint32_t w4[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float raw = __uint_as_float((e & 1) ? (w4[e >> 1] & 0xffff0000u) : (w4[e >> 1] << 16));
+        const float v = fmaxf(fmaf(raw, sc[e], sf[e]), 0.f);
+        // first maximum in scan order wins (PyTorch: val > max || isnan(val))
+        if (v > best[e] || isnan(v)) { best[e] = v; bi[e] = (uint32_t)k; }
+      }
+    }
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    uint32_t ow[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bf16x2_t pr = {(__bf16)best[2 * e], (__bf16)best[2 * e + 1]};
+      ow[e] = __builtin_bit_cast(uint32_t, pr);
+    }
+    reinterpret_cast<uint4*>(y)[i] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    am[i] = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                       bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+  }
+}
+
 __global__ __launch_bounds__(NT) void maxpool_bwd_k(const float* __restrict__ dy, const uchar4* __restrict__ am,
                                                     float* __restrict__ dx, int n, int h, int w,
                                                     int c4, int ho, int wo) {
@@ -250,9 +317,20 @@ TMR_API int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const fl
   TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd_bn_a16: channels %d must be a multiple of 4", c);
   TMR_CHECK_ARG(scale && shift, "tmr_maxpool2d_fwd_bn_a16: null BatchNorm scale/shift");
   const long total = (long)n * ho * wo * (c / 4);
-  hipLaunchKernelGGL((maxpool_fwd_k<true, __bf16, __bf16>), dim3(ew_blocks(total)), dim3(NT), 0,
-                     stream, (const __bf16*)x, (__bf16*)y, (uchar4*)argmax, n, h, w, c / 4, ho, wo,
-                     scale, shift);
+  const int c8 = c / 8;
+  const char* e8 = getenv("TMR_MAXPOOL8");   // A/B switch (0: the 4-wide form)
+  if (!(e8 && e8[0] == '0') && c % 8 == 0 && (c8 & (c8 - 1)) == 0 &&
+      (long)n * h * w * c8 < 0x7fffffffL &&
+      (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
+    const int t8 = (int)(total / 2);
+    hipLaunchKernelGGL(maxpool_fwd_bn8_a16, dim3(ew_blocks(t8)), dim3(NT), 0, stream,
+                       (const __bf16*)x, (__bf16*)y, (uint2*)argmax, t8, h, w, __builtin_ctz(c8),
+                       make_fastdiv((uint32_t)(ho * wo)), make_fastdiv((uint32_t)wo), scale, shift);
+  } else {
+    hipLaunchKernelGGL((maxpool_fwd_k<true, __bf16, __bf16>), dim3(ew_blocks(total)), dim3(NT), 0,
+                       stream, (const __bf16*)x, (__bf16*)y, (uchar4*)argmax, n, h, w, c / 4, ho, wo,
+                       scale, shift);
+  }
   TMR_CHECK_LAUNCH("maxpool_fwd_bn_a16");
   return 0;
 }
