@@ -15,7 +15,7 @@ endif
 SRC := $(wildcard tmrnet_amd/csrc/*.hip) tmrnet_amd/csrc/api.cpp
 OBJ := $(patsubst tmrnet_amd/csrc/%,$(BUILD)/%.o,$(SRC))
 CFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Itmrnet_amd/csrc -munsafe-fp-atomics \
-          -DTMR_PROLOGUES=$(PROLOGUES)
+          -DTMR_PROLOGUES=$(PROLOGUES) $(EXTRA)
 
 $(LIB): $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)

@@ -346,7 +346,7 @@ def test_gemm16_views(dev, case, monkeypatch):
 
 @pytest.mark.parametrize("case", [
     # n, h, w, cin, cout, stride: 1x1 forwards over the tile configs (256x256, 128x128, 256x64)
-    (5, 14, 14, 64, 256, 1), (2, 13, 9, 64, 128, 1), (3, 9, 9, 128, 64, 1),
+    (5, 14, 14, 64, 256, 1), (2, 13, 9, 64, 128, 1), (3, 9, 9, 128, 64, 1), (3, 9, 9, 64, 64, 1),
     (2, 9, 9, 64, 200, 1),     # N not a multiple of 64: a 32-column block with 8 valid columns
     (3, 7, 7, 32, 96, 1),      # N = 96: a partial 64-column wave block
     (2, 12, 12, 64, 512, 2),   # strided
@@ -354,7 +354,8 @@ def test_gemm16_views(dev, case, monkeypatch):
 def test_gemm16_y16_store_forms(dev, case, monkeypatch):
     """bf16 y (TMR_IO_Y_BF16): the whole-line store form of epilogue_batched (default) writes the
     same bytes as the 64-B pair form (TMR_C16W=0) and as the fp32 output rounded to bf16, with
-    the same BN partials, including ragged M and N."""
+    the same BN partials, including ragged M and N; the one-stage form of the one-k-tile forwards
+    (gemm16_kernel NST) the same as the two-stage form (TMR_NST1=0)."""
     n, h, w, cin, cout, st = case
     g = torch.Generator().manual_seed(5 + cin + cout)
     wt = _r(torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5)
@@ -367,6 +368,11 @@ def test_gemm16_y16_store_forms(dev, case, monkeypatch):
     monkeypatch.delenv("TMR_C16W")
     assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
     assert torch.equal(yp.view(torch.int16), yb.view(torch.int16)) and torch.equal(stp, stb)
+    # the one-stage form of the one-k-tile launches (K = 64 on the 4-wave tiles) vs two stages
+    monkeypatch.setenv("TMR_NST1", "0")
+    y2, st2, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
+    monkeypatch.delenv("TMR_NST1")
+    assert torch.equal(y2.view(torch.int16), yb.view(torch.int16)) and torch.equal(st2, stb)
 
 
 def test_bf16_full16_step(dev):

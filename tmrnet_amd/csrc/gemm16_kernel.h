@@ -461,7 +461,13 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // lane transforms the 16-B pieces it issued, after its own LDS-DMA has landed (vmcnt) and
 // before the barrier that publishes the k-tile, so no extra barrier; the coefficient tables
 // are staged in LDS once per workgroup.
-template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0>
+//
+// NST = 1 (FWD launches of one k-tile, K <= BK: the second stage would never be used): one LDS
+// stage -- 32-40 KB instead of 64-80 KB, so three 4-wave workgroups fit a CU instead of one or
+// two: the short-reduction launches are bound by their epilogue's stores, and more workgroups
+// keep more of them in flight.  Same k order and epilogue: bit-identical to NST = 2.
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0,
+          int NST = 2>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && BM * BN <= 128 * 128) ? 4 : 2))
 void gemm16_kernel(const GemmArgs a) {
   constexpr uint32_t ES = F32 ? 4u : 2u;   // element bytes
@@ -480,7 +486,10 @@ void gemm16_kernel(const GemmArgs a) {
   constexpr int CPRA = BM * (int)ES / 16, CPRB = BN * (int)ES / 16;
   using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
   constexpr int EPI = WM * BN * 2 * 4;
-  constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  static_assert(NST == 2 || (NST == 1 && MODE != MODE_WGRAD && PRO == 0), "one-stage form: FWD / DGRAD");
+  constexpr int LDSNEED = MODE == MODE_DGRAD ? (BN + 4) * (BM / WM) * 4 : 0;
+  constexpr int SMEM1 = STAGE > EPI ? (STAGE > LDSNEED ? STAGE : LDSNEED) : (EPI > LDSNEED ? EPI : LDSNEED);
+  constexpr int SMEM = NST == 1 ? SMEM1 : (2 * STAGE > EPI ? 2 * STAGE : EPI);
   static_assert(PRO == 0 || F32, "operand prologues: fp32 form only");
   static_assert(!(PRO & 1) || MODE != MODE_DGRAD, "X prologue: FWD / WGRAD views");
   static_assert(!(PRO & 2) || MODE != MODE_FWD, "dY prologue: DGRAD / WGRAD views");
@@ -900,6 +909,16 @@ void gemm16_kernel(const GemmArgs a) {
       if (kt + 1 < ntiles) stage(kt + 1, (kt + 1) & 1);
       compute(kt & 1);
     }
+  } else if (NST == 1 && ntiles > 0) {
+    // one stage (the host launches this form for one k-tile; a longer reduction is still
+    // correct, serialised: barrier, issue, wait)
+    for (int kt = 0; kt < ntiles; ++kt) {
+      if (kt > 0) __syncthreads();   // every wave's reads of tile kt - 1 done
+      stage(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      compute(0);
+    }
   } else if (ntiles > 0) {
     // PIPE 1: the first k-step's fragment reads go out before the LDS-DMA issue of the next
     // tile (its address arithmetic then overlaps their latency), each later k-step's reads
@@ -941,6 +960,19 @@ void gemm16_kernel(const GemmArgs a) {
 template <int MODE, int BM, int BN, int WM, int WN, int F32, int PRO = 0>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
+  // one-k-tile bf16 FWD launches on the 4-wave 128x128 / 256x64 tiles: the one-stage form
+  // (TMR_NST1=0: the two-stage form, A/B; read per call).  56x56 64->64: 0.427 -> 0.378 ms; the
+  // DGRAD view measured slower in it (its 233-VGPR LDS-staged epilogue caps the occupancy at two
+  // workgroups anyway; profiles/r4/nst1/)
+  if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && WM * WN == 4 &&
+                ((BM == 128 && BN == 128) || (BM == 256 && BN == 64))) {
+    const char* e = getenv("TMR_NST1");
+    if (!tapv && a.K > 0 && a.K <= 64 && !(e && e[0] == '0')) {
+      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, 0, 1>), grid, blk, 0, st, a);
+      TMR_CHECK_LAUNCH("gemm16_kernel (one stage)");
+      return 0;
+    }
+  }
   if constexpr (PRO != 0) {   // one tap per k-tile (pro32_ok)
     hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, PRO>), grid, blk, 0, st, a);
   } else if (tapv) {
