@@ -368,10 +368,13 @@ def test_gemm16_y16_store_forms(dev, case, monkeypatch):
     monkeypatch.delenv("TMR_C16W")
     assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
     assert torch.equal(yp.view(torch.int16), yb.view(torch.int16)) and torch.equal(stp, stb)
-    # the one-stage form of the one-k-tile launches (K = 64 on the 4-wave tiles) vs two stages
+    # the one-stage forms of the one-k-tile launches (K = 64: the 4-wave tiles, and 256x128 for
+    # what the tile rules make 256x256) vs the two-stage launches
     monkeypatch.setenv("TMR_NST1", "0")
+    monkeypatch.setenv("TMR_NST1W", "0")
     y2, st2, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
     monkeypatch.delenv("TMR_NST1")
+    monkeypatch.delenv("TMR_NST1W")
     assert torch.equal(y2.view(torch.int16), yb.view(torch.int16)) and torch.equal(st2, stb)
 
 

@@ -468,7 +468,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // keep more of them in flight.  Same k order and epilogue: bit-identical to NST = 2.
 template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0,
           int NST = 2>
-__global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && BM * BN <= 128 * 128) ? 4 : 2))
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && (BM * BN <= 128 * 128 || NST == 1)) ? 4 : 2))
 void gemm16_kernel(const GemmArgs a) {
   constexpr uint32_t ES = F32 ? 4u : 2u;   // element bytes
   constexpr int EPC = 16 / ES;             // elements per 16-B chunk
@@ -970,6 +970,20 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
     if (!tapv && a.K > 0 && a.K <= 64 && !(e && e[0] == '0')) {
       hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, 0, 1>), grid, blk, 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage)");
+      return 0;
+    }
+  }
+  // ... and the one-k-tile bf16 forwards the tile rules give 256x256 (N >= 256: the 64 -> 256
+  // expansions): 256x128 as 8 waves in the one-stage form at 128 VGPRs -- two workgroups per CU
+  // (one 16-wave 256x256 workgroup fills the register file), so one's epilogue stores overlap
+  // the other's loads.  Same BM (the statistics' part rows), same per-wave tiles: bit-identical.
+  // TMR_NST1W=0: the 256x256 launch (A/B; read per call).
+  if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && BM == 256 && BN == 256) {
+    const char* e = getenv("TMR_NST1W");
+    if (!tapv && a.K > 0 && a.K <= 64 && !(e && e[0] == '0')) {
+      const dim3 g2((unsigned)(cdiv(a.M, 256) * cdiv(a.N, 128)), grid.y, 1);
+      hipLaunchKernelGGL((gemm16_kernel<MODE, 256, 128, 4, 2, 0, 1, F32, 0, 1>), g2, dim3(512), 0, st, a);
+      TMR_CHECK_LAUNCH("gemm16_kernel (one stage, 256x128)");
       return 0;
     }
   }

@@ -406,8 +406,12 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
     const int col = col0 + 32 * j;
     bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
   }
+  // bf16 output, TN even: whole 128-B lines per row (below); its stores go out before the
+  // statistics pass, whose barriers then overlap their drain
+  const bool c16w = c16 && TN % 2 == 0 && a.c16 == 2;
   // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
   // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
+  auto stats_pass = [&]() {
   if (MODE == MODE_FWD && a.stats != nullptr) {
     float* red = smem;  // main loop ended with a barrier: LDS is free
     const int nrows = min(BM, a.M - m0);
@@ -468,6 +472,8 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
       }
     }
   }
+  };
+  if (!c16w) stats_pass();
   // (3) beta, FWD inference epilogue (scale, residual, ReLU), stores
   const bool has_res = MODE == MODE_FWD && a.res != nullptr;
   const __amdgpu_buffer_rsrc_t rR = make_rsrc(has_res ? a.res : Cb, a.Cbytes);
@@ -482,7 +488,6 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
   // the same row, so the 32 lanes of a half-wave write one row's 64 columns = 128 contiguous bytes
   // (the pair form below writes 64-B halves of two rows).  Same values, same bytes.  a.c16 == 2
   // selects it (host: TMR_C16W).
-  const bool c16w = c16 && TN % 2 == 0 && a.c16 == 2;
   if (c16w) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -505,6 +510,7 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+    stats_pass();
     return;
   }
 #pragma unroll
