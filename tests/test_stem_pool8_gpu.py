@@ -72,3 +72,25 @@ def test_stem_bwd_apply8_bit_identical(dev, shape, monkeypatch):
     ref = gamma.double() * inv.double() * (dz - sdz / m - xh * sdx / m)
     err = (d8.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err    # bf16 output
+
+
+@pytest.mark.parametrize("rows,c", [(3 * 56 * 56, 256), (1001, 64), (37, 24)])
+def test_bn_apply8_a16_bit_identical(dev, rows, c, monkeypatch):
+    """bf16 BN applies (relu(bn(y)), relu(bn(y) + residual), relu(bn(y) + bn_ds(y_ds))) 8 per
+    thread (bn_apply8_a16_k) vs the 4-wide forms (TMR_BN_APPLY8=0): identical bytes; c = 24 takes
+    the 4-wide form in both runs."""
+    g = torch.Generator().manual_seed(rows + c)
+    mk = lambda: (torch.randn(rows, c, generator=g) * 2).to(torch.bfloat16).to(dev)
+    y, r, yr = mk(), mk(), mk()
+    sc, sf, rs, rf = [(torch.rand(c, generator=g) + 0.5).to(dev) for _ in range(4)]
+    outs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("TMR_BN_APPLY8", v)
+        outs[v] = [ops.bn_apply(y, sc, sf), ops.bn_apply(y, sc, sf, residual=r),
+                   ops.bn_apply(y, sc, sf, residual=r, relu=False),
+                   ops.bn_apply2(y, sc, sf, yr, rs, rf), ops.bn_apply2(y, sc, sf, yr, rs, rf, relu=False)]
+    monkeypatch.delenv("TMR_BN_APPLY8")
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    ref = torch.relu(y.double() * sc.double() + sf.double() + r.double())
+    assert torch.allclose(outs["1"][1].double(), ref, rtol=1e-2, atol=1e-2)   # one bf16 rounding

@@ -262,6 +262,84 @@ __global__ __launch_bounds__(NT) void bn_apply2_k(const TY* __restrict__ y, cons
   }
 }
 
+// The bf16-activation forms of bn_apply_k / bn_apply2_k (bf16 y, residual or branch input, and z),
+// 8 elements per thread: every access a 16-B lane piece (the 4-wide forms move bf16 in 8-B
+// pieces), two pieces per thread in flight.  Same fmaf / add / max sequence per element:
+// identical outputs.  BR: the residual is the downsample branch's pre-BN y (bn_apply2_k).
+__device__ __forceinline__ void unpack8(const uint4 w, float (&v)[8]) {
+  const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(u[e] << 16);
+    v[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  uint32_t o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16x2_t p = {(__bf16)v[2 * e], (__bf16)v[2 * e + 1]};
+    o[e] = __builtin_bit_cast(uint32_t, p);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+template <bool RES, bool RELU, bool BR>
+__global__ __launch_bounds__(NT) void bn_apply8_a16_k(const __bf16* __restrict__ y,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      const __bf16* __restrict__ res,
+                                                      const float* __restrict__ rscale,
+                                                      const float* __restrict__ rshift,
+                                                      __bf16* __restrict__ z, long n8, int c8) {
+  const long stride = (long)gridDim.x * NT;
+  auto apply = [&](long i, const uint4 yw, const uint4 rw) {
+    const int cc = chan_of(i, c8) * 8;
+    float v[8], r[8];
+    unpack8(yw, v);
+    unpack8(rw, r);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 sc = *reinterpret_cast<const float4*>(scale + cc + 4 * h);
+      const float4 sf = *reinterpret_cast<const float4*>(shift + cc + 4 * h);
+      const float a[4] = {sc.x, sc.y, sc.z, sc.w}, b[4] = {sf.x, sf.y, sf.z, sf.w};
+      float ra[4] = {0.f, 0.f, 0.f, 0.f}, rb[4] = {0.f, 0.f, 0.f, 0.f};
+      if (BR) {
+        const float4 rs = *reinterpret_cast<const float4*>(rscale + cc + 4 * h);
+        const float4 rf = *reinterpret_cast<const float4*>(rshift + cc + 4 * h);
+        ra[0] = rs.x; ra[1] = rs.y; ra[2] = rs.z; ra[3] = rs.w;
+        rb[0] = rf.x; rb[1] = rf.y; rb[2] = rf.z; rb[3] = rf.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t;
+        if (BR) {
+          t = fmaf(v[4 * h + e], a[e], b[e]) + fmaf(r[4 * h + e], ra[e], rb[e]);
+        } else {
+          t = fmaf(v[4 * h + e], a[e], b[e]);
+          if (RES) t += r[4 * h + e];
+        }
+        if (RELU) t = fmaxf(t, 0.f);
+        v[4 * h + e] = t;
+      }
+    }
+    reinterpret_cast<uint4*>(z)[i] = pack8(v);
+  };
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n8;
+    const uint4 y0 = reinterpret_cast<const uint4*>(y)[i];
+    const uint4 r0 = (RES || BR) ? reinterpret_cast<const uint4*>(res)[i] : y0;
+    uint4 y1 = y0, r1 = r0;
+    if (hj) {
+      y1 = reinterpret_cast<const uint4*>(y)[j];
+      if (RES || BR) r1 = reinterpret_cast<const uint4*>(res)[j];
+    }
+    apply(i, y0, r0);
+    if (hj) apply(j, y1, r1);
+  }
+}
+
 // The ReLU mask of a block output as bits (tmr_bn_apply_bits / tmr_bn_apply2_bits): element e is
 // bit e % 32 of word e / 32.  The fp32 residual-gradient dgrads read it (mask 3) instead of
 // re-reading the 4-byte z.  Each lane holds 4 consecutive elements (one float4 index i); the 8
@@ -1344,6 +1422,14 @@ TMR_API int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, con
 // here), the gradients dz / dres stay fp32, dy (a conv operand) is written bf16.  Same arithmetic
 // as the fp32 forms on the bf16 values.
 
+// the 8-wide bf16 applies: channels a multiple of 8, 16-B aligned tensors (TMR_BN_APPLY8=0: the
+// 4-wide forms, A/B; read per call)
+static bool apply8_ok(int c, const void* y, const void* r, const void* z) {
+  const char* e = getenv("TMR_BN_APPLY8");
+  if (e && e[0] == '0') return false;
+  return c % 8 == 0 && (((uintptr_t)y | (uintptr_t)r | (uintptr_t)z) & 15) == 0;
+}
+
 TMR_API int tmr_bn_apply_a16(const void* y, const float* scale, const float* shift,
                              const void* residual, void* z, int rows, int c, int relu,
                              hipStream_t stream) {
@@ -1352,7 +1438,17 @@ TMR_API int tmr_bn_apply_a16(const void* y, const float* scale, const float* shi
   const int nb = ew_blocks(n4), c4 = c / 4;
   const __bf16 *yb = (const __bf16*)y, *rb = (const __bf16*)residual;
   __bf16* zb = (__bf16*)z;
-  if (rb) {
+  if (apply8_ok(c, y, residual, z)) {   // 8 per thread (bn_apply8_a16_k)
+    const long n8 = n4 / 2;
+    const int nb8 = ew_blocks(n8), c8 = c / 8;
+    if (rb) {
+      if (relu) hipLaunchKernelGGL((bn_apply8_a16_k<true, true, false>), dim3(nb8), dim3(NT), 0, stream, yb, scale, shift, rb, nullptr, nullptr, zb, n8, c8);
+      else hipLaunchKernelGGL((bn_apply8_a16_k<true, false, false>), dim3(nb8), dim3(NT), 0, stream, yb, scale, shift, rb, nullptr, nullptr, zb, n8, c8);
+    } else {
+      if (relu) hipLaunchKernelGGL((bn_apply8_a16_k<false, true, false>), dim3(nb8), dim3(NT), 0, stream, yb, scale, shift, nullptr, nullptr, nullptr, zb, n8, c8);
+      else hipLaunchKernelGGL((bn_apply8_a16_k<false, false, false>), dim3(nb8), dim3(NT), 0, stream, yb, scale, shift, nullptr, nullptr, nullptr, zb, n8, c8);
+    }
+  } else if (rb) {
     if (relu) hipLaunchKernelGGL((bn_apply_k<true, true, __bf16, false, __bf16>), dim3(nb), dim3(NT), 0, stream, yb, scale, shift, rb, zb, n4, c4, nullptr);
     else hipLaunchKernelGGL((bn_apply_k<true, false, __bf16, false, __bf16>), dim3(nb), dim3(NT), 0, stream, yb, scale, shift, rb, zb, n4, c4, nullptr);
   } else {
@@ -1371,7 +1467,15 @@ TMR_API int tmr_bn_apply2_a16(const void* y, const float* scale, const float* sh
   TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_a16: the branch input must not alias z");
   const long n4 = (long)rows * c / 4;
   const __bf16 *yb = (const __bf16*)y, *rb = (const __bf16*)yr;
-  if (relu)
+  if (apply8_ok(c, y, yr, z)) {   // 8 per thread (bn_apply8_a16_k)
+    const long n8 = n4 / 2;
+    if (relu)
+      hipLaunchKernelGGL((bn_apply8_a16_k<false, true, true>), dim3(ew_blocks(n8)), dim3(NT), 0,
+                         stream, yb, scale, shift, rb, rscale, rshift, (__bf16*)z, n8, c / 8);
+    else
+      hipLaunchKernelGGL((bn_apply8_a16_k<false, false, true>), dim3(ew_blocks(n8)), dim3(NT), 0,
+                         stream, yb, scale, shift, rb, rscale, rshift, (__bf16*)z, n8, c / 8);
+  } else if (relu)
     hipLaunchKernelGGL((bn_apply2_k<true, false, __bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0,
                        stream, yb, scale, shift, rb, rscale, rshift, (__bf16*)z, n4, c / 4, nullptr);
   else

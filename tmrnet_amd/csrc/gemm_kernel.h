@@ -406,8 +406,7 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
     const int col = col0 + 32 * j;
     bvals[j] = (MODE == MODE_FWD && a.bias && col < a.N) ? a.bias[col] : 0.f;
   }
-  // bf16 output, TN even: whole 128-B lines per row (below); its stores go out before the
-  // statistics pass, whose barriers then overlap their drain
+  // (the stores go out before the statistics pass, whose barriers then overlap their drain)
   const bool c16w = c16 && TN % 2 == 0 && a.c16 == 2;
   // (1b) fused BatchNorm batch statistics of this output tile (FWD only): exact block mean,
   // then M2 about it; combined across tiles by tmr_bn_finalize (shifted sums in double, fixed order).
@@ -473,8 +472,8 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
     }
   }
   };
-  if (!c16w) stats_pass();
-  // (3) beta, FWD inference epilogue (scale, residual, ReLU), stores
+  // (3) beta, FWD inference epilogue (scale, residual, ReLU), stores; then the statistics pass
+  // (acc is not modified by the stores)
   const bool has_res = MODE == MODE_FWD && a.res != nullptr;
   const __amdgpu_buffer_rsrc_t rR = make_rsrc(has_res ? a.res : Cb, a.Cbytes);
   float scj[TN];
@@ -553,6 +552,7 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
         }
       __builtin_amdgcn_sched_barrier(0);
     }
+  stats_pass();
   }
 }
 
