@@ -911,10 +911,16 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply8(const PoolGeo pg, const __
     float4 d0[4], d1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      // (a coinciding candidate is not loaded: 2.25 of the 4 on average)
       const int o = (((int)nn * pg.ho + oys[k >> 1]) * pg.wo + oxs[k & 1]) * c8 + cq;
-      a[k] = am[o];
-      d0[k] = dp[2 * o];
-      d1[k] = dp[2 * o + 1];
+      if (on[k]) {
+        a[k] = am[o];
+        d0[k] = dp[2 * o];
+        d1[k] = dp[2 * o + 1];
+      } else {
+        a[k] = make_uint2(0xffffffffu, 0xffffffffu);
+        d0[k] = d1[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
     const uint4 yw = reinterpret_cast<const uint4*>(y)[i];
     const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
