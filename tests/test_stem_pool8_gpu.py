@@ -37,7 +37,7 @@ def test_maxpool_fwd_bn8_bit_identical(dev, shape, monkeypatch):
     assert int(a8.max()) <= 8
 
 
-@pytest.mark.parametrize("shape", [(3, 112, 112, 64), (2, 13, 11, 16), (2, 9, 10, 24)])
+@pytest.mark.parametrize("shape", [(3, 112, 112, 64), (2, 13, 11, 16), (2, 12, 9, 8), (2, 9, 10, 24)])
 def test_stem_bwd_apply8_bit_identical(dev, shape, monkeypatch):
     n, h, w, c = shape
     y, scale, shift = _stem_case(dev, *shape, seed=7 + sum(shape))
@@ -49,6 +49,12 @@ def test_stem_bwd_apply8_bit_identical(dev, shape, monkeypatch):
     inv = 1.0 / (y.float().var((0, 1, 2), unbiased=False) + 1e-5).sqrt()
     gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
     d8, g8, b8 = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
+    # the per-pixel 8-channel form (TMR_STEM_QUAD=0) against the default 2x2-quad form
+    monkeypatch.setenv("TMR_STEM_QUAD", "0")
+    dp_, gp_, bp_ = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
+    monkeypatch.delenv("TMR_STEM_QUAD")
+    assert torch.equal(dp_.view(torch.int16), d8.view(torch.int16))
+    assert torch.equal(gp_, g8) and torch.equal(bp_, b8)
     monkeypatch.setenv("TMR_STEM_BWD8", "0")
     d4, g4, b4 = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
     monkeypatch.delenv("TMR_STEM_BWD8")

@@ -966,6 +966,103 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply8(const PoolGeo pg, const __
   }
 }
 
+// The same per 2x2 quad of input pixels (rows 2k, 2k+1, columns 2l, 2l+1): the pooled outputs
+// (k .. k+1) x (l .. l+1) are the candidates of all four pixels, so each is loaded once per quad
+// -- one pooled load per pixel instead of 2.25 (the launch is bound by those gathered bytes).
+// Pixel (py, px) of the quad sums candidate (dy, dx) when (dy <= py, dx <= px, in range) with
+// id = (py + 1 - 2dy) * 3 + (px + 1 - 2dx), in the order (0,0), (0,1), (1,0), (1,1): the
+// per-pixel kernels' order, so bit-identical.  nq = n * ceil(h/2) * ceil(w/2) * c/8 < 2^31.
+__global__ __launch_bounds__(NT) void stem_bwd_apply8q(const PoolGeo pg, int h, int w, FastDiv dQHW,
+                                                       FastDiv dQW, const __bf16* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ coef,
+                                                       __bf16* __restrict__ dy, int nq, int lc8) {
+  const int c8 = 1 << lc8, c = c8 * 8;
+  const uint2* am = reinterpret_cast<const uint2*>(pg.am);
+  const float4* dp = reinterpret_cast<const float4*>(pg.dyp);
+  for (int i = blockIdx.x * NT + threadIdx.x; i < nq; i += gridDim.x * NT) {
+    const int cq = i & (c8 - 1);
+    const uint32_t q = (uint32_t)i >> lc8;
+    const uint32_t nn = fdiv(q, dQHW);
+    const uint32_t rem = q - nn * dQHW.d;
+    const int k = (int)fdiv(rem, dQW), l = (int)(rem - (uint32_t)k * dQW.d);
+    const bool pin[2][2] = {{true, l + 1 < pg.wo}, {k + 1 < pg.ho, k + 1 < pg.ho && l + 1 < pg.wo}};
+    uint2 a[2][2];
+    float4 d0[2][2], d1[2][2];
+#pragma unroll
+    for (int ddy = 0; ddy < 2; ++ddy)
+#pragma unroll
+      for (int ddx = 0; ddx < 2; ++ddx) {
+        const int o = (((int)nn * pg.ho + k + ddy) * pg.wo + l + ddx) * c8 + cq;
+        if (pin[ddy][ddx]) {
+          a[ddy][ddx] = am[o];
+          d0[ddy][ddx] = dp[2 * o];
+          d1[ddy][ddx] = dp[2 * o + 1];
+        } else {
+          a[ddy][ddx] = make_uint2(0xffffffffu, 0xffffffffu);
+          d0[ddy][ddx] = d1[ddy][ddx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    float sc[8], sf[8], A[8], B[8], C[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = scale[cq * 8 + e];
+      sf[e] = shift[cq * 8 + e];
+      A[e] = coef[cq * 8 + e];
+      B[e] = coef[c + cq * 8 + e];
+      C[e] = coef[2 * c + cq * 8 + e];
+    }
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+      for (int px = 0; px < 2; ++px) {
+        const int iy = 2 * k + py, ix = 2 * l + px;
+        if (iy >= h || ix >= w) continue;
+        const long pix = ((long)nn * h + iy) * w + ix;
+        const uint4 yw = reinterpret_cast<const uint4*>(y)[pix * c8 + cq];
+        const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
+        float v[8], g[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] = __uint_as_float(yu[e] << 16);
+          v[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+        for (int ddy = 0; ddy < 2; ++ddy)
+#pragma unroll
+          for (int ddx = 0; ddx < 2; ++ddx) {
+            if (ddy > py || ddx > px || !pin[ddy][ddx]) continue;
+            const uint32_t id = (uint32_t)((py + 1 - 2 * ddy) * 3 + (px + 1 - 2 * ddx));
+            const float dv[8] = {d0[ddy][ddx].x, d0[ddy][ddx].y, d0[ddy][ddx].z, d0[ddy][ddx].w,
+                                 d1[ddy][ddx].x, d1[ddy][ddx].y, d1[ddy][ddx].z, d1[ddy][ddx].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t ab = ((e < 4 ? a[ddy][ddx].x : a[ddy][ddx].y) >> (8 * (e & 3))) & 0xffu;
+              if (ab == id) g[e] += dv[e];
+            }
+          }
+        uint32_t ow[4];
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          float o[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int e = 2 * e2 + t;
+            const float gm = fmaf(v[e], sc[e], sf[e]) > 0.f ? g[e] : 0.f;
+            o[t] = fmaf(A[e], gm, fmaf(B[e], v[e], C[e]));
+          }
+          typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+          const bf16x2_t p = {(__bf16)o[0], (__bf16)o[1]};
+          ow[e2] = __builtin_bit_cast(uint32_t, p);
+        }
+        reinterpret_cast<uint4*>(dy)[pix * c8 + cq] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      }
+  }
+}
+
 int ew_blocks(long n4) {
   long b = (n4 + NT - 1) / NT;
   if (b > 2048 * 4) b = 2048 * 4;
@@ -1671,8 +1768,17 @@ TMR_API int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int 
   if (!(e8 && e8[0] == '0') && c % 8 == 0 && (c8 & (c8 - 1)) == 0 && n4 / 2 < 0x7fffffffL &&
       (((uintptr_t)dyp | (uintptr_t)y | (uintptr_t)dy) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
     const long n8 = n4 / 2;
-    hipLaunchKernelGGL(stem_bwd_apply8, dim3(ew_blocks(n8)), dim3(NT), 0, stream, pg, yb, scale,
-                       shift, coef, (__bf16*)dy, (int)n8, __builtin_ctz(c8));
+    const char* eq = getenv("TMR_STEM_QUAD");   // A/B switch (0: one pixel per thread)
+    const int qh = (h + 1) / 2, qw = (w + 1) / 2;
+    if (!(eq && eq[0] == '0')) {
+      const int nq = n * qh * qw * c8;
+      hipLaunchKernelGGL(stem_bwd_apply8q, dim3(ew_blocks(nq)), dim3(NT), 0, stream, pg, h, w,
+                         make_fastdiv((uint32_t)(qh * qw)), make_fastdiv((uint32_t)qw), yb, scale,
+                         shift, coef, (__bf16*)dy, nq, __builtin_ctz(c8));
+    } else {
+      hipLaunchKernelGGL(stem_bwd_apply8, dim3(ew_blocks(n8)), dim3(NT), 0, stream, pg, yb, scale,
+                         shift, coef, (__bf16*)dy, (int)n8, __builtin_ctz(c8));
+    }
   } else {
     hipLaunchKernelGGL((stem_bwd_apply<__bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg,
                        yb, scale, shift, coef, (__bf16*)dy, n4, c / 4);
