@@ -1,13 +1,14 @@
 # one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
-# final build, part 1: GPU test suite + smoke, then PMC traffic records of C2 (fp32), C4 and C5 (bf16)
+# final build, part 2: the bench lines (traffic from profiles/r4/) and rocprofv3 kernel stats
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4h_gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/r4h_gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4h_smoke.log 2>&1 || { tail -3 gpurun_out/r4h_smoke.log; exit 9; }
-tail -1 gpurun_out/r4h_smoke.log
-PROF_NAME=r4h_pmc_c2 MODEL=resnet50 PRECISION=fp32 SEQ=10 LFB=40 bash scripts/pmc.sh > gpurun_out/r4h_pmc_c2.txt 2>&1 || { tail -5 gpurun_out/r4h_pmc_c2.txt; exit 2; }
-echo c2 done
-PROF_NAME=r4h_pmc_c4 MODEL=resnest50 PRECISION=bf16 SEQ=10 LFB=40 bash scripts/pmc.sh > gpurun_out/r4h_pmc_c4.txt 2>&1 || { tail -5 gpurun_out/r4h_pmc_c4.txt; exit 3; }
-echo c4 done
-PROF_NAME=r4h_pmc_c5 MODEL=resnet50 PRECISION=bf16 SEQ=30 LFB=300 bash scripts/pmc.sh > gpurun_out/r4h_pmc_c5.txt 2>&1 || { tail -5 gpurun_out/r4h_pmc_c5.txt; exit 4; }
-echo c5 done
+O=gpurun_out/r4h; mkdir -p $O
+timeout -k 10 600 python bench.py > $O/bench_c2_default.json 2> $O/bench_c2_default.err || exit 2
+cat $O/bench_c2_default.json
+timeout -k 10 300 python bench.py --steps 20 --precision bf16 --model resnest50 --seq 10 --lfb 40 --no-cpu-baseline --conv-table > $O/bench_c4.json 2> $O/bench_c4.err || exit 3
+timeout -k 10 400 python bench.py --steps 20 --precision bf16 --seq 30 --lfb 300 --no-cpu-baseline --conv-table > $O/bench_c5.json 2> $O/bench_c5.err || exit 4
+for c in c4 c5; do python -c "import json;d=json.load(open('$O/bench_$c.json'));r=d['roofline'];print('$c', d['value'], d['ms_per_step'], r.get('traffic'), r.get('traffic_stale'), r.get('frac'))"; done
+PROF_NAME=r4h_prof_c2 STEPS=3 BENCH_ARGS="" bash scripts/profile.sh > $O/prof_c2.txt 2>&1 || exit 5
+PROF_NAME=r4h_prof_c4 STEPS=3 BENCH_ARGS="--precision bf16 --model resnest50 --seq 10 --lfb 40" bash scripts/profile.sh > $O/prof_c4.txt 2>&1 || exit 6
+PROF_NAME=r4h_prof_c5 STEPS=3 BENCH_ARGS="--precision bf16 --seq 30 --lfb 300" bash scripts/profile.sh > $O/prof_c5.txt 2>&1 || exit 7
+echo profiles done
