@@ -823,9 +823,17 @@ TMR_API size_t tmr_conv2d_wgrad_ws_bytes(const tmr_conv_desc* d) {
   if (ngroups(d) > 1 && group_split(d, g)) return 0;   // one group's workspace, reused in turn
   int sp, kc;
   long slab;
-  const tmr_conv_desc c = chunk_desc(&g, frames_per_launch(&g));   // the largest chunk
+  // the plans of the two chunk sizes a launch runs (the largest, and the remainder): a smaller
+  // chunk can keep more splits (its chunk length rounds up less)
+  const int fc = frames_per_launch(&g);
+  const tmr_conv_desc c = chunk_desc(&g, fc < g.n ? fc : g.n);
   wgrad_plan(&c, &sp, &kc, &slab);
   size_t bytes = (size_t)sp * slab * sizeof(float);
+  if (g.n > fc && g.n % fc != 0) {
+    const tmr_conv_desc cr = chunk_desc(&g, g.n % fc);
+    wgrad_plan(&cr, &sp, &kc, &slab);
+    if ((size_t)sp * slab * sizeof(float) > bytes) bytes = (size_t)sp * slab * sizeof(float);
+  }
   if (stem_geometry(d) && bytes < (size_t)kStemSlabs * kStemSlab * sizeof(float))
     bytes = (size_t)kStemSlabs * kStemSlab * sizeof(float);
   if (stem16_wgrad_geometry(d) && bytes < (size_t)kStem16Slabs * kStemSlab * sizeof(float))
