@@ -1,16 +1,13 @@
 # one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
-# wgrad split-K target sweep (TMR_WGRAD_TARGET) after the workspace-query fix
+# final build, part 2: the bench lines (traffic from profiles/r4/) and rocprofv3 kernel stats
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r4h_wgt; mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_bf16_gpu.py -k "wgrad or conv" > $O/t.log 2>&1; rc=$?; tail -1 $O/t.log; [ $rc -eq 0 ] || exit $rc
-for t in 512 768 1024 512 768 1024; do
-  TMR_WGRAD_TARGET=$t timeout -k 10 300 python bench.py --steps 10 --precision bf16 --seq 30 --lfb 300 --no-cpu-baseline > $O/c5_$t.json 2> $O/c5_$t.err || exit 4
-  python -c "import json;d=json.load(open('$O/c5_$t.json'));print('c5 target $t', d['value'], d['ms_per_step'], d['roofline']['per_kind']['conv_wgrad_bf16']['ms'])"
-done
-for t in 512 768 1024; do
-  TMR_WGRAD_TARGET=$t timeout -k 10 300 python bench.py --steps 10 --precision bf16 --model resnest50 --seq 10 --lfb 40 --no-cpu-baseline > $O/c4_$t.json 2> $O/c4_$t.err || exit 3
-  python -c "import json;d=json.load(open('$O/c4_$t.json'));print('c4 target $t', d['value'], d['ms_per_step'])"
-  TMR_WGRAD_TARGET=$t timeout -k 10 300 python bench.py --steps 10 --no-cpu-baseline > $O/c2_$t.json 2> $O/c2_$t.err || exit 2
-  python -c "import json;d=json.load(open('$O/c2_$t.json'));print('c2 target $t', d['value'], d['ms_per_step'])"
-done
+O=gpurun_out/r4i; mkdir -p $O
+timeout -k 10 600 python bench.py > $O/bench_c2_default.json 2> $O/bench_c2_default.err || exit 2
+timeout -k 10 300 python bench.py --steps 20 --precision bf16 --model resnest50 --seq 10 --lfb 40 --no-cpu-baseline --conv-table > $O/bench_c4.json 2> $O/bench_c4.err || exit 3
+timeout -k 10 400 python bench.py --steps 20 --precision bf16 --seq 30 --lfb 300 --no-cpu-baseline --conv-table > $O/bench_c5.json 2> $O/bench_c5.err || exit 4
+for c in c2_default c4 c5; do python -c "import json;d=json.load(open('$O/bench_$c.json'));r=d['roofline'];print('$c', d['value'], d['ms_per_step'], r.get('build_sha'), r.get('traffic_stale'), r.get('frac'), (d.get('cpu_baseline') or {}).get('value'))"; done
+PROF_NAME=r4i_prof_c2 STEPS=3 BENCH_ARGS="" bash scripts/profile.sh > $O/prof_c2.txt 2>&1 || exit 5
+PROF_NAME=r4i_prof_c4 STEPS=3 BENCH_ARGS="--precision bf16 --model resnest50 --seq 10 --lfb 40" bash scripts/profile.sh > $O/prof_c4.txt 2>&1 || exit 6
+PROF_NAME=r4i_prof_c5 STEPS=3 BENCH_ARGS="--precision bf16 --seq 30 --lfb 300" bash scripts/profile.sh > $O/prof_c5.txt 2>&1 || exit 7
+echo profiles done
