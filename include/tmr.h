@@ -87,7 +87,13 @@ typedef struct tmr_conv_desc {
                               stream's gradient of the bf16 train step) */
 #define TMR_IO_WT_BF16 8   /* dgrad only: w is the transposed bf16 weight copy Wt[Cin][R][S][Cout]
                               (tmr_weight_oihw_to_crsk_x), read K-contiguous by the LDS-DMA engine */
-#define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the one io bit fp32 math takes): w is the
+#define TMR_IO_ENGINE 256  /* any math: run the implicit-GEMM engine even where a direct kernel
+                              serves the geometry (the 7x7 stems, stem.hip / stem16.hip; the narrow
+                              3x3 convs, direct3.hip) -- the independent second implementation the
+                              tests compare those kernels with.  Changes the fp32 summation order
+                              only. */
+#define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the io bits fp32 math takes: this one and
+                              TMR_IO_ENGINE): w is the
                               transposed fp32 copy Wt[Cin][R][S][Cout] (tmr_weight_oihw_to_crsk_x,
                               out_bf16 0); the fp32 LDS-DMA engine reads it K-contiguous.  dy, dx
                               16-B aligned, Cin a multiple of 4 */

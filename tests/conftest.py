@@ -19,3 +19,18 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no GPU is visible")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def engine():
+    """engine.use(True): the convs of this test (thread) run on the implicit-GEMM engine also where
+    a direct kernel serves the geometry (ops.engine_only, TMR_IO_ENGINE); use(False): the product
+    routing.  Reset when the test ends."""
+    from tmrnet_amd import ops
+
+    class _Switch:
+        def use(self, on):
+            ops._TLS.engine = bool(on)
+
+    yield _Switch()
+    ops._TLS.engine = False

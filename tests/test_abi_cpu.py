@@ -109,7 +109,7 @@ def test_argument_errors_raise_with_message(built):
 
 def test_stem_entry_points_host_checks(built):
     """The direct stem's host-side contract (no GPU work): the wgrad workspace query covers the
-    direct kernel's 512 partial slabs at the stem geometry (with or without TMR_STEM_DIRECT), and
+    direct kernel's 512 partial slabs at the stem geometry (direct or on the engine), and
     the fused stem entries refuse other geometries / null operands before any launch."""
     import ctypes
     from tmrnet_amd import _lib, ops
@@ -118,3 +118,16 @@ def test_stem_entry_points_host_checks(built):
     # the bf16 stem's (stem16.hip) slabs: 768 persistent workgroups
     d16 = ops.conv_desc(640, 224, 224, 4, 64, 7, 7, 2, 3, math="bf16", io=ops.IO_DY)
     assert _lib.query("tmr_conv2d_wgrad_ws_bytes", ctypes.byref(d16)) >= 768 * 64 * 49 * 4 * 4
+
+
+def test_grouped_bf16_accumulating_dgrad_rejected():
+    """A grouped fused dgrad cannot accumulate (beta != 0) into a bf16 gradient: the
+    wrapper raises before any library call (the C entry point rejects it too, gemm_conv.hip)."""
+    import torch
+    from tmrnet_amd import ops
+    dy = torch.zeros(1, 4, 4, 16, dtype=torch.bfloat16)
+    y = torch.zeros(1, 4, 4, 16, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="grouped dgrad accumulates"):
+        ops.conv_dgrad_bnbwd(dy, torch.zeros(16, 3, 3, 8), (4, 4), 1, 1, y, torch.zeros(16), 2,
+                             scale=torch.ones(16), shift=torch.zeros(16), out=y, beta=1.0,
+                             math="bf16", wt=True, groups=2, g16=True)

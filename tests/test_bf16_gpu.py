@@ -173,15 +173,15 @@ def test_conv_bf16_all_resnet50_shapes(dev):
 
 
 @pytest.mark.parametrize("backbone,time_conv", [("resnet50", False)])
-def test_bf16_storage_bit_identical(dev, monkeypatch, backbone, time_conv):
+def test_bf16_storage_bit_identical(dev, monkeypatch, backbone, time_conv, engine):
     """bf16 storage of the conv-operand-only tensors (KRSC weights, non-residual BN+ReLU outputs,
     BatchNorm-backward outputs; tmr_conv_desc.io) against fp32 storage of the same bf16-math
     step: the convs round those operands to bf16 (RNE) either way, so the logits, every
     gradient and the running statistics are bit-identical.  On the implicit-GEMM engine: the
     direct 3x3 kernels (direct3.hip) take only all-bf16 operands, a different summation order
-    (tested against float64 and the engine in tests/test_direct3_gpu.py), so TMR_DIRECT3=0 here."""
+    (tested against float64 and the engine in tests/test_direct3_gpu.py), so ops.engine_only here."""
     from tmrnet_amd import trunk
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     B, T, L = 2, 5, 7
     frames, off, lt, labels = _inputs(B, T, L, seed=51)
     res = {}
@@ -314,11 +314,6 @@ def test_gemm16_views(dev, case, monkeypatch):
     if not xoff:   # bf16 output (TMR_IO_Y_BF16): the rounded accumulators, BN partials of those
         yb, stb, npb = ops.conv_fwd_bnstats(x16, w16, st, pad, math="bf16", y16=True)
         assert yb.dtype == torch.bfloat16 and torch.equal(yb, y32.to(torch.bfloat16))
-        # the whole-line store form (default) and the 64-B pair form write the same bytes
-        monkeypatch.setenv("TMR_C16W", "0")
-        yp, stp, _ = ops.conv_fwd_bnstats(x16, w16, st, pad, math="bf16", y16=True)
-        monkeypatch.delenv("TMR_C16W")
-        assert torch.equal(yp.view(torch.int16), yb.view(torch.int16)) and torch.equal(stp, stb)
         c = yb.shape[-1]
         mean, inv, _, _ = ops.bn_finalize(stb, npb, torch.ones(c, device=dev),
                                           torch.zeros(c, device=dev), torch.zeros(c, device=dev),
@@ -351,31 +346,26 @@ def test_gemm16_views(dev, case, monkeypatch):
     (3, 7, 7, 32, 96, 1),      # N = 96: a partial 64-column wave block
     (2, 12, 12, 64, 512, 2),   # strided
 ])
-def test_gemm16_y16_store_forms(dev, case, monkeypatch):
-    """bf16 y (TMR_IO_Y_BF16): the whole-line store form of epilogue_batched (default) writes the
-    same bytes as the 64-B pair form (TMR_C16W=0) and as the fp32 output rounded to bf16, with
-    the same BN partials, including ragged M and N; the one-stage form of the one-k-tile forwards
-    (gemm16_kernel NST) the same as the two-stage form (TMR_NST1=0)."""
+def test_gemm16_y16_store_forms(dev, case):
+    """bf16 y (TMR_IO_Y_BF16): the whole-line store form of epilogue_batched (the pair form on
+    tiles with an odd number of 32-column blocks) writes the same bytes as the fp32 output rounded
+    to bf16, including ragged M and N and the one-stage (gemm16_kernel NST = 1) one-k-tile
+    forwards; its BN statistics are those of the stored values (float64)."""
     n, h, w, cin, cout, st = case
     g = torch.Generator().manual_seed(5 + cin + cout)
     wt = _r(torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5)
     x16 = _r(torch.randn(n, h, w, cin, generator=g)).to(dev).to(torch.bfloat16)
     w16 = ops.weight_to_krsc(wt.to(dev), bf16=True)
     y32, st32, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16")
-    yb, stb, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
-    monkeypatch.setenv("TMR_C16W", "0")
-    yp, stp, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
-    monkeypatch.delenv("TMR_C16W")
+    yb, stb, npb = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
     assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
-    assert torch.equal(yp.view(torch.int16), yb.view(torch.int16)) and torch.equal(stp, stb)
-    # the one-stage forms of the one-k-tile launches (K = 64: the 4-wave tiles, and 256x128 for
-    # what the tile rules make 256x256) vs the two-stage launches
-    monkeypatch.setenv("TMR_NST1", "0")
-    monkeypatch.setenv("TMR_NST1W", "0")
-    y2, st2, _ = ops.conv_fwd_bnstats(x16, w16, st, 0, math="bf16", y16=True)
-    monkeypatch.delenv("TMR_NST1")
-    monkeypatch.delenv("TMR_NST1W")
-    assert torch.equal(y2.view(torch.int16), yb.view(torch.int16)) and torch.equal(st2, stb)
+    c = yb.shape[-1]
+    one, zero = torch.ones(c, device=dev), torch.zeros(c, device=dev)
+    mean, inv, _, _ = ops.bn_finalize(stb, npb, one, zero, zero.clone(), one.clone(), 0.1, 1e-5)
+    ye = yb.double().reshape(-1, c)
+    assert torch.allclose(mean.double(), ye.mean(0), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(1.0 / inv.double() ** 2 - 1e-5, ye.var(0, unbiased=False), rtol=1e-4,
+                          atol=1e-6)
 
 
 def test_bf16_full16_step(dev):

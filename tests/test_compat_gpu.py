@@ -107,3 +107,46 @@ def test_models_resnet_lstm_step(dev, opt):
             bound = 1e-5 * exp.abs() + 2.0 ** -22 * p0[n].abs() + 1e-12
             assert ((upd[n] - exp).abs() <= bound).all(), (n, (upd[n] - exp).abs().max().item())
 
+
+
+def test_models_resnet_lstm_threads(dev):
+    """One models.resnet_lstm instance driven from two threads at once with different clip
+    lengths (DataParallel calls its replicas from Python threads, SURVEY.md §8b Threading;
+    code/models.py:38-48): T comes from each call's 5-D input and is never written into the module,
+    so each thread's logits equal a single-threaded call's."""
+    import threading
+    models = _models_module()
+    args = NS(num_frames=10, opt=0, lr=5e-4, momentum=0.9, dampening=0, weightdecay=5e-4,
+              nesterov=False)
+    torch.manual_seed(31)
+    m = models.resnet_lstm(args, 7).to(dev).eval()
+    xs = {}
+    for B, T in ((2, 3), (1, 5)):
+        frames, off, _, _ = _inputs(B, T, 1, seed=32 + T)
+        xs[T] = ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224).to(dev)
+    with torch.no_grad():
+        solo = {T: m(x).cpu() for T, x in xs.items()}
+    got, errs = {}, []
+    barrier = threading.Barrier(len(xs))
+
+    def run(T):
+        try:
+            barrier.wait()
+            with torch.no_grad():
+                for _ in range(3):
+                    o = m(xs[T])
+                    torch.cuda.current_stream().synchronize()
+                    got.setdefault(T, []).append(o.cpu())
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errs.append(e)
+    th = [threading.Thread(target=run, args=(T,)) for T in xs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert m.seq_len == 10
+    for T, outs in got.items():
+        assert len(outs) == 3
+        for o in outs:
+            assert o.shape == solo[T].shape and torch.equal(o, solo[T]), T

@@ -1,7 +1,7 @@
 """The direct 3x3 stride-1 kernels of the bf16 step's narrow 112x112 convs (direct3.hip: ResNeSt-50's
 deep-stem 32 -> 32 and 32 -> 64 convs, third-party resnest50() at
 train_non-local_mutiConv_resnest.py:210) against float64 of the same bf16 operands and against the
-implicit-GEMM engine (TMR_DIRECT3=0).
+implicit-GEMM engine (ops.engine_only, TMR_IO_ENGINE).
 
 Sixteen frames = 1792 output rows over 512-768 persistent workgroups: each takes a contiguous range
 of 2-4 rows, so the input-row ring is reused within a range, ranges cross frame boundaries (the
@@ -39,7 +39,7 @@ def _ulp_bound(y, ref, k=1.0):
 
 
 @pytest.mark.parametrize("cout", [32, 64])
-def test_direct3_fwd_bnstats(dev, monkeypatch, cout):
+def test_direct3_fwd_bnstats(dev, monkeypatch, cout, engine):
     """y = conv(x) stored bf16: within one bf16 ulp of float64 of the bf16 operands (plus the fp32
     accumulation floor), within two of the engine; BatchNorm statistics of the stored values."""
     g = torch.Generator().manual_seed(40 + cout)
@@ -47,9 +47,9 @@ def test_direct3_fwd_bnstats(dev, monkeypatch, cout):
     w = _bf(torch.randn(cout, 32, 3, 3, generator=g) / np.sqrt(288))
     xd = x.to(dev)
     wk = ops.weight_to_krsc(w.float().to(dev).contiguous(), bf16=True)
-    monkeypatch.setenv("TMR_DIRECT3", "1")
+    engine.use(False)
     y, stats, nparts = ops.conv_fwd_bnstats(xd, wk, 1, 1, math="bf16", y16=True)
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     y0, st0, np0 = ops.conv_fwd_bnstats(xd, wk, 1, 1, math="bf16", y16=True)
     torch.cuda.synchronize()
     assert y.dtype == torch.bfloat16 and tuple(y.shape) == (N, 112, 112, cout)
@@ -67,7 +67,7 @@ def test_direct3_fwd_bnstats(dev, monkeypatch, cout):
 
 @pytest.mark.parametrize("cout", [32, 64])
 @pytest.mark.parametrize("mask,beta", [(2, 0.0), (1, 0.0), (0, 1.0)])
-def test_direct3_dgrad_bnbwd(dev, monkeypatch, cout, mask, beta):
+def test_direct3_dgrad_bnbwd(dev, monkeypatch, cout, mask, beta, engine):
     """dx = conv_transpose(dy) on the transposed bf16 weights, masked by the previous unit's ReLU
     (mask 1: z > 0, 2: y * scale + shift > 0; 0: none, with beta * old dx), and the partial sums
     sum(g), sum(g * (y - mean)) per channel: against float64 and against the engine."""
@@ -85,7 +85,7 @@ def test_direct3_dgrad_bnbwd(dev, monkeypatch, cout, mask, beta):
                 beta=beta, math="bf16", wt=True)
     outs = []
     for direct in ("1", "0"):
-        monkeypatch.setenv("TMR_DIRECT3", direct)
+        engine.use(direct == "0")
         dx, parts, nparts = ops.conv_dgrad_bnbwd(dy.to(dev), wt, (112, 112), 1, 1, y.to(dev),
                                                  mean.to(dev), mask, out=old.to(dev).clone(), **args)
         outs.append((dx, parts[:nparts].double().sum(0).cpu(), nparts))
@@ -107,7 +107,7 @@ def test_direct3_dgrad_bnbwd(dev, monkeypatch, cout, mask, beta):
 
 
 @pytest.mark.parametrize("cout", [32, 64])
-def test_direct3_wgrad(dev, monkeypatch, cout):
+def test_direct3_wgrad(dev, monkeypatch, cout, engine):
     """dW = sum over pixels of dy^T x per tap (ds_read_b64_tr_b16 fragments of both [pixel][channel]
     rows, slabs reduced in a fixed order): against float64 of the bf16 operands, with beta
     accumulation, and against the engine."""
@@ -117,18 +117,18 @@ def test_direct3_wgrad(dev, monkeypatch, cout):
     ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (cout, 32, 3, 3),
                                       dy.permute(0, 3, 1, 2).double(), padding=1)
     xd, dyd = x.to(dev), dy.to(dev)
-    monkeypatch.setenv("TMR_DIRECT3", "1")
+    engine.use(False)
     dw = ops.conv_wgrad(xd, dyd, 3, 3, 1, 1, math="bf16")
     prev = torch.randn(cout, 32, 3, 3, generator=g).to(dev)
     acc = ops.conv_wgrad(xd, dyd, 3, 3, 1, 1, math="bf16", out=prev.clone(), beta=0.5)
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     dw0 = ops.conv_wgrad(xd, dyd, 3, 3, 1, 1, math="bf16")
     torch.cuda.synchronize()
     assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
     assert rel_err(acc, 0.5 * prev.double().cpu() + ref) < 2e-6
 
 
-def test_direct3_small_frames(dev, monkeypatch):
+def test_direct3_small_frames(dev, monkeypatch, engine):
     """Fewer rows than workgroups (one 112-row frame: every workgroup one row, no reuse) and a
     short frame height (h = 5: every row range touches a frame edge)."""
     g = torch.Generator().manual_seed(70)
@@ -136,7 +136,7 @@ def test_direct3_small_frames(dev, monkeypatch):
         x = _bf(torch.randn(n, hh, 112, 32, generator=g))
         w = _bf(torch.randn(64, 32, 3, 3, generator=g) / np.sqrt(288))
         wk = ops.weight_to_krsc(w.float().to(dev).contiguous(), bf16=True)
-        monkeypatch.setenv("TMR_DIRECT3", "1")
+        engine.use(False)
         y, stats, nparts = ops.conv_fwd_bnstats(x.to(dev), wk, 1, 1, math="bf16", y16=True)
         dy = _bf(torch.randn(n, hh, 112, 64, generator=g))
         dw = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16")
@@ -149,7 +149,7 @@ def test_direct3_small_frames(dev, monkeypatch):
         assert rel_err(dw, rw) < 2e-6
 
 
-def test_direct3_stem_fwd_bnstats(dev, monkeypatch):
+def test_direct3_stem_fwd_bnstats(dev, monkeypatch, engine):
     """The deep stem's first conv (3x3/2, 3 -> 32) from the NHWC4 fp32 frames, 3 channels packed
     per column: within one bf16 ulp of float64 of the bf16-rounded operands, within two of the
     LDS-DMA engine on the NHWC8 copy; BatchNorm statistics of the stored values."""
@@ -158,9 +158,9 @@ def test_direct3_stem_fwd_bnstats(dev, monkeypatch):
     w = torch.randn(32, 3, 3, 3, generator=g) / np.sqrt(27)
     x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
     wk4 = ops.weight_to_krsc(w.to(dev).contiguous(), cpad=4, bf16=True)
-    monkeypatch.setenv("TMR_DIRECT3", "1")
+    engine.use(False)
     y, stats, nparts = ops.conv_fwd_bnstats(x4, wk4, 2, 1, c_real=3, math="bf16", y16=True)
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     x8 = ops.nhwc4_to_bf16x8(x4)
     wk8 = ops.weight_to_krsc(w.to(dev).contiguous(), cpad=8, bf16=True)
     y0, _, _ = ops.conv_fwd_bnstats(x8, wk8, 2, 1, c_real=3, math="bf16", y16=True)
@@ -178,7 +178,7 @@ def test_direct3_stem_fwd_bnstats(dev, monkeypatch):
     assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
 
 
-def test_direct3_stem_wgrad(dev, monkeypatch):
+def test_direct3_stem_wgrad(dev, monkeypatch, engine):
     """Its weight gradient (per input row im2col columns transposed in LDS, dy by transposed reads):
     against float64 of the bf16 operands, with beta accumulation, and against the engine."""
     g = torch.Generator().manual_seed(81)
@@ -187,12 +187,12 @@ def test_direct3_stem_wgrad(dev, monkeypatch):
     x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
     ref = torch.nn.grad.conv2d_weight(_bf(x).double(), (32, 3, 3, 3),
                                       dy.permute(0, 3, 1, 2).double(), stride=2, padding=1)
-    monkeypatch.setenv("TMR_DIRECT3", "1")
+    engine.use(False)
     dw = ops.conv_wgrad(x4, dy.to(dev), 3, 3, 2, 1, c_real=3, math="bf16")
     prev = torch.randn(32, 3, 3, 3, generator=g).to(dev)
     acc = ops.conv_wgrad(x4, dy.to(dev), 3, 3, 2, 1, c_real=3, math="bf16", out=prev.clone(),
                          beta=0.5)
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     dw0 = ops.conv_wgrad(x4, dy.to(dev), 3, 3, 2, 1, c_real=3, math="bf16")
     torch.cuda.synchronize()
     assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
@@ -202,16 +202,16 @@ def test_direct3_stem_wgrad(dev, monkeypatch):
 W56 = 8   # frames of the 56x56 cases: 448 rows over 384-512 workgroups (ranges of 1-2 rows)
 
 
-def test_direct3_w56_fwd_bnstats(dev, monkeypatch):
+def test_direct3_w56_fwd_bnstats(dev, monkeypatch, engine):
     """ResNet-50 layer1's 3x3 64 -> 64 conv at 56x56 (C5, bf16): 3.5 m-tiles of 16 pixels per row
     (the last half empty: zeros, not counted in the statistics)."""
     g = torch.Generator().manual_seed(90)
     x = _bf(torch.relu(torch.randn(W56, 56, 56, 64, generator=g)))
     w = _bf(torch.randn(64, 64, 3, 3, generator=g) / np.sqrt(576))
     wk = ops.weight_to_krsc(w.float().to(dev).contiguous(), bf16=True)
-    monkeypatch.setenv("TMR_DIRECT3", "1")
+    engine.use(False)
     y, stats, nparts = ops.conv_fwd_bnstats(x.to(dev), wk, 1, 1, math="bf16", y16=True)
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     y0, _, np0 = ops.conv_fwd_bnstats(x.to(dev), wk, 1, 1, math="bf16", y16=True)
     torch.cuda.synchronize()
     assert nparts == min(W56 * 56, 768) and np0 != nparts
@@ -227,7 +227,7 @@ def test_direct3_w56_fwd_bnstats(dev, monkeypatch):
 
 @pytest.mark.parametrize("g16,mask,beta", [(True, 2, 0.0), (False, 2, 0.0), (False, 1, 0.0),
                                            (False, 0, 1.0)])
-def test_direct3_w56_dgrad_bnbwd(dev, monkeypatch, g16, mask, beta):
+def test_direct3_w56_dgrad_bnbwd(dev, monkeypatch, g16, mask, beta, engine):
     """Its dgrad with the fused BatchNorm backward of bn1; g16: the masked gradient stored bf16
     (TMR_IO_G16, the C5 step's contract) with the partial sums of the stored values."""
     g = torch.Generator().manual_seed(91 + mask)
@@ -242,7 +242,7 @@ def test_direct3_w56_dgrad_bnbwd(dev, monkeypatch, g16, mask, beta):
     wt = ops.weight_to_crsk(w.float().to(dev).contiguous())
     outs = []
     for direct in ("1", "0"):
-        monkeypatch.setenv("TMR_DIRECT3", direct)
+        engine.use(direct == "0")
         dx, parts, nparts = ops.conv_dgrad_bnbwd(
             dy.to(dev), wt, (56, 56), 1, 1, y.to(dev), mean.to(dev), mask,
             z=z.to(dev) if mask == 1 else None, scale=scale.to(dev), shift=shift.to(dev),
@@ -268,18 +268,18 @@ def test_direct3_w56_dgrad_bnbwd(dev, monkeypatch, g16, mask, beta):
     assert rel_err(ps, ps0) < (2e-3 if g16 else 1e-5)
 
 
-def test_direct3_w56_wgrad(dev, monkeypatch):
+def test_direct3_w56_wgrad(dev, monkeypatch, engine):
     """Its weight gradient: K = 56 pixels per row padded to 64, 36 accumulator tiles per wave."""
     g = torch.Generator().manual_seed(93)
     x = _bf(torch.relu(torch.randn(W56, 56, 56, 64, generator=g)))
     dy = _bf(torch.randn(W56, 56, 56, 64, generator=g))
     ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (64, 64, 3, 3),
                                       dy.permute(0, 3, 1, 2).double(), padding=1)
-    monkeypatch.setenv("TMR_DIRECT3", "1")
+    engine.use(False)
     dw = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16")
     prev = torch.randn(64, 64, 3, 3, generator=g).to(dev)
     acc = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16", out=prev.clone(), beta=0.5)
-    monkeypatch.setenv("TMR_DIRECT3", "0")
+    engine.use(True)
     dw0 = ops.conv_wgrad(x.to(dev), dy.to(dev), 3, 3, 1, 1, math="bf16")
     torch.cuda.synchronize()
     assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6

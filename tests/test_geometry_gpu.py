@@ -186,6 +186,12 @@ def _geometry_step(dev, monkeypatch, B, T, L, prec, seeds, backbone="resnet50", 
                                                 "head_active": int(act.sum()),
                                                 "trunk_out_flips": _flips(blk_64, zlast),
                                                 "trunk_out_flips_cpu32": _flips(blk_r, zlast)})
+    if prec == "fp32":
+        # the forced active set must not hide a kernel regression: the elements it moves against
+        # float64 are at most twice those the fp32 CPU oracle's own rounding moves (82 vs 68
+        # measured, profiles/r4/geometry/)
+        f_hip, f_cpu = _flips(blk_64, zlast), _flips(blk_r, zlast)
+        assert f_hip <= 2 * f_cpu + 8, (f_hip, f_cpu)
     # the same scale-free bound as the gradients'
     assert e_hip <= GRAD_RATIO * e_cpu + 1e-5, (e_hip, e_cpu)
     top2 = out64.detach().topk(2, dim=1).values
@@ -375,3 +381,40 @@ def test_c4_full_step_properties(dev):
         o_rows = m(x4, LFBRows(bank, rows))
         o_dense = m(x4, ops.lfb_gather(bank, rows))
     assert torch.equal(o_rows, o_dense)
+
+
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_c2_full_logits_vs_oracle(dev, mode):
+    """The headline config's logits at full size (BASELINE.json configs[1]: 64 clips x 10
+    frames, L=40, fp32) against the CPU oracle (train_only_non-local_pretrained.py:226-240) on
+    identical inputs: the bench's frames through the reference train transform on the device
+    (the NHWC4 result handed to the oracle as NCHW), LFB rows of §8d's bank (dense on the oracle
+    side), the same dropout masks.  Train mode normalises with batch statistics over all 640
+    frames; eval mode uses the running statistics that train-mode forward left (HIP's, loaded into
+    the oracle).  north_star: logits within 1e-4 absolute, identical argmax phase ids."""
+    from tests._bf16_grads import full_inputs, masks as mk_masks
+    B, T, L = 64, 10, 40
+    torch.manual_seed(0)
+    m = tmrnet_amd.resnet_lstm(seq_len=T).to(dev)
+    r = ref.TMRNetRef(seq_len=T)
+    r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    x4, lfb, labels = full_inputs(dev, B, T, L, "noise")
+    masks = mk_masks(B, 6)
+    m.nl_block.forced_mask = masks["nl"].to(dev)
+    m.forced_head_mask = masks["head"].to(dev)
+    x_ref = x4[..., :3].permute(0, 3, 1, 2).contiguous().cpu().view(B, T, 3, 224, 224)
+    lt = lfb.dense().cpu()
+    with torch.no_grad():
+        out = m.train()(x4, lfb)
+        if mode == "eval":
+            r.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+            out = m.eval()(x4, lfb)
+            out_r = r.eval()(x_ref, lt)
+        else:
+            out_r = r.train()(x_ref, lt, masks=masks)
+    o, o_r = out.cpu().double(), out_r.double()
+    err = (o - o_r).abs().max().item()
+    _record("c2_full_%s_logits" % mode, {"max_abs_diff": err, "max_abs_logit": o_r.abs().max().item(),
+                                         "argmax_equal": int((o.argmax(1) == o_r.argmax(1)).sum())})
+    assert err < 1e-4, err
+    assert torch.equal(o.argmax(1), o_r.argmax(1))

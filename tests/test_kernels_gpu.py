@@ -683,11 +683,11 @@ def test_bn_apply_relu_bits_bf16(dev, rows, c):
         assert n1 == n3 and torch.equal(d1, d3) and torch.equal(p1[:n1], p3[:n3])
 
 
-def test_stem_direct_fwd_bnstats(dev, monkeypatch):
+def test_stem_direct_fwd_bnstats(dev, monkeypatch, engine):
     """The fp32 7x7/2 stem with BatchNorm statistics as a direct convolution over its 147 real
     (tap, channel) pairs (stem.hip, the train step's 224x224 geometry) against float64: the
     output, and the BN statistics from its per-output-row partials; the implicit-GEMM engine
-    (TMR_STEM_DIRECT=0) agrees to fp32 summation order.  Six frames: 672 output rows, more than
+    (ops.engine_only, TMR_IO_ENGINE) agrees to fp32 summation order.  Six frames: 672 output rows, more than
     the persistent grid's 512 workgroups, so workgroups run the prefetched second row."""
     n = 6
     g = torch.Generator().manual_seed(12)
@@ -695,9 +695,9 @@ def test_stem_direct_fwd_bnstats(dev, monkeypatch):
     wt = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
     x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
     wk = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=4)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    engine.use(False)
     y, stats, nparts = ops.conv_fwd_bnstats(x4, wk, 2, 3, c_real=3)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    engine.use(True)
     y0, stats0, nparts0 = ops.conv_fwd_bnstats(x4, wk, 2, 3, c_real=3)
     torch.cuda.synchronize()
     assert nparts == 4 * 512 and tuple(y.shape) == (n, 112, 112, 64)   # merged per workgroup
@@ -712,13 +712,13 @@ def test_stem_direct_fwd_bnstats(dev, monkeypatch):
         assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
 
 
-def test_stem16_direct_fwd_bnstats(dev, monkeypatch):
+def test_stem16_direct_fwd_bnstats(dev, monkeypatch, engine):
     """The bf16-activation step's 7x7/2 stem as a direct convolution (stem16.hip: the NHWC4 fp32
     input rounded to bf16 in LDS, 147 real of 176 reduction rows on v_mfma_f32_32x32x16_bf16, y
     stored bf16, BatchNorm partials merged per workgroup) against float64 of the bf16-rounded
     operands (y within one bf16 rounding: the fp32 accumulation order decides ties), its
     statistics against float64 statistics of its own stored y, and the LDS-DMA engine on the
-    NHWC8 copy (TMR_STEM_DIRECT=0) within one bf16 ulp.  Sixteen frames: 1792 output rows over the
+    NHWC8 copy (ops.engine_only, TMR_IO_ENGINE) within one bf16 ulp.  Sixteen frames: 1792 output rows over the
     768 persistent workgroups, each a contiguous range of 2-3 rows (the input-row ring reused across
     a range, ranges crossing frame boundaries, statistics merged over a range)."""
     n = 16
@@ -727,9 +727,9 @@ def test_stem16_direct_fwd_bnstats(dev, monkeypatch):
     wt = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
     x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
     wk4 = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=4, bf16=True)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    engine.use(False)
     y, stats, nparts = ops.conv_fwd_bnstats(x4, wk4, 2, 3, c_real=3, math="bf16", y16=True)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    engine.use(True)
     x8 = ops.nhwc4_to_bf16x8(x4)
     wk8 = ops.weight_to_krsc(wt.to(dev).contiguous(), cpad=8, bf16=True)
     y0, _, _ = ops.conv_fwd_bnstats(x8, wk8, 2, 3, c_real=3, math="bf16", y16=True)
@@ -753,11 +753,11 @@ def test_stem16_direct_fwd_bnstats(dev, monkeypatch):
     assert rel_err(inv, 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5)) < 1e-5
 
 
-def test_stem16_direct_wgrad(dev, monkeypatch):
+def test_stem16_direct_wgrad(dev, monkeypatch, engine):
     """The bf16 stem's weight gradient as a direct convolution (stem16.hip: per-row im2col and
     transposed dy in LDS, bf16 MFMA, per-workgroup slabs summed by the tap reduction) against
     float64 of the bf16 operands, with beta accumulation, and against the engine
-    (TMR_STEM_DIRECT=0).  Sixteen frames: 1792 output rows over the 768 persistent workgroups
+    (ops.engine_only, TMR_IO_ENGINE).  Sixteen frames: 1792 output rows over the 768 persistent workgroups
     (contiguous ranges of 2-3 rows: the input-row ring reused, ranges crossing frames)."""
     n = 16
     g = torch.Generator().manual_seed(15)
@@ -767,11 +767,11 @@ def test_stem16_direct_wgrad(dev, monkeypatch):
     dyn = dy.to(dev).permute(0, 2, 3, 1).contiguous()
     ref = torch.nn.grad.conv2d_weight(x.to(torch.bfloat16).double(), (64, 3, 7, 7), dy.double(),
                                       stride=2, padding=3)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    engine.use(False)
     dw = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, math="bf16")
     prev = torch.randn(64, 3, 7, 7, generator=g).to(dev)
     acc = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, math="bf16", out=prev.clone(), beta=0.5)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    engine.use(True)
     dw0 = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, math="bf16")
     torch.cuda.synchronize()
     assert rel_err(dw, ref) < 2e-6 and rel_err(dw0, ref) < 2e-6
@@ -779,10 +779,10 @@ def test_stem16_direct_wgrad(dev, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_stem_direct_wgrad(dev, monkeypatch):
+def test_stem_direct_wgrad(dev, monkeypatch, engine):
     """The fp32 stem's weight gradient as a direct convolution (stem.hip: per-workgroup partial
     slabs over the 147 real (tap, channel) pairs, summed by the engine's tap reduction) against
-    float64, with beta accumulation, and against the implicit-GEMM engine (TMR_STEM_DIRECT=0).
+    float64, with beta accumulation, and against the implicit-GEMM engine (ops.engine_only, TMR_IO_ENGINE).
     Six frames: 672 output rows over the 512 persistent workgroups."""
     n = 6
     g = torch.Generator().manual_seed(13)
@@ -791,11 +791,11 @@ def test_stem_direct_wgrad(dev, monkeypatch):
     x4 = ops.nchw_to_nhwc(x.to(dev), cpad=4)
     dyn = dy.to(dev).permute(0, 2, 3, 1).contiguous()
     ref = torch.nn.grad.conv2d_weight(x.double(), (64, 3, 7, 7), dy.double(), stride=2, padding=3)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "1")
+    engine.use(False)
     dw = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3)
     prev = torch.randn(64, 3, 7, 7, generator=g).to(dev)
     acc = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3, out=prev.clone(), beta=0.5)
-    monkeypatch.setenv("TMR_STEM_DIRECT", "0")
+    engine.use(True)
     dw0 = ops.conv_wgrad(x4, dyn, 7, 7, 2, 3, c_real=3)
     torch.cuda.synchronize()
     assert tuple(dw.shape) == (64, 3, 7, 7)

@@ -158,10 +158,12 @@ def test_split_attention_bn_on_load(dev, n, h, w, C, bf16):
 
 
 @pytest.mark.parametrize("n,h,w,C", [(6, 56, 56, 64), (8, 7, 7, 512), (5, 5, 3, 32)])
-def test_split_attention_8wide_bit_identical(dev, monkeypatch, n, h, w, C):
+def test_split_attention_8wide_bit_identical(dev, n, h, w, C):
     """The 8-channel bf16 combine and backward apply (splat_combine_bn8_k, splat_bwd_apply_bn8_k:
-    both radix halves per thread, coefficients in registers) against the 4-wide forms
-    (TMR_SPLAT8=0): the same arithmetic per element, so out and dy bit-identical."""
+    both radix halves per thread, coefficients in registers) against the 4-wide forms (the same
+    y handed over 8 bytes off a 16-B boundary, which the 8-wide kernels do not take): the same
+    arithmetic per element, so out and dy bit-identical."""
+    from tests.test_stem_pool8_gpu import _off8
     from tmrnet_amd.resnest import SplAtConv2d, _splat_fwd, _splat_bwd
     torch.manual_seed(3 * C + h)
     md = SplAtConv2d(C, C).to(dev).train()
@@ -173,9 +175,9 @@ def test_split_attention_8wide_bit_identical(dev, monkeypatch, n, h, w, C):
                                          bn0.momentum, bn0.eps)
     r2 = {"y": y, "scale": sc, "shift": sh, "mean": mean, "inv": inv}
     outs, dys = [], []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("TMR_SPLAT8", flag)
-        out, spl = _splat_fwd(md, y, sc, sh, [])
+    for yy in (y, _off8(y)):
+        r2["y"] = yy
+        out, spl = _splat_fwd(md, yy, sc, sh, [])
         outs.append(out)
         dys.append(_splat_bwd(md, spl, r2, gy, {}))
     torch.cuda.synchronize()

@@ -1,15 +1,30 @@
-"""The 8-channel forms of the bf16 stem's maxpool forward (maxpool_fwd_bn8_a16, TMR_MAXPOOL8) and
-of its BatchNorm/maxpool backward apply (stem_bwd_apply8, TMR_STEM_BWD8) against the 4-channel
-forms they replace: bit-identical outputs, argmax and gradients, including ties (quantised
-inputs: the first maximum in scan order must win), odd spatial sizes (partial windows at the
-right / bottom edges) and a channel count that takes the 4-wide fallback.  The 4-wide forms are
-checked against the float64 oracle of the stem in tests/test_kernels_gpu.py / test_bf16_gpu.py."""
+"""The 8-channel forms of the bf16 stem's maxpool forward (maxpool_fwd_bn8_a16), of its
+BatchNorm/maxpool backward apply (stem_bwd_apply8q, per 2x2 input quad) and of the bf16 BN applies
+(bn_apply8_a16_k) against the 4-channel forms the library falls back to: the 8-wide kernels need
+16-B aligned tensors, so the same values handed over 8 bytes off a 16-B boundary take the 4-wide
+form (no environment switch).  Bit-identical outputs, argmax and gradients, including ties
+(quantised inputs: the first maximum in scan order must win), odd spatial sizes (partial windows
+at the right / bottom edges) and a channel count that takes the 4-wide form either way; plus
+float64 checks of the values."""
 import pytest
 import torch
 
 from tmrnet_amd import ops
 
 pytestmark = pytest.mark.gpu
+
+
+def _off8(t):
+    """A copy of t whose data starts 8 bytes past a 16-B boundary (contiguous, same values)."""
+    n = t.numel()
+    per = 8 // t.element_size()
+    buf = torch.empty(n + 2 * per, dtype=t.dtype, device=t.device)
+    base = (buf.data_ptr() // t.element_size()) % (16 // t.element_size())
+    start = (per - base) % (16 // t.element_size())
+    v = buf[start:start + n].view(t.shape)
+    v.copy_(t)
+    assert v.data_ptr() % 16 == 8 and v.is_contiguous()
+    return v
 
 
 def _stem_case(dev, n, h, w, c, seed):
@@ -22,23 +37,31 @@ def _stem_case(dev, n, h, w, c, seed):
 
 
 @pytest.mark.parametrize("shape", [(3, 112, 112, 64), (2, 13, 11, 16), (2, 9, 10, 24)])
-def test_maxpool_fwd_bn8_bit_identical(dev, shape, monkeypatch):
+def test_maxpool_fwd_bn8_bit_identical(dev, shape):
     y, scale, shift = _stem_case(dev, *shape, seed=sum(shape))
     p8, a8 = ops.maxpool_fwd_bn(y, scale, shift)
-    monkeypatch.setenv("TMR_MAXPOOL8", "0")
-    p4, a4 = ops.maxpool_fwd_bn(y, scale, shift)
-    monkeypatch.delenv("TMR_MAXPOOL8")
+    p4, a4 = ops.maxpool_fwd_bn(_off8(y), scale, shift)    # the 4-wide form
     assert torch.equal(p8.view(torch.int16), p4.view(torch.int16))
     assert torch.equal(a8, a4)
-    # and the values are relu(bn(y)) maxima of the windows, argmax inside the window
+    # the values are relu(bn(y)) maxima of the windows, argmax inside the window at a maximum
     z = torch.relu(y.float() * scale + shift)
     ref = torch.nn.functional.max_pool2d(z.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
     assert torch.equal(p8.float(), ref.to(torch.bfloat16).float())
     assert int(a8.max()) <= 8
+    n, h, w, c = shape
+    ho, wo = a8.shape[1], a8.shape[2]
+    zp = torch.nn.functional.pad(z.permute(0, 3, 1, 2), (1, 1, 1, 1), value=-1.0)
+    ids = a8.long().permute(0, 3, 1, 2)
+    oy = torch.arange(ho, device=dev).view(1, 1, ho, 1) * 2
+    ox = torch.arange(wo, device=dev).view(1, 1, 1, wo) * 2
+    nn_ = torch.arange(n, device=dev).view(n, 1, 1, 1).expand_as(ids)
+    cc = torch.arange(c, device=dev).view(1, c, 1, 1).expand_as(ids)
+    picked = zp[nn_, cc, oy + ids // 3, ox + ids % 3]
+    assert torch.equal(picked.to(torch.bfloat16).float(), ref.permute(0, 3, 1, 2).to(torch.bfloat16).float())
 
 
 @pytest.mark.parametrize("shape", [(3, 112, 112, 64), (2, 13, 11, 16), (2, 12, 9, 8), (2, 9, 10, 24)])
-def test_stem_bwd_apply8_bit_identical(dev, shape, monkeypatch):
+def test_stem_bwd_apply8_bit_identical(dev, shape):
     n, h, w, c = shape
     y, scale, shift = _stem_case(dev, *shape, seed=7 + sum(shape))
     _, am = ops.maxpool_fwd_bn(y, scale, shift)
@@ -49,15 +72,8 @@ def test_stem_bwd_apply8_bit_identical(dev, shape, monkeypatch):
     inv = 1.0 / (y.float().var((0, 1, 2), unbiased=False) + 1e-5).sqrt()
     gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
     d8, g8, b8 = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
-    # the per-pixel 8-channel form (TMR_STEM_QUAD=0) against the default 2x2-quad form
-    monkeypatch.setenv("TMR_STEM_QUAD", "0")
-    dp_, gp_, bp_ = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
-    monkeypatch.delenv("TMR_STEM_QUAD")
-    assert torch.equal(dp_.view(torch.int16), d8.view(torch.int16))
-    assert torch.equal(gp_, g8) and torch.equal(bp_, b8)
-    monkeypatch.setenv("TMR_STEM_BWD8", "0")
-    d4, g4, b4 = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
-    monkeypatch.delenv("TMR_STEM_BWD8")
+    # the 4-wide, one-pixel-per-thread form against the default 8-channel 2x2-quad form
+    d4, g4, b4 = ops.bn_bwd_maxpool(dyp, am, _off8(y), scale, shift, mean, inv, gamma)
     assert torch.equal(d8.view(torch.int16), d4.view(torch.int16))
     assert torch.equal(g8, g4) and torch.equal(b8, b4)
     # the maxpool gradient routed through argmax, masked by the stem ReLU, then the BN backward
@@ -78,25 +94,30 @@ def test_stem_bwd_apply8_bit_identical(dev, shape, monkeypatch):
     ref = gamma.double() * inv.double() * (dz - sdz / m - xh * sdx / m)
     err = (d8.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err    # bf16 output
+    assert torch.allclose(b8.double(), sdz, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(g8.double(), sdx, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("rows,c", [(3 * 56 * 56, 256), (1001, 64), (37, 24)])
-def test_bn_apply8_a16_bit_identical(dev, rows, c, monkeypatch):
+def test_bn_apply8_a16_bit_identical(dev, rows, c):
     """bf16 BN applies (relu(bn(y)), relu(bn(y) + residual), relu(bn(y) + bn_ds(y_ds))) 8 per
-    thread (bn_apply8_a16_k) vs the 4-wide forms (TMR_BN_APPLY8=0): identical bytes; c = 24 takes
-    the 4-wide form in both runs."""
+    thread (bn_apply8_a16_k) vs the 4-wide forms (misaligned operands): identical bytes; c = 24
+    takes the 4-wide form in both runs.  Values against float64 within one bf16 rounding."""
     g = torch.Generator().manual_seed(rows + c)
     mk = lambda: (torch.randn(rows, c, generator=g) * 2).to(torch.bfloat16).to(dev)
     y, r, yr = mk(), mk(), mk()
     sc, sf, rs, rf = [(torch.rand(c, generator=g) + 0.5).to(dev) for _ in range(4)]
     outs = {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("TMR_BN_APPLY8", v)
-        outs[v] = [ops.bn_apply(y, sc, sf), ops.bn_apply(y, sc, sf, residual=r),
-                   ops.bn_apply(y, sc, sf, residual=r, relu=False),
-                   ops.bn_apply2(y, sc, sf, yr, rs, rf), ops.bn_apply2(y, sc, sf, yr, rs, rf, relu=False)]
-    monkeypatch.delenv("TMR_BN_APPLY8")
-    for a, b in zip(outs["1"], outs["0"]):
+    for form, (yy, rr, yyr) in (("8", (y, r, yr)), ("4", (_off8(y), _off8(r), _off8(yr)))):
+        outs[form] = [ops.bn_apply(yy, sc, sf), ops.bn_apply(yy, sc, sf, residual=rr),
+                      ops.bn_apply(yy, sc, sf, residual=rr, relu=False),
+                      ops.bn_apply2(yy, sc, sf, yyr, rs, rf),
+                      ops.bn_apply2(yy, sc, sf, yyr, rs, rf, relu=False)]
+    for a, b in zip(outs["8"], outs["4"]):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
-    ref = torch.relu(y.double() * sc.double() + sf.double() + r.double())
-    assert torch.allclose(outs["1"][1].double(), ref, rtol=1e-2, atol=1e-2)   # one bf16 rounding
+    yd, rd, yrd = y.double(), r.double(), yr.double()
+    bn = yd * sc.double() + sf.double()
+    bnr = yrd * rs.double() + rf.double()
+    refs = [torch.relu(bn), torch.relu(bn + rd), bn + rd, torch.relu(bn + bnr), bn + bnr]
+    for got, ref in zip(outs["8"], refs):
+        assert torch.allclose(got.double(), ref, rtol=1e-2, atol=1e-2)   # one bf16 rounding

@@ -18,9 +18,9 @@ class resnet_lstm(MemoryBankModel):  # noqa: N801  (reference name)
         self.args = args
 
     def forward(self, x):
-        if x.dim() == 5:
-            self.seq_len = x.shape[1]
-        return super().forward(x)
+        # T from a 5-D (B,T,3,224,224) input, passed down per call: writing it into the module
+        # would race between threads driving one instance (SURVEY.md §8b Threading)
+        return super().forward(x, seq_len=x.shape[1] if x.dim() == 5 else None)
 
     def get_optimizers(self):
         """models.py:50-69: res at lr/10, lstm and fc at lr; opt 0 = SGD, 1 = Adam."""

@@ -882,89 +882,6 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const TY*
   }
 }
 
-// The bf16 form, 8 channels per thread (16-B y / dy pieces; 32 B of the pooled gradient and 8 B
-// of argmax per pooled output): the four pooled outputs whose windows may hold the pixel are all
-// loaded up front (the 4-wide form walks 1, 2 or 4 of them in a data-dependent loop, one
-// dependent load pair at a time); a candidate that coincides with another (even row or column) is
-// masked off.  The gradient sums run in maxpool_grad4's order -- (oy0, ox0), (oy0, ox1),
-// (oy1, ox0), (oy1, ox1) -- from 0, so the result is bit-identical to stem_bwd_apply.
-// 32-bit indices (rows * c / 8 < 2^31, checked on the host); c / 8 a power of two (lc8 = log2).
-__global__ __launch_bounds__(NT) void stem_bwd_apply8(const PoolGeo pg, const __bf16* __restrict__ y,
-                                                      const float* __restrict__ scale,
-                                                      const float* __restrict__ shift,
-                                                      const float* __restrict__ coef,
-                                                      __bf16* __restrict__ dy, int n8, int lc8) {
-  const int c8 = 1 << lc8, c = c8 * 8;
-  const uint2* am = reinterpret_cast<const uint2*>(pg.am);
-  const float4* dp = reinterpret_cast<const float4*>(pg.dyp);
-  for (int i = blockIdx.x * NT + threadIdx.x; i < n8; i += gridDim.x * NT) {
-    const int cq = i & (c8 - 1);
-    const uint32_t row = (uint32_t)i >> lc8;
-    const uint32_t nn = fdiv(row, pg.dHW);
-    const uint32_t rem = row - nn * pg.dHW.d;
-    const int iy = (int)fdiv(rem, pg.dW), ix = (int)(rem - (uint32_t)iy * pg.dW.d);
-    const int oy0 = iy >> 1, oy1 = min((iy + 1) >> 1, pg.ho - 1);
-    const int ox0 = ix >> 1, ox1 = min((ix + 1) >> 1, pg.wo - 1);
-    const int oys[2] = {oy0, oy1}, oxs[2] = {ox0, ox1};
-    const bool on[4] = {true, ox1 != ox0, oy1 != oy0, oy1 != oy0 && ox1 != ox0};
-    uint2 a[4];
-    float4 d0[4], d1[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      // (a coinciding candidate is not loaded: 2.25 of the 4 on average)
-      const int o = (((int)nn * pg.ho + oys[k >> 1]) * pg.wo + oxs[k & 1]) * c8 + cq;
-      if (on[k]) {
-        a[k] = am[o];
-        d0[k] = dp[2 * o];
-        d1[k] = dp[2 * o + 1];
-      } else {
-        a[k] = make_uint2(0xffffffffu, 0xffffffffu);
-        d0[k] = d1[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-    const uint4 yw = reinterpret_cast<const uint4*>(y)[i];
-    const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
-    float v[8], g[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[2 * e] = __uint_as_float(yu[e] << 16);
-      v[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t id = (uint32_t)((iy - (oys[k >> 1] * 2 - 1)) * 3 + (ix - (oxs[k & 1] * 2 - 1)));
-      const float dv[8] = {d0[k].x, d0[k].y, d0[k].z, d0[k].w, d1[k].x, d1[k].y, d1[k].z, d1[k].w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t ab = ((e < 4 ? a[k].x : a[k].y) >> (8 * (e & 3))) & 0xffu;
-        if (on[k] && ab == id) g[e] += dv[e];
-      }
-    }
-    uint32_t ow[4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cc = cq * 8 + 4 * h;
-      const float4 sc = *reinterpret_cast<const float4*>(scale + cc);
-      const float4 sf = *reinterpret_cast<const float4*>(shift + cc);
-      const float4 A = *reinterpret_cast<const float4*>(coef + cc);
-      const float4 B = *reinterpret_cast<const float4*>(coef + c + cc);
-      const float4 C = *reinterpret_cast<const float4*>(coef + 2 * c + cc);
-      const float4 gm = relu_mask4(make_float4(g[4 * h], g[4 * h + 1], g[4 * h + 2], g[4 * h + 3]),
-                                   affine4(make_float4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]), sc, sf));
-      const float o0 = fmaf(A.x, gm.x, fmaf(B.x, v[4 * h], C.x));
-      const float o1 = fmaf(A.y, gm.y, fmaf(B.y, v[4 * h + 1], C.y));
-      const float o2 = fmaf(A.z, gm.z, fmaf(B.z, v[4 * h + 2], C.z));
-      const float o3 = fmaf(A.w, gm.w, fmaf(B.w, v[4 * h + 3], C.w));
-      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-      const bf16x2_t p = {(__bf16)o0, (__bf16)o1}, q = {(__bf16)o2, (__bf16)o3};
-      ow[2 * h] = __builtin_bit_cast(uint32_t, p);
-      ow[2 * h + 1] = __builtin_bit_cast(uint32_t, q);
-    }
-    reinterpret_cast<uint4*>(dy)[i] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-  }
-}
 
 // The same per 2x2 quad of input pixels (rows 2k, 2k+1, columns 2l, 2l+1): the pooled outputs
 // (k .. k+1) x (l .. l+1) are the candidates of all four pixels, so each is loaded once per quad
@@ -1525,11 +1442,8 @@ TMR_API int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, con
 // here), the gradients dz / dres stay fp32, dy (a conv operand) is written bf16.  Same arithmetic
 // as the fp32 forms on the bf16 values.
 
-// the 8-wide bf16 applies: channels a multiple of 8, 16-B aligned tensors (TMR_BN_APPLY8=0: the
-// 4-wide forms, A/B; read per call)
+// the 8-wide bf16 applies: channels a multiple of 8, 16-B aligned tensors (else the 4-wide forms)
 static bool apply8_ok(int c, const void* y, const void* r, const void* z) {
-  const char* e = getenv("TMR_BN_APPLY8");
-  if (e && e[0] == '0') return false;
   return c % 8 == 0 && (((uintptr_t)y | (uintptr_t)r | (uintptr_t)z) & 15) == 0;
 }
 
@@ -1692,8 +1606,8 @@ TMR_API int tmr_bn_bwd_parts_a16(const float* g, const void* y, const void* part
                      dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
   const long n4 = (long)rows * c / 4;
-  const char* w8 = getenv("TMR_BN8");   // A/B switch (0: the 4-wide form)
-  if (!(w8 && w8[0] == '0') && c % 8 == 0 && (((uintptr_t)g | (uintptr_t)y | (uintptr_t)dy) & 15) == 0) {
+  // 8 per thread (else the 4-wide form)
+  if (c % 8 == 0 && (((uintptr_t)g | (uintptr_t)y | (uintptr_t)dy) & 15) == 0) {
     const long n8 = n4 / 2;
     hipLaunchKernelGGL(bn_bwd_apply8_a16<float>, dim3(ew_blocks(n8)), dim3(NT), 0, stream, g,
                        (const __bf16*)y, coef, (__bf16*)dy, n8, c / 8);
@@ -1763,22 +1677,16 @@ TMR_API int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int 
                      save_mean, save_invstd, gamma, dgamma, dbeta, coef);
   TMR_CHECK_LAUNCH("bn_bwd_final");
   const long n4 = rows_l * c / 4;
-  const char* e8 = getenv("TMR_STEM_BWD8");   // A/B switch (0: the 4-wide form)
   const int c8 = c / 8;
-  if (!(e8 && e8[0] == '0') && c % 8 == 0 && (c8 & (c8 - 1)) == 0 && n4 / 2 < 0x7fffffffL &&
+  // 8 channels per thread, per 2x2 input quad (its candidate pooled outputs gathered once; the
+  // per-pixel form it replaced in round 4 was bound by 2.25 gathers per pixel); else 4-wide
+  if (c % 8 == 0 && (c8 & (c8 - 1)) == 0 && n4 / 2 < 0x7fffffffL &&
       (((uintptr_t)dyp | (uintptr_t)y | (uintptr_t)dy) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
-    const long n8 = n4 / 2;
-    const char* eq = getenv("TMR_STEM_QUAD");   // A/B switch (0: one pixel per thread)
     const int qh = (h + 1) / 2, qw = (w + 1) / 2;
-    if (!(eq && eq[0] == '0')) {
-      const int nq = n * qh * qw * c8;
-      hipLaunchKernelGGL(stem_bwd_apply8q, dim3(ew_blocks(nq)), dim3(NT), 0, stream, pg, h, w,
-                         make_fastdiv((uint32_t)(qh * qw)), make_fastdiv((uint32_t)qw), yb, scale,
-                         shift, coef, (__bf16*)dy, nq, __builtin_ctz(c8));
-    } else {
-      hipLaunchKernelGGL(stem_bwd_apply8, dim3(ew_blocks(n8)), dim3(NT), 0, stream, pg, yb, scale,
-                         shift, coef, (__bf16*)dy, (int)n8, __builtin_ctz(c8));
-    }
+    const int nq = n * qh * qw * c8;
+    hipLaunchKernelGGL(stem_bwd_apply8q, dim3(ew_blocks(nq)), dim3(NT), 0, stream, pg, h, w,
+                       make_fastdiv((uint32_t)(qh * qw)), make_fastdiv((uint32_t)qw), yb, scale,
+                       shift, coef, (__bf16*)dy, nq, __builtin_ctz(c8));
   } else {
     hipLaunchKernelGGL((stem_bwd_apply<__bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg,
                        yb, scale, shift, coef, (__bf16*)dy, n4, c / 4);

@@ -961,13 +961,12 @@ template <int MODE, int BM, int BN, int WM, int WN, int F32, int PRO = 0>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
   // one-k-tile bf16 FWD launches on the 4-wave 128x128 / 256x64 tiles: the one-stage form
-  // (TMR_NST1=0: the two-stage form, A/B; read per call).  56x56 64->64: 0.427 -> 0.378 ms; the
-  // DGRAD view measured slower in it (its 233-VGPR LDS-staged epilogue caps the occupancy at two
-  // workgroups anyway; profiles/r4/nst1/)
+  // (bit-identical to the two-stage form, which it replaced in round 4).  56x56 64->64: 0.427 ->
+  // 0.378 ms; the DGRAD view measured slower in it (its 233-VGPR LDS-staged epilogue caps the
+  // occupancy at two workgroups anyway; profiles/r4/nst1/)
   if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && WM * WN == 4 &&
                 ((BM == 128 && BN == 128) || (BM == 256 && BN == 64))) {
-    const char* e = getenv("TMR_NST1");
-    if (!tapv && a.K > 0 && a.K <= 64 && !(e && e[0] == '0')) {
+    if (!tapv && a.K > 0 && a.K <= 64) {
       hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, 0, 1>), grid, blk, 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage)");
       return 0;
@@ -976,11 +975,10 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   // ... and the one-k-tile bf16 forwards the tile rules give 256x256 (N >= 256: the 64 -> 256
   // expansions): 256x128 as 8 waves in the one-stage form at 128 VGPRs -- two workgroups per CU
   // (one 16-wave 256x256 workgroup fills the register file), so one's epilogue stores overlap
-  // the other's loads.  Same BM (the statistics' part rows), same per-wave tiles: bit-identical.
-  // TMR_NST1W=0: the 256x256 launch (A/B; read per call).
+  // the other's loads.  Same BM (the statistics' part rows), same per-wave tiles: bit-identical to
+  // the 256x256 launch it replaced.
   if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && BM == 256 && BN == 256) {
-    const char* e = getenv("TMR_NST1W");
-    if (!tapv && a.K > 0 && a.K <= 64 && !(e && e[0] == '0')) {
+    if (!tapv && a.K > 0 && a.K <= 64) {
       const dim3 g2((unsigned)(cdiv(a.M, 256) * cdiv(a.N, 128)), grid.y, 1);
       hipLaunchKernelGGL((gemm16_kernel<MODE, 256, 128, 4, 2, 0, 1, F32, 0, 1>), g2, dim3(512), 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage, 256x128)");

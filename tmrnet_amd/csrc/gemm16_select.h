@@ -36,8 +36,13 @@ inline bool pro32_ok(const GemmArgs& a, int mode) {
 }
 
 inline bool use32(const GemmArgs& a, int mode) {
-  // A/B switch for the forward view, read per launch (tests flip it in-process)
+#if TMR_PROLOGUES
+  // the A/B build only (make PROLOGUES=1): TMR_GEMM32=0 keeps the fp32 forward / wgrad views on the
+  // register-staged engine, whose prologue form the fold test compares with this engine's
   const bool on = env_int("TMR_GEMM32", 1) != 0;
+#else
+  const bool on = true;
+#endif
   if (a.prec != TMR_MATH_F32 || a.sab) return false;
   if (!pro32_ok(a, mode)) return false;
   if (mode == MODE_DGRAD) return a.wt != 0;
@@ -49,9 +54,8 @@ inline bool use32(const GemmArgs& a, int mode) {
 }
 
 inline bool use16(const GemmArgs& a, int mode) {
-  static const bool on = env_int("TMR_GEMM16", 1) != 0;   // A/B switch (experiments)
   if (a.prec == TMR_MATH_F32) return use32(a, mode);
-  if (!on || a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
+  if (a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
   if (mode == MODE_DGRAD && !a.wt) return false;
   if (a.lds % 8) return false;
   if (mode == MODE_WGRAD) return a.M % 8 == 0 && a.log2C >= 3 && a.ldb % 8 == 0 && a.N % 8 == 0;

@@ -179,7 +179,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
                          const float* bias, float* y, float beta, GemmArgs& a, bool& al) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
-  TMR_CHECK_ARG(d->io == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
+  TMR_CHECK_ARG((d->io & ~TMR_IO_ENGINE) == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
   a = GemmArgs{};
@@ -196,12 +196,8 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
   a.Bbytes = clamp_bytes_e((long)d->k * a.K, esz_w(d));
   a.sab = ((d->io & TMR_IO_X_BF16) ? 1 : 0) | ((d->io & TMR_IO_W_BF16) ? 2 : 0);
   a.Cbytes = clamp_bytes(span((long)d->n * d->ho * d->wo, a.ldc, d->k));
-  a.c16 = (d->io & TMR_IO_Y_BF16) ? 1 : 0;
-  // (2: the whole-line store form of epilogue_batched; TMR_C16W=0 the 64-B pair form, A/B)
-  if (a.c16) {
-    const char* e = getenv("TMR_C16W");
-    if (!(e && e[0] == '0')) a.c16 = 2;
-  }
+  // (2: the whole-line store form of epilogue_batched, where the tile allows it)
+  a.c16 = (d->io & TMR_IO_Y_BF16) ? 2 : 0;
   a.dma32 = d->math == TMR_MATH_F32;
   al = aligned16(x) && aligned16(w_krsc) && (d->k % 4 == 0) && (a.lds % 4 == 0);
   return 0;
@@ -324,8 +320,8 @@ TMR_API int tmr_conv2d_fwd_fused(const tmr_conv_desc* d, const float* x, const f
 
 // The fp32 7x7/2 stem with BatchNorm statistics runs as a direct convolution over its 147 real
 // (tap, channel) pairs (stem.hip): a partial row per output row and wave; its weight gradient too
-// (partial slabs per workgroup, reduced by wgrad_reduce_taps_kernel).  TMR_STEM_DIRECT=0: the
-// implicit-GEMM engine (A/B, tests).
+// (partial slabs per workgroup, reduced by wgrad_reduce_taps_kernel).  TMR_IO_ENGINE: the
+// implicit-GEMM engine (tests).
 int tmr_stem_stats_parts(int n, int ho);
 int tmr_stem_fwd_bnstats(int n, int h, int w, int ho, const float* x, const float* w_krsc,
                          float* y, void* stats, hipStream_t stream);
@@ -340,7 +336,7 @@ static bool stem_geometry(const tmr_conv_desc* d) {
          yld_of(d) == 64;
 }
 static bool stem_direct(const tmr_conv_desc* d) {
-  return env_int("TMR_STEM_DIRECT", 1) != 0 && stem_geometry(d);
+  return !(d->io & TMR_IO_ENGINE) && stem_geometry(d);
 }
 // the bf16-activation step's stem (stem16.hip): bf16 math on the NHWC4 fp32 input, bf16 KRSC
 // weights (4 or 8 channels per tap), y bf16 with the statistics of the rounded values
@@ -354,7 +350,7 @@ static bool stem16_geometry(const tmr_conv_desc* d) {
          yld_of(d) == 64 && (d->h + 6 - 7) / 2 + 1 == d->ho;
 }
 static bool stem16_direct(const tmr_conv_desc* d) {
-  return env_int("TMR_STEM_DIRECT", 1) != 0 && stem16_geometry(d);
+  return !(d->io & TMR_IO_ENGINE) && stem16_geometry(d);
 }
 // its weight gradient (bf16 dy, the NHWC4 fp32 input)
 int tmr_stem16_wgrad_slabs(int n, int h, int w, int ho, const float* x, const void* dy, int dy32,
@@ -371,7 +367,7 @@ static bool stem16_wgrad_geometry(const tmr_conv_desc* d) {
 
 // the narrow stride-1 3x3 convs of the bf16-activation step (ResNeSt-50's deep stem: 32 -> 32,
 // 32 -> 64 at 112x112) as direct convolutions over an LDS ring of input rows (direct3.hip); every
-// operand bf16 in HBM, dense NHWC.  TMR_DIRECT3=0: the implicit-GEMM engine (A/B, tests).
+// operand bf16 in HBM, dense NHWC.  TMR_IO_ENGINE: the implicit-GEMM engine (tests).
 int tmr_d3_stats_parts(int n, int h, int w, int cin, int cout);
 int tmr_d3_dgrad_parts(int n, int h, int w, int cin_conv, int cout_conv);
 size_t tmr_d3_wgrad_ws_bytes(int n, int h, int w, int cin, int cout);
@@ -387,7 +383,7 @@ int tmr_d3_wgrad_slabs(int n, int h, int w, int cin, int cout, const void* x, co
 static bool d3_shape(const tmr_conv_desc* d) {
   const bool wc = (d->w == 112 && d->c == 32 && (d->k == 32 || d->k == 64)) ||
                   (d->w == 56 && d->c == 64 && d->k == 64);
-  return env_int("TMR_DIRECT3", 1) != 0 && d->math == TMR_MATH_BF16 && ngroups(d) == 1 &&
+  return !(d->io & TMR_IO_ENGINE) && d->math == TMR_MATH_BF16 && ngroups(d) == 1 &&
          d->r == 3 && d->s == 3 && d->stride == 1 && d->pad == 1 && d->pad_w == 1 && wc &&
          d->wo == d->w && d->ho == d->h && xld_of(d) == d->c && yld_of(d) == d->k &&
          d->max_frames == 0;
@@ -400,7 +396,7 @@ size_t tmr_d3s_wgrad_ws_bytes(int n, int ho);
 int tmr_d3s_wgrad_slabs(int n, int h, const float* x, const void* dy, float* ws, size_t ws_bytes,
                         int* nslabs, hipStream_t stream);
 static bool d3s_shape(const tmr_conv_desc* d) {
-  return env_int("TMR_DIRECT3", 1) != 0 && d->math == TMR_MATH_BF16 && ngroups(d) == 1 &&
+  return !(d->io & TMR_IO_ENGINE) && d->math == TMR_MATH_BF16 && ngroups(d) == 1 &&
          d->c == 4 && d->k == 32 && d->r == 3 && d->s == 3 && d->stride == 2 && d->pad == 1 &&
          d->pad_w == 1 && d->w == 224 && d->wo == 112 && d->h % 2 == 0 && d->ho == d->h / 2 &&
          xld_of(d) == 4 && yld_of(d) == 32 && d->max_frames == 0;
@@ -524,10 +520,11 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
   TMR_CHECK_ARG(d->c % 4 == 0, "tmr_conv2d_dgrad: input channels %d must be a multiple of 4", d->c);
   TMR_CHECK_ARG(!(d->io & TMR_IO_WT_BF16) || !(d->io & TMR_IO_W_BF16),
                 "tmr_conv2d_dgrad: TMR_IO_WT_BF16 and TMR_IO_W_BF16 are exclusive weight layouts");
-  TMR_CHECK_ARG(!(d->io & TMR_IO_WT_F32) || (d->math == TMR_MATH_F32 && d->io == TMR_IO_WT_F32),
+  TMR_CHECK_ARG(!(d->io & TMR_IO_WT_F32) ||
+                    (d->math == TMR_MATH_F32 && (d->io & ~TMR_IO_ENGINE) == TMR_IO_WT_F32),
                 "tmr_conv2d_dgrad: TMR_IO_WT_F32 (fp32 transposed weights) needs TMR_MATH_F32 and "
                 "no bf16-stored operand");
-  TMR_CHECK_ARG(d->io == 0 || d->io == TMR_IO_WT_F32 || d->math == TMR_MATH_BF16,
+  TMR_CHECK_ARG((d->io & ~(TMR_IO_WT_F32 | TMR_IO_ENGINE)) == 0 || d->math == TMR_MATH_BF16,
                 "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int st = d->stride;
   // one launch per stride-parity class (ph,pw): rows h = st*y + ph
@@ -699,6 +696,10 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
                 "tmr_conv2d_dgrad_bnbwd: a bf16 gradient (TMR_IO_G16) needs bf16 math on the LDS-DMA "
                 "engine (TMR_IO_WT_BF16), no prologue, channels per group a multiple of 8");
   TMR_CHECK_ARG(!dx_old || ngroups(d) == 1, "tmr_conv2d_dgrad_bnbwd: a separate old dx takes no groups");
+  // a grouped dgrad writes each group's channel slice of a bf16 gradient with beta == 0 only (the
+  // trunk's G16 on ResNeSt's radix-2 conv); accumulating into a bf16 dx runs ungrouped
+  TMR_CHECK_ARG(ngroups(d) == 1 || beta == 0.f || !(d->io & TMR_IO_G16),
+                "tmr_conv2d_dgrad_bnbwd: a grouped dgrad accumulates (beta != 0) into fp32 dx only");
   TMR_CHECK_ARG(mask == 0 || (mask == 1 && z) || (mask == 2 && scale && shift) || (mask == 3 && z),
                 "tmr_conv2d_dgrad_bnbwd: mask %d needs z (1, 3: bits) or scale/shift (2)", mask);
   TMR_CHECK_ARG(mask != 3 || ((d->io & (TMR_IO_WT_F32 | TMR_IO_WT_BF16)) &&
@@ -727,6 +728,7 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
       fz.mask = mask;
       fz.part = (float2*)parts + o;
       fz.part_ld = d->c;
+      fz.old16 = 0;   // (beta != 0 with a bf16 dx is rejected above)
       const int rc = dgrad_bnbwd_run(&g, adv(dy, (long)i * g.k, esz_dy(d)), adv(w_krsc, i * group_wsize(&g), esz_w(d)),
                                      adv(dx, o, esz_dx(d)), beta, &fz, stream);
       if (rc) return rc;
@@ -892,7 +894,7 @@ static int conv_wgrad_impl(const tmr_conv_desc* d, const float* x, const float* 
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_wgrad: stored input channels %d must be a power of two >= 4", d->c);
   TMR_CHECK_ARG(c_real >= 1 && c_real <= d->c, "tmr_conv2d_wgrad: bad c_real %d", c_real);
-  const bool s16 = !pro && c_real == 3 && env_int("TMR_STEM_DIRECT", 1) != 0 &&
+  const bool s16 = !pro && c_real == 3 && !(d->io & TMR_IO_ENGINE) &&
                    stem16_wgrad_geometry(d);
   if (s16 || (!pro && c_real == 3 && stem_direct(d))) {
     int ns = 0;

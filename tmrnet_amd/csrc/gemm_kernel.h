@@ -485,8 +485,8 @@ __device__ __forceinline__ void epilogue_batched(const GemmArgs& a, floatx16 (&a
   // bf16 output, TN even: whole 128-B lines per row.  The lane pair (2k, 2k+1) stores columns
   // (2k, 2k+1) of accumulator column block 2jp (even lane) and of block 2jp + 1 (odd lane), both of
   // the same row, so the 32 lanes of a half-wave write one row's 64 columns = 128 contiguous bytes
-  // (the pair form below writes 64-B halves of two rows).  Same values, same bytes.  a.c16 == 2
-  // selects it (host: TMR_C16W).
+  // (the pair form below, kept for tiles with an odd TN, writes 64-B halves of two rows).  Same
+  // values, same bytes.  a.c16 == 2 selects it (every bf16-output forward, gemm_conv.hip).
   if (c16w) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)

@@ -318,8 +318,8 @@ TMR_API int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const fl
   TMR_CHECK_ARG(scale && shift, "tmr_maxpool2d_fwd_bn_a16: null BatchNorm scale/shift");
   const long total = (long)n * ho * wo * (c / 4);
   const int c8 = c / 8;
-  const char* e8 = getenv("TMR_MAXPOOL8");   // A/B switch (0: the 4-wide form)
-  if (!(e8 && e8[0] == '0') && c % 8 == 0 && (c8 & (c8 - 1)) == 0 &&
+  // 8 channels per thread (else the 4-wide form)
+  if (c % 8 == 0 && (c8 & (c8 - 1)) == 0 &&
       (long)n * h * w * c8 < 0x7fffffffL &&
       (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
     const int t8 = (int)(total / 2);

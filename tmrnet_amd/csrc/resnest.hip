@@ -796,13 +796,10 @@ TMR_API int tmr_splat_gap_bn(const void* y, const float* scale, const float* shi
   TMR_CHECK_ARG(c % 4 == 0 && n > 0 && hw > 0, "tmr_splat_gap_bn: bad shape n %d hw %d c %d", n, hw, c);
   int cols, chunks;
   red_shape(c / 4, cols, chunks);
-  const char* wb = getenv("TMR_SPLAT_GAP_BT");   // A/B: threads per block (256: the old shape)
-  const int bt = wb ? atoi(wb) : 1024;
-  if (act16 && bt == 1024)
+  // bf16: 1024-thread blocks (round 4: one 256-thread block per frame and channel chunk had too
+  // few loads in flight)
+  if (act16)
     hipLaunchKernelGGL((splat_gap_bn_k<__bf16, 1024>), dim3(n * chunks), dim3(1024), 0, stream,
-                       (const __bf16*)y, scale, shift, gap, hw, c / 4, cols, chunks);
-  else if (act16)
-    hipLaunchKernelGGL(splat_gap_bn_k<__bf16>, dim3(n * chunks), dim3(NT), 0, stream,
                        (const __bf16*)y, scale, shift, gap, hw, c / 4, cols, chunks);
   else
     hipLaunchKernelGGL(splat_gap_bn_k<float>, dim3(n * chunks), dim3(NT), 0, stream,
@@ -827,8 +824,7 @@ TMR_API int tmr_splat_combine_bn(const void* y, const float* scale, const float*
   TMR_CHECK_ARG(total < (1L << 31), "tmr_splat_combine_bn: %ld element groups exceed 2^31", total);
   const int nb = blocks_for(total);
   const FastDiv dc4 = make_fastdiv((uint32_t)(c / 4)), dhw = make_fastdiv((uint32_t)hw);
-  const char* w8 = getenv("TMR_SPLAT8");   // A/B switch (0: the 4-wide form), read per call
-  if (act16 && !(w8 && w8[0] == '0') && c % 8 == 0 && NT % (c / 8) == 0 &&
+  if (act16 && c % 8 == 0 && NT % (c / 8) == 0 &&
       ((((uintptr_t)y) | ((uintptr_t)out)) & 15) == 0) {
     const long npix = (long)n * hw;
     hipLaunchKernelGGL(splat_combine_bn8_k, dim3(blocks_for(npix * (c / 8))), dim3(NT), 0, stream,
@@ -881,9 +877,7 @@ TMR_API int tmr_splat_bwd_apply_bn(const float* dout, const void* y, const float
   TMR_CHECK_ARG(total < (1L << 31), "tmr_splat_bwd_apply_bn: %ld element groups exceed 2^31", total);
   const int nb = blocks_for(total);
   const FastDiv dj4 = make_fastdiv((uint32_t)(2 * c / 4)), dhw = make_fastdiv((uint32_t)hw);
-  const char* w8 = getenv("TMR_SPLAT8");   // A/B switch (0: the 4-wide form), read per call
-  const bool wide = !(w8 && w8[0] == '0');
-  if (act16 && wide && c % 8 == 0 && NT % (c / 8) == 0 &&
+  if (act16 && c % 8 == 0 && NT % (c / 8) == 0 &&
       ((((uintptr_t)dout) | ((uintptr_t)y) | ((uintptr_t)dy)) & 15) == 0) {
     const long npix = (long)n * hw;
     const int nb8 = blocks_for(npix * (c / 8));   // (a multiple of c/8 threads: NT % (c/8) == 0)

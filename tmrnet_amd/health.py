@@ -8,8 +8,8 @@ the weights.  An inference forward (lstm.LSTM under no_grad) waits and checks at
 `check()` is called once per optimizer step (optim.SGD / Adam .step()).  It never stalls the
 stream: it starts an asynchronous copy of the word into pinned host memory and raises on the value
 of the PREVIOUS step's copy once that copy has landed (so a failure surfaces at most one step
-later, before the model trains on it for long).  `check(sync=True)` waits and checks now (tests,
-end of training).  Reference counterpart: the LSTM of train_only_non-local_pretrained.py:215,
+later, before the model trains on it for long).  `check(sync=True)` waits for the current stream and checks now
+(inference, tests, end of training).  A raised failure clears the word.  Reference counterpart: the LSTM of train_only_non-local_pretrained.py:215,
 :230-231, which cannot fail this way on cuDNN.
 """
 import torch
@@ -38,7 +38,12 @@ def note_lstm(ws):
     call("tmr_lstm_status_or", ws, status_word(ws.device), stream_ptr())
 
 
-def _raise(v):
+def _raise(v, st):
+    """Clear the recorded status (stream-ordered), then raise: a failure is reported once, and a
+    later call on a healthy device succeeds."""
+    call("tmr_fill_f32", st[0], 1, 0.0, stream_ptr(st[0].device))
+    st[1].zero_()
+    st[2] = None
     if v & LSTM_TIMEOUT:
         raise RuntimeError("persistent LSTM kernel gave up a grid barrier (its recurrence results "
                            "are invalid): the GPU was shared or oversubscribed -- rerun with "
@@ -55,15 +60,16 @@ def check(sync=False, device=None):
             continue
         status, host, ev = st
         if sync:
-            torch.cuda.synchronize(status.device)
+            # .item() waits for the current stream only (the one the kernels were enqueued on),
+            # not for the whole device
             v = int(status.item())
             if v:
-                _raise(v)
+                _raise(v, st)
             continue
         if ev is not None and ev.query():
             v = int(host.item())
             if v:
-                _raise(v)
+                _raise(v, st)
             st[2] = None
         if st[2] is None:
             host.copy_(status, non_blocking=True)

@@ -209,8 +209,10 @@ class MemoryBankModel(nn.Module):
     def trunk(self):
         return self.res if hasattr(self, "res") else self.share
 
-    def forward(self, x):
-        T = self.seq_len
+    def forward(self, x, seq_len=None):
+        """seq_len overrides the constructor's T for this call only (no module state is written,
+        so one instance can be driven from several threads, as DataParallel replicas are)."""
+        T = self.seq_len if seq_len is None else int(seq_len)
         feat = _frames_to_features(self.trunk(), x)
         y, _ = self.lstm(feat.view(-1, T, 2048))
         y = y.reshape(-1, 512)

@@ -5,6 +5,9 @@ allocator (the library never allocates), passes raw pointers plus the current
 stream, and raises RuntimeError on a failed call.  No function here computes
 anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 """
+import contextlib
+import threading
+
 import torch
 
 from ._lib import call, query, stream_ptr, has_prologues, ConvDesc, ConvPrologue
@@ -75,6 +78,26 @@ IO_X, IO_W, IO_DY, IO_WT = 1, 2, 4, 8   # tmr_conv_desc.io: bf16-stored x / KRSC
 IO_Y, IO_BN = 16, 32    # bf16 conv output y (forward) / bf16 y, z of the fused BN backward (dgrad)
 IO_WT32 = 64            # dgrad, fp32 math: w is the transposed fp32 copy (fp32 LDS-DMA engine)
 IO_G16 = 128            # fused BN-backward dgrad: g (dx) written bf16 (non-residual bf16 units)
+IO_ENGINE = 256         # the implicit-GEMM engine even where a direct kernel serves the geometry
+
+_TLS = threading.local()
+
+
+@contextlib.contextmanager
+def engine_only():
+    """Within the block (this thread only), every conv runs on the implicit-GEMM engine, also where
+    a direct kernel serves the geometry (the 7x7 stems, the narrow 3x3 convs of direct3.hip):
+    TMR_IO_ENGINE, the independent second implementation tests compare those kernels with."""
+    prev = getattr(_TLS, "engine", False)
+    _TLS.engine = True
+    try:
+        yield
+    finally:
+        _TLS.engine = prev
+
+
+def engine_forced():
+    return getattr(_TLS, "engine", False)
 BF16 = torch.bfloat16
 
 
@@ -122,6 +145,8 @@ def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math
         raise RuntimeError("bf16-stored conv operands need math='bf16'")
     if io & IO_WT32 and math != "fp32":
         raise RuntimeError("fp32 transposed weights (TMR_IO_WT_F32) need math='fp32'")
+    if engine_forced():
+        io |= IO_ENGINE
     return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
                     MAX_FRAMES, io, groups if groups > 1 else 0)
 
@@ -283,6 +308,9 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
                                "prologue / groups")
         if old.dtype not in (f32, BF16) or not old.is_contiguous():
             raise RuntimeError("conv_dgrad_bnbwd: old dx must be a contiguous fp32 / bf16 tensor")
+    if g16 and groups > 1 and beta != 0.0:
+        raise RuntimeError("conv_dgrad_bnbwd: a grouped dgrad accumulates (beta != 0) into an fp32 "
+                           "dx only")
     _req_op(w_krsc, "w"); _req_op(y, "y"); _req(mean, "mean")
     if mask == 3:   # z = ReLU-mask bits of dx's shape (bn_apply_bits)
         if z is None or z.dtype != torch.int32 or z.numel() * 32 < y.numel():

@@ -35,9 +35,7 @@ HBM -- a bf16 copy of its input (written by the producing BN pass next to the fp
 residual / split attention / pools use, or cast once for split-attention and pool outputs), KRSC
 and transposed CRSK bf16 weights, bf16 dy -- and therefore runs on the LDS-DMA engine
 (gemm16_kernel.h).  The contract is unchanged (the bf16 convs round exactly those operands).
-TMR_BF16_FULL=0 keeps the register-staged path.
 """
-import os
 import math
 
 import torch
@@ -59,11 +57,6 @@ def _bn_train_or_eval(y, bn, training):
     return None, None, scale, shift
 
 
-FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
-# the 4-channel stem input as NHWC8 bf16 on the bf16 operand path (trunk.STEM8's switch)
-STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
-# the deep stem's convs as direct kernels (direct3.hip; read again by the library per launch)
-DIRECT3 = os.environ.get("TMR_DIRECT3", "1") != "0"
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -285,8 +278,8 @@ class ResNeStTrunkFn(torch.autograd.Function):
         c = share.conv1
         # the stem input: under bf16 activations the NHWC4 fp32 frames themselves for the direct
         # 3x3/2 stem conv (direct3.hip: rounded to bf16 as it is staged), or an NHWC8 bf16 copy
-        # for the LDS-DMA engine (TMR_DIRECT3=0: its 8-channel pieces)
-        xs = ops.nhwc4_to_bf16x8(x4) if (a16 and not DIRECT3) else x4
+        # for the LDS-DMA engine (ops.engine_only, tests: its 8-channel pieces)
+        xs = ops.nhwc4_to_bf16x8(x4) if (a16 and ops.engine_forced()) else x4
         z = _conv_bn(xs, c[0], c[1], 2, 1, True, True, recs=stem, math=mt, nbt=nbt)
         z = _conv_bn(z, c[3], c[4], 1, 1, True, True, recs=stem, math=mt, nbt=nbt)
         # share.bn1 + relu applied inside the maxpool (its backward recomputes the mask from y)
@@ -442,15 +435,15 @@ def _trunk_node_ok(share):
 
 def conv_bn_act(x, conv, bn, stride, pad, relu, groups=1, residual=None, c_real=None,
                 math="fp32"):
-    """conv -> BN -> (+residual) -> (ReLU).  On the bf16 operand path (bf16 math, train mode,
-    TMR_BF16_FULL) the conv reads x's bf16 copy: the one its producer attached (`_tmr_bf16`), else
-    a cast; the 4-channel stem input as an NHWC8 bf16 copy (tmr_nhwc4_to_bf16x8)."""
+    """conv -> BN -> (+residual) -> (ReLU).  On the bf16 operand path (bf16 math, train mode) the
+    conv reads x's bf16 copy: the one its producer attached (`_tmr_bf16`), else a cast; the
+    4-channel stem input as an NHWC8 bf16 copy (tmr_nhwc4_to_bf16x8)."""
     x16 = None
-    if math == "bf16" and bn.training and FULL16 and x.shape[-1] % 8 == 0:
+    if math == "bf16" and bn.training and x.shape[-1] % 8 == 0:
         x16 = getattr(x, "_tmr_bf16", None)
         if x16 is None:
             x16 = ops.to_bf16(x.contiguous())
-    elif math == "bf16" and bn.training and FULL16 and STEM8 and x.shape[-1] == 4 and groups == 1:
+    elif math == "bf16" and bn.training and x.shape[-1] == 4 and groups == 1:
         x16 = ops.nhwc4_to_bf16x8(x.contiguous())
     z, z16 = ConvBNActFn.apply(x, x16, conv.weight, bn.weight, bn.bias, residual, bn, stride, pad,
                                groups, relu,

@@ -107,14 +107,14 @@ def _store16(math):
     return math == "bf16" and BF16_STORE
 
 
-# bf16 math with EVERY conv operand bf16 in HBM (train mode; TMR_BF16_FULL=0 turns it off): the
-# block outputs are written fp32 (identity residual, ReLU mask) and as a bf16 copy in the same pass
-# (bn_apply_dual / bn_apply2 dual), the stem maxpool output as bf16 only (layer1.0 has a
-# downsample, so it is never a residual), and each conv's dgrad reads a transposed bf16 weight copy
-# (weight_to_crsk).  Every conv but the 4-channel stem then runs on the LDS-DMA engine
-# (gemm16_kernel.h).  Bit-identical to the register-staged bf16 path (same rounding of the same
-# operands), tests/test_bf16_gpu.py.
-FULL16 = os.environ.get("TMR_BF16_FULL", "1") != "0"
+# bf16 math with EVERY conv operand bf16 in HBM (train mode): the block outputs are written fp32
+# (identity residual, ReLU mask) and as a bf16 copy in the same pass (bn_apply_dual / bn_apply2
+# dual), the stem maxpool output as bf16 only (layer1.0 has a downsample, so it is never a
+# residual), and each conv's dgrad reads a transposed bf16 weight copy (weight_to_crsk).  Every conv
+# but the 4-channel stem then runs on the LDS-DMA engine (gemm16_kernel.h).  Same rounding of the
+# same operands as the register-staged bf16 path, tests/test_bf16_gpu.py.  (A module attribute, no
+# environment switch: tests/test_bf16_gpu.py turns it off to reach the fp32-storage forms.)
+FULL16 = True
 
 # bf16 activations (train mode, on top of FULL16; TMR_BF16_ACT=0 turns it off): every conv output
 # y is stored rounded to bf16 by its epilogue (the BN statistics are those of the rounded values)
@@ -127,17 +127,9 @@ ACT16 = os.environ.get("TMR_BF16_ACT", "1") != "0"
 
 
 # fp32 math: the dgrad view runs on the fp32 form of the LDS-DMA engine, reading a transposed fp32
-# weight copy (TMR_IO_WT_F32; the forward view takes that engine by itself).  TMR_GEMM32=0 keeps
-# both views on the register-staged engine (A/B measurements).  Not with FOLD_BN: the LDS-DMA
-# engine has no operand prologues.
-DMA32 = os.environ.get("TMR_GEMM32", "1") != "0"
-
-
-# downsample blocks' backward order: the strided downsample dgrad runs first (plain, beta 0; its
-# tap-less parity classes write zeros) and the previous block's BN backward is fused into conv1's
-# stride-1 dgrad (beta 1).  Bit-identical to the other order (dx = a + b either way); measured
-# 51.1 vs 51.6 ms of dgrads per C2 step (profiles/r3/bench_r4f/).  TMR_DS_FIRST=0: the old order.
-DS_FIRST = os.environ.get("TMR_DS_FIRST", "1") != "0"
+# weight copy (TMR_IO_WT_F32; the forward view takes that engine by itself).  (A module attribute
+# for the prologue A/B test of the retired fold build, tests/test_kernels_gpu.py.)
+DMA32 = True
 
 # bf16-activation step: the masked BN-output gradient of the non-residual units (bn1, bn2 of every
 # Bottleneck) stored bf16 by the fused dgrad (TMR_IO_G16; the residual stream's gradient stays
@@ -156,13 +148,9 @@ G16 = os.environ.get("TMR_G16", "1") != "0"
 # gradient of every block output but the last.
 R16 = os.environ.get("TMR_BF16_RESGRAD", "1") != "0"
 
-# the block outputs' ReLU masks as bits for the mask-3 dgrads (TMR_RELU_BITS=0: re-read z)
-BITS = os.environ.get("TMR_RELU_BITS", "1") != "0"
-# ... and for the bf16-activation step (TMR_RELU_BITS16): under the round-3 fp32 residual gradient
-# the bits measured no faster than re-reading the 2-byte z (C5 dgrads 56.6 vs 58.8 ms/step,
-# profiles/r3/bench_r4i/); under the bf16 residual gradient (R16) z is a quarter of the residual
-# dgrads' epilogue bytes (round-4 A/B: profiles/r4/bits16_ab/)
-BITS16 = os.environ.get("TMR_RELU_BITS16", "0") == "1"
+# the fp32 block outputs' ReLU masks as bits for the mask-3 dgrads (round 2: 3622 -> 3634 frames/s,
+# profiles/r2/bench_r3a/).  The bf16-activation step re-reads its 2-byte z instead: bits measured no
+# faster there (profiles/r3/bench_r4i/, round-4 A/B under R16: the step unchanged) and were retired.
 
 
 def _dma32(math):
@@ -170,12 +158,11 @@ def _dma32(math):
     return math == "fp32" and DMA32
 
 
-# bf16 activations: the stem input as NHWC8 bf16 (TMR_BF16_STEM8=0: the NHWC4 fp32 input on the
-# register-staged engine, A/B measurements)
-STEM8 = os.environ.get("TMR_BF16_STEM8", "1") != "0"
-# ... unless the direct bf16 stem takes the NHWC4 fp32 input itself (stem16.hip, round 4: 147 of
-# 176 multiplies useful instead of 147 of 392, no NHWC8 copy; TMR_STEM_DIRECT=0 turns it off)
-STEM16 = os.environ.get("TMR_STEM_DIRECT", "1") != "0"
+# bf16 activations: the direct bf16 stem takes the NHWC4 fp32 input itself (stem16.hip, round 4:
+# 147 of 176 multiplies useful instead of 147 of 392); on the implicit-GEMM engine
+# (ops.engine_only, tests) the stem reads an NHWC8 bf16 copy of it (LDS-DMA engine pieces)
+
+
 def _full16(math):
     return _store16(math) and FULL16 and not FOLD_BN
 
@@ -233,10 +220,8 @@ def _conv_bn(x, conv, bn, stride, pad, relu, training, residual=None, recs=None,
     # produces their gradient reads 1 bit instead of z's 4 bytes (mask 3)
     zbits = None
     # (bf16 activations too: the bits of the rounded z, tmr_bn_apply_bits_a16)
-    bits = (recs is not None and relu and not dual and
-            ((_dma32(math) and y.dtype == torch.float32) or
-             (_act16(math) and y.dtype == torch.bfloat16 and BITS16))
-            and (residual is not None or branch is not None) and BITS)
+    bits = (recs is not None and relu and not dual and _dma32(math) and y.dtype == torch.float32
+            and (residual is not None or branch is not None))
     if defer:
         z = None
     elif branch is not None and bits:
@@ -383,7 +368,7 @@ class TrunkFn(torch.autograd.Function):
         if training:
             # bf16 activations: the stem reads an NHWC8 bf16 copy of its input (8-channel
             # pieces: the LDS-DMA engine; exact, the bf16 math rounds x anyway)
-            xs = ops.nhwc4_to_bf16x8(x4) if (a16 and STEM8 and not STEM16) else x4
+            xs = ops.nhwc4_to_bf16x8(x4) if (a16 and ops.engine_forced()) else x4
             # share.bn1 + relu applied inside the maxpool (the backward recomputes the ReLU
             # mask from y, so the stem's BN output is never needed)
             y0, sc0, sh0 = _conv_bn(xs, conv1, bn1, 2, 3, True, training, recs=recs, math=mt,
@@ -441,7 +426,6 @@ class TrunkFn(torch.autograd.Function):
         grads = {}
         g = ops.avgpool_bwd(dfeat.contiguous(), ctx.last_hw)   # grad at the last block output
         blocks = ctx.blocks
-        fuse = os.environ.get("TMR_FUSE_BN_BWD", "1") != "0"
         pending = None     # BN-backward partials of g when the dgrad that produced it was fused
         ready = get_grad_ready(ctx.share)   # ddp.GradAllReduce.grads_ready, or None
         while blocks:
@@ -451,23 +435,20 @@ class TrunkFn(torch.autograd.Function):
             rd = brec[2] if has_ds else None
             r3 = brec[-1]
             # the previous block's last unit: its BN output gradient is this block's dx
-            prev3 = blocks[-1][1][-1] if (blocks and fuse) else None
+            prev3 = blocks[-1][1][-1] if blocks else None
             # g (owned here) becomes the masked pre-ReLU gradient = the identity-branch grad
             dz2, dres, fz2 = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True,
-                                          parts=pending, fuse_prev=r2 if fuse else None, g16=True)
-            dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1 if fuse else None,
-                                       g16=True)
+                                          parts=pending, fuse_prev=r2, g16=True)
+            dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1, g16=True)
             del dz2
-            if has_ds and DS_FIRST:
+            if has_ds:
                 # the strided downsample dgrad writes dx (its tap-less parity classes as zeros),
                 # the stride-1 conv1 dgrad accumulates into it with the fused BN backward
+                # (measured 51.1 vs 51.6 ms of dgrads per C2 step against the other order,
+                # profiles/r3/bench_r4f/)
                 dx, _, _ = _conv_bn_bwd(rd, dres, grads)
                 dx, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dx, dx_beta=1.0,
                                               fuse_prev=prev3, r16=True)
-            elif has_ds:
-                dx, _, _ = _conv_bn_bwd(r1, dz1, grads, parts=fz1)
-                _, _, pending = _conv_bn_bwd(rd, dres, grads, dx_out=dx, dx_beta=1.0,
-                                             fuse_prev=prev3)
             else:
                 dx, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dres, dx_beta=1.0,
                                               fuse_prev=prev3, r16=True)
