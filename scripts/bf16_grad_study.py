@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--traj-variants", default="fp32,bf16")
     ap.add_argument("--out", default="gpurun_out/bf16_grads")
+    ap.add_argument("--ensemble", type=int, default=0,
+                    help="K: gradient ensembles over perturbed inputs (bf16: 1-ulp, fp32n: 2^-9)")
+    ap.add_argument("--ens-variants", default="bf16,fp32n")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     backbone, tc, T, L = GEOS[a.geo]
@@ -46,8 +49,7 @@ def main():
             m = bg.make_model(dev, T, backbone, tc, prec, sd)
             if sd is None:
                 sd = {k: t.detach().clone() for k, t in m.state_dict().items()}
-            xin = bg.perturb_ulp(x4) if v == "fp32p" else x4
-            loss, out, g = bg.grads_of(m, xin, lfb, labels, mk)
+            loss, out, g = bg.grads_of(m, bg.inputs_for(v, x4), lfb, labels, mk)
         del m
         torch.cuda.empty_cache()
         if g_ref is None:
@@ -66,15 +68,61 @@ def main():
         sys.stdout.flush()
     with open(os.path.join(a.out, "grads_%s.json" % tag), "w") as f:
         json.dump(res, f, indent=1)
+    if a.ensemble:
+        ens = {}
+        for v in a.ens_variants.split(","):
+            base = "fp32" if v == "fp32n" else v
+            gs = []
+            t0 = time.time()
+            for k in range(2 * a.ensemble):
+                with bg.variant(base) as prec:
+                    m = bg.make_model(dev, T, backbone, tc, prec, sd)
+                    xin = (bg.perturb_rel(x4, 2.0 ** -9, 100 + k) if v == "fp32n"
+                           else bg.perturb_ulp(x4, 100 + k))
+                    _, _, g = bg.grads_of(m, xin, lfb, labels, mk)
+                del m
+                gs.append({n: t.float() for n, t in g.items()})
+            ens[v] = gs
+            print("ensemble %s: %d samples (%.1f s)" % (v, len(gs), time.time() - t0), flush=True)
+        K = a.ensemble
+        rec = {}
+        names = list(ens)
+        for v in names:
+            A, B = ens[v][:K], ens[v][K:]
+            rec[v + "_self"] = bg.ensemble_stats(A + B, A + B, same=True)   # |g*|^2
+            rec[v + "_AB"] = bg.ensemble_stats(A, B)
+        for i, v in enumerate(names):
+            for w in names[i + 1:]:
+                rec[v + "_x_" + w] = bg.ensemble_stats(ens[v], ens[w])
+        gref = {n: t.float() for n, t in g_ref.items()}
+        for v in names:
+            rec[v + "_x_fp32"] = bg.ensemble_stats(ens[v], [gref])
+        rec["fp32_norm2"] = bg.ensemble_stats([gref], [gref])
+        # smooth-gradient cosine between two variants: <g*_v, g*_w> / sqrt(|g*_v|^2 |g*_w|^2)
+        print("group      " + "  ".join("%-22s" % k for k in ("c*(%s,%s)" % (names[0], names[-1]),
+                                                                "c1(%s,fp32)" % names[0],
+                                                                "c1(%s,fp32)" % names[-1])))
+        summ = {}
+        for grp in rec["fp32_norm2"]:
+            s0, s1 = rec[names[0] + "_self"].get(grp), rec[names[-1] + "_self"].get(grp)
+            x = rec[names[0] + "_x_" + names[-1]].get(grp) if len(names) > 1 else None
+            c_star = x / (max(s0, 1e-300) * max(s1, 1e-300)) ** 0.5 if (x is not None and s0 > 0
+                                                                           and s1 > 0) else None
+            summ[grp] = {"c_star": c_star, "self": {v: rec[v + "_self"][grp] for v in names},
+                         "x_fp32": {v: rec[v + "_x_fp32"][grp] for v in names},
+                         "fp32_norm2": rec["fp32_norm2"][grp]}
+            print("%-10s %s" % (grp, c_star))
+        with open(os.path.join(a.out, "ensemble_%s_K%d.json" % (tag, K)), "w") as f:
+            json.dump({"K": K, "stats": rec, "summary": summ}, f, indent=1)
     if a.lrs:
         traj = {}
-        batches = [(x4, lfb, labels)]
         for lr in [float(s) for s in a.lrs.split(",")]:
             for v in a.traj_variants.split(","):
                 t0 = time.time()
                 with bg.variant(v) as prec:
                     m = bg.make_model(dev, T, backbone, tc, prec, sd)
-                    losses = bg.trajectory(m, batches, mk, lr, a.steps)
+                    losses = bg.trajectory(m, [(bg.inputs_for(v, x4), lfb, labels)], mk, lr,
+                                           a.steps)
                 del m
                 torch.cuda.empty_cache()
                 traj["%s_lr%g" % (v, lr)] = losses

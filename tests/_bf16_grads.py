@@ -22,6 +22,8 @@ from tmrnet_amd import ops, trunk, LFBRows
 VARIANTS = {
     "fp32": ("fp32", {}),
     "fp32p": ("fp32", {}),
+    "fp32xb": ("fp32", {}),     # the fp32 step on the input frames rounded to bf16 (see inputs_for)
+    "fp32n": ("fp32", {}),      # ... on the input frames with +-2^-9 relative noise (inputs_for)
     "bf16": ("bf16", {}),
     "bf16_g16off": ("bf16", {"G16": False}),
     "bf16_r16off": ("bf16", {"R16": False}),
@@ -71,6 +73,46 @@ def perturb_ulp(x4, seed=9):
     bits = x4.contiguous().view(torch.int32)
     out = (bits + sgn * (x4 != 0).to(torch.int32)).view(torch.float32)
     return out
+
+
+def perturb_rel(x4, eps, seed):
+    """x4 * (1 + eps * s), s = +-1 at random per element (seeded): input noise of a chosen
+    relative size (eps = 2^-9: one bf16 rounding)."""
+    g = torch.Generator(device=x4.device).manual_seed(seed)
+    sgn = torch.randint(0, 2, x4.shape, generator=g, device=x4.device).to(x4.dtype) * 2 - 1
+    return x4 * (1 + eps * sgn)
+
+
+def ensemble_stats(gs_a, gs_b, same=False):
+    """Per group: the mean pairwise inner product of two gradient ensembles, <g_i, g_j> over
+    i in a, j in b (i != j when `same`).  For samples g = g* + n with independent zero-mean noise
+    this estimates <g*_a, g*_b> without the noise terms."""
+    out = {}
+    names = [n for n in gs_a[0] if not (n == "nl_block.linear2.bias" or n.endswith("fc1.bias"))]
+    for n in names:
+        grp = group_of(n)
+        tot, cnt = 0.0, 0
+        for i, ga in enumerate(gs_a):
+            for j, gb_ in enumerate(gs_b):
+                if same and j <= i:
+                    continue
+                tot += float((ga[n].double() * gb_[n].double()).sum())
+                cnt += 1
+        out[grp] = out.get(grp, 0.0) + tot / max(cnt, 1)
+    return out
+
+
+def inputs_for(v, x4):
+    """The frames a variant runs on: fp32p one fp32 ulp off (perturb_ulp), fp32xb rounded to bf16
+    (one bf16 rounding of the input alone: the size of the operand rounding the bf16 step applies
+    at every conv), every other variant x4 itself."""
+    if v == "fp32p":
+        return perturb_ulp(x4)
+    if v == "fp32xb":
+        return x4.to(torch.bfloat16).to(torch.float32)
+    if v == "fp32n":
+        return perturb_rel(x4, 2.0 ** -9, 9)
+    return x4
 
 
 def masks(B, seed):

@@ -23,14 +23,14 @@ def dev():
 
 @pytest.fixture
 def engine():
-    """engine.use(True): the convs of this test (thread) run on the implicit-GEMM engine also where
+    """engine.use(True): the convs of this test run on the implicit-GEMM engine also where
     a direct kernel serves the geometry (ops.engine_only, TMR_IO_ENGINE); use(False): the product
     routing.  Reset when the test ends."""
     from tmrnet_amd import ops
 
     class _Switch:
         def use(self, on):
-            ops._TLS.engine = bool(on)
+            ops._ENGINE[0] = bool(on)
 
     yield _Switch()
-    ops._TLS.engine = False
+    ops._ENGINE[0] = False

@@ -6,7 +6,6 @@ stream, and raises RuntimeError on a failed call.  No function here computes
 anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 """
 import contextlib
-import threading
 
 import torch
 
@@ -80,24 +79,26 @@ IO_WT32 = 64            # dgrad, fp32 math: w is the transposed fp32 copy (fp32 
 IO_G16 = 128            # fused BN-backward dgrad: g (dx) written bf16 (non-residual bf16 units)
 IO_ENGINE = 256         # the implicit-GEMM engine even where a direct kernel serves the geometry
 
-_TLS = threading.local()
+# test instrumentation (process-wide: autograd runs the backward of a CUDA graph on its own
+# device thread, which must see the same routing as the forward)
+_ENGINE = [False]
 
 
 @contextlib.contextmanager
 def engine_only():
-    """Within the block (this thread only), every conv runs on the implicit-GEMM engine, also where
-    a direct kernel serves the geometry (the 7x7 stems, the narrow 3x3 convs of direct3.hip):
-    TMR_IO_ENGINE, the independent second implementation tests compare those kernels with."""
-    prev = getattr(_TLS, "engine", False)
-    _TLS.engine = True
+    """Within the block every conv runs on the implicit-GEMM engine, also where a direct kernel
+    serves the geometry (the 7x7 stems, the narrow 3x3 convs of direct3.hip): TMR_IO_ENGINE, the
+    independent second implementation tests compare those kernels with.  Tests only."""
+    prev = _ENGINE[0]
+    _ENGINE[0] = True
     try:
         yield
     finally:
-        _TLS.engine = prev
+        _ENGINE[0] = prev
 
 
 def engine_forced():
-    return getattr(_TLS, "engine", False)
+    return _ENGINE[0]
 BF16 = torch.bfloat16
 
 
