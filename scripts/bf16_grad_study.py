@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--out", default="gpurun_out/bf16_grads")
     ap.add_argument("--ensemble", type=int, default=0,
                     help="K: gradient ensembles over perturbed inputs (bf16: 1-ulp, fp32n: 2^-9)")
-    ap.add_argument("--ens-variants", default="bf16,fp32n")
+    ap.add_argument("--ens-variants", default="bf16n,fp32n")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     backbone, tc, T, L = GEOS[a.geo]
@@ -71,13 +71,16 @@ def main():
     if a.ensemble:
         ens = {}
         for v in a.ens_variants.split(","):
-            base = "fp32" if v == "fp32n" else v
+            # <variant>n: the variant on input frames with +-2^-9 relative noise (one bf16 rounding:
+            # a perturbation the bf16 step's own input rounding cannot absorb); else 1 fp32 ulp
+            noisy = v.endswith("n") and v[:-1] in bg.VARIANTS
+            base = v[:-1] if noisy else v
             gs = []
             t0 = time.time()
             for k in range(2 * a.ensemble):
                 with bg.variant(base) as prec:
                     m = bg.make_model(dev, T, backbone, tc, prec, sd)
-                    xin = (bg.perturb_rel(x4, 2.0 ** -9, 100 + k) if v == "fp32n"
+                    xin = (bg.perturb_rel(x4, 2.0 ** -9, 100 + k) if noisy
                            else bg.perturb_ulp(x4, 100 + k))
                     _, _, g = bg.grads_of(m, xin, lfb, labels, mk)
                 del m

@@ -24,6 +24,7 @@ VARIANTS = {
     "fp32p": ("fp32", {}),
     "fp32xb": ("fp32", {}),     # the fp32 step on the input frames rounded to bf16 (see inputs_for)
     "fp32n": ("fp32", {}),      # ... on the input frames with +-2^-9 relative noise (inputs_for)
+    "bf16n": ("bf16", {}),      # the bf16 step on those frames
     "bf16": ("bf16", {}),
     "bf16_g16off": ("bf16", {"G16": False}),
     "bf16_r16off": ("bf16", {"R16": False}),
@@ -110,7 +111,7 @@ def inputs_for(v, x4):
         return perturb_ulp(x4)
     if v == "fp32xb":
         return x4.to(torch.bfloat16).to(torch.float32)
-    if v == "fp32n":
+    if v in ("fp32n", "bf16n"):
         return perturb_rel(x4, 2.0 ** -9, 9)
     return x4
 

@@ -10,28 +10,33 @@ from the fp32 model the reference runs:
 * small geometry, against the fp32 CPU oracle (TMRNetRef(precision="fp32")) on the same weights,
   inputs, LFB rows and dropout masks, train mode (batch-stat BN) and eval mode (running stats):
     - |logit_bf16 - logit_fp32| <= bound * max|logit_fp32|, bound = max(LOGIT_TOL, EMU_RATIO *
-      e_emu): LOGIT_TOL = 2e-2 (§8c line 451), e_emu = the same distance for the CPU float
-      emulation of the bf16 contract (oracle.emulate_bf16_convs), EMU_RATIO = 1.25 -- the kernels
-      add no drift beyond the contract's own, and meet 2e-2 wherever the contract does
+      e_emu, e_64 + SENS_RATIO * e_sens): LOGIT_TOL = 2e-2 (§8c line 451); e_emu = the same
+      distance for the CPU float emulation of the bf16 contract (oracle.emulate_bf16_convs),
+      EMU_RATIO = 1.25 -- the kernels add no drift beyond the contract's own; e_64 = the
+      emulation with exact (float64) accumulation vs fp32, e_sens = the fp32 emulation vs the
+      float64 one (how far fp32 summation order alone moves the contract: which way its bf16
+      roundings break), SENS_RATIO = 2 -- the HIP kernels, another fp32 summation order, at most
+      twice as far from the exact contract as the CPU emulation is
     - identical argmax on every clip whose fp32 top-2 margin exceeds 2 * bound * max|logit|
   C5: ResNet-50 + LSTM + NLBlock, T=30, L=300, LFB rows from a resident bank;
   C4: ResNeSt-50 + LSTM + TimeConv + NLBlock, T=10, L=40.
 * full size (C4: 64 clips x 10 frames; C5: 64 clips x 30 frames = 1920 frames), HIP bf16 against
   HIP fp32 (the fp32 HIP path is itself pinned to the oracle at 1e-4, test_geometry_gpu.py):
-  eval mode within LOGIT_TOL, train mode within FULL_TRAIN_TOL = 6e-2, the argmax rule, the
-  agreement rates recorded in gpurun_out/ (measured: eval <= 1e-2, train 4.6-5.3e-2; argmax
-  identical on every sure clip, 62-64 of 64 clips overall).
+  eval mode within LOGIT_TOL, train mode within FULL_TRAIN_TOL = 6e-2 on structured frames and
+  within max(FULL_TRAIN_TOL, XB_RATIO x e_xb) on noise frames, e_xb = how far the fp32 step moves
+  when only its input frames are rounded to bf16 (XB_RATIO = 4: the bf16 step rounds ~50 operands
+  per frame; measured 2.3-3.2x), the argmax rule, agreement rates recorded in gpurun_out/.
 
-Frames.  The bound is asserted on structured synthetic frames (a random 6x6 colour field,
-bilinearly upsampled, plus pixel noise of sigma 20): frames that differ in their global statistics,
-as video frames do.  On frames of i.i.d. uniform pixel noise (the benchmark's data) every frame has
-the same global statistics to ~1%, so a batch-statistic BatchNorm over per-frame pooled features
-(ResNeSt's split attention: GAP -> fc1 -> BN over the frames; the head's BN-free layers then carry
-it) normalises differences of that size and amplifies any rounding of its inputs ~100x.  There the
-train-mode drift is a property of the bf16 contract itself, not of the kernels: the CPU float
-emulation of the contract is 5e-2 from the fp32 oracle at C4's geometry on noise frames, and the
-HIP bf16 path 1e-1 (two independent roundings of a chaotic map).  Noise frames are still run
-here: eval mode asserted, train mode recorded.
+Frames.  Structured synthetic frames (a random 6x6 colour field, bilinearly upsampled, plus pixel
+noise of sigma 20) differ in their global statistics, as video frames do.  On frames of i.i.d.
+uniform pixel noise (the benchmark's data) every frame has the same global statistics to ~1%, so a
+batch-statistic BatchNorm over per-frame pooled features (ResNeSt's split attention: GAP -> fc1 ->
+BN over the frames; the head's BN-free layers then carry it) normalises differences of that size
+and amplifies any rounding of its inputs ~100x.  There the train-mode drift is a property of the
+bf16 contract itself, not of the kernels: the CPU float emulation of the contract is 5e-2 from the
+fp32 oracle at C4's geometry on noise frames, and the HIP bf16 path 1e-1 (two independent roundings
+of a chaotic map), which the e_sens term bounds.  Every case is asserted.
+The gradients: tests/test_bf16_grads_gpu.py.
 
 Why train mode drifts at all.  A randomly initialised deep network with batch-statistic BatchNorm
 is chaotic in its forward map (each BN re-normalises the perturbation along with the signal):
@@ -58,7 +63,10 @@ pytestmark = pytest.mark.gpu
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
 
 LOGIT_TOL = 2e-2      # relative to max|logit| of the fp32 result
-EMU_RATIO = 1.25      # small geometry: bound = max(LOGIT_TOL, EMU_RATIO x the contract's own drift)
+EMU_RATIO = 1.25      # small geometry: bound = max(LOGIT_TOL, EMU_RATIO x the contract's own drift,
+SENS_RATIO = 2.0      #   |emu64 - fp32| + SENS_RATIO x |emu32 - emu64|)
+XB_RATIO = 4.0        # full size, noise frames, train: within XB_RATIO x the fp32 step's own drift
+                      # when only its input frames are rounded to bf16
 FULL_TRAIN_TOL = 6e-2  # full-size train mode (batch statistics), structured frames
 
 
@@ -90,17 +98,14 @@ def structured_frames(n, seed):
     return img.clamp(0, 255).round().to(torch.uint8).permute(0, 2, 3, 1).contiguous()
 
 
-def _check(name, out16, out32, bound, extra=None, enforce=True):
+def _check(name, out16, out32, bound, extra=None):
     rel, sure, same = _agreement(out16, out32, bound)
     rec = {"rel_max_diff": rel, "bound": bound, "clips": int(same.numel()),
            "sure_clips": int(sure.sum()), "argmax_agree_sure": int(same[sure].sum()),
            "argmax_agree_all": int(same.sum()),
            "max_abs_logit": out32.detach().abs().max().item()}
     rec.update(extra or {})
-    rec["asserted"] = enforce
     _record(name, rec)
-    if not enforce or os.environ.get("TMR_RECORD_ONLY"):
-        return rec
     assert rel <= bound, rec
     assert bool(same[sure].all()), rec
     return rec
@@ -144,8 +149,20 @@ def test_bf16_vs_fp32_oracle(dev, geo, train, frames_kind):
     with torch.no_grad():
         out_e = r16(x_ref, lt, masks=masks)
     e_emu, _, same_e = _agreement(out_e, out_r)
-    extra = {"emu_rel_max_diff": e_emu, "emu_argmax_agree_all": int(same_e.sum())}
-    bound = max(LOGIT_TOL, EMU_RATIO * e_emu)
+    # ... and how far the contract's own rounding ties move it: the emulation with exact (float64)
+    # accumulation against the fp32 emulation.  The HIP kernels accumulate in fp32 in another
+    # order, so they may sit up to SENS_RATIO x that far from the exact contract:
+    # |hip - fp32| <= |emu64 - fp32| + SENS_RATIO * |emu32 - emu64|
+    import copy
+    r64 = copy.deepcopy(r16).double()
+    with torch.no_grad():
+        out_e64 = r64(x_ref.double(), lt.double(),
+                      masks={k: v.double() for k, v in masks.items()} if masks else None)
+    e_sens, _, _ = _agreement(out_e, out_e64)
+    e64, _, _ = _agreement(out_e64, out_r)
+    extra = {"emu_rel_max_diff": e_emu, "emu_argmax_agree_all": int(same_e.sum()),
+             "emu64_rel_max_diff": e64, "emu32_vs_emu64": e_sens}
+    bound = max(LOGIT_TOL, EMU_RATIO * e_emu, e64 + SENS_RATIO * e_sens)
     if train:
         # the bf16 step's gradients against the fp32 reference's, recorded (informative: at
         # random init with 20-60 frames per BN batch the trunk gradients are ill-conditioned,
@@ -158,8 +175,7 @@ def test_bf16_vs_fp32_oracle(dev, geo, train, frames_kind):
         extra["grad_rel_l2"] = {n: e for n, e in rows_}
         head = [e for n, e in rows_ if not n.startswith("share")]
         extra["grad_rel_l2_head_max"] = max(head)
-    _check("%s_%s_%s" % (geo, "train" if train else "eval", frames_kind), out, out_r, bound, extra,
-           enforce=not (train and frames_kind == "noise"))
+    _check("%s_%s_%s" % (geo, "train" if train else "eval", frames_kind), out, out_r, bound, extra)
 
 
 def _full_inputs(dev, B, T, L, frames_kind):
@@ -192,9 +208,10 @@ def test_bf16_vs_fp32_full_size(dev, geo, frames_kind):
     outs = {}
     torch.manual_seed(0)
     sd = None
-    for prec in ("fp32", "bf16"):
-        m = tmrnet_amd.resnet_lstm(seq_len=T, precision=prec, backbone=backbone, time_conv=tc)
+    for prec in ("fp32", "bf16", "fp32xb"):
+        m = tmrnet_amd.resnet_lstm(seq_len=T, precision=prec[:4], backbone=backbone, time_conv=tc)
         m = m.to(dev)
+        xin = x4.to(torch.bfloat16).float() if prec == "fp32xb" else x4
         if sd is None:
             sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
         else:
@@ -202,11 +219,17 @@ def test_bf16_vs_fp32_full_size(dev, geo, frames_kind):
         m.nl_block.forced_mask = masks["nl"].to(dev)
         m.forced_head_mask = masks["head"].to(dev)
         with torch.no_grad():
-            outs[prec, "train"] = m.train()(x4, lfb).cpu()
-            outs[prec, "eval"] = m.eval()(x4, lfb).cpu()
+            outs[prec, "train"] = m.train()(xin, lfb).cpu()
+            outs[prec, "eval"] = m.eval()(xin, lfb).cpu()
         del m
         torch.cuda.empty_cache()
     for mode in ("train", "eval"):
+        e_xb, _, _ = _agreement(outs["fp32xb", mode], outs["fp32", mode])
+        bound = LOGIT_TOL if mode == "eval" else FULL_TRAIN_TOL
+        if mode == "train" and frames_kind == "noise":
+            # i.i.d.-noise frames: batch-statistic BN over near-identical frames amplifies any
+            # rounding (module doc); the bound scales with what rounding the fp32 step's input
+            # frames to bf16 alone does to it
+            bound = max(bound, XB_RATIO * e_xb)
         _check("%s_full_%s_%s" % (geo, mode, frames_kind), outs["bf16", mode], outs["fp32", mode],
-               FULL_TRAIN_TOL if mode == "train" else LOGIT_TOL,
-               enforce=not (mode == "train" and frames_kind == "noise"))
+               bound, {"fp32_bf16_input_rel_max_diff": e_xb})

@@ -102,7 +102,12 @@ __device__ __forceinline__ void unpack_old8(const GemmArgs& a, const uint4& c0, 
 #ifndef TMR_EPI_DEPTH
 #define TMR_EPI_DEPTH 3
 #endif
-template <int BM, int BN, int WM, int WN, int SMEMB>
+// rows in flight of the 8-wave tiles' epilogue, loads issued after the main loop (0: their
+// one-row-at-a-time epilogue_lds_bnbwd; 1-2 spill at the 128-VGPR budget of those tiles)
+#ifndef TMR_EPI_LATE
+#define TMR_EPI_LATE 0
+#endif
+template <int BM, int BN, int WM, int WN, int SMEMB, int DEPTH = TMR_EPI_DEPTH>
 struct LdsBnbwd {
   static constexpr int NT = 64 * WM * WN;
   static constexpr int LDC = BN + 4;                   // padded fp32 row of the staged tile
@@ -116,7 +121,7 @@ struct LdsBnbwd {
   static constexpr int NCH = (BM + RCH - 1) / RCH;
   static constexpr int PC = (RCH + RPP - 1) / RPP;     // row slots of a thread per chunk
   static constexpr int NR = NCH * PC;                  // row slots of a thread
-  static constexpr int D = NR < TMR_EPI_DEPTH ? NR : TMR_EPI_DEPTH;   // rows in flight
+  static constexpr int D = NR < DEPTH ? NR : DEPTH;   // rows in flight
   static_assert(NT % CG == 0, "epilogue row partition");
 
   struct In {         // one row's global operands as loaded
@@ -487,9 +492,14 @@ void gemm16_kernel(const GemmArgs a) {
   using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
   constexpr int EPI = WM * BN * 2 * 4;
   static_assert(NST == 2 || (NST == 1 && MODE != MODE_WGRAD && PRO == 0), "one-stage form: FWD / DGRAD");
-  constexpr int LDSNEED = MODE == MODE_DGRAD ? (BN + 4) * (BM / WM) * 4 : 0;
+  // the DGRAD view's LDS-staged BN-backward epilogue stages the whole tile at once where it fits
+  // 70 KB (every dgrad tile but 256x256: a few KB over the two k-tile stages), so the
+  // accumulators are dead before its global loads start; else whole wave row-blocks per chunk
+  constexpr int LDSROWB = (BN + 4) * (BM / WM) * 4, LDSFULL = (BN + 4) * BM * 4;
+  constexpr int LDSNEED = MODE != MODE_DGRAD ? 0 : (LDSFULL <= 70 * 1024 ? LDSFULL : LDSROWB);
   constexpr int SMEM1 = STAGE > EPI ? (STAGE > LDSNEED ? STAGE : LDSNEED) : (EPI > LDSNEED ? EPI : LDSNEED);
-  constexpr int SMEM = NST == 1 ? SMEM1 : (2 * STAGE > EPI ? 2 * STAGE : EPI);
+  constexpr int SMEM2 = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  constexpr int SMEM = NST == 1 ? SMEM1 : (SMEM2 > LDSNEED ? SMEM2 : LDSNEED);
   static_assert(PRO == 0 || F32, "operand prologues: fp32 form only");
   static_assert(!(PRO & 1) || MODE != MODE_DGRAD, "X prologue: FWD / WGRAD views");
   static_assert(!(PRO & 2) || MODE != MODE_FWD, "dY prologue: DGRAD / WGRAD views");
@@ -809,12 +819,14 @@ void gemm16_kernel(const GemmArgs a) {
   // the LDS-staged BN-backward epilogue (whole wave row-blocks of (BM / WM) padded rows must fit:
   // all configs but 256x256, which the dgrad tile rules never pick): its first rows' global
   // operands are loaded now and land under the main loop
-  constexpr bool LDSEPI = MODE == MODE_DGRAD && (BN + 4) * (BM / WM) * 4 <= SMEM;
-  // prefetching form (LdsBnbwd) on the 4-wave tiles; the 8/16-wave ones (128-VGPR budget) keep
-  // epilogue_lds_bnbwd
+  constexpr bool LDSEPI = MODE == MODE_DGRAD && LDSROWB <= SMEM;
+  // prefetching form (LdsBnbwd): the 4-wave tiles issue their first rows' loads before the main
+  // loop; the 8-wave ones (128-VGPR budget) right after it, two rows deep, once the whole tile is
+  // staged (their accumulators are dead by then); the 16-wave ones keep epilogue_lds_bnbwd
   constexpr bool PRE = LDSEPI && NW < 8;
-  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM>;
-  typename Epi::In pf[PRE ? Epi::D : 1];
+  constexpr bool LATE = LDSEPI && NW == 8 && LDSNEED == LDSFULL && TMR_EPI_LATE > 0;
+  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM, PRE ? TMR_EPI_DEPTH : (TMR_EPI_LATE > 0 ? TMR_EPI_LATE : 1)>;
+  typename Epi::In pf[(PRE || LATE) ? Epi::D : 1];
   if constexpr (PRE) {
     if (a.bn_part != nullptr) Epi::prefetch(a, m0, n0, pf);
   }
@@ -945,9 +957,12 @@ void gemm16_kernel(const GemmArgs a) {
 
   if constexpr (LDSEPI) {
     if (a.bn_part != nullptr) {   // (the only form that reads mask-3 bits: launch_gemm16_t)
-      if constexpr (PRE)
+      if constexpr (PRE) {
         Epi::run(a, acc, reinterpret_cast<float*>(smem), m0, n0, pf);
-      else
+      } else if constexpr (LATE) {
+        Epi::prefetch(a, m0, n0, pf);
+        Epi::run(a, acc, reinterpret_cast<float*>(smem), m0, n0, pf);
+      } else
         epilogue_lds_bnbwd<BM, BN, WM, WN, TM, TN>(a, acc, reinterpret_cast<float*>(smem), SMEM / 4,
                                                     m0, n0);
       return;
