@@ -11,11 +11,9 @@ TAG=${TAG:-${MODEL}_${PRECISION}_s${SEQ:-10}_l${LFB:-40}}
 BENCH_ARGS="${BENCH_ARGS} --seq ${SEQ:-10} --lfb ${LFB:-40}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-# Profiled runs take the LSTM's per-step path (TMR_LSTM_PERSIST=0): with the persistent
-# (cooperative) LSTM launch, the HIP runtime's exit handler faults in a torn-down HSA runtime after
-# rocprofv3 has finalized (scripts/exit_probe.py, profiles/r3/exit_probe/); every other kernel is
-# the same as in the unprofiled step.
-export TMR_LSTM_PERSIST=0
+# Profiled runs take the benchmarked step's persistent LSTM (round 5: a plain launch after an
+# occupancy check; the cooperative launch of rounds 2-4 made the process fault at exit under
+# rocprofv3, profiles/r3/exit_probe/, so those profiles used the per-step path).
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/$C" -o run -- \
     python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-roofline --model $MODEL --precision $PRECISION ${BENCH_ARGS} \

@@ -7,9 +7,7 @@ mkdir -p "$OUT"
 python3 -c "import sys; sys.path.insert(0, '$R/scripts'); import pmc_summary as p; print(p.lib_sha('$R/tmrnet_amd/libtmr.so'))" > "$OUT/build_sha.txt"
 cd /tmp && export TMPDIR=/tmp
 export TMR_EXIT_MAPS="$OUT/exit_maps.txt"
-# the LSTM's per-step path under the profiler (see scripts/pmc.sh: the cooperative launch makes the
-# HIP runtime fault at exit after rocprofv3 finalizes); TMR_LSTM_PERSIST=1 profiles it anyway
-export TMR_LSTM_PERSIST=${TMR_LSTM_PERSIST:-0}
+# (the benchmarked step's persistent LSTM included: see scripts/pmc.sh)
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
   python3 "$R/bench.py" --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$OUT/bench.log" 2>&1
 rc=$?

@@ -979,9 +979,13 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   // (bit-identical to the two-stage form, which it replaced in round 4).  56x56 64->64: 0.427 ->
   // 0.378 ms; the DGRAD view measured slower in it (its 233-VGPR LDS-staged epilogue caps the
   // occupancy at two workgroups anyway; profiles/r4/nst1/)
+  // (fp32, round 5: the same forms for K <= 64 / 128 / 256, two to eight k-tiles serialised
+  // through the one stage, measured no faster: C2 forward family 47.1 -> 46.9 / 47.2 / 47.7 ms,
+  // profiles/r5/nst1_f32/; not taken)
+  constexpr int kmax = 64;
   if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && WM * WN == 4 &&
                 ((BM == 128 && BN == 128) || (BM == 256 && BN == 64))) {
-    if (!tapv && a.K > 0 && a.K <= 64) {
+    if (!tapv && a.K > 0 && a.K <= kmax) {
       hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, 0, 1>), grid, blk, 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage)");
       return 0;
@@ -993,7 +997,7 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   // the other's loads.  Same BM (the statistics' part rows), same per-wave tiles: bit-identical to
   // the 256x256 launch it replaced.
   if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && BM == 256 && BN == 256) {
-    if (!tapv && a.K > 0 && a.K <= 64) {
+    if (!tapv && a.K > 0 && a.K <= kmax) {
       const dim3 g2((unsigned)(cdiv(a.M, 256) * cdiv(a.N, 128)), grid.y, 1);
       hipLaunchKernelGGL((gemm16_kernel<MODE, 256, 128, 4, 2, 0, 1, F32, 0, 1>), g2, dim3(512), 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage, 256x128)");

@@ -12,9 +12,11 @@
 // steps, in registers -- and clips 16*by..16*by+15; 64 x ceil(b/16) workgroups, one per CU.  Consecutive steps
 // hand h_t (forward) / dgates_t (backward) between workgroups behind a grid barrier: write-through
 // (sc1) stores, one monotonic counter, sc1 loads (every spin bounded; a give-up sets the timeout
-// word).  The launch is cooperative, so
-// a grid that is not fully resident is refused at launch instead of deadlocking; it then falls
-// back to the per-step path (one gate GEMM + one cell kernel per step).
+// word).  The launch happens only when the whole grid fits the device at once (occupancy query x
+// compute units, resident()); otherwise, or if the launch fails, the per-step path runs (one gate
+// GEMM + one cell kernel per step).  A plain launch, not hipLaunchCooperativeKernel: the same
+// residency rule, and a process that made a cooperative launch faulted in an exit handler under
+// rocprofv3 (profiles/r3/exit_probe/), which kept the profiled step off this kernel.
 #include "common.h"
 #include "tmr.h"
 
@@ -318,6 +320,19 @@ __global__ void copy_k(const float* __restrict__ a, float* __restrict__ o, int n
   if (i < n) o[i] = a[i];
 }
 
+// every workgroup of `grid` resident at once on this device (no other work assumed): the
+// condition of a grid barrier that cannot deadlock
+bool resident(const void* kernel, dim3 grid, int threads) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return (long)per * cus >= (long)grid.x * grid.y;
+}
+
 // TMR_LSTM_PERSIST=0 forces the per-step path (tests exercise both; read per call, no state)
 bool persist_allowed() {
   const char* v = getenv("TMR_LSTM_PERSIST");
@@ -404,12 +419,12 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
     dim3 grid(LH / HU, cdiv(b, BBC));
     const float* gxc = gx;
     unsigned lim = spin_limit();
-    void* args[] = {(void*)&gxc, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&hn,
-                    (void*)&cn, (void*)&b, (void*)&t, (void*)&sync, (void*)&lim};
-    hipError_t e = hipLaunchCooperativeKernel((const void*)lstm_rec_fwd_k, grid, dim3(256), args,
-                                              0, stream);
-    if (e == hipSuccess) return 0;
-    (void)hipGetLastError();   // not resident (cooperative check): per-step path below
+    if (resident((const void*)lstm_rec_fwd_k, grid, 256)) {
+      hipLaunchKernelGGL(lstm_rec_fwd_k, grid, dim3(256), 0, stream, gxc, w_hh, y, cs, acts, hn, cn,
+                         b, t, sync, lim);
+      if (hipGetLastError() == hipSuccess) return 0;
+    }
+    // not resident: per-step path below
   }
   // per-step path: gate GEMM + fused cell kernel per step
   float* ghh = (float*)(w + L.ghh);
@@ -473,12 +488,11 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
   if (persist_allowed() && lstm_persistent_shape(b, t, h)) {
     dim3 grid(LH / HU, cdiv(b, BBC));
     unsigned lim = spin_limit();
-    void* args[] = {(void*)&dy, (void*)&w_hh, (void*)&y, (void*)&cs, (void*)&acts, (void*)&dg,
-                    (void*)&hprev, (void*)&b, (void*)&t, (void*)&sync, (void*)&lim};
-    hipError_t e = hipLaunchCooperativeKernel((const void*)lstm_rec_bwd_k, grid, dim3(256), args,
-                                              0, stream);
-    if (e == hipSuccess) done = true;
-    else (void)hipGetLastError();
+    if (resident((const void*)lstm_rec_bwd_k, grid, 256)) {
+      hipLaunchKernelGGL(lstm_rec_bwd_k, grid, dim3(256), 0, stream, dy, w_hh, y, cs, acts, dg,
+                         hprev, b, t, sync, lim);
+      done = hipGetLastError() == hipSuccess;
+    }
   }
   if (!done) {
     float* dcp[2] = {(float*)(w + L.dcp), (float*)(w + L.dcp) + (size_t)b * h};
