@@ -608,6 +608,47 @@ def test_bn_fold_bit_identical(dev, engine):
         assert torch.equal(res[True][2][n], res[False][2][n]), n
 
 
+def test_bn_fold16_bit_identical(dev):
+    """The bf16 form (trunk.FOLD16, round 5): under the bf16-activation step the relu(bn1) /
+    relu(bn2) outputs are never written -- conv2 / conv3 read the bf16 pre-BN y through the bf16
+    X-operand prologue of the LDS-DMA engine, forward and wgrad views -- against the explicit
+    bn_apply8_a16 passes: the same rounded operand values by construction, so logits, every
+    gradient and the running statistics bit-identical.  A/B build only (make PROLOGUES=1;
+    TMR_LIB_PATH=tmrnet_amd/libtmr_pro.so), skipped on the product library."""
+    import tmrnet_amd
+    from tmrnet_amd import trunk, _lib
+    if not _lib.has_prologues():
+        pytest.skip("operand prologues: A/B build only (make PROLOGUES=1, TMR_LIB_PATH)")
+    B, T, L = 2, 5, 7
+    g = torch.Generator().manual_seed(4)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)
+    lt = (torch.rand(B, L, 512, generator=g) * 2 - 1).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=g).to(dev)
+    res = {}
+    saved = trunk.FOLD16
+    try:
+        for fold in (True, False):
+            trunk.FOLD16 = fold
+            torch.manual_seed(0)
+            m = tmrnet_amd.resnet_lstm(seq_len=T, precision="bf16").to(dev).train()
+            m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+            m.forced_head_mask = torch.ones(B, 512, device=dev)
+            x4 = ops.crop_normalize(frames, off, T)
+            out = m(x4, lt)
+            tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels).backward()
+            torch.cuda.synchronize()
+            res[fold] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                         {n: b.clone() for n, b in m.named_buffers()})
+    finally:
+        trunk.FOLD16 = saved
+    assert torch.equal(res[True][0], res[False][0])
+    for n in res[True][1]:
+        assert torch.equal(res[True][1][n], res[False][1][n]), n
+    for n in res[True][2]:
+        assert torch.equal(res[True][2][n], res[False][2][n]), n
+
+
 def _pack_bits(m):
     """(numel,) bool -> int32 words, element e = bit e % 32 of word e // 32."""
     m = m.reshape(-1).to(torch.int64)

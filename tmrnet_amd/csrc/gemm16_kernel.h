@@ -491,7 +491,8 @@ void gemm16_kernel(const GemmArgs a) {
   constexpr int CPRA = BM * (int)ES / 16, CPRB = BN * (int)ES / 16;
   using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
   constexpr int EPI = WM * BN * 2 * 4;
-  static_assert(NST == 2 || (NST == 1 && MODE != MODE_WGRAD && PRO == 0), "one-stage form: FWD / DGRAD");
+  static_assert(NST == 2 || (NST == 1 && MODE != MODE_WGRAD && (PRO & 2) == 0),
+                "one-stage form: FWD / DGRAD, no dY prologue");
   // the DGRAD view's LDS-staged BN-backward epilogue stages the whole tile at once where it fits
   // 70 KB (every dgrad tile but 256x256: a few KB over the two k-tile stages), so the
   // accumulators are dead before its global loads start; else whole wave row-blocks per chunk
@@ -500,7 +501,7 @@ void gemm16_kernel(const GemmArgs a) {
   constexpr int SMEM1 = STAGE > EPI ? (STAGE > LDSNEED ? STAGE : LDSNEED) : (EPI > LDSNEED ? EPI : LDSNEED);
   constexpr int SMEM2 = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   constexpr int SMEM = NST == 1 ? SMEM1 : (SMEM2 > LDSNEED ? SMEM2 : LDSNEED);
-  static_assert(PRO == 0 || F32, "operand prologues: fp32 form only");
+  static_assert(PRO == 0 || F32 || PRO == 1, "operand prologues: the bf16 form takes the X prologue only");
   static_assert(!(PRO & 1) || MODE != MODE_DGRAD, "X prologue: FWD / WGRAD views");
   static_assert(!(PRO & 2) || MODE != MODE_FWD, "dY prologue: DGRAD / WGRAD views");
   // prologue regions after the stages / epilogue buffer: dY's y image (one stage: each lane reads
@@ -754,8 +755,6 @@ void gemm16_kernel(const GemmArgs a) {
 #pragma unroll
       for (int q = 0; q < NX; ++q) {
         unsigned char* img = MODE == MODE_FWD ? As : Bs;
-        float4* p = reinterpret_cast<float4*>(img + 1024 * (wave + NW * q) + 16 * lane);
-        const float4 v = *p;
         int c;
         bool ok;
         if constexpr (MODE == MODE_FWD) {
@@ -765,14 +764,40 @@ void gemm16_kernel(const GemmArgs a) {
           c = (int)(bco[q] / ES);
           ok = pokB[q];
         }
-        const float4 sc = *reinterpret_cast<const float4*>(xcoef + c);
-        const float4 sh = *reinterpret_cast<const float4*>(xcoef + PRO_XMAX + c);
-        float4 o;
-        o.x = fmaxf(fmaf(v.x, sc.x, sh.x), 0.f);
-        o.y = fmaxf(fmaf(v.y, sc.y, sh.y), 0.f);
-        o.z = fmaxf(fmaf(v.z, sc.z, sh.z), 0.f);
-        o.w = fmaxf(fmaf(v.w, sc.w, sh.w), 0.f);
-        *p = ok ? o : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (F32) {
+          float4* p = reinterpret_cast<float4*>(img + 1024 * (wave + NW * q) + 16 * lane);
+          const float4 v = *p;
+          const float4 sc = *reinterpret_cast<const float4*>(xcoef + c);
+          const float4 sh = *reinterpret_cast<const float4*>(xcoef + PRO_XMAX + c);
+          float4 o;
+          o.x = fmaxf(fmaf(v.x, sc.x, sh.x), 0.f);
+          o.y = fmaxf(fmaf(v.y, sc.y, sh.y), 0.f);
+          o.z = fmaxf(fmaf(v.z, sc.z, sh.z), 0.f);
+          o.w = fmaxf(fmaf(v.w, sc.w, sh.w), 0.f);
+          *p = ok ? o : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          // bf16 piece: 8 channels c .. c + 7 of the stored pre-BN y; relu(fmaf(y, sc, sh))
+          // rounded RNE -- bn_apply8_a16_k's arithmetic, so the operand equals the z it would
+          // have stored
+          uint4* p = reinterpret_cast<uint4*>(img + 1024 * (wave + NW * q) + 16 * lane);
+          const uint4 v = *p;
+          const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+          uint32_t w[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float4 sc = *reinterpret_cast<const float4*>(xcoef + c + 4 * h);
+            const float4 sh = *reinterpret_cast<const float4*>(xcoef + PRO_XMAX + c + 4 * h);
+            const float o0 = fmaxf(fmaf(__uint_as_float(u[2 * h] << 16), sc.x, sh.x), 0.f);
+            const float o1 = fmaxf(fmaf(__uint_as_float(u[2 * h] & 0xffff0000u), sc.y, sh.y), 0.f);
+            const float o2 = fmaxf(fmaf(__uint_as_float(u[2 * h + 1] << 16), sc.z, sh.z), 0.f);
+            const float o3 = fmaxf(fmaf(__uint_as_float(u[2 * h + 1] & 0xffff0000u), sc.w, sh.w), 0.f);
+            typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+            const bf16x2_t lo = {(__bf16)o0, (__bf16)o1}, hi = {(__bf16)o2, (__bf16)o3};
+            w[2 * h] = __builtin_bit_cast(uint32_t, lo);
+            w[2 * h + 1] = __builtin_bit_cast(uint32_t, hi);
+          }
+          *p = ok ? make_uint4(w[0], w[1], w[2], w[3]) : make_uint4(0u, 0u, 0u, 0u);
+        }
       }
     }
   };
@@ -928,6 +953,7 @@ void gemm16_kernel(const GemmArgs a) {
       if (kt > 0) __syncthreads();   // every wave's reads of tile kt - 1 done
       stage(kt, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (PRO != 0) transform(0);
       __syncthreads();
       compute(0);
     }
@@ -983,10 +1009,10 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   // through the one stage, measured no faster: C2 forward family 47.1 -> 46.9 / 47.2 / 47.7 ms,
   // profiles/r5/nst1_f32/; not taken)
   constexpr int kmax = 64;
-  if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && WM * WN == 4 &&
+  if constexpr (MODE == MODE_FWD && (PRO & 2) == 0 && F32 == 0 && WM * WN == 4 &&
                 ((BM == 128 && BN == 128) || (BM == 256 && BN == 64))) {
     if (!tapv && a.K > 0 && a.K <= kmax) {
-      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, 0, 1>), grid, blk, 0, st, a);
+      hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, PRO, 1>), grid, blk, 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage)");
       return 0;
     }
@@ -996,10 +1022,10 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   // (one 16-wave 256x256 workgroup fills the register file), so one's epilogue stores overlap
   // the other's loads.  Same BM (the statistics' part rows), same per-wave tiles: bit-identical to
   // the 256x256 launch it replaced.
-  if constexpr (MODE == MODE_FWD && PRO == 0 && F32 == 0 && BM == 256 && BN == 256) {
+  if constexpr (MODE == MODE_FWD && (PRO & 2) == 0 && F32 == 0 && BM == 256 && BN == 256) {
     if (!tapv && a.K > 0 && a.K <= kmax) {
       const dim3 g2((unsigned)(cdiv(a.M, 256) * cdiv(a.N, 128)), grid.y, 1);
-      hipLaunchKernelGGL((gemm16_kernel<MODE, 256, 128, 4, 2, 0, 1, F32, 0, 1>), g2, dim3(512), 0, st, a);
+      hipLaunchKernelGGL((gemm16_kernel<MODE, 256, 128, 4, 2, 0, 1, F32, PRO, 1>), g2, dim3(512), 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage, 256x128)");
       return 0;
     }
@@ -1047,7 +1073,7 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                 "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
   const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32, a.pro);
   const Cfg16 c = kCfgs16[cfg];
-  TMR_CHECK_ARG(!a.pro || (f32 && pro32_ok(a, MODE)),
+  TMR_CHECK_ARG(!a.pro || (f32 ? pro32_ok(a, MODE) : pro16_ok(a, MODE)),
                 "gemm (LDS-DMA path): operand prologue %d not supported here (view %d)", a.pro, MODE);
   // ReLU-mask bits are read by the LDS-staged BN-backward epilogue only (every dgrad tile but
   // 256x256, whose wave row-blocks do not fit the staging buffer)
@@ -1073,6 +1099,12 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
 #if TMR_PROLOGUES
+  if constexpr (F32 == 0) {   // bf16: the X prologue, FWD / WGRAD (pro16_ok)
+    if (a.pro) {
+      if constexpr (MODE == MODE_DGRAD) return -1;
+      else return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
+    }
+  }
   if constexpr (F32 != 0) {
     // prologue variants (fp32 only, A/B build): FWD X, DGRAD dY, WGRAD dY / dY + X
     if (a.pro) {

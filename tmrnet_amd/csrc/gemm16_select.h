@@ -53,9 +53,17 @@ inline bool use32(const GemmArgs& a, int mode) {
   return a.lds % 4 == 0 && a.ldb % 4 == 0 && a.log2C >= 2 && (a.ntaps != 1 || a.K % 4 == 0);
 }
 
+// bf16 form (A/B build, round 5): the X prologue only (relu(bn) of the operand, rounded to bf16 as
+// the BN pass would store it), one tap per 64-element k-tile, 8-channel pieces
+inline bool pro16_ok(const GemmArgs& a, int mode) {
+  if (!a.pro) return true;
+  if (a.pro != 1 || mode == MODE_DGRAD || a.lds > PRO_XMAX || a.lds % 8) return false;
+  return mode == MODE_WGRAD || a.ntaps == 1 || a.log2C >= 6;
+}
+
 inline bool use16(const GemmArgs& a, int mode) {
   if (a.prec == TMR_MATH_F32) return use32(a, mode);
-  if (a.prec != TMR_MATH_BF16 || a.sab != 3 || a.pro) return false;
+  if (a.prec != TMR_MATH_BF16 || a.sab != 3 || !pro16_ok(a, mode)) return false;
   if (mode == MODE_DGRAD && !a.wt) return false;
   if (a.lds % 8) return false;
   if (mode == MODE_WGRAD) return a.M % 8 == 0 && a.log2C >= 3 && a.ldb % 8 == 0 && a.N % 8 == 0;

@@ -94,6 +94,17 @@ def _bn_momentum(bn):
 # tmrnet_amd/libtmr_pro.so (run with TMR_LIB_PATH pointing at it); the default library rejects
 # TMR_FOLD_BN=1 at the first conv.
 FOLD_BN = os.environ.get("TMR_FOLD_BN", "0") == "1"
+# The bf16 form (round 5, same A/B build, TMR_FOLD16=1): under the bf16-activation step the relu(bn)
+# outputs of each Bottleneck's bn1 / bn2 are never written -- conv2 / conv3 read the bf16 pre-BN y
+# through the bf16 X-operand prologue of the LDS-DMA engine (relu(fmaf(y, scale, shift)) rounded
+# RNE: bn_apply8_a16_k's arithmetic, so bit-identical), forward and wgrad views.  Not for an input
+# the direct 3x3 kernels read (direct3.hip: ResNet-50 layer1's 56x56 64 -> 64 conv2).
+FOLD16 = os.environ.get("TMR_FOLD16", "0") == "1"
+
+
+def _direct3_input(blk, h):
+    """The direct 3x3 kernel (direct3.hip d3_shape) serves conv2 of this block at input width h."""
+    return tuple(blk.conv2.weight.shape) == (64, 64, 3, 3) and blk.stride == 1 and h == 56
 
 # bf16 math (configs C4/C5): the tensors consumed only as conv operands -- the KRSC weights, the
 # BN+ReLU outputs of each Bottleneck's first two units, every BatchNorm-backward output dy -- are
@@ -387,10 +398,12 @@ class TrunkFn(torch.autograd.Function):
             for blk in layer:
                 brec = [] if keep else None
                 fold = training and FOLD_BN
+                fd16 = a16 and FOLD16
                 z1 = _conv_bn(hx, blk.conv1, blk.bn1, 1, 0, True, training, recs=brec, math=mt,
-                              nbt=nbt, defer=fold)
+                              nbt=nbt,
+                              defer=fold or (fd16 and not _direct3_input(blk, hx.shape[2])))
                 z2 = _conv_bn(z1, blk.conv2, blk.bn2, blk.stride, 1, True, training, recs=brec,
-                              math=mt, nbt=nbt, defer=fold)
+                              math=mt, nbt=nbt, defer=fold or fd16)
                 if blk.downsample is not None:
                     # train: the branch's BN is applied inside the BN3 pass (bn_apply2)
                     idn = _conv_bn(hx, blk.downsample[0], blk.downsample[1], blk.stride, 0, False,
