@@ -310,3 +310,4 @@ def test_tmrnet_muticonv_parity(dev):
     out_r = r(ref.crop_normalize_ref(frames, off, T).view(B, T, 3, 224, 224), lt)
     assert (out.detach().cpu() - out_r.detach()).abs().max().item() < 1e-4
     assert torch.equal(out.detach().cpu().argmax(1), out_r.argmax(1))
+
