@@ -114,11 +114,13 @@ inline int pick_cfg16_base(long M, long N, long K, int mode, bool f32) {
   if (mode == MODE_WGRAD) {
     if (M <= 64) cfg = N <= 64 ? 5 : (N >= 512 ? 4 : 2);
     else if (N <= 64) cfg = 3;
-    // short reductions (layer3/4 spatial): 4x the tiles of 256x256 at the same occupancy, so
-    // fewer split-K slabs to write and reduce
-    else if (M >= 256 && N >= 256 && K <= 131072) cfg = 7;
-    else if (M >= 256 && M <= 512 && N >= 256) cfg = 6;
-    else cfg = 2;
+    // round 5 (profiles/r5/tile_rules/): 128x128 as 8 waves, or 256x256 as 16 waves for the wide
+    // wgrads (N >= 1024: 3x3, 1024-channel inputs) while each of the ~512 / tiles split-K slices
+    // still reduces >= 4096 rows; shorter slices (layer3/4 spatial at 640 frames, the grouped
+    // split-attention convs one group at a time) spend the 256x256 tile's time on its prologue and
+    // its 256 KB slab.  Replaced the round-2 rule (128x128 4-wave / 256x256 by M and K): C5 wgrads
+    // -1.1 ms, C4 -0.4 ms per step.
+    else cfg = (M >= 256 && N >= 1024 && K * cfg16_tiles(M, N, 6) >= (1L << 21)) ? 6 : 7;
   } else if (N <= 64) {
     cfg = M >= 256 ? 3 : 5;
   } else if (mode == MODE_FWD && N >= 256 && M >= 256) {
@@ -126,7 +128,9 @@ inline int pick_cfg16_base(long M, long N, long K, int mode, bool f32) {
   } else {
     cfg = 2;
   }
-  if (mode != MODE_WGRAD && cfg16_tiles(M, N, cfg) < 256) {
+  // too few tiles to fill the 256 CUs: smaller tiles -- except the fp32 256x256 forwards at >= 224
+  // tiles (layer4 at 640 frames: 246), which measured 4-6% faster than 492 256x128 tiles (round 5)
+  if (mode != MODE_WGRAD && cfg16_tiles(M, N, cfg) < (f32 && cfg == 6 ? 224 : 256)) {
     for (const int c2 : {1, 2, 5}) {
       if ((long)kCfgs16[c2].bm * kCfgs16[c2].bn >= (long)kCfgs16[cfg].bm * kCfgs16[cfg].bn ||
           cfg16_tiles(M, N, c2) <= cfg16_tiles(M, N, cfg))
