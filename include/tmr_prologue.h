@@ -25,7 +25,9 @@ extern "C" {
  *     relu, train_only_non-local_pretrained.py:210-213), whose output z = relu(bn(y)) then never
  *     exists: the consumer conv reads y.  Identical values to tmr_bn_apply(y, ..., relu = 1).
  *   dy_y/dy_coef: the dY operand (dgrad and wgrad output gradient) is read as
- *     A[k]*g + B[k]*y + C[k] (fmaf(A, g, fmaf(B, y, C))), g = the ReLU-masked gradient at this
+ *     A[k]*g + B[k]*y + C[k] (fmaf(A, g, fmaf(B, y, C))) -- with bf16 math on the LDS-DMA engine
+ *     g and y are bf16 (dY's element type) and the result is rounded RNE, as
+ *     tmr_bn_bwd_parts_g16 stores dy --, g = the ReLU-masked gradient at this
  *     conv's BatchNorm output, y = this conv's pre-BN output, coef = [3][k] from
  *     tmr_bn_bwd_coefs(_dense) -- the BatchNorm backward, whose dy then never exists.  Identical
  *     values to the apply pass of tmr_bn_bwd_parts.
@@ -46,6 +48,14 @@ int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy, const fl
                                const float* scale, const float* shift, const float* mean,
                                int mask, void* parts, size_t parts_bytes,
                                const tmr_conv_prologue* pro, hipStream_t stream);
+/* tmr_conv2d_dgrad_bnbwd_acc with a dY-operand prologue (bf16 LDS-DMA engine: the conv1 dgrad of
+ * a Bottleneck under the bf16 residual gradient, reading bn1's g and y1) */
+int tmr_conv2d_dgrad_bnbwd_acc_pro(const tmr_conv_desc* d, const float* dy, const float* w_krsc,
+                                   void* dx, float beta, const void* dx_old, int old_bf16,
+                                   const float* y, const float* z, const float* scale,
+                                   const float* shift, const float* mean, int mask, void* parts,
+                                   size_t parts_bytes, const tmr_conv_prologue* pro,
+                                   hipStream_t stream);
 int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy, float* dw_oihw,
                          int c_real, float beta, float* ws, size_t ws_bytes,
                          const tmr_conv_prologue* pro, hipStream_t stream);
@@ -63,6 +73,12 @@ int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, const float
                            const float* shift, const float* save_mean, const float* save_invstd,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, int rows,
                            int c, int relu, void* ws, size_t ws_bytes, hipStream_t stream);
+/* The bf16-activation step's downsample BN (no ReLU, output gradient g the bf16 residual-stream
+ * gradient, y bf16): tmr_bn_bwd_g16 without its apply pass (ws >= tmr_bn_ws_bytes(rows, c)). */
+int tmr_bn_bwd_coefs_g16(const void* g, const void* y, const float* save_mean,
+                         const float* save_invstd, const float* gamma, float* coef, float* dgamma,
+                         float* dbeta, int rows, int c, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
 
 #ifdef __cplusplus
 }

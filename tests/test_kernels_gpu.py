@@ -608,11 +608,15 @@ def test_bn_fold_bit_identical(dev, engine):
         assert torch.equal(res[True][2][n], res[False][2][n]), n
 
 
-def test_bn_fold16_bit_identical(dev):
-    """The bf16 form (trunk.FOLD16, round 5): under the bf16-activation step the relu(bn1) /
+@pytest.mark.parametrize("folds", [("FOLD16",), ("FOLD16DY",), ("FOLD16", "FOLD16DY")])
+def test_bn_fold16_bit_identical(dev, folds):
+    """The bf16 forms (round 5): under the bf16-activation step (FOLD16) the relu(bn1) /
     relu(bn2) outputs are never written -- conv2 / conv3 read the bf16 pre-BN y through the bf16
-    X-operand prologue of the LDS-DMA engine, forward and wgrad views -- against the explicit
-    bn_apply8_a16 passes: the same rounded operand values by construction, so logits, every
+    X-operand prologue of the LDS-DMA engine, forward and wgrad views -- and (FOLD16DY) no
+    BatchNorm backward writes dy -- every conv whose BN output gradient g is bf16 reads g and y
+    through the bf16 dY-operand prologue, dgrad (fused BN-backward epilogues, the accumulating
+    conv1 dgrads included) and wgrad views -- against the explicit bn_apply8_a16 /
+    bn_bwd_apply8_a16 passes: the same rounded operand values by construction, so logits, every
     gradient and the running statistics bit-identical.  A/B build only (make PROLOGUES=1;
     TMR_LIB_PATH=tmrnet_amd/libtmr_pro.so), skipped on the product library."""
     import tmrnet_amd
@@ -626,10 +630,23 @@ def test_bn_fold16_bit_identical(dev):
     lt = (torch.rand(B, L, 512, generator=g) * 2 - 1).to(dev)
     labels = torch.randint(0, 7, (B,), generator=g).to(dev)
     res = {}
-    saved = trunk.FOLD16
+    saved = {f: getattr(trunk, f) for f in folds}
+    # the dY prologue really runs: count the coefficient-only BN backwards it takes
+    ncoef = [0]
+    wrapped = {n: getattr(ops, n) for n in ("bn_bwd_coefs", "bn_bwd_coefs_g16")}
+
+    def counting(fn):
+        def f(*a, **k):
+            ncoef[0] += 1
+            return fn(*a, **k)
+        return f
     try:
+        for n, fn in wrapped.items():
+            setattr(ops, n, counting(fn))
         for fold in (True, False):
-            trunk.FOLD16 = fold
+            for f in folds:
+                setattr(trunk, f, fold)
+            ncoef[0] = 0
             torch.manual_seed(0)
             m = tmrnet_amd.resnet_lstm(seq_len=T, precision="bf16").to(dev).train()
             m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
@@ -640,8 +657,14 @@ def test_bn_fold16_bit_identical(dev):
             torch.cuda.synchronize()
             res[fold] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()},
                          {n: b.clone() for n, b in m.named_buffers()})
+            # ResNet-50: bn1 x 16, bn2 x 13 (layer1's conv2 runs direct), bn3 x 15 (not the last
+            # block's: its gradient is fp32), downsample x 4
+            assert ncoef[0] == (48 if fold and "FOLD16DY" in folds else 0), ncoef[0]
     finally:
-        trunk.FOLD16 = saved
+        for f, v in saved.items():
+            setattr(trunk, f, v)
+        for n, fn in wrapped.items():
+            setattr(ops, n, fn)
     assert torch.equal(res[True][0], res[False][0])
     for n in res[True][1]:
         assert torch.equal(res[True][1][n], res[False][1][n]), n

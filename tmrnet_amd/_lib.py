@@ -178,6 +178,8 @@ PROLOGUE_SIGNATURES = {
     "tmr_conv2d_wgrad_pro": [DP, P, P, P, I, F, P, SZ, PP, P],
     "tmr_bn_bwd_coefs": [P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_coefs_dense": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
+    "tmr_conv2d_dgrad_bnbwd_acc_pro": [DP, P, P, P, F, P, I, P, P, P, P, P, I, P, SZ, PP, P],
+    "tmr_bn_bwd_coefs_g16": [P, P, P, P, P, P, P, P, I, I, P, SZ, P],
 }
 _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,

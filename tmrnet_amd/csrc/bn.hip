@@ -1435,6 +1435,27 @@ TMR_API int tmr_bn_bwd_coefs_dense(float* g, const float* y, const float* z, con
   TMR_CHECK_LAUNCH("bn_bwd_final");
   return 0;
 }
+
+// the coefficient half of tmr_bn_bwd_g16 (a unit without ReLU whose output gradient is the bf16
+// residual-stream gradient: the downsample BN of the bf16-activation step)
+TMR_API int tmr_bn_bwd_coefs_g16(const void* g, const void* y, const float* save_mean,
+                                 const float* save_invstd, const float* gamma, float* coef,
+                                 float* dgamma, float* dbeta, int rows, int c, void* ws,
+                                 size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 8 == 0 && c >= 8 && rows > 0, "tmr_bn_bwd_coefs_g16: bad shape rows=%d c=%d", rows, c);
+  TMR_CHECK_ARG(g && y && save_mean && save_invstd && coef, "tmr_bn_bwd_coefs_g16: null operand");
+  TMR_CHECK_ARG(ws && ws_bytes >= ws_need(rows, c), "tmr_bn_bwd_coefs_g16: workspace too small");
+  Plan p = make_plan(rows, c);
+  double* part = (double*)ws;
+  hipLaunchKernelGGL((bn_bwd_partial<0, false, __bf16, const __bf16>), dim3(p.nrb, p.cblocks), dim3(NT),
+                     0, stream, (const __bf16*)g, (const __bf16*)y, nullptr, nullptr, nullptr,
+                     save_mean, rows, c, p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_bwd_partial_g16");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c,
+                     save_mean, save_invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  return 0;
+}
 #endif
 
 // ---- bf16-activation forms (TMR_MATH_BF16 train step, include/tmr.h "_a16"): y, z and the

@@ -501,7 +501,6 @@ void gemm16_kernel(const GemmArgs a) {
   constexpr int SMEM1 = STAGE > EPI ? (STAGE > LDSNEED ? STAGE : LDSNEED) : (EPI > LDSNEED ? EPI : LDSNEED);
   constexpr int SMEM2 = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   constexpr int SMEM = NST == 1 ? SMEM1 : (SMEM2 > LDSNEED ? SMEM2 : LDSNEED);
-  static_assert(PRO == 0 || F32 || PRO == 1, "operand prologues: the bf16 form takes the X prologue only");
   static_assert(!(PRO & 1) || MODE != MODE_DGRAD, "X prologue: FWD / WGRAD views");
   static_assert(!(PRO & 2) || MODE != MODE_FWD, "dY prologue: DGRAD / WGRAD views");
   // prologue regions after the stages / epilogue buffer: dY's y image (one stage: each lane reads
@@ -732,7 +731,39 @@ void gemm16_kernel(const GemmArgs a) {
   auto transform = [&](int buf) {
     unsigned char* As = smem + buf * STAGE;
     unsigned char* Bs = As + ABYTES;
-    if constexpr ((PRO & 2) != 0) {   // dY = A operand (DGRAD, WGRAD)
+    if constexpr ((PRO & 2) != 0 && F32 == 0) {   // dY = A operand (DGRAD, WGRAD), bf16 pieces
+      // 8 channels c .. c + 7 of the masked gradient g and of y, both stored bf16:
+      // fmaf(A, g, fmaf(B, y, C)) rounded RNE -- bn_bwd_apply8_a16's arithmetic, so the operand
+      // equals the dy that pass would have stored
+#pragma unroll
+      for (int q = 0; q < NIA; ++q) {
+        uint4* p = reinterpret_cast<uint4*>(As + 1024 * (wave + NW * q) + 16 * lane);
+        const uint4 gw = *p;
+        const uint4 yw = *reinterpret_cast<const uint4*>(ysm + 1024 * (wave + NW * q) + 16 * lane);
+        const uint32_t gu[4] = {gw.x, gw.y, gw.z, gw.w}, yu[4] = {yw.x, yw.y, yw.z, yw.w};
+        const int c = pcA[q];
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 A4 = *reinterpret_cast<const float4*>(dcoef + c + 4 * h);
+          const float4 B4 = *reinterpret_cast<const float4*>(dcoef + PRO_DMAX + c + 4 * h);
+          const float4 C4 = *reinterpret_cast<const float4*>(dcoef + 2 * PRO_DMAX + c + 4 * h);
+          const float o0 = fmaf(A4.x, __uint_as_float(gu[2 * h] << 16),
+                                fmaf(B4.x, __uint_as_float(yu[2 * h] << 16), C4.x));
+          const float o1 = fmaf(A4.y, __uint_as_float(gu[2 * h] & 0xffff0000u),
+                                fmaf(B4.y, __uint_as_float(yu[2 * h] & 0xffff0000u), C4.y));
+          const float o2 = fmaf(A4.z, __uint_as_float(gu[2 * h + 1] << 16),
+                                fmaf(B4.z, __uint_as_float(yu[2 * h + 1] << 16), C4.z));
+          const float o3 = fmaf(A4.w, __uint_as_float(gu[2 * h + 1] & 0xffff0000u),
+                                fmaf(B4.w, __uint_as_float(yu[2 * h + 1] & 0xffff0000u), C4.w));
+          typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+          const bf16x2_t lo = {(__bf16)o0, (__bf16)o1}, hi = {(__bf16)o2, (__bf16)o3};
+          w[2 * h] = __builtin_bit_cast(uint32_t, lo);
+          w[2 * h + 1] = __builtin_bit_cast(uint32_t, hi);
+        }
+        *p = pokA[q] ? make_uint4(w[0], w[1], w[2], w[3]) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    } else if constexpr ((PRO & 2) != 0) {   // dY = A operand (DGRAD, WGRAD), fp32
 #pragma unroll
       for (int q = 0; q < NIA; ++q) {
         float4* p = reinterpret_cast<float4*>(As + 1024 * (wave + NW * q) + 16 * lane);
@@ -1073,6 +1104,9 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                 "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
   const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32, a.pro);
   const Cfg16 c = kCfgs16[cfg];
+  // the BN-partial rows of a fused dgrad were counted with the prologue-free tile rows
+  TMR_CHECK_ARG(MODE != MODE_DGRAD || !a.bn_part || c.bm == kCfgs16[pick_cfg16(a.M, a.N, a.K, MODE, f32)].bm,
+                "gemm (LDS-DMA path): the dY prologue changed a fused dgrad's tile rows");
   TMR_CHECK_ARG(!a.pro || (f32 ? pro32_ok(a, MODE) : pro16_ok(a, MODE)),
                 "gemm (LDS-DMA path): operand prologue %d not supported here (view %d)", a.pro, MODE);
   // ReLU-mask bits are read by the LDS-staged BN-backward epilogue only (every dgrad tile but
@@ -1099,22 +1133,14 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
 #if TMR_PROLOGUES
-  if constexpr (F32 == 0) {   // bf16: the X prologue, FWD / WGRAD (pro16_ok)
-    if (a.pro) {
-      if constexpr (MODE == MODE_DGRAD) return -1;
-      else return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
-    }
-  }
-  if constexpr (F32 != 0) {
-    // prologue variants (fp32 only, A/B build): FWD X, DGRAD dY, WGRAD dY / dY + X
-    if (a.pro) {
-      if constexpr (MODE == MODE_FWD) return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
-      if constexpr (MODE == MODE_DGRAD) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
-      if constexpr (MODE == MODE_WGRAD) {
-        if (a.pro == 2) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
-        if (a.pro == 3) return launch16_switch<MODE, F32, 3>(a, cfg, tapv, grid, st);
-        return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
-      }
+  // prologue variants (A/B build; fp32 and bf16): FWD X, DGRAD dY, WGRAD dY / dY + X / X
+  if (a.pro) {
+    if constexpr (MODE == MODE_FWD) return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
+    if constexpr (MODE == MODE_DGRAD) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
+    if constexpr (MODE == MODE_WGRAD) {
+      if (a.pro == 2) return launch16_switch<MODE, F32, 2>(a, cfg, tapv, grid, st);
+      if (a.pro == 3) return launch16_switch<MODE, F32, 3>(a, cfg, tapv, grid, st);
+      return launch16_switch<MODE, F32, 1>(a, cfg, tapv, grid, st);
     }
   }
 #endif

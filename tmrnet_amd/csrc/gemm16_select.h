@@ -53,12 +53,19 @@ inline bool use32(const GemmArgs& a, int mode) {
   return a.lds % 4 == 0 && a.ldb % 4 == 0 && a.log2C >= 2 && (a.ntaps != 1 || a.K % 4 == 0);
 }
 
-// bf16 form (A/B build, round 5): the X prologue only (relu(bn) of the operand, rounded to bf16 as
-// the BN pass would store it), one tap per 64-element k-tile, 8-channel pieces
+// bf16 form (A/B build, round 5): the X prologue (relu(bn) of the operand, rounded to bf16 as the
+// BN pass would store it) and the dY prologue (the BN backward of bf16 g and y, rounded as
+// bn_bwd_apply8_a16 stores dy), one tap per 64-element k-tile, 8-channel pieces
 inline bool pro16_ok(const GemmArgs& a, int mode) {
   if (!a.pro) return true;
-  if (a.pro != 1 || mode == MODE_DGRAD || a.lds > PRO_XMAX || a.lds % 8) return false;
-  return mode == MODE_WGRAD || a.ntaps == 1 || a.log2C >= 6;
+  if (mode != MODE_WGRAD && a.ntaps != 1 && a.log2C < 6) return false;
+  if ((a.pro & 1) && (mode == MODE_DGRAD || a.lds > PRO_XMAX || a.lds % 8)) return false;
+  if (a.pro & 2) {
+    if (mode == MODE_FWD || ((uintptr_t)a.pd_y & 15)) return false;
+    const int cd = mode == MODE_WGRAD ? a.ldb : a.lds;
+    if (cd > PRO_DMAX || cd % 8) return false;
+  }
+  return true;
 }
 
 inline bool use16(const GemmArgs& a, int mode) {

@@ -161,7 +161,7 @@ int set_prologue(GemmArgs& a, const tmr_conv_prologue* pro, const tmr_conv_desc*
     TMR_CHECK_ARG(dy_ok, "tmr_conv2d: a dY-operand prologue applies to the dgrad and wgrad views");
     TMR_CHECK_ARG(pro->dy_y && pro->dy_coef, "tmr_conv2d: dY prologue needs y and coefficients");
     TMR_CHECK_ARG(!d->y_ld || d->y_ld == d->k, "tmr_conv2d: dY prologue needs a dense dy (y_ld == k)");
-    a.pd_y = pro->dy_y + y_off;
+    a.pd_y = adv(pro->dy_y, y_off, esz_dy(d));   // y has dY's element type
     a.pd_a = pro->dy_coef;
     a.pd_b = pro->dy_coef + d->k;
     a.pd_c = pro->dy_coef + 2 * d->k;
@@ -593,7 +593,7 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
 // the prologue of the frame chunk starting at frame f0 (dY's y moves with dY)
 static tmr_conv_prologue chunk_pro(const tmr_conv_prologue* pro, const tmr_conv_desc* d, int f0) {
   tmr_conv_prologue p = *pro;
-  if (p.dy_y) p.dy_y += f0 * y_frame(d);
+  if (p.dy_y) p.dy_y = adv(p.dy_y, f0 * y_frame(d), esz_dy(d));
   return p;
 }
 
@@ -691,10 +691,10 @@ static int dgrad_bnbwd_entry(const tmr_conv_desc* d, const float* dy, const floa
                 "tmr_conv2d_dgrad_bnbwd: a grouped dgrad takes no ReLU-mask bits / prologue");
   TMR_CHECK_ARG(y && mean && parts, "tmr_conv2d_dgrad_bnbwd: null y / mean / parts");
   TMR_CHECK_ARG(!(d->io & TMR_IO_G16) ||
-                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) && !pro &&
+                    (d->math == TMR_MATH_BF16 && (d->io & TMR_IO_WT_BF16) &&
                      (d->c / ngroups(d)) % 8 == 0),
                 "tmr_conv2d_dgrad_bnbwd: a bf16 gradient (TMR_IO_G16) needs bf16 math on the LDS-DMA "
-                "engine (TMR_IO_WT_BF16), no prologue, channels per group a multiple of 8");
+                "engine (TMR_IO_WT_BF16), channels per group a multiple of 8");
   TMR_CHECK_ARG(!dx_old || ngroups(d) == 1, "tmr_conv2d_dgrad_bnbwd: a separate old dx takes no groups");
   // a grouped dgrad writes each group's channel slice of a bf16 gradient with beta == 0 only (the
   // trunk's G16 on ResNeSt's radix-2 conv); accumulating into a bf16 dx runs ungrouped
@@ -1043,6 +1043,22 @@ TMR_API int tmr_conv2d_dgrad_bnbwd_pro(const tmr_conv_desc* d, const float* dy,
                                        hipStream_t stream) {
   return conv_dgrad_bnbwd_pro(d, dy, w_krsc, dx, beta, y, z, scale, shift, mean, mask, parts,
                               parts_bytes, pro, stream);
+}
+
+TMR_API int tmr_conv2d_dgrad_bnbwd_acc_pro(const tmr_conv_desc* d, const float* dy,
+                                           const float* w_krsc, void* dx, float beta,
+                                           const void* dx_old, int old_bf16, const float* y,
+                                           const float* z, const float* scale, const float* shift,
+                                           const float* mean, int mask, void* parts,
+                                           size_t parts_bytes, const tmr_conv_prologue* pro,
+                                           hipStream_t stream) {
+  TMR_CHECK_ARG(d, "tmr_conv2d_dgrad_bnbwd_acc_pro: null descriptor");
+  TMR_CHECK_ARG(beta != 0.f && dx_old && ((uintptr_t)dx_old & 15) == 0 &&
+                    (d->io & TMR_IO_G16) && (d->io & TMR_IO_WT_BF16),
+                "tmr_conv2d_dgrad_bnbwd_acc_pro: needs beta != 0, a 16-B aligned old dx and a bf16 "
+                "output (TMR_IO_G16) on the bf16 LDS-DMA engine (TMR_IO_WT_BF16)");
+  return dgrad_bnbwd_entry(d, dy, w_krsc, (float*)dx, beta, dx_old, old_bf16 ? 1 : 0, y, z, scale,
+                           shift, mean, mask, parts, parts_bytes, pro, stream);
 }
 
 TMR_API int tmr_conv2d_wgrad_pro(const tmr_conv_desc* d, const float* x, const float* dy,

@@ -219,7 +219,8 @@ def _prologue(xpro=None, dpro=None):
     if xpro is not None:
         p.x_scale, p.x_shift = _req(xpro[0], "x_scale").data_ptr(), _req(xpro[1], "x_shift").data_ptr()
     if dpro is not None:
-        p.dy_y, p.dy_coef = _req(dpro[0], "dy_y").data_ptr(), _req(dpro[1], "dy_coef").data_ptr()
+        # (y fp32, or bf16 with the bf16 engine's dY prologue: g's element type)
+        p.dy_y, p.dy_coef = _req_op(dpro[0], "dy_y").data_ptr(), _req(dpro[1], "dy_coef").data_ptr()
     return p
 
 
@@ -304,9 +305,9 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
     the old dx is `out` itself (bf16, in place) or `old` (fp32 or bf16; tmr_conv2d_dgrad_bnbwd_acc,
     a new bf16 dx is returned)."""
     if old is not None:
-        if not (g16 and beta != 0.0 and out is None and dpro is None and groups == 1):
+        if not (g16 and beta != 0.0 and out is None and groups == 1):
             raise RuntimeError("conv_dgrad_bnbwd: a separate old dx needs g16, beta, no out / "
-                               "prologue / groups")
+                               "groups")
         if old.dtype not in (f32, BF16) or not old.is_contiguous():
             raise RuntimeError("conv_dgrad_bnbwd: old dx must be a contiguous fp32 / bf16 tensor")
     if g16 and groups > 1 and beta != 0.0:
@@ -348,10 +349,14 @@ def conv_dgrad_bnbwd(dy, w_krsc, in_hw, stride, pad, y, mean, mask, z=None, scal
                + y.element_size() * n * h * w * c * (2 if z is not None and mask != 3 else 1)
                + (n * h * w * c // 8 if mask == 3 else 0)):
         pro = _prologue(None, dpro)
-        if old is not None:
+        if old is not None and pro is None:
             call("tmr_conv2d_dgrad_bnbwd_acc", ctypes.byref(d), dy, w_krsc, out, float(beta), old,
                  int(old.dtype == BF16), y, z, scale, shift, mean, int(mask), parts,
                  ctypes.c_size_t(parts.numel() * 4), stream_ptr())
+        elif old is not None:
+            call("tmr_conv2d_dgrad_bnbwd_acc_pro", ctypes.byref(d), dy, w_krsc, out, float(beta),
+                 old, int(old.dtype == BF16), y, z, scale, shift, mean, int(mask), parts,
+                 ctypes.c_size_t(parts.numel() * 4), ctypes.byref(pro), stream_ptr())
         elif pro is None:
             call("tmr_conv2d_dgrad_bnbwd", ctypes.byref(d), dy, w_krsc, out, float(beta), y, z,
                  scale, shift, mean, int(mask), parts, ctypes.c_size_t(parts.numel() * 4),
@@ -409,6 +414,23 @@ def bn_bwd_coefs_dense(g, y, z, scale, shift, mean, inv, gamma, relu):
     ws, nb = _bn_ws(rows, c, y.device)
     call("tmr_bn_bwd_coefs_dense", g, y, z, scale, shift, mean, inv, gamma, coef, dgamma, dbeta,
          rows, c, int(relu), ws, ctypes.c_size_t(nb), stream_ptr())
+    return coef, dgamma, dbeta
+
+
+def bn_bwd_coefs_g16(g, y, mean, inv, gamma):
+    """BN backward coefficients of a unit without ReLU from its bf16 output gradient g and bf16 y
+    (the downsample BN of the bf16-activation step) -> (coef [3][c], dgamma, dbeta)."""
+    _need_prologues()
+    c = y.shape[-1]
+    rows = y.numel() // c
+    if g.dtype != BF16 or y.dtype != BF16 or g.shape != y.shape:
+        raise RuntimeError("bn_bwd_coefs_g16: g and y must be bf16 tensors of one shape")
+    _req_op(g, "g"); _req_op(y, "y")
+    coef = _empty((3, c), mean)
+    dgamma = _empty((c,), mean); dbeta = _empty((c,), mean)
+    ws, nb = _bn_ws(rows, c, y.device)
+    call("tmr_bn_bwd_coefs_g16", g, y, mean, inv, gamma, coef, dgamma, dbeta, rows, c, ws,
+         ctypes.c_size_t(nb), stream_ptr())
     return coef, dgamma, dbeta
 
 

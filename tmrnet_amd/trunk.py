@@ -100,6 +100,21 @@ FOLD_BN = os.environ.get("TMR_FOLD_BN", "0") == "1"
 # RNE: bn_apply8_a16_k's arithmetic, so bit-identical), forward and wgrad views.  Not for an input
 # the direct 3x3 kernels read (direct3.hip: ResNet-50 layer1's 56x56 64 -> 64 conv2).
 FOLD16 = os.environ.get("TMR_FOLD16", "0") == "1"
+# ... and its dY half (round 5, same A/B build, TMR_FOLD16_DY=1): no BatchNorm backward writes dy --
+# the conv's dgrad and wgrad read the bf16 masked gradient g and the bf16 y through the bf16
+# dY-operand prologue (fmaf(A, g, fmaf(B, y, C)) rounded RNE: bn_bwd_apply8_a16's arithmetic, so
+# bit-identical), for every unit whose g is stored bf16 (bn1 / bn2 under G16, bn3 / downsample
+# under R16: all but the last block's bn3) and whose conv is not a direct 3x3 (direct3.hip).
+FOLD16DY = os.environ.get("TMR_FOLD16_DY", "0") == "1"
+
+
+def _direct3_conv(rec):
+    """This unit's conv runs on the direct 3x3 kernels (direct3.hip d3_shape: 56x56 64 -> 64,
+    ResNeSt's deep-stem 112x112 32 -> 32 / 64), which take no operand prologue."""
+    k, c, r, s = rec["conv"].weight.shape
+    w = rec["x"].shape[2]
+    return (r == 3 and s == 3 and rec["stride"] == 1 and rec.get("groups", 1) == 1
+            and ((w == 56 and c == 64 and k == 64) or (w == 112 and c == 32 and k in (32, 64))))
 
 
 def _direct3_input(blk, h):
@@ -312,6 +327,18 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
                                                   bn.weight.detach(), rec["relu"])
         dy, dpro = dz, (rec["y"], coef)
         dres = dz if want_dres else None
+    elif (FOLD16DY and dz.dtype == torch.bfloat16 and rec["y"].dtype == torch.bfloat16
+          and (parts is not None or not rec["relu"]) and rec.get("groups", 1) == 1
+          and not _direct3_conv(rec)):
+        # the bf16 dY prologue: coefficients only, the consumers read g and y
+        if parts is not None:
+            coef, dg, db = ops.bn_bwd_coefs(parts[0], parts[1], rec["mean"], rec["inv"],
+                                            bn.weight.detach(), rec["y"].numel() // rec["y"].shape[-1])
+        else:   # the downsample BN (no ReLU): one reduction pass over g and y
+            coef, dg, db = ops.bn_bwd_coefs_g16(dz, rec["y"], rec["mean"], rec["inv"],
+                                                bn.weight.detach())
+        dy, dpro = dz, (rec["y"], coef)
+        dres = dz if want_dres else None
     elif parts is not None:
         dy, dg, db = ops.bn_bwd_parts(dz, rec["y"], parts[0], parts[1], rec["mean"], rec["inv"],
                                       bn.weight.detach(), bf16=s16)
@@ -341,7 +368,8 @@ def _conv_bn_bwd(rec, dz, grads, want_dres=False, dx_out=None, dx_beta=0.0, need
             zm = p["z"]
             if mask == 1 and wt and p.get("zbits") is not None:
                 mask, zm = 3, p["zbits"]   # the ReLU mask as bits (fp32 LDS-DMA dgrad)
-            bf8 = (wt and dpro is None and p["y"].dtype == torch.bfloat16 and
+            bf8 = (wt and (dpro is None or dpro[0].dtype == torch.bfloat16) and
+                   p["y"].dtype == torch.bfloat16 and
                    (p["y"].shape[-1] // grp) % 8 == 0)
             # (a grouped dgrad -- ResNeSt's radix-2 conv -- stores its per-group channel slices bf16
             # too; the residual accumulation stays ungrouped)
