@@ -44,6 +44,40 @@ def test_avgpool2d(dev, case):
     assert rel_err(xd.grad.permute(0, 3, 1, 2), xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("case", [(2, 56, 56, 64, 3, 2, 1, True, False),
+                                  (2, 56, 56, 256, 2, 2, 0, False, True),
+                                  (3, 7, 7, 32, 3, 1, 1, True, False),
+                                  (2, 15, 13, 8, 2, 2, 0, False, True),
+                                  (2, 15, 13, 8, 3, 2, 1, True, False),
+                                  (2, 14, 14, 512, 3, 2, 1, True, False)])
+def test_avgpool2d_a16_exact(dev, case):
+    """The bf16 AvgPool2d forward (ResNeSt's avd / avg_down under bf16 activations; the 3x3/2 and
+    2x2/2 windows take the compile-time-window kernel, the rest the generic one) against the
+    kernels' arithmetic restated in fp32 torch ops: taps summed in window order (dy, then dx) from
+    0, scaled by 1/count, rounded to bf16 -- equal values."""
+    n, h, w, c, k, s, p, incl, ceil = case
+    g = torch.Generator().manual_seed(7 + sum(case[:4]))
+    x = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16)
+    y = ops.avgpool2d_fwd(x.to(dev), k, s, p, incl, ceil).cpu()
+    ho, wo = ops.pool_out(h, k, s, p, ceil), ops.pool_out(w, k, s, p, ceil)
+    xf = x.float()
+    acc = torch.zeros(n, ho, wo, c)
+    cnt = torch.zeros(1, ho, wo, 1)
+    oy = torch.arange(ho).view(ho, 1) * s - p
+    ox = torch.arange(wo).view(1, wo) * s - p
+    for dy in range(k):
+        for dx in range(k):
+            iy, ix = oy + dy, ox + dx
+            ok = (iy >= 0) & (iy < h) & (ix >= 0) & (ix < w)
+            v = xf[:, iy.clamp(0, h - 1), ix.clamp(0, w - 1), :]
+            acc = acc + torch.where(ok.view(1, ho, wo, 1), v, torch.zeros_like(v))
+            cnt = cnt + ok.view(1, ho, wo, 1).float()
+    inv = (1.0 / torch.full_like(cnt, float(k * k))) if incl else 1.0 / cnt.clamp(min=1)
+    ref = (acc * inv).to(torch.bfloat16)
+    assert y.shape == ref.shape
+    assert torch.equal(y.float(), ref.float())
+
+
 def _zero_grad_scales(g64):
     """fc1.bias feeds batch-stat BatchNorm: its exact gradient is 0; judge it on the scale of
     the fc1.weight gradient instead of its own (rounding-noise) magnitude."""

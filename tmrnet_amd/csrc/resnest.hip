@@ -225,12 +225,16 @@ __global__ __launch_bounds__(NT) void avgpool2d_bwd_k(const float* __restrict__ 
 
 // The same with the pixel / channel indices by magic-number division (the element-group count
 // fits 32 bits, checked on the host): the generic form's three 32-bit divisions per 4 elements
-// made it instruction-bound (~2 TB/s).  Same sums in the same order.
+// made it instruction-bound (~2 TB/s).  Same sums in the same order.  KK / SS / PP: ResNeSt's two
+// pools as compile-time windows (the avd 3x3/2 pad 1 and the avg_down 2x2/2), so the window
+// bounds divide by a constant; 0: the runtime k / s / p.
+template <int KK, int SS, int PP>
 __global__ __launch_bounds__(NT) void avgpool2d_bwd_fd_k(const float* __restrict__ dy,
                                                          float* __restrict__ dx, uint32_t total,
                                                          FastDiv dc4, FastDiv dw, FastDiv dh,
-                                                         int ho, int wo, int k, int s, int p,
+                                                         int ho, int wo, int k_, int s_, int p_,
                                                          int incl) {
+  const int k = KK ? KK : k_, s = KK ? SS : s_, p = KK ? PP : p_;
   const uint32_t c4 = dc4.d, w = dw.d, h = dh.d;
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
     const uint32_t t0 = fdiv(i, dc4);
@@ -675,6 +679,45 @@ __global__ __launch_bounds__(NT) void avgpool2d_fwd_a16_k(const __bf16* __restri
   }
 }
 
+// The same with magic-number index division (the output element-group count fits 32 bits) for
+// ResNeSt's two windows at compile time (the avd 3x3/2 pad 1, the avg_down 2x2/2): same sums,
+// same order
+template <int KK, int SS, int PP>
+__global__ __launch_bounds__(NT) void avgpool2d_fwd_a16_fd_k(const __bf16* __restrict__ x,
+                                                             __bf16* __restrict__ y, uint32_t total,
+                                                             FastDiv dc4, FastDiv dwo, FastDiv dho,
+                                                             int h, int w, int incl) {
+  static_assert(KK > 0 && SS > 0, "compile-time window");
+  constexpr int k = KK, s = SS, p = PP;
+  const uint32_t c4 = dc4.d, wo = dwo.d, ho = dho.d;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const uint32_t t0 = fdiv(i, dc4);
+    const int cq = (int)(i - t0 * c4);
+    const uint32_t t1 = fdiv(t0, dwo);
+    const int ox = (int)(t0 - t1 * wo);
+    const uint32_t nn = fdiv(t1, dho);
+    const int oy = (int)(t1 - nn * ho);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+#pragma unroll
+    for (int dy = 0; dy < k; ++dy) {
+      const int iy = oy * s - p + dy;
+      if (iy < 0 || iy >= h) continue;
+#pragma unroll
+      for (int dx = 0; dx < k; ++dx) {
+        const int ix = ox * s - p + dx;
+        if (ix < 0 || ix >= w) continue;
+        const float4 v = Act<__bf16>::ld(x, (((long)nn * h + iy) * w + ix) * c4 + cq);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        ++cnt;
+      }
+    }
+    const float inv = 1.0f / (float)(incl ? k * k : (cnt > 0 ? cnt : 1));
+    acc.x *= inv; acc.y *= inv; acc.z *= inv; acc.w *= inv;
+    Act<__bf16>::st(y, i, acc);
+  }
+}
+
 // Column means over the frames: block = 64 columns x 16 row groups (1024 threads), each thread
 // sums its rows in double, the 16 partial sums are added in a fixed order (deterministic).
 __global__ __launch_bounds__(CC_COLS * CC_RG) void center_cols_k(const float* __restrict__ x, int rows, int cols,
@@ -779,12 +822,21 @@ TMR_API int tmr_avgpool2d_bwd(const float* dy, float* dx, int n, int h, int w, i
                               int wo, int k, int s, int p, int count_include_pad,
                               hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_bwd: channels %d must be a multiple of 4", c);
-  if ((long)n * h * w * c / 4 < (1L << 31))
-    hipLaunchKernelGGL(avgpool2d_bwd_fd_k, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
-                       dy, dx, (uint32_t)((long)n * h * w * c / 4), make_fastdiv((uint32_t)(c / 4)),
-                       make_fastdiv((uint32_t)w), make_fastdiv((uint32_t)h), ho, wo, k, s, p,
-                       count_include_pad);
-  else
+  if ((long)n * h * w * c / 4 < (1L << 31)) {
+    const uint32_t total = (uint32_t)((long)n * h * w * c / 4);
+    const dim3 g(blocks_for((long)n * h * w * c / 4));
+    const FastDiv dc4 = make_fastdiv((uint32_t)(c / 4)), dw = make_fastdiv((uint32_t)w),
+                  dh = make_fastdiv((uint32_t)h);
+    if (k == 3 && s == 2 && p == 1)
+      hipLaunchKernelGGL((avgpool2d_bwd_fd_k<3, 2, 1>), g, dim3(NT), 0, stream, dy, dx, total, dc4,
+                         dw, dh, ho, wo, k, s, p, count_include_pad);
+    else if (k == 2 && s == 2 && p == 0)
+      hipLaunchKernelGGL((avgpool2d_bwd_fd_k<2, 2, 0>), g, dim3(NT), 0, stream, dy, dx, total, dc4,
+                         dw, dh, ho, wo, k, s, p, count_include_pad);
+    else
+      hipLaunchKernelGGL((avgpool2d_bwd_fd_k<0, 0, 0>), g, dim3(NT), 0, stream, dy, dx, total, dc4,
+                         dw, dh, ho, wo, k, s, p, count_include_pad);
+  } else
     hipLaunchKernelGGL(avgpool2d_bwd_k<long>, dim3(blocks_for((long)n * h * w * c / 4)), dim3(NT), 0, stream,
                      dy, dx, n, h, w, c / 4, ho, wo, k, s, p, count_include_pad);
   TMR_CHECK_LAUNCH("avgpool2d_bwd");
@@ -900,7 +952,19 @@ TMR_API int tmr_avgpool2d_fwd_a16(const void* x, void* y, int n, int h, int w, i
                                   int wo, int k, int s, int p, int count_include_pad,
                                   hipStream_t stream) {
   TMR_CHECK_ARG(c % 4 == 0, "tmr_avgpool2d_fwd_a16: channels %d must be a multiple of 4", c);
-  if ((long)n * ho * wo * c / 4 < (1L << 31))
+  const long groups = (long)n * ho * wo * c / 4;
+  if (groups < (1L << 31) && ((k == 3 && s == 2 && p == 1) || (k == 2 && s == 2 && p == 0))) {
+    const FastDiv dc4 = make_fastdiv((uint32_t)(c / 4)), dwo = make_fastdiv((uint32_t)wo),
+                  dho = make_fastdiv((uint32_t)ho);
+    if (k == 3)
+      hipLaunchKernelGGL((avgpool2d_fwd_a16_fd_k<3, 2, 1>), dim3(blocks_for(groups)), dim3(NT), 0,
+                         stream, (const __bf16*)x, (__bf16*)y, (uint32_t)groups, dc4, dwo, dho, h, w,
+                         count_include_pad);
+    else
+      hipLaunchKernelGGL((avgpool2d_fwd_a16_fd_k<2, 2, 0>), dim3(blocks_for(groups)), dim3(NT), 0,
+                         stream, (const __bf16*)x, (__bf16*)y, (uint32_t)groups, dc4, dwo, dho, h, w,
+                         count_include_pad);
+  } else if (groups < (1L << 31))
     hipLaunchKernelGGL(avgpool2d_fwd_a16_k<uint32_t>, dim3(blocks_for((long)n * ho * wo * c / 4)), dim3(NT), 0,
                      stream, (const __bf16*)x, (__bf16*)y, n, h, w, c / 4, ho, wo, k, s, p,
                      count_include_pad);
