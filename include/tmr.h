@@ -346,6 +346,21 @@ int tmr_bn_bwd_parts_g16(const void* g, const void* y, const void* parts, int np
 int tmr_bn_bwd_g16(const void* dz, const void* y, const float* save_mean,
                    const float* save_invstd, const float* gamma, void* dy, float* dgamma,
                    float* dbeta, int rows, int c, void* ws, size_t ws_bytes, hipStream_t stream);
+/* The BatchNorm2d backward of a downsample Bottleneck's bn3 and downsample BN together (both take
+ * the gradient g of the block's pre-ReLU sum; train_only_non-local_pretrained.py:210-213 /
+ * torchvision Bottleneck `out += identity`): bn3 from the fused dgrad's partials (as
+ * tmr_bn_bwd_parts_x / _g16), the downsample BN from one pass over (g, y_ds) (as tmr_bn_bwd_x /
+ * tmr_bn_bwd_g16), then one apply pass reading g once and writing dy (bn3) and dy_ds -- the same
+ * values as the two separate calls.  bf16 = 0: g, y, y_ds, dy, dy_ds fp32; 1: all bf16 (the
+ * bf16-activation step's residual gradient).  c a multiple of 8, operands 16-B aligned;
+ * ws >= tmr_bn_bwd_parts_ds_ws_bytes(nparts, rows, c). */
+size_t tmr_bn_bwd_parts_ds_ws_bytes(int nparts, int rows, int c);
+int tmr_bn_bwd_parts_ds(const void* g, const void* y, const void* parts, int nparts,
+                        const float* save_mean, const float* save_invstd, const float* gamma,
+                        void* dy, float* dgamma, float* dbeta, const void* y_ds,
+                        const float* save_mean_ds, const float* save_invstd_ds,
+                        const float* gamma_ds, void* dy_ds, float* dgamma_ds, float* dbeta_ds,
+                        int rows, int c, int bf16, void* ws, size_t ws_bytes, hipStream_t stream);
 int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int n, int h, int w, int ho,
                            int wo, const void* y, const float* scale, const float* shift,
                            const float* save_mean, const float* save_invstd, const float* gamma,

@@ -672,6 +672,56 @@ def test_bn_fold16_bit_identical(dev, folds):
         assert torch.equal(res[True][2][n], res[False][2][n]), n
 
 
+@pytest.mark.parametrize("precision,backbone", [("fp32", "resnet50"), ("bf16", "resnet50"),
+                                                ("bf16", "resnest50"), ("fp32", "resnest50")])
+def test_bn_bwd_ds_dual_bit_identical(dev, precision, backbone):
+    """trunk.DS_DUAL (tmr_bn_bwd_parts_ds): the BatchNorm backward of each downsample block's bn3
+    and downsample BN with one apply pass that reads the shared gradient once, against the two
+    separate passes (tmr_bn_bwd_parts_x / _g16 and tmr_bn_bwd_x / tmr_bn_bwd_g16): logits, every
+    gradient and the running statistics bit-identical, fp32 and bf16 steps of both trunks
+    (ResNet-50 / ResNeSt-50: all four downsample blocks take it -- each one's g comes from the
+    next block's fused dgrad)."""
+    import tmrnet_amd
+    from tmrnet_amd import trunk
+    B, T, L = 2, 5, 7
+    g = torch.Generator().manual_seed(5)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)
+    lt = (torch.rand(B, L, 512, generator=g) * 2 - 1).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=g).to(dev)
+    res, calls = {}, [0]
+    saved, fn = trunk.DS_DUAL, ops.bn_bwd_parts_ds
+
+    def counting(*a, **k):
+        calls[0] += 1
+        return fn(*a, **k)
+    try:
+        ops.bn_bwd_parts_ds = counting
+        for dual in (True, False):
+            trunk.DS_DUAL = dual
+            calls[0] = 0
+            torch.manual_seed(0)
+            kw = {} if backbone == "resnet50" else {"time_conv": True, "backbone": backbone}
+            m = tmrnet_amd.resnet_lstm(seq_len=T, precision=precision, **kw).to(dev).train()
+            m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+            m.forced_head_mask = torch.ones(B, 512, device=dev)
+            x4 = ops.crop_normalize(frames, off, T)
+            out = m(x4, lt)
+            tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels).backward()
+            torch.cuda.synchronize()
+            res[dual] = (out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                         {n: b.clone() for n, b in m.named_buffers()})
+            assert calls[0] == (4 if dual else 0), calls[0]
+    finally:
+        trunk.DS_DUAL = saved
+        ops.bn_bwd_parts_ds = fn
+    assert torch.equal(res[True][0], res[False][0])
+    for n in res[True][1]:
+        assert torch.equal(res[True][1][n], res[False][1][n]), n
+    for n in res[True][2]:
+        assert torch.equal(res[True][2][n], res[False][2][n]), n
+
+
 def _pack_bits(m):
     """(numel,) bool -> int32 words, element e = bit e % 32 of word e // 32."""
     m = m.reshape(-1).to(torch.int64)

@@ -77,6 +77,8 @@ SIGNATURES = {
     "tmr_bn_bwd_parts_a16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_g16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_g16": [P, P, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_bn_bwd_parts_ds_ws_bytes": [I, I, I],
+    "tmr_bn_bwd_parts_ds": [P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_bn_bwd_maxpool_a16": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],
     "tmr_maxpool2d_fwd_bn_a16": [P, P, P, P, P, I, I, I, I, I, I, P],
     "tmr_avgpool_fwd_a16": [P, P, I, I, I, P],
@@ -188,6 +190,7 @@ _RESTYPES = {
     "tmr_resize_tmp_bytes": SZ,
     "tmr_bn_ws_bytes": SZ,
     "tmr_bn_parts_ws_bytes": SZ,
+    "tmr_bn_bwd_parts_ds_ws_bytes": SZ,
     "tmr_sgd_chunk": ctypes.c_int64,
     "tmr_nl_attn_ws_bytes": SZ,
     "tmr_nlblock_saved_bytes": SZ,

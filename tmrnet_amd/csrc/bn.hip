@@ -1668,6 +1668,138 @@ TMR_API int tmr_bn_bwd_parts_g16(const void* g, const void* y, const void* parts
   return 0;
 }
 
+// The BatchNorm backward of a downsample block's two units that share one output gradient g (the
+// masked gradient of bn3(y3) + bn_ds(y_ds)): bn3's coefficients from the fused dgrad's partials,
+// the downsample BN's from one reduction pass over (g, y_ds), then one apply pass that reads g once
+// for both -- dy3 = fmaf(A3, g, fmaf(B3, y3, C3)), dyd = fmaf(Ad, g, fmaf(Bd, yd, Cd)), the fmaf
+// sequence of bn_bwd_apply / bn_bwd_apply8_a16 -- instead of two apply passes that each read g.
+// T: float (fp32 step: g, y, dy fp32) or __bf16 (bf16-activation step under R16: all bf16, dy
+// rounded RNE).  8 elements per thread, 16-B accesses.
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, long i, float (&v)[8]);
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, long i, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[2 * i], b = reinterpret_cast<const float4*>(p)[2 * i + 1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void ld8<__bf16>(const __bf16* p, long i, float (&v)[8]) {
+  const uint4 w = reinterpret_cast<const uint4*>(p)[i];
+  const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(u[e] << 16);
+    v[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, long i, const float (&v)[8]);
+template <>
+__device__ __forceinline__ void st8<float>(float* p, long i, const float (&v)[8]) {
+  reinterpret_cast<float4*>(p)[2 * i] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[2 * i + 1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <>
+__device__ __forceinline__ void st8<__bf16>(__bf16* p, long i, const float (&v)[8]) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16x2_t q = {(__bf16)v[2 * e], (__bf16)v[2 * e + 1]};
+    w[e] = __builtin_bit_cast(uint32_t, q);
+  }
+  reinterpret_cast<uint4*>(p)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_ds8(const T* __restrict__ g, const T* __restrict__ y,
+                                                       const T* __restrict__ yd,
+                                                       const float* __restrict__ coef,
+                                                       const float* __restrict__ coefd,
+                                                       T* __restrict__ dy, T* __restrict__ dyd, long n8,
+                                                       int c8) {
+  const int c = c8 * 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const int cc = chan_of(i, c8) * 8;
+    float gv[8], yv[8], dv[8], o[8], od[8];
+    ld8(g, i, gv);
+    ld8(y, i, yv);
+    ld8(yd, i, dv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = fmaf(coef[cc + e], gv[e], fmaf(coef[c + cc + e], yv[e], coef[2 * c + cc + e]));
+      od[e] = fmaf(coefd[cc + e], gv[e], fmaf(coefd[c + cc + e], dv[e], coefd[2 * c + cc + e]));
+    }
+    st8(dy, i, o);
+    st8(dyd, i, od);
+  }
+}
+
+TMR_API size_t tmr_bn_bwd_parts_ds_ws_bytes(int nparts, int rows, int c) {
+  if (nparts <= 0 || rows <= 0 || c < 8 || c % 8) {
+    tmr_set_error("tmr_bn_bwd_parts_ds_ws_bytes: bad size (parts %d, rows %d, channels %d)", nparts,
+                  rows, c);
+    return 0;
+  }
+  return (tmr_bn_parts_ws_bytes(nparts, c) + 255) / 256 * 256 + ws_need(rows, c);
+}
+
+TMR_API int tmr_bn_bwd_parts_ds(const void* g, const void* y, const void* parts, int nparts,
+                                const float* mean, const float* invstd, const float* gamma,
+                                void* dy, float* dgamma, float* dbeta, const void* yd,
+                                const float* mean_d, const float* invstd_d, const float* gamma_d,
+                                void* dyd, float* dgamma_d, float* dbeta_d, int rows, int c,
+                                int bf16, void* ws, size_t ws_bytes, hipStream_t stream) {
+  TMR_CHECK_ARG(c % 8 == 0 && c >= 8 && rows > 0 && nparts > 0,
+                "tmr_bn_bwd_parts_ds: bad shape rows=%d c=%d parts=%d", rows, c, nparts);
+  TMR_CHECK_ARG(g && y && parts && yd && dy && dyd && mean && invstd && gamma && mean_d && invstd_d &&
+                    gamma_d, "tmr_bn_bwd_parts_ds: null operand");
+  TMR_CHECK_ARG((((uintptr_t)g | (uintptr_t)y | (uintptr_t)yd | (uintptr_t)dy | (uintptr_t)dyd) & 15) == 0,
+                "tmr_bn_bwd_parts_ds: g / y / y_ds / dy / dy_ds must be 16-B aligned");
+  const size_t a_bytes = (tmr_bn_parts_ws_bytes(nparts, c) + 255) / 256 * 256;
+  TMR_CHECK_ARG(ws && ws_bytes >= a_bytes + ws_need(rows, c),
+                "tmr_bn_bwd_parts_ds: workspace too small (need tmr_bn_bwd_parts_ds_ws_bytes)");
+  // bn3: the fused dgrad's partials (tmr_bn_bwd_parts_x / _g16's kernels)
+  const SlabPlan sp = slab_plan(nparts, c);
+  double* slabs = (double*)ws;
+  float* coef = (float*)((char*)ws + slab_ws_bytes(nparts, c));
+  hipLaunchKernelGGL(parts_slab_k<1>, dim3(sp.groups, sp.nslabs), dim3(256), 0, stream, parts,
+                     nparts, c, sp.rows, slabs);
+  TMR_CHECK_LAUNCH("bn_parts_slab");
+  hipLaunchKernelGGL(bwd_final_slabs_k, dim3(sp.groups), dim3(SLAB_CH * SLAB_PH), 0, stream,
+                     (const double*)slabs, sp.nslabs, rows, c, mean, invstd, gamma, dgamma, dbeta, coef);
+  TMR_CHECK_LAUNCH("bn_bwd_final_slabs");
+  // the downsample BN: one reduction pass over (g, y_ds) (tmr_bn_bwd_x / tmr_bn_bwd_g16's kernels)
+  char* wb = (char*)ws + a_bytes;
+  Plan p = make_plan(rows, c);
+  double* part = (double*)wb;
+  float* coefd = (float*)(wb + (size_t)p.nrb * c * 2 * sizeof(double));
+  const dim3 pg(p.nrb, p.cblocks);
+  if (bf16)
+    hipLaunchKernelGGL((bn_bwd_partial<0, false, __bf16, const __bf16>), pg, dim3(NT), 0, stream,
+                       (const __bf16*)g, (const __bf16*)yd, (const __bf16*)nullptr,
+                       (const float*)nullptr, (const float*)nullptr, mean_d, rows, c, p.rpb,
+                       p.cthreads, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial<0>), pg, dim3(NT), 0, stream, (float*)g, (const float*)yd,
+                       (const float*)nullptr, (const float*)nullptr, (const float*)nullptr, mean_d,
+                       rows, c, p.rpb, p.cthreads, part);
+  TMR_CHECK_LAUNCH("bn_bwd_partial");
+  hipLaunchKernelGGL(bn_bwd_final, dim3(c), dim3(NT), 0, stream, part, p.nrb, rows, c, mean_d,
+                     invstd_d, gamma_d, dgamma_d, dbeta_d, coefd);
+  TMR_CHECK_LAUNCH("bn_bwd_final");
+  const long n8 = (long)rows * c / 8;
+  if (bf16)
+    hipLaunchKernelGGL(bn_bwd_apply_ds8<__bf16>, dim3(ew_blocks(n8)), dim3(NT), 0, stream,
+                       (const __bf16*)g, (const __bf16*)y, (const __bf16*)yd, coef, coefd,
+                       (__bf16*)dy, (__bf16*)dyd, n8, c / 8);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_ds8<float>, dim3(ew_blocks(n8)), dim3(NT), 0, stream,
+                       (const float*)g, (const float*)y, (const float*)yd, coef, coefd, (float*)dy,
+                       (float*)dyd, n8, c / 8);
+  TMR_CHECK_LAUNCH("bn_bwd_apply_ds");
+  return 0;
+}
+
 TMR_API int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int n, int h, int w,
                                    int ho, int wo, const void* y, const float* scale,
                                    const float* shift, const float* save_mean,

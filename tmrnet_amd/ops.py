@@ -434,6 +434,29 @@ def bn_bwd_coefs_g16(g, y, mean, inv, gamma):
     return coef, dgamma, dbeta
 
 
+def bn_bwd_parts_ds(g, y, parts, nparts, mean, inv, gamma, yd, mean_d, inv_d, gamma_d):
+    """BN backward of a downsample block's bn3 (from the fused dgrad's partials, g already
+    masked) and of its downsample BN (a reduction pass over g and y_ds), with one apply pass that
+    reads g once -> (dy, dgamma, dbeta, dy_ds, dgamma_ds, dbeta_ds); the values of bn_bwd_parts +
+    bn_bwd.  g, y, y_ds all fp32 or all bf16 (the dy's take their dtype)."""
+    c = y.shape[-1]
+    rows = y.numel() // c
+    t = y.dtype
+    if not (g.dtype == t and yd.dtype == t and t in (f32, BF16) and g.shape == y.shape == yd.shape
+            and g.is_contiguous() and y.is_contiguous() and yd.is_contiguous()):
+        raise RuntimeError("bn_bwd_parts_ds: g, y and y_ds must be contiguous tensors of one shape "
+                           "and one dtype (fp32 or bf16)")
+    nb = query("tmr_bn_bwd_parts_ds_ws_bytes", int(nparts), rows, c)
+    ws = torch.empty(((nb + 7) // 8,), dtype=torch.float64, device=y.device)
+    dy, dyd = torch.empty_like(y), torch.empty_like(yd)
+    dg, db = _empty((c,), mean), _empty((c,), mean)
+    dgd, dbd = _empty((c,), mean), _empty((c,), mean)
+    call("tmr_bn_bwd_parts_ds", g, y, parts, int(nparts), mean, inv, gamma, dy, dg, db, yd, mean_d,
+         inv_d, gamma_d, dyd, dgd, dbd, rows, c, int(t == BF16), ws, ctypes.c_size_t(ws.numel() * 8),
+         stream_ptr())
+    return dy, dg, db, dyd, dgd, dbd
+
+
 def bn_bwd_parts(g, y, parts, nparts, mean, inv, gamma, bf16=False):
     """BN backward from conv_dgrad_bnbwd partials: g already masked -> (dy, dgamma, dbeta);
     bf16=True stores dy rounded (consumed only by the bf16-math dgrad / wgrad)."""

@@ -326,6 +326,7 @@ class ResNeStTrunkFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dfeat):
+        from . import trunk
         from .trunk import _conv_bn_bwd, get_grad_ready
         if not ctx.keep:
             raise RuntimeError("trunk backward needs train mode and a forward with grad enabled")
@@ -339,8 +340,23 @@ class ResNeStTrunkFn(torch.autograd.Function):
             blk = rec["blk"]
             prev3 = blocks[-1]["r3"] if blocks else None
             # bn3 (+ReLU) backward; g (owned) becomes the masked gradient = the residual branch's
-            dout, dres, _ = _conv_bn_bwd(rec["r3"], g, grads, want_dres=True, dres_inplace=True,
-                                         parts=pending)
+            r3, rd, dyd = rec["r3"], rec["rd"], None
+            if (rd is not None and trunk.DS_DUAL and pending is not None and g.is_contiguous()
+                    and g.dtype == r3["y"].dtype == rd["y"].dtype and r3["y"].shape == rd["y"].shape
+                    and r3["y"].shape[-1] % 8 == 0):
+                # bn3 and the downsample BN share g: one apply pass (trunk.DS_DUAL)
+                dy3, dg3, db3, dyd, dgd, dbd = ops.bn_bwd_parts_ds(
+                    g, r3["y"], pending[0], pending[1], r3["mean"], r3["inv"],
+                    r3["bn"].weight.detach(), rd["y"], rd["mean"], rd["inv"],
+                    rd["bn"].weight.detach())
+                grads[r3["bn"].weight], grads[r3["bn"].bias] = dg3, db3
+                grads[rd["bn"].weight], grads[rd["bn"].bias] = dgd, dbd
+                dout, _, _ = _conv_bn_bwd(r3, None, grads, dy=dy3)
+                dres = g
+                del dy3
+            else:
+                dout, dres, _ = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True,
+                                             parts=pending)
             if blk.avd:
                 dout = ops.avgpool2d_bwd(dout, rec["avd_hw"], 3, blk.avd_stride, 1, True)
             # split attention + bn0 backward -> dy of the grouped conv
@@ -350,8 +366,12 @@ class ResNeStTrunkFn(torch.autograd.Function):
             # (relu(bn1)'s gradient stored bf16 by the grouped dgrad: trunk.G16, round 4)
             dz1, _, fz1 = _conv_bn_bwd(r2, None, grads, dy=dy2, fuse_prev=rec["r1"], g16=True)
             del dy2
-            if rec["rd"] is not None:
-                dxr, _, _ = _conv_bn_bwd(rec["rd"], dres, grads)
+            if rd is not None:
+                if dyd is not None:
+                    dxr, _, _ = _conv_bn_bwd(rd, None, grads, dy=dyd)
+                    del dyd
+                else:
+                    dxr, _, _ = _conv_bn_bwd(rd, dres, grads)
                 if "pool" in rec:
                     k, st = rec["pool"]
                     dxr = ops.avgpool2d_bwd(dxr, rec["in_hw"], k, st, 0, False)

@@ -174,6 +174,12 @@ G16 = os.environ.get("TMR_G16", "1") != "0"
 # gradient of every block output but the last.
 R16 = os.environ.get("TMR_BF16_RESGRAD", "1") != "0"
 
+# downsample blocks: the BatchNorm backward of bn3 and of the downsample BN -- both take the
+# block's masked pre-ReLU gradient g -- in one call whose apply pass reads g once for both dy's
+# (tmr_bn_bwd_parts_ds: the values of the two separate passes; C2 174.2 -> 173.6 ms/step, C5
+# 161.8 -> 161.5, profiles/r5/ds_dual/.  A module attribute for the bit-identity test.)
+DS_DUAL = True
+
 # the fp32 block outputs' ReLU masks as bits for the mask-3 dgrads (round 2: 3622 -> 3634 frames/s,
 # profiles/r2/bench_r3a/).  The bf16-activation step re-reads its 2-byte z instead: bits measured no
 # faster there (profiles/r3/bench_r4i/, round-4 A/B under R16: the step unchanged) and were retired.
@@ -478,8 +484,22 @@ class TrunkFn(torch.autograd.Function):
             # the previous block's last unit: its BN output gradient is this block's dx
             prev3 = blocks[-1][1][-1] if blocks else None
             # g (owned here) becomes the masked pre-ReLU gradient = the identity-branch grad
-            dz2, dres, fz2 = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True,
-                                          parts=pending, fuse_prev=r2, g16=True)
+            dyd = None
+            if (has_ds and DS_DUAL and pending is not None and g.is_contiguous()
+                    and g.dtype == r3["y"].dtype == rd["y"].dtype and r3["y"].shape[-1] % 8 == 0):
+                # (g came masked from the next block's fused dgrad)
+                dy3, dg3, db3, dyd, dgd, dbd = ops.bn_bwd_parts_ds(
+                    g, r3["y"], pending[0], pending[1], r3["mean"], r3["inv"],
+                    r3["bn"].weight.detach(), rd["y"], rd["mean"], rd["inv"],
+                    rd["bn"].weight.detach())
+                grads[r3["bn"].weight], grads[r3["bn"].bias] = dg3, db3
+                grads[rd["bn"].weight], grads[rd["bn"].bias] = dgd, dbd
+                dz2, _, fz2 = _conv_bn_bwd(r3, None, grads, fuse_prev=r2, g16=True, dy=dy3)
+                dres = g
+                del dy3
+            else:
+                dz2, dres, fz2 = _conv_bn_bwd(r3, g, grads, want_dres=True, dres_inplace=True,
+                                              parts=pending, fuse_prev=r2, g16=True)
             dz1, _, fz1 = _conv_bn_bwd(r2, dz2, grads, parts=fz2, fuse_prev=r1, g16=True)
             del dz2
             if has_ds:
@@ -487,7 +507,11 @@ class TrunkFn(torch.autograd.Function):
                 # the stride-1 conv1 dgrad accumulates into it with the fused BN backward
                 # (measured 51.1 vs 51.6 ms of dgrads per C2 step against the other order,
                 # profiles/r3/bench_r4f/)
-                dx, _, _ = _conv_bn_bwd(rd, dres, grads)
+                if dyd is not None:
+                    dx, _, _ = _conv_bn_bwd(rd, None, grads, dy=dyd)
+                    del dyd
+                else:
+                    dx, _, _ = _conv_bn_bwd(rd, dres, grads)
                 dx, _, pending = _conv_bn_bwd(r1, dz1, grads, parts=fz1, dx_out=dx, dx_beta=1.0,
                                               fuse_prev=prev3, r16=True)
             else:
