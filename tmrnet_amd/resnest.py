@@ -341,9 +341,7 @@ class ResNeStTrunkFn(torch.autograd.Function):
             prev3 = blocks[-1]["r3"] if blocks else None
             # bn3 (+ReLU) backward; g (owned) becomes the masked gradient = the residual branch's
             r3, rd, dyd = rec["r3"], rec["rd"], None
-            if (rd is not None and trunk.DS_DUAL and pending is not None and g.is_contiguous()
-                    and g.dtype == r3["y"].dtype == rd["y"].dtype and r3["y"].shape == rd["y"].shape
-                    and r3["y"].shape[-1] % 8 == 0):
+            if rd is not None and pending is not None and trunk._ds_dual(g, r3, rd):
                 # bn3 and the downsample BN share g: one apply pass (trunk.DS_DUAL)
                 dy3, dg3, db3, dyd, dgd, dbd = ops.bn_bwd_parts_ds(
                     g, r3["y"], pending[0], pending[1], r3["mean"], r3["inv"],

@@ -180,6 +180,16 @@ R16 = os.environ.get("TMR_BF16_RESGRAD", "1") != "0"
 # 161.8 -> 161.5, profiles/r5/ds_dual/.  A module attribute for the bit-identity test.)
 DS_DUAL = True
 
+
+def _ds_dual(g, r3, rd):
+    """DS_DUAL applies: g, y3 and y_ds of one dtype, which is also the dy dtype the separate passes
+    would write (fp32 y under bf16 storage writes bf16 dy: not this path), 8-channel multiples;
+    not under the dY-prologue A/B (FOLD16DY), which writes no dy at all."""
+    y = r3["y"]
+    return (DS_DUAL and not FOLD16DY and g.is_contiguous() and g.dtype == y.dtype == rd["y"].dtype
+            and y.shape == rd["y"].shape and y.shape[-1] % 8 == 0
+            and not (_store16(r3["math"]) and y.dtype == torch.float32))
+
 # the fp32 block outputs' ReLU masks as bits for the mask-3 dgrads (round 2: 3622 -> 3634 frames/s,
 # profiles/r2/bench_r3a/).  The bf16-activation step re-reads its 2-byte z instead: bits measured no
 # faster there (profiles/r3/bench_r4i/, round-4 A/B under R16: the step unchanged) and were retired.
@@ -485,8 +495,7 @@ class TrunkFn(torch.autograd.Function):
             prev3 = blocks[-1][1][-1] if blocks else None
             # g (owned here) becomes the masked pre-ReLU gradient = the identity-branch grad
             dyd = None
-            if (has_ds and DS_DUAL and pending is not None and g.is_contiguous()
-                    and g.dtype == r3["y"].dtype == rd["y"].dtype and r3["y"].shape[-1] % 8 == 0):
+            if (has_ds and _ds_dual(g, r3, rd) and pending is not None):
                 # (g came masked from the next block's fused dgrad)
                 dy3, dg3, db3, dyd, dgd, dbd = ops.bn_bwd_parts_ds(
                     g, r3["y"], pending[0], pending[1], r3["mean"], r3["inv"],
