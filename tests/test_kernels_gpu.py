@@ -672,6 +672,29 @@ def test_bn_fold16_bit_identical(dev, folds):
         assert torch.equal(res[True][2][n], res[False][2][n]), n
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,c", [(3 * 56 * 56, 256), (1001, 8), (77, 2048)])
+def test_bn_bwd_parts_ds_op(dev, dtype, rows, c):
+    """tmr_bn_bwd_parts_ds against the two calls it replaces (bn_bwd_parts of bn3 from partials,
+    bn_bwd of the downsample BN): dy, dy_ds, dgamma and dbeta of both bit-identical (fp32: the
+    fp32 passes; bf16: the _g16 passes), ragged row counts and 8 / 2048 channels."""
+    g = torch.Generator().manual_seed(rows + c)
+    mk = lambda s=1.0: (torch.randn(rows, c, generator=g) * s).to(dtype).to(dev)
+    gr, y, yd = mk(0.1), mk(), mk()
+    mean, inv = [torch.randn(c, generator=g).to(dev) for _ in range(2)]
+    md, invd = [torch.randn(c, generator=g).to(dev) for _ in range(2)]
+    inv, invd = inv.abs() + 0.5, invd.abs() + 0.5
+    gam, gamd = [(torch.rand(c, generator=g) + 0.5).to(dev) for _ in range(2)]
+    nparts = 37
+    parts = torch.randn(nparts, c, 2, generator=g).to(dev)
+    dy, dg, db, dyd, dgd, dbd = ops.bn_bwd_parts_ds(gr, y, parts, nparts, mean, inv, gam, yd, md,
+                                                    invd, gamd)
+    dy2, dg2, db2 = ops.bn_bwd_parts(gr, y, parts, nparts, mean, inv, gam)
+    dyd2, _, dgd2, dbd2 = ops.bn_bwd(gr, yd, None, md, invd, gamd, relu=False)
+    for a, b in ((dy, dy2), (dg, dg2), (db, db2), (dyd, dyd2), (dgd, dgd2), (dbd, dbd2)):
+        assert a.dtype == b.dtype and torch.equal(a, b)
+
+
 @pytest.mark.parametrize("precision,backbone", [("fp32", "resnet50"), ("bf16", "resnet50"),
                                                 ("bf16", "resnest50"), ("fp32", "resnest50")])
 def test_bn_bwd_ds_dual_bit_identical(dev, precision, backbone):
