@@ -1,5 +1,5 @@
-"""The 8-channel forms of the bf16 stem's maxpool forward (maxpool_fwd_bn8_a16), of its
-BatchNorm/maxpool backward apply (stem_bwd_apply8q, per 2x2 input quad) and of the bf16 BN applies
+"""The 8-channel forms of the stem's maxpool forward (maxpool_fwd_bn8; bf16 and, since round 5, fp32 y), of its
+BatchNorm/maxpool backward apply (stem_bwd_apply8q, per 2x2 input quad; fp32 y too) and of the bf16 BN applies
 (bn_apply8_a16_k) against the 4-channel forms the library falls back to: the 8-wide kernels need
 16-B aligned tensors, so the same values handed over 8 bytes off a 16-B boundary take the 4-wide
 form (no environment switch).  Bit-identical outputs, argmax and gradients, including ties
@@ -27,26 +27,33 @@ def _off8(t):
     return v
 
 
-def _stem_case(dev, n, h, w, c, seed):
+def _stem_case(dev, n, h, w, c, seed, dtype=torch.bfloat16):
     g = torch.Generator().manual_seed(seed)
     # quantised to a few levels: many equal values inside a window (ties)
-    y = (torch.randint(-6, 7, (n, h, w, c), generator=g).float() / 4).to(torch.bfloat16).to(dev)
+    y = (torch.randint(-6, 7, (n, h, w, c), generator=g).float() / 4).to(dtype).to(dev)
     scale = (torch.rand(c, generator=g) + 0.5).to(dev)
     shift = (torch.randn(c, generator=g) * 0.2).to(dev)
     return y, scale, shift
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape", [(3, 112, 112, 64), (2, 13, 11, 16), (2, 9, 10, 24)])
-def test_maxpool_fwd_bn8_bit_identical(dev, shape):
-    y, scale, shift = _stem_case(dev, *shape, seed=sum(shape))
+def test_maxpool_fwd_bn8_bit_identical(dev, shape, dtype):
+    """(fp32 y in and out: the fp32 step's stem takes the 8-channel form since round 5.)"""
+    y, scale, shift = _stem_case(dev, *shape, seed=sum(shape), dtype=dtype)
     p8, a8 = ops.maxpool_fwd_bn(y, scale, shift)
     p4, a4 = ops.maxpool_fwd_bn(_off8(y), scale, shift)    # the 4-wide form
+    assert p8.dtype == dtype
     assert torch.equal(p8.view(torch.int16), p4.view(torch.int16))
     assert torch.equal(a8, a4)
     # the values are relu(bn(y)) maxima of the windows, argmax inside the window at a maximum
-    z = torch.relu(y.float() * scale + shift)
+    # (float64 products: the kernels' single-rounding fmaf)
+    z = torch.relu((y.double() * scale.double() + shift.double()).float())
     ref = torch.nn.functional.max_pool2d(z.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
-    assert torch.equal(p8.float(), ref.to(torch.bfloat16).float())
+    if dtype == torch.bfloat16:
+        assert torch.equal(p8.float(), ref.to(torch.bfloat16).float())
+    else:
+        assert torch.allclose(p8, ref, rtol=1e-6, atol=1e-7)
     assert int(a8.max()) <= 8
     n, h, w, c = shape
     ho, wo = a8.shape[1], a8.shape[2]
@@ -57,13 +64,16 @@ def test_maxpool_fwd_bn8_bit_identical(dev, shape):
     nn_ = torch.arange(n, device=dev).view(n, 1, 1, 1).expand_as(ids)
     cc = torch.arange(c, device=dev).view(1, c, 1, 1).expand_as(ids)
     picked = zp[nn_, cc, oy + ids // 3, ox + ids % 3]
-    assert torch.equal(picked.to(torch.bfloat16).float(), ref.permute(0, 3, 1, 2).to(torch.bfloat16).float())
+    assert torch.allclose(picked.to(dtype).float(), ref.permute(0, 3, 1, 2).to(dtype).float(),
+                          rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape", [(3, 112, 112, 64), (2, 13, 11, 16), (2, 12, 9, 8), (2, 9, 10, 24)])
-def test_stem_bwd_apply8_bit_identical(dev, shape):
+def test_stem_bwd_apply8_bit_identical(dev, shape, dtype):
+    """(fp32 y: the fp32 step's stem takes the same quad form since round 5.)"""
     n, h, w, c = shape
-    y, scale, shift = _stem_case(dev, *shape, seed=7 + sum(shape))
+    y, scale, shift = _stem_case(dev, *shape, seed=7 + sum(shape), dtype=dtype)
     _, am = ops.maxpool_fwd_bn(y, scale, shift)
     ho, wo = am.shape[1], am.shape[2]
     g = torch.Generator().manual_seed(11)
@@ -74,7 +84,7 @@ def test_stem_bwd_apply8_bit_identical(dev, shape):
     d8, g8, b8 = ops.bn_bwd_maxpool(dyp, am, y, scale, shift, mean, inv, gamma)
     # the 4-wide, one-pixel-per-thread form against the default 8-channel 2x2-quad form
     d4, g4, b4 = ops.bn_bwd_maxpool(dyp, am, _off8(y), scale, shift, mean, inv, gamma)
-    assert torch.equal(d8.view(torch.int16), d4.view(torch.int16))
+    assert torch.equal(d8.view(torch.int16), d4.view(torch.int16))   # (fp32: both halves)
     assert torch.equal(g8, g4) and torch.equal(b8, b4)
     # the maxpool gradient routed through argmax, masked by the stem ReLU, then the BN backward
     ids = am.long()

@@ -883,18 +883,56 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply(const PoolGeo pg, const TY*
 }
 
 
+// 8 consecutive elements (index i in units of 8) of an fp32 or bf16 tensor, as fp32 values
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, long i, float (&v)[8]);
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, long i, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[2 * i], b = reinterpret_cast<const float4*>(p)[2 * i + 1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void ld8<__bf16>(const __bf16* p, long i, float (&v)[8]) {
+  const uint4 w = reinterpret_cast<const uint4*>(p)[i];
+  const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(u[e] << 16);
+    v[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, long i, const float (&v)[8]);
+template <>
+__device__ __forceinline__ void st8<float>(float* p, long i, const float (&v)[8]) {
+  reinterpret_cast<float4*>(p)[2 * i] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[2 * i + 1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <>
+__device__ __forceinline__ void st8<__bf16>(__bf16* p, long i, const float (&v)[8]) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16x2_t q = {(__bf16)v[2 * e], (__bf16)v[2 * e + 1]};
+    w[e] = __builtin_bit_cast(uint32_t, q);
+  }
+  reinterpret_cast<uint4*>(p)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
 // The same per 2x2 quad of input pixels (rows 2k, 2k+1, columns 2l, 2l+1): the pooled outputs
 // (k .. k+1) x (l .. l+1) are the candidates of all four pixels, so each is loaded once per quad
 // -- one pooled load per pixel instead of 2.25 (the launch is bound by those gathered bytes).
 // Pixel (py, px) of the quad sums candidate (dy, dx) when (dy <= py, dx <= px, in range) with
 // id = (py + 1 - 2dy) * 3 + (px + 1 - 2dx), in the order (0,0), (0,1), (1,0), (1,1): the
 // per-pixel kernels' order, so bit-identical.  nq = n * ceil(h/2) * ceil(w/2) * c/8 < 2^31.
+// TY / TD: y and dy fp32 or bf16 (round 5: the fp32 step's stem too).
+template <typename TY, typename TD>
 __global__ __launch_bounds__(NT) void stem_bwd_apply8q(const PoolGeo pg, int h, int w, FastDiv dQHW,
-                                                       FastDiv dQW, const __bf16* __restrict__ y,
+                                                       FastDiv dQW, const TY* __restrict__ y,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const float* __restrict__ coef,
-                                                       __bf16* __restrict__ dy, int nq, int lc8) {
+                                                       TD* __restrict__ dy, int nq, int lc8) {
   const int c8 = 1 << lc8, c = c8 * 8;
   const uint2* am = reinterpret_cast<const uint2*>(pg.am);
   const float4* dp = reinterpret_cast<const float4*>(pg.dyp);
@@ -937,14 +975,8 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply8q(const PoolGeo pg, int h, 
         const int iy = 2 * k + py, ix = 2 * l + px;
         if (iy >= h || ix >= w) continue;
         const long pix = ((long)nn * h + iy) * w + ix;
-        const uint4 yw = reinterpret_cast<const uint4*>(y)[pix * c8 + cq];
-        const uint32_t yu[4] = {yw.x, yw.y, yw.z, yw.w};
         float v[8], g[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[2 * e] = __uint_as_float(yu[e] << 16);
-          v[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
-        }
+        ld8(y, pix * c8 + cq, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
@@ -961,21 +993,13 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply8q(const PoolGeo pg, int h, 
               if (ab == id) g[e] += dv[e];
             }
           }
-        uint32_t ow[4];
+        float o[8];
 #pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-          float o[2];
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const int e = 2 * e2 + t;
-            const float gm = fmaf(v[e], sc[e], sf[e]) > 0.f ? g[e] : 0.f;
-            o[t] = fmaf(A[e], gm, fmaf(B[e], v[e], C[e]));
-          }
-          typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-          const bf16x2_t p = {(__bf16)o[0], (__bf16)o[1]};
-          ow[e2] = __builtin_bit_cast(uint32_t, p);
+        for (int e = 0; e < 8; ++e) {
+          const float gm = fmaf(v[e], sc[e], sf[e]) > 0.f ? g[e] : 0.f;
+          o[e] = fmaf(A[e], gm, fmaf(B[e], v[e], C[e]));
         }
-        reinterpret_cast<uint4*>(dy)[pix * c8 + cq] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        st8(dy, pix * c8 + cq, o);
       }
   }
 }
@@ -1332,7 +1356,21 @@ static int bn_bwd_maxpool_impl(const float* dyp, const uint8_t* argmax, int n, i
   TMR_CHECK_LAUNCH("bn_bwd_final");
   if (!dyv) return 0;   // coefficients only: the stem's direct wgrad applies them on load
   const long n4 = rows_l * c / 4;
-  if (out_bf16)
+  const int c8 = c / 8;
+  // per 2x2 input quad, 8 channels per thread (stem_bwd_apply8q, as the bf16-activation step's
+  // stem; round 5 for fp32 y), else one pixel and 4 channels per thread
+  if (c % 8 == 0 && (c8 & (c8 - 1)) == 0 && n4 / 2 < 0x7fffffffL &&
+      (((uintptr_t)dyp | (uintptr_t)y | (uintptr_t)dyv) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
+    const int qh = (h + 1) / 2, qw = (w + 1) / 2;
+    const int nq = n * qh * qw * c8;
+    const FastDiv dqhw = make_fastdiv((uint32_t)(qh * qw)), dqw = make_fastdiv((uint32_t)qw);
+    if (out_bf16)
+      hipLaunchKernelGGL((stem_bwd_apply8q<float, __bf16>), dim3(ew_blocks(nq)), dim3(NT), 0, stream,
+                         pg, h, w, dqhw, dqw, y, scale, shift, coef, (__bf16*)dyv, nq, __builtin_ctz(c8));
+    else
+      hipLaunchKernelGGL((stem_bwd_apply8q<float, float>), dim3(ew_blocks(nq)), dim3(NT), 0, stream,
+                         pg, h, w, dqhw, dqw, y, scale, shift, coef, (float*)dyv, nq, __builtin_ctz(c8));
+  } else if (out_bf16)
     hipLaunchKernelGGL(stem_bwd_apply<__bf16>, dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg, y, scale,
                        shift, coef, (__bf16*)dyv, n4, c / 4);
   else
@@ -1676,41 +1714,6 @@ TMR_API int tmr_bn_bwd_parts_g16(const void* g, const void* y, const void* parts
 // T: float (fp32 step: g, y, dy fp32) or __bf16 (bf16-activation step under R16: all bf16, dy
 // rounded RNE).  8 elements per thread, 16-B accesses.
 template <typename T>
-__device__ __forceinline__ void ld8(const T* p, long i, float (&v)[8]);
-template <>
-__device__ __forceinline__ void ld8<float>(const float* p, long i, float (&v)[8]) {
-  const float4 a = reinterpret_cast<const float4*>(p)[2 * i], b = reinterpret_cast<const float4*>(p)[2 * i + 1];
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-template <>
-__device__ __forceinline__ void ld8<__bf16>(const __bf16* p, long i, float (&v)[8]) {
-  const uint4 w = reinterpret_cast<const uint4*>(p)[i];
-  const uint32_t u[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    v[2 * e] = __uint_as_float(u[e] << 16);
-    v[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
-  }
-}
-template <typename T>
-__device__ __forceinline__ void st8(T* p, long i, const float (&v)[8]);
-template <>
-__device__ __forceinline__ void st8<float>(float* p, long i, const float (&v)[8]) {
-  reinterpret_cast<float4*>(p)[2 * i] = make_float4(v[0], v[1], v[2], v[3]);
-  reinterpret_cast<float4*>(p)[2 * i + 1] = make_float4(v[4], v[5], v[6], v[7]);
-}
-template <>
-__device__ __forceinline__ void st8<__bf16>(__bf16* p, long i, const float (&v)[8]) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  uint32_t w[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const bf16x2_t q = {(__bf16)v[2 * e], (__bf16)v[2 * e + 1]};
-    w[e] = __builtin_bit_cast(uint32_t, q);
-  }
-  reinterpret_cast<uint4*>(p)[i] = make_uint4(w[0], w[1], w[2], w[3]);
-}
-template <typename T>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_ds8(const T* __restrict__ g, const T* __restrict__ y,
                                                        const T* __restrict__ yd,
                                                        const float* __restrict__ coef,
@@ -1837,9 +1840,9 @@ TMR_API int tmr_bn_bwd_maxpool_a16(const float* dyp, const uint8_t* argmax, int 
       (((uintptr_t)dyp | (uintptr_t)y | (uintptr_t)dy) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
     const int qh = (h + 1) / 2, qw = (w + 1) / 2;
     const int nq = n * qh * qw * c8;
-    hipLaunchKernelGGL(stem_bwd_apply8q, dim3(ew_blocks(nq)), dim3(NT), 0, stream, pg, h, w,
-                       make_fastdiv((uint32_t)(qh * qw)), make_fastdiv((uint32_t)qw), yb, scale,
-                       shift, coef, (__bf16*)dy, nq, __builtin_ctz(c8));
+    hipLaunchKernelGGL((stem_bwd_apply8q<__bf16, __bf16>), dim3(ew_blocks(nq)), dim3(NT), 0, stream,
+                       pg, h, w, make_fastdiv((uint32_t)(qh * qw)), make_fastdiv((uint32_t)qw), yb,
+                       scale, shift, coef, (__bf16*)dy, nq, __builtin_ctz(c8));
   } else {
     hipLaunchKernelGGL((stem_bwd_apply<__bf16, __bf16>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, pg,
                        yb, scale, shift, coef, (__bf16*)dy, n4, c / 4);

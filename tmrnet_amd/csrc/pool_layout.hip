@@ -83,17 +83,39 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_k(const TX* __restrict__ x, TY
   }
 }
 
-// The bf16-activation form (bf16 pre-BN input, bf16 output), 8 channels per thread: 32-bit
-// magic-number index division instead of maxpool_fwd_k's 64-bit divides, the 9 window loads
-// (16 B each) issued before any is consumed, 16-B y and 8-B argmax stores.  Same BN+ReLU
-// arithmetic and scan order as maxpool_fwd_k: identical outputs.  total = n*ho*wo*c/8 < 2^31,
-// c / 8 a power of two (lc8 = log2), both checked on the host.
-__global__ __launch_bounds__(NT) void maxpool_fwd_bn8_a16(const __bf16* __restrict__ x,
-                                                         __bf16* __restrict__ y,
-                                                         uint2* __restrict__ am, int total, int h,
-                                                         int w, int lc8, FastDiv dHWo, FastDiv dWo,
-                                                         const float* __restrict__ scale,
-                                                         const float* __restrict__ shift) {
+// 8 consecutive values (index i in units of 8) of an fp32 / bf16 tensor as raw words, and their
+// fp32 values
+struct Raw8 { uint4 a, b; };
+__device__ __forceinline__ Raw8 ld_raw8(const float* p, int i) {
+  return {reinterpret_cast<const uint4*>(p)[2 * i], reinterpret_cast<const uint4*>(p)[2 * i + 1]};
+}
+__device__ __forceinline__ Raw8 ld_raw8(const __bf16* p, int i) {
+  return {reinterpret_cast<const uint4*>(p)[i], make_uint4(0u, 0u, 0u, 0u)};
+}
+template <typename T>
+__device__ __forceinline__ float raw_val(const Raw8& r, int e) {
+  if constexpr (std::is_same<T, float>::value) {
+    const uint4 q = e < 4 ? r.a : r.b;
+    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+    return __uint_as_float(w4[e & 3]);
+  } else {
+    const uint32_t w4[4] = {r.a.x, r.a.y, r.a.z, r.a.w};
+    return __uint_as_float((e & 1) ? (w4[e >> 1] & 0xffff0000u) : (w4[e >> 1] << 16));
+  }
+}
+
+// The 8-channel form (the bf16-activation step's bf16 pre-BN input and bf16 output; round 5: the
+// fp32 step's fp32 input too), 8 channels per thread: 32-bit magic-number index division instead
+// of maxpool_fwd_k's 64-bit divides, the 9 window loads issued before any is consumed, 16-B
+// stores of y and 8-B argmax stores.  Same BN+ReLU arithmetic and scan order as maxpool_fwd_k:
+// identical outputs.  total = n*ho*wo*c/8 < 2^31, c / 8 a power of two (lc8 = log2), both
+// checked on the host.
+template <typename TX, typename TY>
+__global__ __launch_bounds__(NT) void maxpool_fwd_bn8(const TX* __restrict__ x, TY* __restrict__ y,
+                                                     uint2* __restrict__ am, int total, int h,
+                                                     int w, int lc8, FastDiv dHWo, FastDiv dWo,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift) {
   const int c8 = 1 << lc8;
   for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
     const int cq = i & (c8 - 1);
@@ -101,14 +123,14 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_bn8_a16(const __bf16* __restri
     const uint32_t nn = fdiv(p, dHWo);
     const uint32_t rem = p - nn * dHWo.d;
     const int oy = (int)fdiv(rem, dWo), ox = (int)(rem - (uint32_t)oy * dWo.d);
-    uint4 u[9];
+    Raw8 u[9];
     bool ok[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const int iy = oy * 2 - 1 + k / 3, ix = ox * 2 - 1 + k % 3;
       ok[k] = iy >= 0 && iy < h && ix >= 0 && ix < w;
       const int src = ok[k] ? (((int)nn * h + iy) * w + ix) * c8 + cq : i;
-      u[k] = reinterpret_cast<const uint4*>(x)[src];
+      u[k] = ld_raw8(x, src);
     }
     float sc[8], sf[8];
     {
@@ -128,23 +150,27 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_bn8_a16(const __bf16* __restri
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       if (!ok[k]) continue;
-      const uint32_t w4[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float raw = __uint_as_float((e & 1) ? (w4[e >> 1] & 0xffff0000u) : (w4[e >> 1] << 16));
+        const float raw = raw_val<TX>(u[k], e);
         const float v = fmaxf(fmaf(raw, sc[e], sf[e]), 0.f);
         // first maximum in scan order wins (PyTorch: val > max || isnan(val))
         if (v > best[e] || isnan(v)) { best[e] = v; bi[e] = (uint32_t)k; }
       }
     }
-    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-    uint32_t ow[4];
+    if constexpr (std::is_same<TY, float>::value) {
+      reinterpret_cast<float4*>(y)[2 * i] = make_float4(best[0], best[1], best[2], best[3]);
+      reinterpret_cast<float4*>(y)[2 * i + 1] = make_float4(best[4], best[5], best[6], best[7]);
+    } else {
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      uint32_t ow[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bf16x2_t pr = {(__bf16)best[2 * e], (__bf16)best[2 * e + 1]};
-      ow[e] = __builtin_bit_cast(uint32_t, pr);
+      for (int e = 0; e < 4; ++e) {
+        const bf16x2_t pr = {(__bf16)best[2 * e], (__bf16)best[2 * e + 1]};
+        ow[e] = __builtin_bit_cast(uint32_t, pr);
+      }
+      reinterpret_cast<uint4*>(y)[i] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
     }
-    reinterpret_cast<uint4*>(y)[i] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
     am[i] = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
                        bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
   }
@@ -301,7 +327,21 @@ TMR_API int tmr_maxpool2d_fwd_bn_x(const float* x, const float* scale, const flo
   TMR_CHECK_ARG(c % 4 == 0, "tmr_maxpool2d_fwd_bn: channels %d must be a multiple of 4", c);
   TMR_CHECK_ARG(scale && shift, "tmr_maxpool2d_fwd_bn: null BatchNorm scale/shift");
   const long total = (long)n * ho * wo * (c / 4);
-  if (out_bf16)
+  const int c8 = c / 8;
+  // 8 channels per thread (maxpool_fwd_bn8, as the bf16 step's stem; round 5), else 4-wide
+  if (c % 8 == 0 && (c8 & (c8 - 1)) == 0 && (long)n * h * w * c8 < 0x7fffffffL &&
+      (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
+    const int t8 = (int)(total / 2);
+    const FastDiv dhwo = make_fastdiv((uint32_t)(ho * wo)), dwo = make_fastdiv((uint32_t)wo);
+    if (out_bf16)
+      hipLaunchKernelGGL((maxpool_fwd_bn8<float, __bf16>), dim3(ew_blocks(t8)), dim3(NT), 0, stream,
+                         x, (__bf16*)y, (uint2*)argmax, t8, h, w, __builtin_ctz(c8), dhwo, dwo,
+                         scale, shift);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_bn8<float, float>), dim3(ew_blocks(t8)), dim3(NT), 0, stream,
+                         x, (float*)y, (uint2*)argmax, t8, h, w, __builtin_ctz(c8), dhwo, dwo,
+                         scale, shift);
+  } else if (out_bf16)
     hipLaunchKernelGGL((maxpool_fwd_k<true, __bf16>), dim3(ew_blocks(total)), dim3(NT), 0, stream, x,
                        (__bf16*)y, (uchar4*)argmax, n, h, w, c / 4, ho, wo, scale, shift);
   else
@@ -323,7 +363,7 @@ TMR_API int tmr_maxpool2d_fwd_bn_a16(const void* x, const float* scale, const fl
       (long)n * h * w * c8 < 0x7fffffffL &&
       (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && ((uintptr_t)argmax & 7) == 0) {
     const int t8 = (int)(total / 2);
-    hipLaunchKernelGGL(maxpool_fwd_bn8_a16, dim3(ew_blocks(t8)), dim3(NT), 0, stream,
+    hipLaunchKernelGGL((maxpool_fwd_bn8<__bf16, __bf16>), dim3(ew_blocks(t8)), dim3(NT), 0, stream,
                        (const __bf16*)x, (__bf16*)y, (uint2*)argmax, t8, h, w, __builtin_ctz(c8),
                        make_fastdiv((uint32_t)(ho * wo)), make_fastdiv((uint32_t)wo), scale, shift);
   } else {
