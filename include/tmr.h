@@ -288,6 +288,21 @@ int tmr_weight_oihw_to_krsc_x(const float* w, void* wk, int k, int c, int r, int
  * only a conv operand). */
 int tmr_weight_oihw_to_crsk_x(const float* w, void* wt, int k, int c, int r, int s, int out_bf16,
                               hipStream_t stream);
+/* Every weight layout of a train step in one launch: the table (device memory, n entries, block0
+ * ascending from 0, each entry ceil(n_out / tmr_weight_layouts_epb()) blocks; total_blocks their
+ * sum) lists OIHW fp32 sources and their KRSC (kind 0, channels zero-padded to cpad) or CRSK
+ * (kind 1) destinations, fp32 or bf16 (RNE) -- the values of tmr_weight_oihw_to_krsc_x /
+ * tmr_weight_oihw_to_crsk_x per entry (the per-conv launches of the trunk's forward, ~70 a step). */
+typedef struct tmr_wlayout {
+  const float* w;
+  void* out;
+  long long n;       /* destination elements */
+  long long block0;  /* first block of this entry */
+  int k, c, rs, cpad;
+  int kind, bf16;
+} tmr_wlayout;
+int tmr_weight_layouts_epb(void);
+int tmr_weight_layouts_multi(const tmr_wlayout* table, int n, int total_blocks, hipStream_t stream);
 int tmr_bn_apply_dual(const float* y, const float* scale, const float* shift, const float* residual,
                       float* z, void* z16, int rows, int c, int relu, hipStream_t stream);
 /* Block outputs of the fp32 train step: tmr_bn_apply (residual optional) / tmr_bn_apply2 with

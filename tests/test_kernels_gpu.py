@@ -745,6 +745,51 @@ def test_bn_bwd_ds_dual_bit_identical(dev, precision, backbone):
         assert torch.equal(res[True][2][n], res[False][2][n]), n
 
 
+@pytest.mark.parametrize("precision,backbone", [("fp32", "resnet50"), ("bf16", "resnet50"),
+                                                ("bf16", "resnest50")])
+def test_weight_layout_sessions(dev, precision, backbone):
+    """ops.layout_session: the trunk's weight layouts (KRSC / CRSK, fp32 / bf16, grouped) recorded
+    on the first step and refreshed by one tmr_weight_layouts_multi launch on later steps --
+    three SGD steps with sessions give bit-identical logits, gradients, weights and running
+    statistics to three steps with per-conv conversions (the refresh must see every update)."""
+    import tmrnet_amd
+    B, T, L = 2, 5, 7
+    g = torch.Generator().manual_seed(9)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)
+    lt = (torch.rand(B, L, 512, generator=g) * 2 - 1).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=g).to(dev)
+    res = {}
+    saved = ops.LAYOUT_SESSIONS
+    try:
+        for on in (True, False):
+            ops.LAYOUT_SESSIONS = on
+            torch.manual_seed(0)
+            kw = {} if backbone == "resnet50" else {"time_conv": True, "backbone": backbone}
+            m = tmrnet_amd.resnet_lstm(seq_len=T, precision=precision, **kw).to(dev).train()
+            m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+            m.forced_head_mask = torch.ones(B, 512, device=dev)
+            opt = tmrnet_amd.SGD(m.parameters(), lr=1e-3, momentum=0.9)
+            outs = []
+            for _ in range(3):
+                opt.zero_grad(set_to_none=True)
+                out = m(ops.crop_normalize(frames, off, T), lt)
+                tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels).backward()
+                opt.step()
+                outs.append(out.detach().clone())
+            torch.cuda.synchronize()
+            res[on] = (outs, {n: p.detach().clone() for n, p in m.named_parameters()},
+                       {n: b.clone() for n, b in m.named_buffers()})
+    finally:
+        ops.LAYOUT_SESSIONS = saved
+    for a, b in zip(res[True][0], res[False][0]):
+        assert torch.equal(a, b)
+    for n in res[True][1]:
+        assert torch.equal(res[True][1][n], res[False][1][n]), n
+    for n in res[True][2]:
+        assert torch.equal(res[True][2][n], res[False][2][n]), n
+
+
 def _pack_bits(m):
     """(numel,) bool -> int32 words, element e = bit e % 32 of word e // 32."""
     m = m.reshape(-1).to(torch.int64)

@@ -77,6 +77,8 @@ SIGNATURES = {
     "tmr_bn_bwd_parts_a16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_parts_g16": [P, P, P, I, P, P, P, P, P, P, I, I, P, SZ, P],
     "tmr_bn_bwd_g16": [P, P, P, P, P, P, P, P, I, I, P, SZ, P],
+    "tmr_weight_layouts_epb": [],
+    "tmr_weight_layouts_multi": [P, I, I, P],
     "tmr_bn_bwd_parts_ds_ws_bytes": [I, I, I],
     "tmr_bn_bwd_parts_ds": [P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, SZ, P],
     "tmr_bn_bwd_maxpool_a16": [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, I, P, SZ, P],

@@ -440,6 +440,52 @@ TMR_API int tmr_weight_oihw_to_crsk_x(const float* w, void* wt, int k, int c, in
   return 0;
 }
 
+// Every weight layout of a train step in one launch (tmr_weight_layouts_multi): block b converts
+// elements [ (b - block0) * NT * WL_EPB, ... ) of the entry whose block range holds it (binary
+// search over block0); the element mapping and rounding of oihw_to_krsc_k / oihw_to_crsk_k.
+constexpr int WL_EPB = 8;
+__global__ __launch_bounds__(NT) void wlayout_multi_k(const tmr_wlayout* __restrict__ tab, int n) {
+  int lo = 0, hi = n - 1;
+  const long long b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].block0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const tmr_wlayout e = tab[lo];
+  const long long base = (b - e.block0) * (long long)NT * WL_EPB;
+#pragma unroll
+  for (int j = 0; j < WL_EPB; ++j) {
+    const long long i = base + (long long)j * NT + threadIdx.x;
+    if (i >= e.n) break;
+    float v;
+    if (e.kind == 0) {   // KRSC, channels zero-padded to cpad
+      const int ci = (int)(i % e.cpad);
+      const long long t = i / e.cpad;
+      const int tap = (int)(t % e.rs);
+      const int ko = (int)(t / e.rs);
+      v = ci < e.c ? e.w[((long long)ko * e.c + ci) * e.rs + tap] : 0.f;
+    } else {             // CRSK
+      const int ko = (int)(i % e.k);
+      const long long t = i / e.k;
+      const int tap = (int)(t % e.rs);
+      const int ci = (int)(t / e.rs);
+      v = e.w[((long long)ko * e.c + ci) * e.rs + tap];
+    }
+    if (e.bf16) reinterpret_cast<__bf16*>(e.out)[i] = (__bf16)v;   // RNE
+    else reinterpret_cast<float*>(e.out)[i] = v;
+  }
+}
+
+TMR_API int tmr_weight_layouts_multi(const tmr_wlayout* tab_dev, int n, int total_blocks,
+                                     hipStream_t stream) {
+  TMR_CHECK_ARG(tab_dev && n > 0 && total_blocks > 0, "tmr_weight_layouts_multi: empty table");
+  hipLaunchKernelGGL(wlayout_multi_k, dim3(total_blocks), dim3(NT), 0, stream, tab_dev, n);
+  TMR_CHECK_LAUNCH("weight_layouts_multi");
+  return 0;
+}
+
+TMR_API int tmr_weight_layouts_epb(void) { return NT * WL_EPB; }
+
 // fp32 -> bf16 (RNE) copy: the bf16 conv operand of a tensor produced in fp32 (ResNeSt split-
 // attention / pool outputs), 8 elements per thread
 __global__ __launch_bounds__(NT) void cast_bf16_k(const float* __restrict__ x, __bf16* __restrict__ y,

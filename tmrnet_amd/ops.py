@@ -6,7 +6,9 @@ stream, and raises RuntimeError on a failed call.  No function here computes
 anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 """
 import contextlib
+import threading
 
+import numpy as np
 import torch
 
 from ._lib import call, query, stream_ptr, has_prologues, ConvDesc, ConvPrologue
@@ -560,35 +562,139 @@ def col_sum(x, rows, cols, ld, out=None, beta=0.0):
 
 
 # --------------------------------------------------------------------- layout
+# ---- weight layouts of a train step in one launch (round 5) ---------------------------------
+# A trunk forward converts every conv weight (OIHW fp32) to its KRSC forward / CRSK dgrad operand,
+# ~70 small launches a step.  Inside `layout_session(key)`, the first forward records the
+# conversions it asks for (normal launches, outputs kept); every later forward with the same key
+# refreshes all of them with one tmr_weight_layouts_multi launch at the session's start, and the
+# weight_to_* calls return the refreshed tensors -- the same values (copies and RNE roundings).
+# A request the record lacks (other weights, shapes, flags) is converted directly and the record
+# is rebuilt on the next forward.
+class _LayoutRecord:
+    def __init__(self):
+        self.lookup = {}     # request key -> returned tensor
+        self.rows = []       # table rows (w ptr, out tensor, k, c, rs, cpad, kind, bf16)
+        self.table = None    # device table (uint8 bytes of _WL_DTYPE rows)
+        self.blocks = 0
+        self.valid = True
+
+
+_LAYOUTS = {}   # (session key, thread) -> _LayoutRecord: each thread refreshes its own copies
+_TLS = threading.local()   # .session = [active record, recording?]
+
+
+# include/tmr.h tmr_wlayout (56 bytes, no padding)
+_WL_DTYPE = np.dtype([("w", "<u8"), ("out", "<u8"), ("n", "<i8"), ("block0", "<i8"),
+                      ("k", "<i4"), ("c", "<i4"), ("rs", "<i4"), ("cpad", "<i4"),
+                      ("kind", "<i4"), ("bf16", "<i4")])
+
+
+def _session():
+    st = getattr(_TLS, "session", None)
+    if st is None:
+        st = _TLS.session = [None, False]
+    return st
+
+
+LAYOUT_SESSIONS = True   # (the equality test turns it off for its reference run)
+
+
+@contextlib.contextmanager
+def layout_session(key):
+    """See above.  key: one per trunk, mode and precision (the set of conversions it asks for)."""
+    if not LAYOUT_SESSIONS:
+        yield
+        return
+    key = (key, threading.get_ident())
+    rec = _LAYOUTS.get(key)
+    recording = rec is None or not rec.valid or rec.table is None
+    if recording:
+        rec = _LAYOUTS[key] = _LayoutRecord()
+    else:
+        call("tmr_weight_layouts_multi", rec.table, len(rec.rows), rec.blocks, stream_ptr())
+    st = _session()
+    prev = list(st)
+    st[0], st[1] = rec, recording
+    try:
+        yield
+    finally:
+        st[0], st[1] = prev
+        if recording and rec.rows and rec.valid:
+            epb = int(query("tmr_weight_layouts_epb"))
+            tab = np.zeros(len(rec.rows), dtype=_WL_DTYPE)
+            b0 = 0
+            for j, (wp, out, k, c, rs, cpad, kind, b16) in enumerate(rec.rows):
+                n = out.numel()
+                tab[j] = (wp, out.data_ptr(), n, b0, k, c, rs, cpad, kind, b16)
+                b0 += (n + epb - 1) // epb
+            rec.table = torch.from_numpy(tab.view(np.uint8).copy()).to(rec.rows[0][1].device)
+            rec.blocks = b0
+
+
+def _layout(key, convert, rows):
+    """The tensor for request `key`: from the active session's record when it holds it, else
+    convert() (recorded with its table rows -- rows(out) -- when the session is recording)."""
+    rec, recording = _session()
+    if rec is None:
+        return convert()
+    out = rec.lookup.get(key)
+    if out is not None and not recording:
+        return out
+    out = convert()
+    if recording:
+        rec.lookup[key] = out
+        rec.rows.extend(rows(out))
+    else:
+        rec.valid = False   # a conversion the record lacks: re-record on the next forward
+    return out
+
+
 def weight_to_krsc(w, cpad=None, bf16=False):
     """OIHW fp32 -> KRSC (channels zero-padded to cpad); bf16=True stores it rounded (RNE), for
     the bf16-math convs (tmr_conv_desc.io TMR_IO_W_BF16)."""
     k, c, r, s = w.shape
     cpad = c if cpad is None else cpad
-    out = _empty((k, r, s, cpad), w, dtype=torch.bfloat16 if bf16 else f32)
-    call("tmr_weight_oihw_to_krsc_x", _req(w, "w"), out, k, c, r, s, cpad, int(bf16), stream_ptr())
-    return out
+    _req(w, "w")
+
+    def convert():
+        out = _empty((k, r, s, cpad), w, dtype=torch.bfloat16 if bf16 else f32)
+        call("tmr_weight_oihw_to_krsc_x", w, out, k, c, r, s, cpad, int(bf16), stream_ptr())
+        return out
+    return _layout((w.data_ptr(), "krsc", k, c, r * s, cpad, int(bf16)), convert,
+                   lambda out: [(w.data_ptr(), out, k, c, r * s, cpad, 0, int(bf16))])
 
 
 def weight_to_crsk(w, bf16=True):
     """OIHW fp32 -> the transposed dgrad operand (Cin, R, S, Cout): the weights of the LDS-DMA
     engine's dgrad view, bf16 (RNE; TMR_IO_WT_BF16) or fp32 (bf16=False; TMR_IO_WT_F32)."""
     k, c, r, s = w.shape
-    out = _empty((c, r, s, k), w, dtype=torch.bfloat16 if bf16 else f32)
-    call("tmr_weight_oihw_to_crsk_x", _req(w, "w"), out, k, c, r, s, int(bf16), stream_ptr())
-    return out
+    _req(w, "w")
+
+    def convert():
+        out = _empty((c, r, s, k), w, dtype=torch.bfloat16 if bf16 else f32)
+        call("tmr_weight_oihw_to_crsk_x", w, out, k, c, r, s, int(bf16), stream_ptr())
+        return out
+    return _layout((w.data_ptr(), "crsk", k, c, r * s, c, int(bf16)), convert,
+                   lambda out: [(w.data_ptr(), out, k, c, r * s, c, 1, int(bf16))])
 
 
 def weight_to_crsk_grouped(w, groups, bf16=True):
     """Grouped OIHW (K, C/G, R, S) -> the per-group transposed dgrad operand (G, C/G, R, S, K/G)."""
     k, cg, r, s = w.shape
     kg = k // groups
-    out = _empty((groups, cg, r, s, kg), w, dtype=torch.bfloat16 if bf16 else f32)
     _req(w, "w")
-    for g in range(groups):
-        call("tmr_weight_oihw_to_crsk_x", w[g * kg:(g + 1) * kg], out[g], kg, cg, r, s, int(bf16),
-             stream_ptr())
-    return out
+
+    def convert():
+        out = _empty((groups, cg, r, s, kg), w, dtype=torch.bfloat16 if bf16 else f32)
+        for g in range(groups):
+            call("tmr_weight_oihw_to_crsk_x", w[g * kg:(g + 1) * kg], out[g], kg, cg, r, s,
+                 int(bf16), stream_ptr())
+        return out
+
+    def rows(out):
+        return [(w[g * kg:(g + 1) * kg].data_ptr(), out[g], kg, cg, r * s, cg, 1, int(bf16))
+                for g in range(groups)]
+    return _layout((w.data_ptr(), "crsk_g", k, cg, r * s, groups, int(bf16)), convert, rows)
 
 
 def nhwc4_to_bf16x8(x4):

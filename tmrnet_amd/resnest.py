@@ -270,6 +270,13 @@ class ResNeStTrunkFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x4, share, keep, *params):
+        # every conv weight layout of the step in one launch (ops.layout_session)
+        with ops.layout_session(("resnest50", id(share), share.training, bool(keep),
+                                 share.precision)):
+            return ResNeStTrunkFn._forward(ctx, x4, share, keep, params)
+
+    @staticmethod
+    def _forward(ctx, x4, share, keep, params):
         from .trunk import _conv_bn, _act16
         mt = share.precision
         a16 = _act16(mt)
