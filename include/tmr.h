@@ -92,6 +92,9 @@ typedef struct tmr_conv_desc {
                               3x3 convs, direct3.hip) -- the independent second implementation the
                               tests compare those kernels with.  Changes the fp32 summation order
                               only. */
+#define TMR_IO_CLASSES 512 /* dgrad, any math: a strided dgrad as one launch per stride-parity
+                              class, as before round 5 -- the form the one-launch path
+                              (every class's tiles in one grid) is compared with; same values */
 #define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the io bits fp32 math takes: this one and
                               TMR_IO_ENGINE): w is the
                               transposed fp32 copy Wt[Cin][R][S][Cout] (tmr_weight_oihw_to_crsk_x,

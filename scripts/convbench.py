@@ -63,7 +63,12 @@ def main():
                     help="comma list of cin:cout:r:h filters, e.g. 64:256:1:56")
     ap.add_argument("--dgrad-beta", type=float, default=0.0,
                     help="accumulate dgrad into its output (the train step does for conv1/ds)")
+    ap.add_argument("--classes", action="store_true",
+                    help="strided dgrads as one launch per stride-parity class (TMR_IO_CLASSES, "
+                         "the A/B of the one-launch form)")
     args = ap.parse_args()
+    if args.classes:
+        ops._CLASSES[0] = True
     dev = torch.device("cuda:0")
     shapes = Counter(resnet50_convs(args.frames))
     kinds = args.kinds.split(",")

@@ -512,6 +512,61 @@ def test_conv_dgrad_fused_bn_backward_frame_chunks(dev, wtr):
     assert torch.equal(a[0], b[0]) and rel_err(yb, ya) < 1e-6
 
 
+@pytest.mark.parametrize("case", [
+    # n, h, w, cin (dx channels), cout (dy channels), r, pad
+    (3, 14, 14, 128, 128, 3, 1),   # the layer3.0 conv2 geometry: classes of 1 / 2 / 2 / 4 taps
+    (2, 7, 9, 64, 128, 3, 1),      # odd sizes: classes of unequal tile counts
+    (2, 14, 14, 256, 512, 1, 0),   # 1x1 downsample: three tap-less (epilogue-only) classes
+    (5, 13, 13, 64, 64, 3, 1),     # 64-channel dy (the 256x64 / 64x64 tiles)
+])
+@pytest.mark.parametrize("math", ["fp32", "bf16"])
+def test_dgrad_parity_classes_one_launch(dev, case, math):
+    """A stride-2 dgrad runs its four stride-parity classes as one launch (gemm16_par_kernel,
+    round 5): bit-identical to one launch per class (TMR_IO_CLASSES) -- the plain dgrad, the fused
+    BN-backward dgrad (masks 1 / 2 / 3; accumulating into an old dx) and its partial rows."""
+    n, h, w, cin, cout, r, pad = case
+    g = torch.Generator().manual_seed(31)
+    ho = (h + 2 * pad - r) // 2 + 1
+    wo = (w + 2 * pad - r) // 2 + 1
+    b16 = math == "bf16"
+    dt = torch.bfloat16 if b16 else torch.float32
+    dy = torch.randn(n, ho, wo, cout, generator=g).to(dev).to(dt)
+    w0 = (torch.randn(cout, cin, r, r, generator=g) / np.sqrt(cout * r * r)).to(dev)
+    wct = ops.weight_to_crsk(w0, bf16=b16)
+    y = torch.randn(n, h, w, cin, generator=g).to(dev).to(dt)
+    ye = y.float()
+    mean = ye.view(-1, cin).mean(0)
+    inv = 1.0 / (ye.view(-1, cin).var(0, unbiased=False) + 1e-5).sqrt()
+    sc = (torch.rand(cin, generator=g) + 0.5).to(dev) * inv
+    sh = (torch.randn(cin, generator=g) * 0.1).to(dev) - mean * sc
+    z = torch.relu(ye + torch.randn(n, h, w, cin, generator=g).to(dev) * 0.5).to(dt)
+    bits = _pack_bits((z.float() > 0).cpu()).to(dev)
+    old = torch.randn(n, h, w, cin, generator=g).to(dev)
+
+    def run():
+        out = [ops.conv_dgrad(dy, wct, (h, w), 2, pad, math=math, wt=True),
+               ops.conv_dgrad(dy, wct, (h, w), 2, pad, out=old.clone(), beta=1.0, math=math, wt=True)]
+        kw = dict(math=math, wt=True)
+        out += ops.conv_dgrad_bnbwd(dy, wct, (h, w), 2, pad, y, mean, 2, scale=sc, shift=sh, **kw)[:2]
+        out += ops.conv_dgrad_bnbwd(dy, wct, (h, w), 2, pad, y, mean, 1, z=z, out=old.clone(),
+                                    beta=1.0, **kw)[:2]
+        out += ops.conv_dgrad_bnbwd(dy, wct, (h, w), 2, pad, y, mean, 3, z=bits, out=old.clone(),
+                                    beta=1.0, **kw)[:2]
+        if b16:   # the bf16 step's g16 forms: non-residual (mask 2) and residual (old fp32 -> bf16)
+            out += ops.conv_dgrad_bnbwd(dy, wct, (h, w), 2, pad, y, mean, 2, scale=sc, shift=sh,
+                                        g16=True, **kw)[:2]
+            out += ops.conv_dgrad_bnbwd(dy, wct, (h, w), 2, pad, y, mean, 1, z=z, beta=1.0, g16=True,
+                                        old=old, **kw)[:2]
+        return out
+
+    one = run()
+    with ops.dgrad_class_launches():
+        per = run()
+    torch.cuda.synchronize()
+    for i, (u, v) in enumerate(zip(one, per)):
+        assert u.shape == v.shape and torch.equal(u, v), i
+
+
 def test_bn_apply_fused_consumers(dev):
     """The two BN applications folded into their consumers are bit-identical to the unfused
     sequence: bn_apply2 (Bottleneck bn3 + downsample-branch BN + ReLU, torchvision

@@ -25,6 +25,7 @@
 // path's, so FWD / DGRAD results are bit-identical to it.
 #pragma once
 #include "gemm16_select.h"
+#include <cstring>
 #include <type_traits>
 
 namespace tmrg {
@@ -471,10 +472,15 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // stage -- 32-40 KB instead of 64-80 KB, so three 4-wave workgroups fit a CU instead of one or
 // two: the short-reduction launches are bound by their epilogue's stores, and more workgroups
 // keep more of them in flight.  Same k order and epilogue: bit-identical to NST = 2.
-template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0,
-          int NST = 2>
-__global__ __launch_bounds__(64 * WM * WN, (WM * WN >= 16 || (WM * WN == 8 && (BM * BN <= 128 * 128 || NST == 1)) ? 4 : 2))
-void gemm16_kernel(const GemmArgs a) {
+// waves per SIMD the launch bounds promise (the register budget of a config)
+template <int BM, int BN, int WM, int WN, int NST>
+constexpr int occ16() {
+  return (WM * WN >= 16 || (WM * WN == 8 && (BM * BN <= 128 * 128 || NST == 1))) ? 4 : 2;
+}
+
+// the body of one workgroup: output tile `bid` (m-major over the n-tiles), reduction split `split`
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE, int F32, int PRO, int NST>
+__device__ __forceinline__ void gemm16_body(const GemmArgs& a, const int bid, const int split) {
   constexpr uint32_t ES = F32 ? 4u : 2u;   // element bytes
   constexpr int EPC = 16 / ES;             // elements per 16-B chunk
   constexpr int BK = 128 / ES;             // elements per k-tile (128-B image rows)
@@ -519,10 +525,7 @@ void gemm16_kernel(const GemmArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int l31 = lane & 31, hh = lane >> 5;
 
-  // XCD-aware tile order (gemm_kernel's)
   const int nnt = (a.N + BN - 1) / BN;
-  int bid, split;
-  xcd_work(bid, split);   // gemm_kernel.h
   const int m0 = (bid / nnt) * BM;
   const int n0 = (bid % nnt) * BN;
 
@@ -1029,6 +1032,79 @@ void gemm16_kernel(const GemmArgs a) {
                                                  split);
 }
 
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0,
+          int NST = 2>
+__global__ __launch_bounds__(64 * WM * WN, (occ16<BM, BN, WM, WN, NST>()))
+void gemm16_kernel(const GemmArgs a) {
+  int bid, split;
+  xcd_work(bid, split);   // XCD-aware tile order (gemm_kernel.h)
+  gemm16_body<MODE, BM, BN, WM, WN, TAPV, PIPE, F32, PRO, NST>(a, bid, split);
+}
+
+// Tile w of a GemmPar launch -> (class, tile of that class).  The classes' tiles go out in
+// chunks of PAR_G consecutive tiles, round-robin over the classes (sorted by tile count, largest
+// first; chunk round r holds chunk r of every class with more than r chunks), so each XCD's
+// contiguous range of w holds every class in proportion while the workgroups resident on one XCD
+// at a time mostly belong to one class.  Measured (profiles/r5/dgrad_par/): per-tile round-robin,
+// which puts the classes side by side on every CU, and class-major order (two XCDs per class)
+// both ran the strided dgrads ~1.3-2x slower than four launches; chunks of 32-128 tiles ran them
+// 5-7% faster (launch ramps and tails gone).  The grid is padded to whole chunks: t past the
+// class's tiles is a workgroup with nothing to do.
+__device__ __forceinline__ void par_tile(const GemmPar& p, int w, int& cls, int& t) {
+  const int ch = w / PAR_G, off = w - ch * PAR_G;
+  int base = 0, prev = 0;
+  cls = 0;
+  t = 1 << 30;
+  for (int n = p.n; n > 0; --n) {
+    const int tn = (p.c[n - 1].tiles + PAR_G - 1) / PAR_G;
+    const int span = n * (tn - prev);
+    if (ch < base + span) {
+      const int q = ch - base;
+      cls = q % n;
+      t = (prev + q / n) * PAR_G + off;
+      return;
+    }
+    base += span;
+    prev = tn;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int F32>
+__global__ __launch_bounds__(64 * WM * WN, (occ16<BM, BN, WM, WN, 2>()))
+void gemm16_par_kernel(const GemmPar p) {
+  int w, split;
+  xcd_work(w, split);
+  int cls, t;
+  par_tile(p, w, cls, t);
+  cls = __builtin_amdgcn_readfirstlane(cls);
+  t = __builtin_amdgcn_readfirstlane(t);
+  if (t >= p.c[cls].tiles) return;   // the padding of a class's last chunk
+  // the class's own values, each made opaque in an SGPR: loaded from the kernel arguments at a
+  // class-dependent offset, the compiler would otherwise re-load them inside the main loop (its
+  // waits on those scalar loads also drain the LDS reads, lgkmcnt)
+  GemmArgs a = p.a;
+  const ParClass& c = p.c[cls];
+  auto own = [](auto v) {
+    asm volatile("" : "+s"(v));
+    return v;
+  };
+  a.M = own(c.M);
+  a.K = own(c.K);
+  a.ntaps = own(c.ntaps);
+  a.tapS = own(c.tapS);
+  a.tapSinv = own(c.tapSinv);
+  a.oy0 = own(c.oy0);
+  a.ox0 = own(c.ox0);
+  a.wr0 = own(c.wr0);
+  a.ws0 = own(c.ws0);
+  a.oyc = own(c.oyc);
+  a.oxc = own(c.oxc);
+  a.dHW = FastDiv{own(c.dHW.d), own(c.dHW.m), own(c.dHW.s)};
+  a.dW = FastDiv{own(c.dW.d), own(c.dW.m), own(c.dW.s)};
+  a.bn_part = own(c.bn_part);
+  gemm16_body<MODE_DGRAD, BM, BN, WM, WN, 0, 1, F32, 0, 2>(a, t, 0);
+}
+
 template <int MODE, int BM, int BN, int WM, int WN, int F32, int PRO = 0>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
@@ -1091,8 +1167,9 @@ int launch16_switch(const GemmArgs& a, int cfg, bool tapv, dim3 grid, hipStream_
   return 1;
 }
 
+// the launch's arguments against what the engine and tile config `cfg` support
 template <int MODE, int F32>
-int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
+int check16(const GemmArgs& a, int cfg) {
   TMR_CHECK_ARG(((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0,
                 "gemm (LDS-DMA path): operands must be 16-B aligned");
   constexpr bool f32 = F32 != 0;
@@ -1102,7 +1179,6 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                                                 ((uintptr_t)a.C & 15) == 0)
                                              : a.ldb % 4 == 0)),
                 "gemm (fp32 LDS-DMA path): 4-channel pieces, 16-B row strides (view %d)", MODE);
-  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32, a.pro);
   const Cfg16 c = kCfgs16[cfg];
   // the BN-partial rows of a fused dgrad were counted with the prologue-free tile rows
   TMR_CHECK_ARG(MODE != MODE_DGRAD || !a.bn_part || c.bm == kCfgs16[pick_cfg16(a.M, a.N, a.K, MODE, f32)].bm,
@@ -1125,6 +1201,15 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
                      ((uintptr_t)(a.Cold ? a.Cold : a.C) & 15) == 0),
                 "gemm: a separate / bf16 old dx needs the fused LDS-staged dgrad epilogue (tile %dx%d)",
                 c.bm, c.bn);
+  return 0;
+}
+
+template <int MODE, int F32>
+int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
+  constexpr bool f32 = F32 != 0;
+  const int cfg = pick_cfg16(a.M, a.N, a.K, MODE, f32, a.pro);
+  const Cfg16 c = kCfgs16[cfg];
+  if (const int rc = check16<MODE, F32>(a, cfg)) return rc;
   dim3 grid(cdiv(a.M, c.bm) * cdiv(a.N, c.bn), splits, 1);
   if (grid.x == 0) return 0;
   // a k-tile (64 bf16 / 32 fp32) spans several taps when the channels per tap are fewer (or not
@@ -1150,6 +1235,72 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
 template <int MODE, int F32>
 int launch_gemm16(const GemmArgs& a, int splits, hipStream_t st) {
   return launch_gemm16_t<MODE, F32>(a, splits, st);
+}
+
+// The stride-parity classes of one strided dgrad in one launch (gemm16_par_kernel): every class
+// on the tile config its own launch would use, one tap per k-tile (no TAPV form), no operand
+// prologue.  Returns -1 (nothing launched) when the classes do not qualify: the caller launches
+// them one by one.  Each tile computes exactly what its class's own launch computes.
+template <int F32>
+int launch_gemm16_par(const GemmArgs* as, int n, hipStream_t st) {
+  constexpr bool f32 = F32 != 0;
+  static_assert(sizeof(GemmPar) <= 4096, "kernel argument size");
+  if (n < 2 || n > PAR_MAX) return -1;
+  const int cfg = pick_cfg16(as[0].M, as[0].N, as[0].K, MODE_DGRAD, f32, as[0].pro);
+  const int bk = f32 ? 32 : 64;
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& a = as[i];
+    if (a.pro || (a.prec == TMR_MATH_F32) != f32 || !use16(a, MODE_DGRAD)) return -1;
+    if (pick_cfg16(a.M, a.N, a.K, MODE_DGRAD, f32, 0) != cfg) return -1;
+    if (a.ntaps > 1 && ((1 << a.log2C) % bk) != 0) return -1;   // the TAPV form
+  }
+  switch (cfg) {
+    case 1: case 2: case 3: case 5: case 7: break;
+    default: return -1;
+  }
+  GemmPar p{};
+  p.n = n;
+
+  const Cfg16 c = kCfgs16[cfg];
+  // the class's own fields (ParClass); every other argument must be the first class's
+  auto own = [](const GemmArgs& a, int tiles) {
+    return ParClass{a.M, a.K, a.ntaps, a.tapS, a.tapSinv, a.oy0, a.ox0, a.wr0, a.ws0, a.oyc, a.oxc,
+                    tiles, a.dHW, a.dW, a.bn_part};
+  };
+  auto put = [](GemmArgs& a, const ParClass& q) {
+    a.M = q.M; a.K = q.K; a.ntaps = q.ntaps; a.tapS = q.tapS; a.tapSinv = q.tapSinv;
+    a.oy0 = q.oy0; a.ox0 = q.ox0; a.wr0 = q.wr0; a.ws0 = q.ws0; a.oyc = q.oyc; a.oxc = q.oxc;
+    a.dHW = q.dHW; a.dW = q.dW; a.bn_part = q.bn_part;
+  };
+  // classes by tile count, largest first (par_tile's round-robin)
+  int ord[PAR_MAX];
+  for (int i = 0; i < n; ++i) ord[i] = i;
+  auto tiles = [&](const GemmArgs& a) { return (int)(cdiv(a.M, c.bm) * cdiv(a.N, c.bn)); };
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && tiles(as[ord[j]]) > tiles(as[ord[j - 1]]); --j) std::swap(ord[j], ord[j - 1]);
+  p.a = as[ord[0]];
+  long total = 0;
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& a = as[ord[i]];
+    if (const int rc = check16<MODE_DGRAD, F32>(a, cfg)) return rc;
+    p.c[i] = own(a, tiles(a));
+    GemmArgs b = p.a;
+    put(b, p.c[i]);
+    if (std::memcmp(&b, &a, sizeof(GemmArgs)) != 0) return -1;   // differs elsewhere: not a class
+    total += (long)(p.c[i].tiles + PAR_G - 1) / PAR_G * PAR_G;   // whole chunks (par_tile)
+  }
+  if (total == 0) return 0;
+  TMR_CHECK_ARG(total < (1L << 31), "gemm (parity classes): %ld tiles", total);
+  const dim3 grid((unsigned)total, 1, 1);
+  switch (cfg) {
+    case 1: hipLaunchKernelGGL((gemm16_par_kernel<256, 128, 4, 2, F32>), grid, dim3(512), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm16_par_kernel<128, 128, 2, 2, F32>), grid, dim3(256), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((gemm16_par_kernel<256, 64, 4, 1, F32>), grid, dim3(256), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((gemm16_par_kernel<64, 64, 2, 2, F32>), grid, dim3(256), 0, st, p); break;
+    case 7: hipLaunchKernelGGL((gemm16_par_kernel<128, 128, 4, 2, F32>), grid, dim3(512), 0, st, p); break;
+  }
+  TMR_CHECK_LAUNCH("gemm16_par_kernel");
+  return 0;
 }
 
 }  // namespace tmrg

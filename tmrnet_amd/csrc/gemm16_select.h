@@ -160,8 +160,28 @@ inline long gemm_tiles(const GemmArgs& a, int mode) {
                         : cfg_tiles(a.M, a.N, pick_cfg(a.M, a.N, a.K, mode));
 }
 
+// the stride-parity classes of one strided dgrad as one launch (launch_gemm16_par): the
+// arguments every class shares once, the few that differ per class in a table
+constexpr int PAR_MAX = 4;
+struct ParClass {
+  int M, K, ntaps, tapS, tapSinv, oy0, ox0, wr0, ws0, oyc, oxc, tiles;
+  FastDiv dHW, dW;
+  float2* bn_part;
+};
+struct GemmPar {
+  GemmArgs a;               // the first class's arguments
+  ParClass c[PAR_MAX];      // by tile count, largest first
+  int n;
+};
+// tiles of one class in a row (par_tile): a round of one XCD's workgroup slots (32 CUs x 2)
+constexpr int PAR_G = 64;
+
 // one view x precision per translation unit (gemm16_<view>_<prec>.hip, explicit instantiations:
 // they compile in parallel)
+template <int F32>
+int launch_gemm16_par(const GemmArgs* as, int n, hipStream_t st);
+extern template int launch_gemm16_par<0>(const GemmArgs*, int, hipStream_t);
+extern template int launch_gemm16_par<1>(const GemmArgs*, int, hipStream_t);
 template <int MODE, int F32>
 int launch_gemm16(const GemmArgs& a, int splits, hipStream_t st);
 extern template int launch_gemm16<MODE_FWD, 0>(const GemmArgs&, int, hipStream_t);

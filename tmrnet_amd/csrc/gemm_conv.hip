@@ -179,7 +179,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
                          const float* bias, float* y, float beta, GemmArgs& a, bool& al) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
-  TMR_CHECK_ARG((d->io & ~TMR_IO_ENGINE) == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
+  TMR_CHECK_ARG((d->io & ~(TMR_IO_ENGINE | TMR_IO_CLASSES)) == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
   a = GemmArgs{};
@@ -521,13 +521,19 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
   TMR_CHECK_ARG(!(d->io & TMR_IO_WT_BF16) || !(d->io & TMR_IO_W_BF16),
                 "tmr_conv2d_dgrad: TMR_IO_WT_BF16 and TMR_IO_W_BF16 are exclusive weight layouts");
   TMR_CHECK_ARG(!(d->io & TMR_IO_WT_F32) ||
-                    (d->math == TMR_MATH_F32 && (d->io & ~TMR_IO_ENGINE) == TMR_IO_WT_F32),
+                    (d->math == TMR_MATH_F32 && (d->io & ~(TMR_IO_ENGINE | TMR_IO_CLASSES)) == TMR_IO_WT_F32),
                 "tmr_conv2d_dgrad: TMR_IO_WT_F32 (fp32 transposed weights) needs TMR_MATH_F32 and "
                 "no bf16-stored operand");
-  TMR_CHECK_ARG((d->io & ~(TMR_IO_WT_F32 | TMR_IO_ENGINE)) == 0 || d->math == TMR_MATH_BF16,
+  TMR_CHECK_ARG((d->io & ~(TMR_IO_WT_F32 | TMR_IO_ENGINE | TMR_IO_CLASSES)) == 0 ||
+                    d->math == TMR_MATH_BF16,
                 "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int st = d->stride;
-  // one launch per stride-parity class (ph,pw): rows h = st*y + ph
+  // one GEMM per stride-parity class (ph,pw): rows h = st*y + ph.  Stride 2 on the LDS-DMA
+  // engine: the classes go out as one launch (launch_gemm_dgrad_par; TMR_IO_CLASSES: one each)
+  const bool par = st == 2 && !pro && !(d->io & TMR_IO_CLASSES);
+  GemmArgs pend[PAR_MAX];
+  bool pend_al[PAR_MAX];
+  int npend = 0;
   for (int ph = 0; ph < st; ++ph) {
     for (int pw = 0; pw < st; ++pw) {
       // valid kernel rows r with (ph + pad - r) % st == 0
@@ -583,9 +589,23 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
       }
       bool al = aligned16(dy) && aligned16(w_krsc) && aligned16(dx) && a.lds % 4 == 0;
       int rc = set_prologue(a, pro, d, false, true, 0);
+      if (!rc && par) {
+        pend[npend] = a;
+        pend_al[npend++] = al;
+        continue;
+      }
       if (!rc) rc = launch_gemm<MODE_DGRAD>(a, al, 1, stream);
       if (rc) return rc;
     }
+  }
+  if (npend > 0) {
+    int rc = launch_gemm_dgrad_par(pend, npend, stream);
+    if (rc < 0) {   // not eligible: one launch per class
+      rc = 0;
+      for (int i = 0; i < npend && rc == 0; ++i)
+        rc = launch_gemm<MODE_DGRAD>(pend[i], pend_al[i], 1, stream);
+    }
+    if (rc) return rc;
   }
   return 0;
 }

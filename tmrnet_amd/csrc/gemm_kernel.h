@@ -1454,6 +1454,7 @@ int launch_gemm_t(const GemmArgs& a, bool al, int splits, hipStream_t st) {
 // per-view launchers (gemm_fwd.hip / gemm_dgrad.hip / gemm_wgrad.hip)
 int launch_gemm_fwd(const GemmArgs& a, bool al, int splits, hipStream_t st);
 int launch_gemm_dgrad(const GemmArgs& a, bool al, int splits, hipStream_t st);
+int launch_gemm_dgrad_par(const GemmArgs* as, int n, hipStream_t st);
 int launch_gemm_wgrad(const GemmArgs& a, bool al, int splits, hipStream_t st);
 
 }  // namespace tmrg

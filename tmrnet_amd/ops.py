@@ -80,6 +80,7 @@ IO_Y, IO_BN = 16, 32    # bf16 conv output y (forward) / bf16 y, z of the fused 
 IO_WT32 = 64            # dgrad, fp32 math: w is the transposed fp32 copy (fp32 LDS-DMA engine)
 IO_G16 = 128            # fused BN-backward dgrad: g (dx) written bf16 (non-residual bf16 units)
 IO_ENGINE = 256         # the implicit-GEMM engine even where a direct kernel serves the geometry
+IO_CLASSES = 512        # strided dgrad: one launch per stride-parity class (tests' comparison form)
 
 # test instrumentation (process-wide: autograd runs the backward of a CUDA graph on its own
 # device thread, which must see the same routing as the forward)
@@ -101,6 +102,22 @@ def engine_only():
 
 def engine_forced():
     return _ENGINE[0]
+
+
+_CLASSES = [False]
+
+
+@contextlib.contextmanager
+def dgrad_class_launches():
+    """Within the block a strided dgrad runs as one launch per stride-parity class
+    (TMR_IO_CLASSES) instead of one launch over every class's tiles.  Tests only."""
+    prev = _CLASSES[0]
+    _CLASSES[0] = True
+    try:
+        yield
+    finally:
+        _CLASSES[0] = prev
+
 BF16 = torch.bfloat16
 
 
@@ -150,6 +167,8 @@ def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math
         raise RuntimeError("fp32 transposed weights (TMR_IO_WT_F32) need math='fp32'")
     if engine_forced():
         io |= IO_ENGINE
+    if _CLASSES[0] and stride == 2:
+        io |= IO_CLASSES
     return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
                     MAX_FRAMES, io, groups if groups > 1 else 0)
 
