@@ -184,17 +184,27 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    if reducer is not None:
+        reducer.timing = True
+        c0 = dict(reducer.counts)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step events on the compute stream (no host sync inside the timed region): the per-rank
+    # step-time spread of the diagnostics below
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     for i in range(args.warmup, args.warmup + args.steps):
         loss = step(i)
+        marks[i - args.warmup + 1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    diag = rank_diagnostics(dist, world, dev, elapsed, marks, reducer,
+                            c0 if reducer is not None else None, args.steps)
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -310,11 +320,56 @@ def main():
                        "input_transform": ("reference train transform (use_flip=1) on device"
                                            if aug is not None else "crop+normalize")},
             "loss_last": loss_v,
+            "ranks": diag,
             "roofline": roof,
             "hbm": hbm,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+
+
+def rank_diagnostics(dist, world, dev, elapsed, marks, reducer, c0, steps):
+    """What limits a multi-GPU line, from every rank: its wall time over the
+    timed steps, its per-step GPU times (min / mean / max from the stream events), the time its
+    compute stream waited on the gradient exchange per step (GradAllReduce.exposed_ms: the part
+    of the all-reduce the backward overlap did not hide) and the exchange's launches per step
+    (early = the trunk's per-block launches during the backward, 16 expected; buckets = the
+    post-backward buckets of the LSTM / NLBlock / head gradients) -> a dict for the JSON line:
+    stragglers show as a spread of `step_ms_mean`, RCCL as `allreduce_wait_ms`, input feeding as
+    `wall_ms_per_step` above the GPU step time."""
+    st = [a.elapsed_time(b) for a, b in zip(marks[:-1], marks[1:])]
+    row = [elapsed * 1e3 / steps, min(st), sum(st) / len(st), max(st)]
+    if reducer is not None:
+        waits = reducer.exposed_ms()
+        c = {k: reducer.counts[k] - c0[k] for k in reducer.counts}
+        n = max(1, c["reduces"])
+        row += [sum(waits) / max(1, len(waits)), max(waits) if waits else 0.0,
+                c["early_launches"] / n, c["bucket_launches"] / n, c["bytes"] / n]
+        reducer.timing = False
+    else:
+        row += [0.0, 0.0, 0.0, 0.0, 0.0]
+    t = torch.tensor(row, dtype=torch.float64, device=dev)
+    if dist is not None:
+        if dist.get_backend() != "nccl":
+            t = t.cpu()
+        allr = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        rows = [r.tolist() for r in allr]
+    else:
+        rows = [t.tolist()]
+    means = [r[2] for r in rows]
+    return {"wall_ms_per_step": [round(r[0], 3) for r in rows],
+            "step_ms_min": [round(r[1], 3) for r in rows],
+            "step_ms_mean": [round(r[2], 3) for r in rows],
+            "step_ms_max": [round(r[3], 3) for r in rows],
+            "step_ms_spread": round(max(means) - min(means), 3),
+            "allreduce_wait_ms": [round(r[4], 3) for r in rows],
+            "allreduce_wait_ms_max": [round(r[5], 3) for r in rows],
+            "early_launches_per_step": rows[0][6], "bucket_launches_per_step": rows[0][7],
+            "allreduce_mb_per_step": round(rows[0][8] / 2 ** 20, 2),
+            "exchange": ("none (one rank)" if reducer is None else
+                         "RCCL all-reduce SUM, %d trunk blocks launched during the backward"
+                         % rows[0][6])}
 
 
 def workload_name(args):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 6
+#define TMR_ABI_VERSION 7
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
@@ -663,10 +663,14 @@ int tmr_timeconv_wgrad(const float* dy, const float* x, int b, int l, const floa
 /* nn.LSTM(i, h, batch_first=True) forward / BPTT (train_only_non-local_pretrained.py:215,
  * :230-231; gates i,f,g,o).  x (b,t,i) -> y (b,t,h); hn, cn (b,h) may be NULL; saved NULL =
  * inference.  Forward: x W_ih^T + b_ih + b_hh for all b*t frames in one GEMM, then the t-step
- * recurrence (gate GEMM h W_hh^T + sigma/tanh + cell update) in ONE persistent cooperative
- * launch (h = 512; per-step launches otherwise, or when the grid would not be resident).  The
- * backward likewise runs BPTT in one launch, then dW_ih, dW_hh, dx (may be NULL) as GEMMs and
- * db_ih = db_hh = colsum(dgates).  dy = dL/dy for every step (zeros where unused). */
+ * recurrence (gate GEMM h W_hh^T + sigma/tanh + cell update) in ONE persistent launch with grid
+ * barriers (h = 512; per-step launches otherwise, or when the grid could not be resident at
+ * once).  The backward likewise runs BPTT in one launch, then dW_ih, dW_hh, dx (may be NULL) as
+ * GEMMs and db_ih = db_hh = colsum(dgates).  dy = dL/dy for every step (zeros where unused).
+ * Shared device: if a barrier gives up (another stream or process held CUs, so the grid was not
+ * resident in time), the next launch on the stream recomputes the recurrence in barrier-free
+ * workgroups with the same arithmetic (same bits) and marks the word "recovered" (2); in a
+ * normal step that launch exits at once.  TMR_LSTM_RECOVER=0 (env, test hook) skips it. */
 size_t tmr_lstm_saved_bytes(int b, int t, int h);
 size_t tmr_lstm_ws_bytes(int b, int t, int i, int h);
 int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float* w_ih,
@@ -677,14 +681,20 @@ int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, int h, co
                  const float* w_hh, const float* y, const void* saved, size_t saved_bytes,
                  float* dx, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, void* ws,
                  size_t ws_bytes, hipStream_t stream);
-/* timeout word of the last persistent LSTM launch on ws (0 = every grid barrier completed);
+/* timeout word of the last persistent LSTM launch on ws (0 = every grid barrier completed,
+ * 1 = a barrier gave up and the results are invalid, 2 = gave up and recomputed);
  * synchronises the stream */
 int tmr_lstm_sync_status(const void* ws, unsigned* timeout_out, hipStream_t stream);
-/* *status |= 1 when the last persistent LSTM launch on ws gave up a grid barrier (its results are
- * then invalid); enqueued on the stream, no synchronisation -- the caller reads the status word
- * once per train step (tmrnet_amd/health.py) and raises.  TMR_LSTM_SPIN_LIMIT (env) overrides
- * the barrier's spin limit (tests force a give-up with it). */
+/* *status |= 1 when the last persistent LSTM launch on ws gave up a grid barrier and was not
+ * recomputed (its results are then invalid); enqueued on the stream, no synchronisation -- the
+ * caller reads the status word once per train step (tmrnet_amd/health.py) and raises.
+ * TMR_LSTM_SPIN_LIMIT (env) overrides the barrier's spin limit (tests force a give-up with it). */
 int tmr_lstm_status_or(const void* ws, int32_t* status, hipStream_t stream);
+/* Test instrumentation: `wgs` workgroups of 1024 threads that sleep about `ms` milliseconds on
+ * `stream` (every wave leaves after a bounded sleep count), to hold wave slots while another
+ * stream launches work -- the persistent LSTM next to a resident kernel (no reference
+ * counterpart). */
+int tmr_test_hold_cus(int wgs, float ms, hipStream_t stream);
 
 /* TimeConv (NLBlock_MutiConv6_3.py:43-79, generalised in L): the three Conv1d branches run
  * on tmr_conv2d_* (L as H, W=1); these kernels take the elementwise max of

@@ -327,6 +327,9 @@ def bf16_round(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+ROUND_ALL = ("fx", "fw", "dy", "bx", "bw")
+
+
 class _RoundFn(torch.autograd.Function):
     """Storage rounding to bf16 (RNE) with a straight-through gradient."""
 
@@ -354,23 +357,31 @@ class _GradRoundFn(torch.autograd.Function):
 
 
 class _Bf16ConvFn(torch.autograd.Function):
+    """Conv with bf16-rounded operands.  `ops` names the roundings applied (all five by default,
+    the contract; subsets are the attribution study of tests/golden/make_bf16_ensemble.py):
+    fx / fw the forward's x and w, dy the output gradient, bx / bw the x and w the backward
+    views read."""
+
     @staticmethod
-    def forward(ctx, x, w, stride, padding, groups):
-        xb, wb = bf16_round(x), bf16_round(w)
-        ctx.save_for_backward(xb, wb)
-        ctx.cfg = (stride, padding, groups)
-        return F.conv2d(xb, wb, None, stride, padding, 1, groups)
+    def forward(ctx, x, w, stride, padding, groups, ops=ROUND_ALL):
+        xf = bf16_round(x) if "fx" in ops else x
+        wf = bf16_round(w) if "fw" in ops else w
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, padding, groups, ops)
+        return F.conv2d(xf, wf, None, stride, padding, 1, groups)
 
     @staticmethod
     def backward(ctx, gy):
-        xb, wb = ctx.saved_tensors
-        stride, padding, groups = ctx.cfg
-        gyb = bf16_round(gy)
+        x, w = ctx.saved_tensors
+        stride, padding, groups, ops = ctx.cfg
+        xb = bf16_round(x) if "bx" in ops else x
+        wb = bf16_round(w) if "bw" in ops else w
+        gyb = bf16_round(gy) if "dy" in ops else gy
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.nn.grad.conv2d_input(xb.shape, wb, gyb, stride, padding, 1, groups)
         dw = torch.nn.grad.conv2d_weight(xb, wb.shape, gyb, stride, padding, 1, groups)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 class Bf16Conv2d(nn.Conv2d):
@@ -378,13 +389,15 @@ class Bf16Conv2d(nn.Conv2d):
 
     def forward(self, x):
         assert self.bias is None
-        y = _Bf16ConvFn.apply(x, self.weight, self.stride, self.padding, self.groups)
+        y = _Bf16ConvFn.apply(x, self.weight, self.stride, self.padding, self.groups,
+                              getattr(self, "round_ops", ROUND_ALL))
         if getattr(self, "round_out", False) and self.training:   # bf16-stored conv output
             y = _RoundFn.apply(y)
         return y
 
 
-def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=None, res_grads=None):
+def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=None, res_grads=None,
+                       ops=ROUND_ALL):
     """Switch every trunk Conv2d of `module` to bf16-operand math (class swap, so deepcopy
     and .double() keep it); the split-attention fc1/fc2 (GEMMs in fp32 on the device) stay.
     activations=True: in train mode the conv outputs and the Bottleneck outputs are rounded to
@@ -396,7 +409,8 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
     gradient of every Bottleneck (ResNeSt: BottleneckS) output but the last (trunk.R16: the
     residual stream's gradient, written by the next block's conv1 dgrad; the last block's comes
     from the avgpool in fp32).
-    res_grads (default: grads) switches the second part alone."""
+    res_grads (default: grads) switches the second part alone.  ops: the operand roundings of
+    every conv (_Bf16ConvFn; the contract rounds all five)."""
     grads = activations if grads is None else grads
     res_grads = grads if res_grads is None else res_grads
     blocks = [m for m in module.modules() if isinstance(m, (Bottleneck, BottleneckS))]
@@ -404,6 +418,7 @@ def emulate_bf16_convs(module, skip=("fc1", "fc2"), activations=False, grads=Non
         if type(m) is nn.Conv2d and name.split(".")[-1] not in skip:
             m.__class__ = Bf16Conv2d
             m.round_out = activations
+            m.round_ops = tuple(ops)
         elif isinstance(m, (Bottleneck, BottleneckS, SplAtConv2d)):
             m.round_out = activations
             if isinstance(m, (Bottleneck, BottleneckS)):

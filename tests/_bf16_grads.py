@@ -86,8 +86,10 @@ def perturb_rel(x4, eps, seed):
 
 def ensemble_stats(gs_a, gs_b, same=False):
     """Per group: the mean pairwise inner product of two gradient ensembles, <g_i, g_j> over
-    i in a, j in b (i != j when `same`).  For samples g = g* + n with independent zero-mean noise
-    this estimates <g*_a, g*_b> without the noise terms."""
+    i in a, j in b, leaving out i == j: within one ensemble (`same`) a sample with itself, across
+    two a pair run on the same input-noise sample (both ensembles draw noise sample k for their
+    k-th member, so that pair shares its noise term).  For samples g = g* + n with independent
+    zero-mean noise this estimates <g*_a, g*_b> without the noise terms."""
     out = {}
     names = [n for n in gs_a[0] if not (n == "nl_block.linear2.bias" or n.endswith("fc1.bias"))]
     for n in names:
@@ -95,7 +97,7 @@ def ensemble_stats(gs_a, gs_b, same=False):
         tot, cnt = 0.0, 0
         for i, ga in enumerate(gs_a):
             for j, gb_ in enumerate(gs_b):
-                if same and j <= i:
+                if (same and j <= i) or i == j:
                     continue
                 tot += float((ga[n].double() * gb_[n].double()).sum())
                 cnt += 1

@@ -42,6 +42,17 @@ def test_bench_two_ranks_one_gpu():
     # what the communicator saw: two ranks, an all-reduce of ones = 2 (bench.check_ranks)
     assert d["config"]["ranks_seen"] == {"world_size": 2, "backend": "gloo", "allreduce_ones": 2}
     assert d["loss_last"] == d["loss_last"]       # finite
+    # the per-rank diagnostics an 8-GPU line is read by (bench.rank_diagnostics)
+    r = d["ranks"]
+    for k in ("wall_ms_per_step", "step_ms_min", "step_ms_mean", "step_ms_max",
+              "allreduce_wait_ms", "allreduce_wait_ms_max"):
+        assert len(r[k]) == 2 and all(v >= 0 for v in r[k]), (k, r[k])
+    assert all(a <= b <= c for a, b, c in zip(r["step_ms_min"], r["step_ms_mean"],
+                                              r["step_ms_max"]))
+    assert r["early_launches_per_step"] == 16             # one per bottleneck block
+    assert r["bucket_launches_per_step"] >= 1
+    # every parameter's gradient travels once per step (+ the bucket presence flags)
+    assert 115 <= r["allreduce_mb_per_step"] <= 117, r["allreduce_mb_per_step"]
 
 
 def test_overlap_matches_post_backward():

@@ -1039,3 +1039,63 @@ def test_stem_direct_wgrad(dev, monkeypatch, engine):
     # fp32 sums of 75,264 products per weight (random-sign dy): ~1e-6 of the largest weight
     assert rel_err(dw, ref) < 4e-6 and rel_err(dw0, ref) < 4e-6
     assert rel_err(acc, ref + 0.5 * prev.double().cpu()) < 4e-6
+
+
+def test_layout_sessions_model_lifetime(dev):
+    """a layout record belongs to its trunk module.  Build a model and step it, delete
+    it and release its memory (empty_cache), then build a second model -- which may reuse the
+    first one's id() and addresses -- and step it: its logits and gradients must be bit-identical
+    to the same model run without layout sessions, and the first model's records (and the
+    converted weight copies they hold) must be gone.  A parameter replaced in place of its
+    storage (p.data = ...) forces a re-record instead of a refresh from the old address."""
+    import gc
+    import tmrnet_amd
+    B, T, L = 2, 3, 5
+    g = torch.Generator().manual_seed(19)
+    frames = torch.randint(0, 256, (B * T, 250, 250, 3), generator=g, dtype=torch.uint8).to(dev)
+    off = torch.randint(0, 27, (B, 2), generator=g, dtype=torch.int32).to(dev)
+    lt = (torch.rand(B, L, 512, generator=g) * 2 - 1).to(dev)
+    labels = torch.randint(0, 7, (B,), generator=g).to(dev)
+
+    def model(seed):
+        torch.manual_seed(seed)
+        m = tmrnet_amd.resnet_lstm(seq_len=T, precision="bf16").to(dev).train()
+        m.nl_block.forced_mask = torch.ones(B, 512, device=dev)
+        m.forced_head_mask = torch.ones(B, 512, device=dev)
+        return m
+
+    def step(m):
+        m.zero_grad(set_to_none=True)
+        out = m(ops.crop_normalize(frames, off, T), lt)
+        tmrnet_amd.CrossEntropyLoss(size_average=False)(out, labels).backward()
+        torch.cuda.synchronize()
+        return out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()}
+
+    saved = ops.LAYOUT_SESSIONS
+    try:
+        ops.LAYOUT_SESSIONS = False
+        ref = step(model(2))
+        ops.LAYOUT_SESSIONS = True
+        ops.clear_layout_sessions()
+        m1 = model(1)
+        step(m1); step(m1)
+        assert ops.layout_session_count() == 1
+        del m1
+        gc.collect()
+        torch.cuda.empty_cache()
+        assert ops.layout_session_count() == 0        # freed with its model
+        m2 = model(2)
+        for _ in range(2):                            # record, then refresh
+            out, grads = step(m2)
+            assert torch.equal(out, ref[0])
+            for n in grads:
+                assert torch.equal(grads[n], ref[1][n]), n
+        # new storage for one conv weight: the refresh must not read the old address
+        w = m2.share.layer1[0].conv2.weight
+        w.data = w.data.clone()
+        torch.cuda.empty_cache()
+        out, grads = step(m2)
+        assert torch.equal(out, ref[0])
+    finally:
+        ops.LAYOUT_SESSIONS = saved
+        ops.clear_layout_sessions()

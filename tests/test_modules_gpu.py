@@ -5,17 +5,22 @@ tmr_linear_*) against float64 torch, and their two execution paths.
   workgroups behind a grid barrier) and the per-step path it falls back to (TMR_LSTM_PERSIST=0,
   other hidden sizes, or a grid the cooperative launch refuses: B > 64 at one workgroup per CU)
   -- both against nn.LSTM in float64 (train_only_non-local_pretrained.py:215, :230-231), and the
-  barrier's timeout word must read 0.
+  barrier's timeout word must read 0; a barrier give-up (forced, or caused by a kernel resident
+  on another stream) is recomputed by the solo kernels, bit-identical.
 * tmr_nl_attn split over 32-row chunks at the C5 shape (B=64, L=300, bank rows) against float64.
 * tmr_linear_fwd/bwd against float64 nn.Linear.
 """
+import json
 import os
 
 import pytest
 import torch
 
 from tmrnet_amd import ops
+from tmrnet_amd._lib import call, stream_ptr
 from tmrnet_amd.lstm import LSTM
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -85,11 +90,83 @@ def test_lstm_persistent_barrier_status(dev):
         assert rel(a, b) < 1e-4
 
 
+def _lstm_operands(dev, B=64, T=10, seed=3):
+    torch.manual_seed(seed)
+    I, H = 2048, 512
+    x = torch.randn(B, T, I, device=dev)
+    w_ih = torch.randn(4 * H, I, device=dev) * (2.0 / (I + 4 * H)) ** 0.5
+    w_hh = torch.randn(4 * H, H, device=dev) * (2.0 / (H + 4 * H)) ** 0.5
+    b_ih = torch.rand(4 * H, device=dev) * 0.08 - 0.04
+    b_hh = torch.rand(4 * H, device=dev) * 0.08 - 0.04
+    return x, w_ih, w_hh, b_ih, b_hh
+
+
+def _lstm_fwd_bwd(ops_args, dy):
+    x, w_ih, w_hh, b_ih, b_hh = ops_args
+    y, hn, cn, saved, ws = ops.lstm_fwd(x, w_ih, w_hh, b_ih, b_hh)
+    st_f = ops.lstm_sync_status(ws)
+    g = ops.lstm_bwd(dy, x, w_ih, w_hh, y, saved)
+    st_b = ops.lstm_sync_status(g[-1])
+    return [y, hn, cn, saved] + list(g[:5]), st_f, st_b
+
+
+@pytest.mark.parametrize("B,T", [(64, 10), (64, 30), (5, 7)])
+def test_lstm_giveup_recovers(dev, monkeypatch, B, T):
+    """A persistent launch that gives up a grid barrier (forced: TMR_LSTM_SPIN_LIMIT=1, so the
+    first wait on another workgroup fails) is recomputed on the same stream by the barrier-free
+    solo kernels (lstm.hip lstm_rec_{fwd,bwd}_solo_k): every output -- y, h_n, c_n, the saved cell
+    states / gate activations, dx, dW, db -- is bit-identical to the run whose barriers all
+    completed, the timeout word reads 2 ("recovered") and the health word stays clear."""
+    from tmrnet_amd import health
+    health.reset()
+    monkeypatch.setenv("TMR_LSTM_PERSIST", "1")
+    args = _lstm_operands(dev, B, T, seed=B + T)
+    dy = torch.randn(B, T, 512, device=dev)
+    ref, s0f, s0b = _lstm_fwd_bwd(args, dy)
+    assert (s0f, s0b) == (0, 0)
+    monkeypatch.setenv("TMR_LSTM_SPIN_LIMIT", "1")
+    out, s1f, s1b = _lstm_fwd_bwd(args, dy)
+    monkeypatch.delenv("TMR_LSTM_SPIN_LIMIT")
+    assert (s1f, s1b) == (2, 2), (s1f, s1b)
+    for i, (a, b) in enumerate(zip(out, ref)):
+        assert torch.equal(a, b), i
+    health.check(sync=True)          # recovered: nothing to report
+
+
+def test_lstm_next_to_resident_kernel(dev, monkeypatch):
+    """the persistent LSTM while another stream holds most of the device's wave
+    slots (tmr_test_hold_cus: ~1.5 s of resident workgroups on a side stream, launched first).
+    Whether the grid barrier gives up depends on how the dispatcher places the workgroups; either
+    way the step must return the same bits as on an idle device and raise nothing -- the recovery
+    above is what makes that hold on a shared device.  The status seen is recorded."""
+    from tmrnet_amd import health
+    health.reset()
+    monkeypatch.setenv("TMR_LSTM_PERSIST", "1")
+    args = _lstm_operands(dev, 64, 10, seed=77)
+    dy = torch.randn(64, 10, 512, device=dev)
+    ref, _, _ = _lstm_fwd_bwd(args, dy)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    side = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        # two 1024-thread workgroups fill a CU's 32 wave slots; leave 16 CUs free
+        call("tmr_test_hold_cus", 2 * (cus - 16), 1500.0, stream_ptr())
+    out, sf, sb = _lstm_fwd_bwd(args, dy)
+    torch.cuda.synchronize()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "lstm_resident_kernel.json"), "w") as f:
+        json.dump({"status_fwd": sf, "status_bwd": sb, "cus": cus}, f)
+    assert sf in (0, 2) and sb in (0, 2), (sf, sb)
+    for i, (a, b) in enumerate(zip(out, ref)):
+        assert torch.equal(a, b), i
+    health.check(sync=True)
+
+
 def test_lstm_giveup_is_loud(dev, monkeypatch):
-    """A persistent LSTM launch that gives up a grid barrier (forced: TMR_LSTM_SPIN_LIMIT=1, so
-    the first wait on another workgroup fails) is reported: the train step's optimizer raises
-    RuntimeError at its next step (tmrnet_amd/health.py), and health.check(sync=True) at once --
-    instead of training on a garbage recurrence."""
+    """An unrecovered give-up (TMR_LSTM_RECOVER=0 skips the solo re-computation; forced:
+    TMR_LSTM_SPIN_LIMIT=1) is reported: the train step's optimizer raises RuntimeError at its next
+    step (tmrnet_amd/health.py), and health.check(sync=True) at once -- instead of training on a
+    garbage recurrence."""
     import tmrnet_amd
     from tmrnet_amd import health
     health.reset()
@@ -104,6 +181,7 @@ def _giveup_steps(dev, monkeypatch):
     from tmrnet_amd import health
     monkeypatch.setenv("TMR_LSTM_PERSIST", "1")
     monkeypatch.setenv("TMR_LSTM_SPIN_LIMIT", "1")
+    monkeypatch.setenv("TMR_LSTM_RECOVER", "0")
     torch.manual_seed(5)
     m = tmrnet_amd.LSTM(2048, 512).to(dev)
     opt = tmrnet_amd.SGD(m.parameters(), lr=1e-3, momentum=0.9)

@@ -168,6 +168,7 @@ SIGNATURES = {
     "tmr_lstm_bwd": [P, P, I, I, I, I, P, P, P, P, SZ, P, P, P, P, P, P, SZ, P],
     "tmr_lstm_sync_status": [P, ctypes.POINTER(ctypes.c_uint), P],
     "tmr_lstm_status_or": [P, P, P],
+    "tmr_test_hold_cus": [I, F, P],
     "tmr_timeconv_max5_fwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_timeconv_max5_bwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],

@@ -952,8 +952,8 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply8q(const PoolGeo pg, int h, 
         const int o = (((int)nn * pg.ho + k + ddy) * pg.wo + l + ddx) * c8 + cq;
         if (pin[ddy][ddx]) {
           a[ddy][ddx] = am[o];
-          d0[ddy][ddx] = dp[2 * o];
-          d1[ddy][ddx] = dp[2 * o + 1];
+          d0[ddy][ddx] = dp[2 * (long)o];       // 64-bit: o < 2^31 is checked, 2 o is not
+          d1[ddy][ddx] = dp[2 * (long)o + 1];
         } else {
           a[ddy][ddx] = make_uint2(0xffffffffu, 0xffffffffu);
           d0[ddy][ddx] = d1[ddy][ddx] = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -37,6 +37,28 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Cell arithmetic of one (clip, unit), shared by the persistent kernels and their solo
+// re-computation (below), so both produce the same bits.
+__device__ __forceinline__ float cell_fwd(const float gi, const float gf, const float gc,
+                                          const float go, float& c, float& ig, float& fg,
+                                          float& gg, float& og) {
+  ig = sigm(gi); fg = sigm(gf);
+  gg = tanhf(gc); og = sigm(go);
+  c = fg * c + ig * gg;
+  return og * tanhf(c);
+}
+__device__ __forceinline__ void cell_bwd(const float dh, const float ig, const float fg,
+                                         const float gg, const float og, const float cv,
+                                         const float cp, float& dc, float d[4]) {
+  const float tc = tanhf(cv);
+  const float dct = dh * og * (1.f - tc * tc) + dc;
+  d[0] = dct * gg * ig * (1.f - ig);
+  d[1] = dct * cp * fg * (1.f - fg);
+  d[2] = dct * ig * (1.f - gg * gg);
+  d[3] = dh * tc * og * (1.f - og);
+  dc = dct * fg;
+}
+
 // Hand-off between steps (MI355X_MICROARCH.md, visibility: the counter row of the sc1 table).
 // The handed-off bytes (h_t forward, dgates_t backward) are stored write-through (sc1) and every
 // load of them in the kernel is an sc1 load, so no release / acquire fence is needed: each
@@ -175,10 +197,9 @@ __global__ __launch_bounds__(256) void lstm_rec_fwd_k(const float* __restrict__ 
     }
     __syncthreads();
     if (cell) {
-      const float ig = sigm(gs[cb][cu]), fg = sigm(gs[cb][HU + cu]);
-      const float gg = tanhf(gs[cb][2 * HU + cu]), og = sigm(gs[cb][3 * HU + cu]);
-      creg = fg * creg + ig * gg;
-      const float h = og * tanhf(creg);
+      float ig, fg, gg, og;
+      const float h = cell_fwd(gs[cb][cu], gs[cb][HU + cu], gs[cb][2 * HU + cu],
+                               gs[cb][3 * HU + cu], creg, ig, fg, gg, og);
       st_sc1(&y[((long)cgb * T + t) * LH + cj], h);   // handed to every workgroup
       if (cs) cs[((long)t * B + cgb) * LH + cj] = creg;
       if (acts) {
@@ -279,18 +300,178 @@ __global__ __launch_bounds__(256) void lstm_rec_bwd_k(const float* __restrict__ 
         for (int q = 0; q < NG; ++q) rec += red[tid][q];
       }
       const float dh = dyv + rec;
-      const float tc = tanhf(cv);
-      const float dct = dh * og * (1.f - tc * tc) + dc;
+      float dv[4];
+      cell_bwd(dh, ig, fg, gg, og, cv, cp, dc, dv);
       float* d = dg + ((long)cgb * T + t) * G4;
-      st_sc1(&d[cj], dct * gg * ig * (1.f - ig));            // handed to every workgroup
-      st_sc1(&d[LH + cj], dct * cp * fg * (1.f - fg));
-      st_sc1(&d[2 * LH + cj], dct * ig * (1.f - gg * gg));
-      st_sc1(&d[3 * LH + cj], dh * tc * og * (1.f - og));
-      dc = dct * fg;
+      st_sc1(&d[cj], dv[0]);                                 // handed to every workgroup
+      st_sc1(&d[LH + cj], dv[1]);
+      st_sc1(&d[2 * LH + cj], dv[2]);
+      st_sc1(&d[3 * LH + cj], dv[3]);
       hprev[((long)cgb * T + t) * LH + cj] = hp;
     }
     if (t > 0 && !grid_barrier(sync, (unsigned)((T - t) * nwg), limit)) return;
   }
+}
+
+// ---------------------------------------------------------------- solo re-computation
+// After a persistent launch that gave up a grid barrier (another stream or process held CUs, so
+// not every workgroup became resident in time), the same stream runs the recurrence again in
+// workgroups that need no barrier: each owns SPC clips and ALL hidden units (clips are
+// independent; W_hh is streamed from L2 every step instead of held in registers).  The arithmetic
+// is the persistent kernels' -- per 64-wide k-slice fmaf chains, slices added in order, the
+// shared cell helpers -- so the outputs are the same bits.  A launch whose timeout word is 0 (the
+// persistent kernel completed: every normal step) exits at once.  The word is set to 2
+// ("recovered") so tmr_lstm_status_or does not report the step as failed.
+constexpr int SPC = 4;   // clips per workgroup of the solo kernels
+
+__global__ __launch_bounds__(256) void lstm_rec_fwd_solo_k(const float* __restrict__ gx,
+                                                           const float* __restrict__ whh,
+                                                           float* __restrict__ y,
+                                                           float* __restrict__ cs,
+                                                           float* __restrict__ acts,
+                                                           float* __restrict__ hn,
+                                                           float* __restrict__ cn, int B, int T,
+                                                           unsigned* sync) {
+  if (sync[1] == 0u) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sync[1] = 2u;
+  constexpr int G4 = 4 * LH, KG = 64;
+  __shared__ __attribute__((aligned(16))) float hs[SPC][LH];
+  __shared__ float gs[SPC][G4];
+  const int tid = threadIdx.x, b0 = blockIdx.x * SPC;
+  float creg[2][SPC];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int bl = 0; bl < SPC; ++bl) creg[e][bl] = 0.f;
+  for (int t = 0; t < T; ++t) {
+    for (int r = 0; r < G4 / 256; ++r) {      // gate column (row of W_hh) col, all SPC clips
+      const int col = tid + 256 * r;
+      float a[SPC];
+#pragma unroll
+      for (int bl = 0; bl < SPC; ++bl) a[bl] = 0.f;
+      if (t > 0) {
+        const float* wr = whh + (long)col * LH;
+        for (int kg = 0; kg < LH / KG; ++kg) {
+          float pa[SPC];
+#pragma unroll
+          for (int bl = 0; bl < SPC; ++bl) pa[bl] = 0.f;
+#pragma unroll 4
+          for (int i = 0; i < KG; i += 4) {
+            const float4 w4 = *reinterpret_cast<const float4*>(wr + kg * KG + i);
+#pragma unroll
+            for (int bl = 0; bl < SPC; ++bl) {
+              const float4 h4 = *reinterpret_cast<const float4*>(&hs[bl][kg * KG + i]);
+              pa[bl] = fmaf(h4.x, w4.x, pa[bl]); pa[bl] = fmaf(h4.y, w4.y, pa[bl]);
+              pa[bl] = fmaf(h4.z, w4.z, pa[bl]); pa[bl] = fmaf(h4.w, w4.w, pa[bl]);
+            }
+          }
+#pragma unroll
+          for (int bl = 0; bl < SPC; ++bl) a[bl] += pa[bl];
+        }
+      }
+#pragma unroll
+      for (int bl = 0; bl < SPC; ++bl)
+        if (b0 + bl < B) gs[bl][col] = gx[((long)(b0 + bl) * T + t) * G4 + col] + a[bl];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = tid + 256 * e;
+#pragma unroll
+      for (int bl = 0; bl < SPC; ++bl) {
+        const int cgb = b0 + bl;
+        if (cgb >= B) continue;
+        float ig, fg, gg, og;
+        const float h = cell_fwd(gs[bl][j], gs[bl][LH + j], gs[bl][2 * LH + j],
+                                 gs[bl][3 * LH + j], creg[e][bl], ig, fg, gg, og);
+        y[((long)cgb * T + t) * LH + j] = h;
+        hs[bl][j] = h;
+        if (cs) cs[((long)t * B + cgb) * LH + j] = creg[e][bl];
+        if (acts) {
+          float* ap = acts + ((long)t * B + cgb) * G4;
+          ap[j] = ig; ap[LH + j] = fg; ap[2 * LH + j] = gg; ap[3 * LH + j] = og;
+        }
+        if (t + 1 == T) {
+          if (hn) hn[(long)cgb * LH + j] = h;
+          if (cn) cn[(long)cgb * LH + j] = creg[e][bl];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void lstm_rec_bwd_solo_k(const float* __restrict__ dy,
+                                                           const float* __restrict__ whh,
+                                                           const float* __restrict__ y,
+                                                           const float* __restrict__ cs,
+                                                           const float* __restrict__ acts,
+                                                           float* __restrict__ dg,
+                                                           float* __restrict__ hprev, int B,
+                                                           int T, unsigned* sync) {
+  if (sync[1] == 0u) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sync[1] = 2u;
+  constexpr int G4 = 4 * LH, KG = 64;
+  __shared__ float ds[2][SPC][G4];   // dg of step t + 1 (read) and t (written), per clip
+  const int tid = threadIdx.x, b0 = blockIdx.x * SPC;
+  float dc[2][SPC];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int bl = 0; bl < SPC; ++bl) dc[e][bl] = 0.f;
+  for (int t = T - 1; t >= 0; --t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = tid + 256 * e;
+      float rec[SPC];
+#pragma unroll
+      for (int bl = 0; bl < SPC; ++bl) rec[bl] = 0.f;
+      if (t + 1 < T) {
+        for (int q = 0; q < G4 / KG; ++q) {
+          float pa[SPC];
+#pragma unroll
+          for (int bl = 0; bl < SPC; ++bl) pa[bl] = 0.f;
+#pragma unroll 8
+          for (int i = 0; i < KG; ++i) {
+            const float w = whh[(long)(q * KG + i) * LH + j];
+#pragma unroll
+            for (int bl = 0; bl < SPC; ++bl) pa[bl] = fmaf(ds[nxt][bl][q * KG + i], w, pa[bl]);
+          }
+#pragma unroll
+          for (int bl = 0; bl < SPC; ++bl) rec[bl] += pa[bl];
+        }
+      }
+#pragma unroll
+      for (int bl = 0; bl < SPC; ++bl) {
+        const int cgb = b0 + bl;
+        if (cgb >= B) continue;
+        const float dyv = dy[((long)cgb * T + t) * LH + j];
+        const float* ap = acts + ((long)t * B + cgb) * G4;
+        const float cv = cs[((long)t * B + cgb) * LH + j];
+        const float cp = t > 0 ? cs[((long)(t - 1) * B + cgb) * LH + j] : 0.f;
+        const float hp = t > 0 ? y[((long)cgb * T + (t - 1)) * LH + j] : 0.f;
+        float dv[4];
+        cell_bwd(dyv + rec[bl], ap[j], ap[LH + j], ap[2 * LH + j], ap[3 * LH + j], cv, cp,
+                 dc[e][bl], dv);
+        float* d = dg + ((long)cgb * T + t) * G4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          d[q * LH + j] = dv[q];
+          ds[cur][bl][q * LH + j] = dv[q];
+        }
+        hprev[((long)cgb * T + t) * LH + j] = hp;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Test instrumentation (tmr_test_hold_cus): workgroups that occupy wave slots for a bounded
+// number of s_sleep periods, so a test can make part of the device unavailable to another
+// stream's launch.  Every wave leaves after `periods` sleeps.
+__global__ __launch_bounds__(1024) void hold_cus_k(unsigned periods) {
+  for (unsigned i = 0; i < periods; ++i) __builtin_amdgcn_s_sleep(127);
 }
 
 // ---------------------------------------------------------------- per-step fallback pieces
@@ -312,7 +493,7 @@ __global__ void copy_hprev_k(const float* __restrict__ y, float* __restrict__ hp
 
 // status |= timeout word of the last persistent launch on a workspace (stream-ordered, no sync)
 __global__ void status_or_k(const unsigned* __restrict__ sync, int* __restrict__ status) {
-  if (threadIdx.x == 0 && sync[1] != 0u) status[0] |= 1;
+  if (threadIdx.x == 0 && sync[1] == 1u) status[0] |= 1;   // 2 = recovered by the solo kernel
 }
 
 __global__ void copy_k(const float* __restrict__ a, float* __restrict__ o, int n) {
@@ -336,6 +517,11 @@ bool resident(const void* kernel, dim3 grid, int threads) {
 // TMR_LSTM_PERSIST=0 forces the per-step path (tests exercise both; read per call, no state)
 bool persist_allowed() {
   const char* v = getenv("TMR_LSTM_PERSIST");
+  return !(v && v[0] == '0');
+}
+// TMR_LSTM_RECOVER=0 leaves a give-up unrecovered (test hook: the health word's loud path)
+bool recover_allowed() {
+  const char* v = getenv("TMR_LSTM_RECOVER");
   return !(v && v[0] == '0');
 }
 
@@ -422,7 +608,14 @@ TMR_API int tmr_lstm_fwd(const float* x, int b, int t, int i, int h, const float
     if (resident((const void*)lstm_rec_fwd_k, grid, 256)) {
       hipLaunchKernelGGL(lstm_rec_fwd_k, grid, dim3(256), 0, stream, gxc, w_hh, y, cs, acts, hn, cn,
                          b, t, sync, lim);
-      if (hipGetLastError() == hipSuccess) return 0;
+      if (hipGetLastError() == hipSuccess) {
+        if (recover_allowed()) {   // exits at once unless the launch above gave up
+          hipLaunchKernelGGL(lstm_rec_fwd_solo_k, dim3(cdiv(b, SPC)), dim3(256), 0, stream, gxc,
+                             w_hh, y, cs, acts, hn, cn, b, t, sync);
+          TMR_CHECK_LAUNCH("lstm_rec_fwd_solo_k");
+        }
+        return 0;
+      }
     }
     // not resident: per-step path below
   }
@@ -492,6 +685,11 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
       hipLaunchKernelGGL(lstm_rec_bwd_k, grid, dim3(256), 0, stream, dy, w_hh, y, cs, acts, dg,
                          hprev, b, t, sync, lim);
       done = hipGetLastError() == hipSuccess;
+      if (done && recover_allowed()) {   // exits at once unless the launch above gave up
+        hipLaunchKernelGGL(lstm_rec_bwd_solo_k, dim3(cdiv(b, SPC)), dim3(256), 0, stream, dy, w_hh,
+                           y, cs, acts, dg, hprev, b, t, sync);
+        TMR_CHECK_LAUNCH("lstm_rec_bwd_solo_k");
+      }
     }
   }
   if (!done) {
@@ -532,7 +730,9 @@ TMR_API int tmr_lstm_bwd(const float* dy, const float* x, int b, int t, int i, i
 }
 
 // Timeout word of the last persistent launch on this workspace (0 = every grid barrier
-// completed).  Read it after the stream has drained; for tests and diagnostics.
+// completed, 1 = a barrier gave up and the results are invalid, 2 = a barrier gave up and the
+// solo kernel recomputed the recurrence).  Read it after the stream has drained; for tests and
+// diagnostics.
 TMR_API int tmr_lstm_sync_status(const void* ws, unsigned* timeout_out, hipStream_t stream) {
   TMR_CHECK_ARG(ws && timeout_out, "tmr_lstm_sync_status: null pointer");
   unsigned v[2] = {0, 0};
@@ -553,5 +753,18 @@ TMR_API int tmr_lstm_status_or(const void* ws, int32_t* status, hipStream_t stre
   TMR_CHECK_ARG(ws && status, "tmr_lstm_status_or: null pointer");
   hipLaunchKernelGGL(status_or_k, dim3(1), dim3(64), 0, stream, (const unsigned*)ws, (int*)status);
   TMR_CHECK_LAUNCH("lstm status_or");
+  return 0;
+}
+
+// Test instrumentation: `wgs` workgroups of 1024 threads that sleep `ms` milliseconds on `stream`
+// (bounded: every wave leaves after its sleep count), to hold wave slots while another stream
+// launches work (tests/test_modules_gpu.py: the persistent LSTM next to a resident kernel).
+TMR_API int tmr_test_hold_cus(int wgs, float ms, hipStream_t stream) {
+  TMR_CHECK_ARG(wgs > 0 && wgs <= 65536 && ms >= 0.f && ms <= 10000.f,
+                "tmr_test_hold_cus: wgs=%d ms=%g out of range", wgs, (double)ms);
+  // s_sleep 127 = 127 x 64 clocks; at the 2.4 GHz shader clock about 3.4 us
+  const unsigned periods = (unsigned)(ms * 1000.f / 3.4f) + 1u;
+  hipLaunchKernelGGL(hold_cus_k, dim3(wgs), dim3(1024), 0, stream, periods);
+  TMR_CHECK_LAUNCH("hold_cus_k");
   return 0;
 }

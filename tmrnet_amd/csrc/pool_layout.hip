@@ -87,7 +87,9 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_k(const TX* __restrict__ x, TY
 // fp32 values
 struct Raw8 { uint4 a, b; };
 __device__ __forceinline__ Raw8 ld_raw8(const float* p, int i) {
-  return {reinterpret_cast<const uint4*>(p)[2 * i], reinterpret_cast<const uint4*>(p)[2 * i + 1]};
+  // 64-bit element offset: the host guard bounds i (< 2^31), not 2 i
+  const long j = 2 * (long)i;
+  return {reinterpret_cast<const uint4*>(p)[j], reinterpret_cast<const uint4*>(p)[j + 1]};
 }
 __device__ __forceinline__ Raw8 ld_raw8(const __bf16* p, int i) {
   return {reinterpret_cast<const uint4*>(p)[i], make_uint4(0u, 0u, 0u, 0u)};
@@ -159,8 +161,9 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_bn8(const TX* __restrict__ x, 
       }
     }
     if constexpr (std::is_same<TY, float>::value) {
-      reinterpret_cast<float4*>(y)[2 * i] = make_float4(best[0], best[1], best[2], best[3]);
-      reinterpret_cast<float4*>(y)[2 * i + 1] = make_float4(best[4], best[5], best[6], best[7]);
+      const long j = 2 * (long)i;
+      reinterpret_cast<float4*>(y)[j] = make_float4(best[0], best[1], best[2], best[3]);
+      reinterpret_cast<float4*>(y)[j + 1] = make_float4(best[4], best[5], best[6], best[7]);
     } else {
       typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
       uint32_t ow[4];

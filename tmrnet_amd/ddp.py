@@ -18,6 +18,11 @@ Semantics kept from torch.optim + DataParallel:
   backward touched it since; otherwise the accumulated ``p.grad`` goes through the buckets;
 * ``p.grad is None`` stays None when it is None on every rank (torch.optim.SGD then skips the
   parameter); a presence flag per parameter rides in the same bucket, so no extra collective.
+
+Diagnostics (``counts``, ``timing``): launches and bytes per exchange, and with ``timing=True``
+the time the compute stream spends from the end of the backward to the reduced gradients being
+installed (``exposed_ms()``: the exchange's cost the overlap did not hide; events on the compute
+stream, no host synchronisation inside the step).
 """
 import warnings
 
@@ -56,6 +61,9 @@ class GradAllReduce:
         self.stale_ids = set()  # early-launched params touched again by a later backward
         self.overlap = bool(overlap) and self._multi()
         self._warned_accum = False
+        self.counts = {"reduces": 0, "early_launches": 0, "bucket_launches": 0, "bytes": 0}
+        self.timing = False
+        self._events = []       # (start, end) CUDA events around each exchange's waits
         share = getattr(model, "share", None)
         if self.overlap and share is not None:
             from .trunk import set_grad_ready
@@ -92,6 +100,8 @@ class GradAllReduce:
         flat = _flatten([g for _, g in pairs])
         self.early.append((params, flat, self.dist.all_reduce(flat, async_op=True)))
         self.early_ids.update(ids)
+        self.counts["early_launches"] += 1
+        self.counts["bytes"] += flat.numel() * flat.element_size()
 
     def reset(self):
         """Drop (after waiting for) early launches of a backward that is not being reduced."""
@@ -120,6 +130,13 @@ class GradAllReduce:
             flat = _flatten(grads + [present])
             handles.append((bucket, grads + [present], flat, all(local),
                             self.dist.all_reduce(flat, async_op=True)))
+            self.counts["bucket_launches"] += 1
+            self.counts["bytes"] += flat.numel() * flat.element_size()
+        self.counts["reduces"] += 1
+        ev = None
+        if self.timing and torch.cuda.is_available() and self.params and self.params[0].is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for params, flat, h in early:
             h.wait()
             for p, g in zip(params, _unflatten(flat, params)):
@@ -137,3 +154,17 @@ class GradAllReduce:
                     p.grad = g
                 else:
                     p.grad.copy_(g)
+        if ev is not None:
+            ev[1].record()
+            self._events.append(ev)
+
+    def exposed_ms(self, clear=True):
+        """Per exchange since the last call (timing=True): milliseconds of the compute stream from
+        the end of the backward to the reduced gradients being installed.  Synchronises."""
+        if not self._events:
+            return []
+        self._events[-1][1].synchronize()
+        out = [a.elapsed_time(b) for a, b in self._events]
+        if clear:
+            self._events = []
+        return out

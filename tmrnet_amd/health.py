@@ -1,6 +1,10 @@
 """Device-side health word of the train step: failures that kernels can only report on the device
-(today: a persistent LSTM launch that gave up a grid barrier, include/tmr.h tmr_lstm_status_or)
-are OR-ed into one int32 per device, stream-ordered and without a host sync.
+(today: a persistent LSTM launch that gave up a grid barrier and was not recomputed, include/tmr.h
+tmr_lstm_status_or) are OR-ed into one int32 per device, stream-ordered and without a host sync.
+A give-up on a shared device (another stream or process holding CUs) is normally recovered on
+the device by the LSTM's barrier-free solo kernels (csrc/lstm.hip, bit-identical results; the
+launch's timeout word then reads 2 and nothing is reported); only with that re-computation
+switched off (TMR_LSTM_RECOVER=0, a test hook) does a give-up reach this word.
 
 The fused optimizer kernels (optim.SGD / Adam, tmr_sgd_step_multi / tmr_adam_step_multi) read
 the word on the device and skip the update when it is non-zero, so a failed step never changes
@@ -46,8 +50,8 @@ def _raise(v, st):
     st[2] = None
     if v & LSTM_TIMEOUT:
         raise RuntimeError("persistent LSTM kernel gave up a grid barrier (its recurrence results "
-                           "are invalid): the GPU was shared or oversubscribed -- rerun with "
-                           "TMR_LSTM_PERSIST=0 (per-step path) or free the device")
+                           "are invalid) and was not recomputed (TMR_LSTM_RECOVER=0): rerun "
+                           "without it, or with TMR_LSTM_PERSIST=0 (per-step path)")
     raise RuntimeError("device status word %#x" % v)
 
 

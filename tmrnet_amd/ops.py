@@ -7,6 +7,7 @@ anything itself: all arithmetic runs in the HIP kernels of libtmr.so.
 """
 import contextlib
 import threading
+import weakref
 
 import numpy as np
 import torch
@@ -589,16 +590,33 @@ def col_sum(x, rows, cols, ld, out=None, beta=0.0):
 # weight_to_* calls return the refreshed tensors -- the same values (copies and RNE roundings).
 # A request the record lacks (other weights, shapes, flags) is converted directly and the record
 # is rebuilt on the next forward.
+# Lifetime: records hang off their owner module (the trunk) in a weak table, so a
+# model's converted copies are freed with it, and a new model can never reuse a dead one's record
+# (its id() may be reused, its table would hold freed weight addresses).  Before every refresh the
+# record checks that each parameter it was recorded from is alive at the same address; if not it
+# re-records instead of reading stale pointers.  clear_layout_sessions() drops every record.
 class _LayoutRecord:
-    def __init__(self):
+    def __init__(self, owner):
         self.lookup = {}     # request key -> returned tensor
         self.rows = []       # table rows (w ptr, out tensor, k, c, rs, cpad, kind, bf16)
         self.table = None    # device table (uint8 bytes of _WL_DTYPE rows)
         self.blocks = 0
         self.valid = True
+        # the owner's parameters at recording time: (weakref, data_ptr)
+        self.sources = [(weakref.ref(p), p.data_ptr()) for p in owner.parameters()]
+
+    def live(self):
+        """Every source parameter alive at its recorded address (the table's pointers hold)."""
+        for ref, ptr in self.sources:
+            p = ref()
+            if p is None or p.data_ptr() != ptr:
+                return False
+        return True
 
 
-_LAYOUTS = {}   # (session key, thread) -> _LayoutRecord: each thread refreshes its own copies
+# owner module -> {(session key, thread): _LayoutRecord}: each thread refreshes its own copies;
+# an exited thread's records go with `clear_layout_sessions` or the owner
+_LAYOUTS = weakref.WeakKeyDictionary()
 _TLS = threading.local()   # .session = [active record, recording?]
 
 
@@ -618,17 +636,35 @@ def _session():
 LAYOUT_SESSIONS = True   # (the equality test turns it off for its reference run)
 
 
+def clear_layout_sessions(owner=None):
+    """Drop the recorded weight layouts (of `owner`, or of every module) and the converted
+    copies they hold; the next forward records again."""
+    if owner is None:
+        _LAYOUTS.clear()
+    else:
+        _LAYOUTS.pop(owner, None)
+
+
+def layout_session_count():
+    """Records held (tests)."""
+    return sum(len(v) for v in _LAYOUTS.values())
+
+
 @contextlib.contextmanager
-def layout_session(key):
-    """See above.  key: one per trunk, mode and precision (the set of conversions it asks for)."""
+def layout_session(owner, key):
+    """See above.  owner: the module whose parameters are converted (the trunk); key: one per
+    mode and precision (the set of conversions it asks for)."""
     if not LAYOUT_SESSIONS:
         yield
         return
+    recs = _LAYOUTS.get(owner)
+    if recs is None:
+        recs = _LAYOUTS[owner] = {}
     key = (key, threading.get_ident())
-    rec = _LAYOUTS.get(key)
-    recording = rec is None or not rec.valid or rec.table is None
+    rec = recs.get(key)
+    recording = rec is None or not rec.valid or rec.table is None or not rec.live()
     if recording:
-        rec = _LAYOUTS[key] = _LayoutRecord()
+        rec = recs[key] = _LayoutRecord(owner)
     else:
         call("tmr_weight_layouts_multi", rec.table, len(rec.rows), rec.blocks, stream_ptr())
     st = _session()

@@ -271,7 +271,7 @@ class ResNeStTrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x4, share, keep, *params):
         # every conv weight layout of the step in one launch (ops.layout_session)
-        with ops.layout_session(("resnest50", id(share), share.training, bool(keep),
+        with ops.layout_session(share, ("resnest50", share.training, bool(keep),
                                  share.precision)):
             return ResNeStTrunkFn._forward(ctx, x4, share, keep, params)
 

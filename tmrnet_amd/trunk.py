@@ -413,7 +413,7 @@ class TrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x4, share, keep, *params):
         # every conv weight layout of the step in one launch (ops.layout_session)
-        with ops.layout_session(("resnet50", id(share), share.training, bool(keep),
+        with ops.layout_session(share, ("resnet50", share.training, bool(keep),
                                  share.precision)):
             return TrunkFn._forward(ctx, x4, share, keep, params)
 
