@@ -38,10 +38,13 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Cell arithmetic of one (clip, unit), shared by the persistent kernels and their solo
-// re-computation (below), so both produce the same bits.
+// re-computation (below), so both produce the same bits.  No implicit FMA contraction: whether
+// the compiler fuses a product into an add depended on how it vectorised the surrounding code
+// (measured: 1 - g*g fused in one kernel, not in the other), so every product is rounded.
 __device__ __forceinline__ float cell_fwd(const float gi, const float gf, const float gc,
                                           const float go, float& c, float& ig, float& fg,
                                           float& gg, float& og) {
+#pragma clang fp contract(off)
   ig = sigm(gi); fg = sigm(gf);
   gg = tanhf(gc); og = sigm(go);
   c = fg * c + ig * gg;
@@ -50,6 +53,7 @@ __device__ __forceinline__ float cell_fwd(const float gi, const float gf, const 
 __device__ __forceinline__ void cell_bwd(const float dh, const float ig, const float fg,
                                          const float gg, const float og, const float cv,
                                          const float cp, float& dc, float d[4]) {
+#pragma clang fp contract(off)
   const float tc = tanhf(cv);
   const float dct = dh * og * (1.f - tc * tc) + dc;
   d[0] = dct * gg * ig * (1.f - ig);
