@@ -151,6 +151,9 @@ def test_lstm_next_to_resident_kernel(dev, monkeypatch):
     with torch.cuda.stream(side):
         # two 1024-thread workgroups fill a CU's 32 wave slots; leave 16 CUs free
         call("tmr_test_hold_cus", 2 * (cus - 16), 1500.0, stream_ptr())
+    # the LSTM's stream first waits 50 ms (one sleeping workgroup), so the side stream's
+    # workgroups are resident when the persistent grid is dispatched
+    call("tmr_test_hold_cus", 1, 50.0, stream_ptr())
     out, sf, sb = _lstm_fwd_bwd(args, dy)
     torch.cuda.synchronize()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

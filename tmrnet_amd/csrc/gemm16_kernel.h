@@ -75,18 +75,22 @@ __device__ __forceinline__ void store_g8(const GemmArgs& a, long off, const floa
 
 // the 8 old-dx values of the fused BN-backward epilogue's beta at element offset `off` (fp32, or
 // bf16 when GemmArgs::cold16), raw: (c0, c1) = 32 B of fp32, or c0 = 16 B of bf16
-__device__ __forceinline__ void load_old8(const GemmArgs& a, long off, uint4& c0, uint4& c1) {
+__device__ __forceinline__ void load_old8(const GemmArgs& a, long off, uint4& c0, uint4& c1,
+                                          bool c16) {
   const void* base = a.Cold ? a.Cold : (const void*)a.C;
-  if (a.cold16) {
+  if (c16) {
     c0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(base) + off);
   } else {
     c0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + off);
     c1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + off + 4);
   }
 }
-__device__ __forceinline__ void unpack_old8(const GemmArgs& a, const uint4& c0, const uint4& c1,
-                                            float (&old)[8]) {
-  if (a.cold16) {
+__device__ __forceinline__ void load_old8(const GemmArgs& a, long off, uint4& c0, uint4& c1) {
+  load_old8(a, off, c0, c1, a.cold16);
+}
+__device__ __forceinline__ void unpack_old8(const uint4& c0, const uint4& c1, float (&old)[8],
+                                            bool c16) {
+  if (c16) {
     const uint32_t u[4] = {c0.x, c0.y, c0.z, c0.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -99,6 +103,32 @@ __device__ __forceinline__ void unpack_old8(const GemmArgs& a, const uint4& c0, 
     for (int e = 0; e < 8; ++e) old[e] = __uint_as_float(u[e]);
   }
 }
+__device__ __forceinline__ void unpack_old8(const GemmArgs& a, const uint4& c0, const uint4& c1,
+                                            float (&old)[8]) {
+  unpack_old8(c0, c1, old, a.cold16);
+}
+
+// Epilogue forms of the fused BN-backward dgrads (round 6): the flags a form fixes at compile time,
+// so its row slots hold only the fields it loads.  EPF 1: the bf16-activation step -- y, z
+// (mask 1) and the old gradient (beta) bf16, no ReLU bits; EPF 2: the fp32 step -- y and the old
+// gradient fp32, no stored z (mask 0 / 2 / 3); EPF 0: every flag read at run time.
+template <int EPF>
+struct EpiForm {
+  __device__ __forceinline__ static bool bn16(const GemmArgs& a) {
+    return EPF == 1 ? true : (EPF == 2 ? false : a.bn16 != 0);
+  }
+  __device__ __forceinline__ static bool mask1(const GemmArgs& a) { return EPF == 2 ? false : a.bn_mask == 1; }
+  __device__ __forceinline__ static bool mask3(const GemmArgs& a) { return EPF == 1 ? false : a.bn_mask == 3; }
+  __device__ __forceinline__ static bool cold16(const GemmArgs& a) {
+    return EPF == 1 ? true : (EPF == 2 ? false : a.cold16 != 0);
+  }
+};
+// the form a launch qualifies for (host)
+inline int epi_form(const GemmArgs& a) {
+  if (a.bn16 && a.bn_mask != 3 && (a.beta == 0.f || a.cold16)) return 1;
+  if (!a.bn16 && a.bn_mask != 1 && !a.cold16) return 2;
+  return 0;
+}
 
 #ifndef TMR_EPI_DEPTH
 #define TMR_EPI_DEPTH 3
@@ -108,8 +138,26 @@ __device__ __forceinline__ void unpack_old8(const GemmArgs& a, const uint4& c0, 
 #ifndef TMR_EPI_LATE
 #define TMR_EPI_LATE 0
 #endif
-template <int BM, int BN, int WM, int WN, int SMEMB, int DEPTH = TMR_EPI_DEPTH>
+// rows whose loads the 4-wave tiles add once the accumulators are staged (round 6): the
+// accumulators are dead then, so the registers of TOP more rows are free; issued before the
+// first row is consumed, so the whole tile's epilogue operands are in flight at once
+#ifndef TMR_EPI_TOPUP
+#define TMR_EPI_TOPUP 0
+#endif
+#ifndef TMR_EPI_TOPUP_F16
+#define TMR_EPI_TOPUP_F16 0
+#endif
+#ifndef TMR_EPI_TOPUP_F32
+#define TMR_EPI_TOPUP_F32 0
+#endif
+// the compile-time epilogue forms (EpiForm) for the 4-wave dgrads; 0 = the run-time form only
+#ifndef TMR_EPI_FORMS
+#define TMR_EPI_FORMS 0
+#endif
+template <int BM, int BN, int WM, int WN, int SMEMB, int DEPTH = TMR_EPI_DEPTH, int TOP = 0,
+          int EPF = 0>
 struct LdsBnbwd {
+  using Form = EpiForm<EPF>;
   static constexpr int NT = 64 * WM * WN;
   static constexpr int LDC = BN + 4;                   // padded fp32 row of the staged tile
   static constexpr int CG = BN / 8;                    // column groups of 8
@@ -122,7 +170,8 @@ struct LdsBnbwd {
   static constexpr int NCH = (BM + RCH - 1) / RCH;
   static constexpr int PC = (RCH + RPP - 1) / RPP;     // row slots of a thread per chunk
   static constexpr int NR = NCH * PC;                  // row slots of a thread
-  static constexpr int D = NR < DEPTH ? NR : DEPTH;   // rows in flight
+  static constexpr int D = NR < DEPTH ? NR : DEPTH;   // rows in flight during the main loop
+  static constexpr int DT = NR < D + TOP ? NR : D + TOP;   // ... once the tile is staged
   static_assert(NT % CG == 0, "epilogue row partition");
 
   struct In {         // one row's global operands as loaded
@@ -153,30 +202,30 @@ struct LdsBnbwd {
     x.off = pix * a.ldc + col;
     if (!x.ok) return;
     const long off = x.off;
-    if (a.bn16) {
+    if (Form::bn16(a)) {
       x.y0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.bn_y) + off);
-      if (a.bn_mask == 1)
+      if (Form::mask1(a))
         x.z0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.bn_z) + off);
     } else {
       x.y0 = *reinterpret_cast<const uint4*>(a.bn_y + off);
       x.y1 = *reinterpret_cast<const uint4*>(a.bn_y + off + 4);
-      if (a.bn_mask == 1) {
+      if (Form::mask1(a)) {
         x.z0 = *reinterpret_cast<const uint4*>(a.bn_z + off);
         x.z1 = *reinterpret_cast<const uint4*>(a.bn_z + off + 4);
       }
     }
-    if (a.bn_mask == 3) x.bits = reinterpret_cast<const uint32_t*>(a.bn_z)[off >> 5];
-    if (a.beta != 0.f) load_old8(a, off, x.c0, x.c1);
+    if (Form::mask3(a)) x.bits = reinterpret_cast<const uint32_t*>(a.bn_z)[off >> 5];
+    if (a.beta != 0.f) load_old8(a, off, x.c0, x.c1, Form::cold16(a));
   }
 
-  __device__ __forceinline__ static void prefetch(const GemmArgs& a, int m0, int n0, In (&pf)[D]) {
+  __device__ __forceinline__ static void prefetch(const GemmArgs& a, int m0, int n0, In (&pf)[DT]) {
 #pragma unroll
     for (int t = 0; t < D; ++t) issue(a, t, m0, n0, pf[t]);
   }
 
   template <int TM, int TN>
   __device__ __forceinline__ static void run(const GemmArgs& a, floatx16 (&acc)[TM][TN], float* lds,
-                                             int m0, int n0, In (&pf)[D]) {
+                                             int m0, int n0, In (&pf)[DT]) {
     int etid = threadIdx.x;
     asm volatile("" : "+v"(etid));   // keep the epilogue's index math out of the main loop
     const int lane = etid & 63, wave = etid >> 6;
@@ -214,22 +263,26 @@ struct LdsBnbwd {
             }
       }
       __syncthreads();
+      if (ci == 0) {   // the accumulators are staged: top the rows in flight up to DT
+#pragma unroll
+        for (int t = D; t < DT; ++t) issue(a, t, m0, n0, pf[t]);
+      }
       // (2) this thread's rows of the chunk, 8 columns each
 #pragma unroll
       for (int j = 0; j < PC; ++j) {
         const int t = ci * PC + j;
-        In& x = pf[t % D];
+        In& x = pf[t % DT];
         if (x.ok) {
           const long off = x.off;
           float yv[8], zv[8], old[8];
-          if (a.bn16) {
+          if (Form::bn16(a)) {
             const uint32_t yu[4] = {x.y0.x, x.y0.y, x.y0.z, x.y0.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               yv[2 * e] = __uint_as_float(yu[e] << 16);
               yv[2 * e + 1] = __uint_as_float(yu[e] & 0xffff0000u);
             }
-            if (a.bn_mask == 1) {
+            if (Form::mask1(a)) {
               const uint32_t zu[4] = {x.z0.x, x.z0.y, x.z0.z, x.z0.w};
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
@@ -241,22 +294,22 @@ struct LdsBnbwd {
             const uint32_t yu[8] = {x.y0.x, x.y0.y, x.y0.z, x.y0.w, x.y1.x, x.y1.y, x.y1.z, x.y1.w};
 #pragma unroll
             for (int e = 0; e < 8; ++e) yv[e] = __uint_as_float(yu[e]);
-            if (a.bn_mask == 1) {
+            if (Form::mask1(a)) {
               const uint32_t zu[8] = {x.z0.x, x.z0.y, x.z0.z, x.z0.w, x.z1.x, x.z1.y, x.z1.z, x.z1.w};
 #pragma unroll
               for (int e = 0; e < 8; ++e) zv[e] = __uint_as_float(zu[e]);
             }
           }
-          if (a.bn_mask == 3) {   // ReLU mask bits: this thread's 8 elements share one word
+          if (Form::mask3(a)) {   // ReLU mask bits: this thread's 8 elements share one word
             const uint32_t b8 = x.bits >> (off & 31);
 #pragma unroll
             for (int e = 0; e < 8; ++e) zv[e] = ((b8 >> e) & 1u) ? 1.f : 0.f;
-          } else if (a.bn_mask != 1) {
+          } else if (!Form::mask1(a)) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) zv[e] = 0.f;
           }
           if (has_beta) {
-            unpack_old8(a, x.c0, x.c1, old);
+            unpack_old8(x.c0, x.c1, old, Form::cold16(a));
           } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) old[e] = 0.f;
@@ -278,7 +331,7 @@ struct LdsBnbwd {
           }
           store_g8(a, off, v);
         }
-        if (t + D < NR) issue(a, t + D, m0, n0, x);   // the slot's next row
+        if (t + DT < NR) issue(a, t + DT, m0, n0, x);   // the slot's next row
       }
     }
     // (3) column sums over the RPP row slots -> bn_part
@@ -479,7 +532,8 @@ constexpr int occ16() {
 }
 
 // the body of one workgroup: output tile `bid` (m-major over the n-tiles), reduction split `split`
-template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE, int F32, int PRO, int NST>
+template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE, int F32, int PRO, int NST,
+          int EPF = 0>
 __device__ __forceinline__ void gemm16_body(const GemmArgs& a, const int bid, const int split) {
   constexpr uint32_t ES = F32 ? 4u : 2u;   // element bytes
   constexpr int EPC = 16 / ES;             // elements per 16-B chunk
@@ -884,8 +938,12 @@ __device__ __forceinline__ void gemm16_body(const GemmArgs& a, const int bid, co
   // staged (their accumulators are dead by then); the 16-wave ones keep epilogue_lds_bnbwd
   constexpr bool PRE = LDSEPI && NW < 8;
   constexpr bool LATE = LDSEPI && NW == 8 && LDSNEED == LDSFULL && TMR_EPI_LATE > 0;
-  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM, PRE ? TMR_EPI_DEPTH : (TMR_EPI_LATE > 0 ? TMR_EPI_LATE : 1)>;
-  typename Epi::In pf[(PRE || LATE) ? Epi::D : 1];
+  // a compile-time form (EPF 1 / 2) drops the fields its rows never load: then every row of the
+  // tile goes in flight once the accumulators are staged (TOP), else TMR_EPI_TOPUP more rows
+  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM, PRE ? TMR_EPI_DEPTH : (TMR_EPI_LATE > 0 ? TMR_EPI_LATE : 1),
+                      PRE ? (EPF == 1 ? TMR_EPI_TOPUP_F16 : (EPF == 2 ? TMR_EPI_TOPUP_F32 : TMR_EPI_TOPUP)) : 0,
+                      EPF>;
+  typename Epi::In pf[(PRE || LATE) ? Epi::DT : 1];
   if constexpr (PRE) {
     if (a.bn_part != nullptr) Epi::prefetch(a, m0, n0, pf);
   }
@@ -1033,12 +1091,12 @@ __device__ __forceinline__ void gemm16_body(const GemmArgs& a, const int bid, co
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int TAPV, int PIPE = 1, int F32 = 0, int PRO = 0,
-          int NST = 2>
+          int NST = 2, int EPF = 0>
 __global__ __launch_bounds__(64 * WM * WN, (occ16<BM, BN, WM, WN, NST>()))
 void gemm16_kernel(const GemmArgs a) {
   int bid, split;
   xcd_work(bid, split);   // XCD-aware tile order (gemm_kernel.h)
-  gemm16_body<MODE, BM, BN, WM, WN, TAPV, PIPE, F32, PRO, NST>(a, bid, split);
+  gemm16_body<MODE, BM, BN, WM, WN, TAPV, PIPE, F32, PRO, NST, EPF>(a, bid, split);
 }
 
 // Tile w of a GemmPar launch -> (class, tile of that class).  The classes' tiles go out in
@@ -1134,6 +1192,20 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
       const dim3 g2((unsigned)(cdiv(a.M, 256) * cdiv(a.N, 128)), grid.y, 1);
       hipLaunchKernelGGL((gemm16_kernel<MODE, 256, 128, 4, 2, 0, 1, F32, PRO, 1>), g2, dim3(512), 0, st, a);
       TMR_CHECK_LAUNCH("gemm16_kernel (one stage, 256x128)");
+      return 0;
+    }
+  }
+  // the fused BN-backward dgrads of the 4-wave tiles in their compile-time epilogue form
+  // (EpiForm: bf16 step EPF 1, fp32 step EPF 2)
+  constexpr bool FORMS = MODE == MODE_DGRAD && PRO == 0 && WM * WN == 4 && TMR_EPI_FORMS;
+  if constexpr (FORMS) {
+    const int f = a.bn_part != nullptr ? epi_form(a) : 0;
+    if (f == (F32 ? 2 : 1)) {
+      if (tapv)
+        hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 1, 1, F32, 0, 2, F32 ? 2 : 1>), grid, blk, 0, st, a);
+      else
+        hipLaunchKernelGGL((gemm16_kernel<MODE, BM, BN, WM, WN, 0, 1, F32, 0, 2, F32 ? 2 : 1>), grid, blk, 0, st, a);
+      TMR_CHECK_LAUNCH("gemm16_kernel (dgrad epilogue form)");
       return 0;
     }
   }
