@@ -145,14 +145,27 @@ inline int epi_form(const GemmArgs& a) {
 #define TMR_EPI_TOPUP 0
 #endif
 #ifndef TMR_EPI_TOPUP_F16
-#define TMR_EPI_TOPUP_F16 0
+#define TMR_EPI_TOPUP_F16 5
 #endif
 #ifndef TMR_EPI_TOPUP_F32
-#define TMR_EPI_TOPUP_F32 0
+#define TMR_EPI_TOPUP_F32 2
 #endif
-// the compile-time epilogue forms (EpiForm) for the 4-wave dgrads; 0 = the run-time form only
+// the compile-time epilogue forms (EpiForm) for the 4-wave dgrads; 0 = the run-time form only.
+// Round 6 (profiles/r6/epi_forms/): with the forms the bf16 tiles take every row of the tile in
+// flight once the accumulators are staged (3 before the main loop + 5), the fp32 ones 3 + 2 (more
+// spills): C5 dgrad view 50.1 -> 46.5 ms/step (304 -> 328 TF), C2 50.6 -> 49.9 ms; bit-identical.
+// Tried: 5 bf16 rows before the main loop (no gain), the fp32 N >= 512 dgrads on the 4-wave tile
+// (slower), 2 / 4 late rows in the 8-wave tiles (spill: C2 dgrad +2.4 ms).
 #ifndef TMR_EPI_FORMS
-#define TMR_EPI_FORMS 0
+#define TMR_EPI_FORMS 1
+#endif
+// rows in flight before the main loop in the bf16 form (4-wave tiles)
+#ifndef TMR_EPI_DEPTH_F16
+#define TMR_EPI_DEPTH_F16 TMR_EPI_DEPTH
+#endif
+// rows in flight after the main loop in the forms of the 8-wave tiles (0: one row at a time)
+#ifndef TMR_EPI_LATE_F
+#define TMR_EPI_LATE_F 0
 #endif
 template <int BM, int BN, int WM, int WN, int SMEMB, int DEPTH = TMR_EPI_DEPTH, int TOP = 0,
           int EPF = 0>
@@ -937,10 +950,12 @@ __device__ __forceinline__ void gemm16_body(const GemmArgs& a, const int bid, co
   // loop; the 8-wave ones (128-VGPR budget) right after it, two rows deep, once the whole tile is
   // staged (their accumulators are dead by then); the 16-wave ones keep epilogue_lds_bnbwd
   constexpr bool PRE = LDSEPI && NW < 8;
-  constexpr bool LATE = LDSEPI && NW == 8 && LDSNEED == LDSFULL && TMR_EPI_LATE > 0;
-  // a compile-time form (EPF 1 / 2) drops the fields its rows never load: then every row of the
-  // tile goes in flight once the accumulators are staged (TOP), else TMR_EPI_TOPUP more rows
-  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM, PRE ? TMR_EPI_DEPTH : (TMR_EPI_LATE > 0 ? TMR_EPI_LATE : 1),
+  constexpr int LATED = EPF != 0 ? TMR_EPI_LATE_F : TMR_EPI_LATE;
+  constexpr bool LATE = LDSEPI && NW == 8 && LDSNEED == LDSFULL && LATED > 0;
+  // a compile-time form (EPF 1 / 2) drops the fields its rows never load: then more rows of the
+  // tile go in flight -- before the main loop (DEPTH) and once the accumulators are staged (TOP)
+  using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM,
+                      PRE ? (EPF == 1 ? TMR_EPI_DEPTH_F16 : TMR_EPI_DEPTH) : (LATE ? LATED : 1),
                       PRE ? (EPF == 1 ? TMR_EPI_TOPUP_F16 : (EPF == 2 ? TMR_EPI_TOPUP_F32 : TMR_EPI_TOPUP)) : 0,
                       EPF>;
   typename Epi::In pf[(PRE || LATE) ? Epi::DT : 1];
@@ -1127,7 +1142,7 @@ __device__ __forceinline__ void par_tile(const GemmPar& p, int w, int& cls, int&
   }
 }
 
-template <int BM, int BN, int WM, int WN, int F32>
+template <int BM, int BN, int WM, int WN, int F32, int EPF = 0>
 __global__ __launch_bounds__(64 * WM * WN, (occ16<BM, BN, WM, WN, 2>()))
 void gemm16_par_kernel(const GemmPar p) {
   int w, split;
@@ -1160,7 +1175,7 @@ void gemm16_par_kernel(const GemmPar p) {
   a.dHW = FastDiv{own(c.dHW.d), own(c.dHW.m), own(c.dHW.s)};
   a.dW = FastDiv{own(c.dW.d), own(c.dW.m), own(c.dW.s)};
   a.bn_part = own(c.bn_part);
-  gemm16_body<MODE_DGRAD, BM, BN, WM, WN, 0, 1, F32, 0, 2>(a, t, 0);
+  gemm16_body<MODE_DGRAD, BM, BN, WM, WN, 0, 1, F32, 0, 2, EPF>(a, t, 0);
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int F32, int PRO = 0>
@@ -1197,7 +1212,8 @@ int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   }
   // the fused BN-backward dgrads of the 4-wave tiles in their compile-time epilogue form
   // (EpiForm: bf16 step EPF 1, fp32 step EPF 2)
-  constexpr bool FORMS = MODE == MODE_DGRAD && PRO == 0 && WM * WN == 4 && TMR_EPI_FORMS;
+  constexpr bool FORMS = MODE == MODE_DGRAD && PRO == 0 && TMR_EPI_FORMS &&
+                         (WM * WN == 4 || (WM * WN == 8 && TMR_EPI_LATE_F > 0));
   if constexpr (FORMS) {
     const int f = a.bn_part != nullptr ? epi_form(a) : 0;
     if (f == (F32 ? 2 : 1)) {
@@ -1364,11 +1380,23 @@ int launch_gemm16_par(const GemmArgs* as, int n, hipStream_t st) {
   if (total == 0) return 0;
   TMR_CHECK_ARG(total < (1L << 31), "gemm (parity classes): %ld tiles", total);
   const dim3 grid((unsigned)total, 1, 1);
+  // the 4-wave tiles' fused BN-backward dgrads in their compile-time epilogue form (EpiForm)
+  constexpr int EF = F32 ? 2 : 1;
+  const bool form = TMR_EPI_FORMS && p.a.bn_part != nullptr && epi_form(p.a) == EF;
   switch (cfg) {
     case 1: hipLaunchKernelGGL((gemm16_par_kernel<256, 128, 4, 2, F32>), grid, dim3(512), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((gemm16_par_kernel<128, 128, 2, 2, F32>), grid, dim3(256), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((gemm16_par_kernel<256, 64, 4, 1, F32>), grid, dim3(256), 0, st, p); break;
-    case 5: hipLaunchKernelGGL((gemm16_par_kernel<64, 64, 2, 2, F32>), grid, dim3(256), 0, st, p); break;
+    case 2:
+      if (form) hipLaunchKernelGGL((gemm16_par_kernel<128, 128, 2, 2, F32, EF>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((gemm16_par_kernel<128, 128, 2, 2, F32>), grid, dim3(256), 0, st, p);
+      break;
+    case 3:
+      if (form) hipLaunchKernelGGL((gemm16_par_kernel<256, 64, 4, 1, F32, EF>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((gemm16_par_kernel<256, 64, 4, 1, F32>), grid, dim3(256), 0, st, p);
+      break;
+    case 5:
+      if (form) hipLaunchKernelGGL((gemm16_par_kernel<64, 64, 2, 2, F32, EF>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((gemm16_par_kernel<64, 64, 2, 2, F32>), grid, dim3(256), 0, st, p);
+      break;
     case 7: hipLaunchKernelGGL((gemm16_par_kernel<128, 128, 4, 2, F32>), grid, dim3(512), 0, st, p); break;
   }
   TMR_CHECK_LAUNCH("gemm16_par_kernel");
