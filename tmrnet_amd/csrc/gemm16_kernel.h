@@ -954,9 +954,11 @@ __device__ __forceinline__ void gemm16_body(const GemmArgs& a, const int bid, co
   constexpr bool LATE = LDSEPI && NW == 8 && LDSNEED == LDSFULL && LATED > 0;
   // a compile-time form (EPF 1 / 2) drops the fields its rows never load: then more rows of the
   // tile go in flight -- before the main loop (DEPTH) and once the accumulators are staged (TOP)
+  // (the late rows of the 8-wave tiles are issued once the accumulators are staged: DEPTH 0)
   using Epi = LdsBnbwd<BM, BN, WM, WN, SMEM,
-                      PRE ? (EPF == 1 ? TMR_EPI_DEPTH_F16 : TMR_EPI_DEPTH) : (LATE ? LATED : 1),
-                      PRE ? (EPF == 1 ? TMR_EPI_TOPUP_F16 : (EPF == 2 ? TMR_EPI_TOPUP_F32 : TMR_EPI_TOPUP)) : 0,
+                      PRE ? (EPF == 1 ? TMR_EPI_DEPTH_F16 : TMR_EPI_DEPTH) : (LATE ? 0 : 1),
+                      PRE ? (EPF == 1 ? TMR_EPI_TOPUP_F16 : (EPF == 2 ? TMR_EPI_TOPUP_F32 : TMR_EPI_TOPUP))
+                          : (LATE ? LATED : 0),
                       EPF>;
   typename Epi::In pf[(PRE || LATE) ? Epi::DT : 1];
   if constexpr (PRE) {
