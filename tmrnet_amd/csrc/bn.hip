@@ -919,6 +919,46 @@ __device__ __forceinline__ void st8<__bf16>(__bf16* p, long i, const float (&v)[
   }
   reinterpret_cast<uint4*>(p)[i] = make_uint4(w[0], w[1], w[2], w[3]);
 }
+// The BatchNorm-backward apply with g already masked (MASK 0; tmr_bn_bwd_parts), 8 elements per
+// thread, two groups in flight: the fp32 step's form of bn_bwd_apply8_a16 (64 B of g and y per
+// group instead of 32; round 6).  Same fmaf sequence per element as bn_bwd_apply: identical dy.
+template <typename TG, typename TY, typename TD>
+__global__ __launch_bounds__(NT) void bn_bwd_apply8_k(const TG* __restrict__ g,
+                                                      const TY* __restrict__ y,
+                                                      const float* __restrict__ coef,
+                                                      TD* __restrict__ dy, long n8, int c8) {
+  const int c = c8 * 8;
+  const long stride = (long)gridDim.x * NT;
+  auto apply = [&](long i, const float (&gv)[8], const float (&yv)[8]) {
+    const int cc = chan_of(i, c8) * 8;
+    float o[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 A = *reinterpret_cast<const float4*>(coef + cc + 4 * h);
+      const float4 B = *reinterpret_cast<const float4*>(coef + c + cc + 4 * h);
+      const float4 C = *reinterpret_cast<const float4*>(coef + 2 * c + cc + 4 * h);
+      o[4 * h] = fmaf(A.x, gv[4 * h], fmaf(B.x, yv[4 * h], C.x));
+      o[4 * h + 1] = fmaf(A.y, gv[4 * h + 1], fmaf(B.y, yv[4 * h + 1], C.y));
+      o[4 * h + 2] = fmaf(A.z, gv[4 * h + 2], fmaf(B.z, yv[4 * h + 2], C.z));
+      o[4 * h + 3] = fmaf(A.w, gv[4 * h + 3], fmaf(B.w, yv[4 * h + 3], C.w));
+    }
+    st8(dy, i, o);
+  };
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n8;
+    float ga[8], ya[8], gb[8], yb[8];
+    ld8(g, i, ga);
+    ld8(y, i, ya);
+    if (hj) {
+      ld8(g, j, gb);
+      ld8(y, j, yb);
+    }
+    apply(i, ga, ya);
+    if (hj) apply(j, gb, yb);
+  }
+}
+
 // The same per 2x2 quad of input pixels (rows 2k, 2k+1, columns 2l, 2l+1): the pooled outputs
 // (k .. k+1) x (l .. l+1) are the candidates of all four pixels, so each is loaded once per quad
 // -- one pooled load per pixel instead of 2.25 (the launch is bound by those gathered bytes).
@@ -1411,6 +1451,9 @@ TMR_API int tmr_bn_bwd_parts_x(const float* g, const float* y, const void* parts
   if (out_bf16)
     hipLaunchKernelGGL((bn_bwd_apply<0, false, __bf16, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g,
                        y, nullptr, nullptr, nullptr, coef, (__bf16*)dyv, nullptr, n4, c / 4);
+  else if (c % 8 == 0 && (((uintptr_t)g | (uintptr_t)y | (uintptr_t)dyv) & 15) == 0)
+    hipLaunchKernelGGL((bn_bwd_apply8_k<float, float, float>), dim3(ew_blocks(n4 / 2)), dim3(NT), 0,
+                       stream, g, y, coef, (float*)dyv, n4 / 2, c / 8);
   else
     hipLaunchKernelGGL((bn_bwd_apply<0, false, float, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, g, y,
                        nullptr, nullptr, nullptr, coef, (float*)dyv, nullptr, n4, c / 4);
