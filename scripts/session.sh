@@ -1,24 +1,23 @@
 # one GPU session (edited per call; the records it writes are copied into profiles/<round>/)
-# round 6d: epilogue forms, second sweep -- fa (round-6c leader), fd (bf16: 5 rows before the main
-# loop + 3 after staging), fa with the fp32 N >= 512 dgrads on the 4-wave tile
-# (TMR_DGRAD32_WIDE_CFG=2), fe (8-wave tiles: 2 rows in flight after staging, spills)
+# round 6 final build, part 1: full GPU suite, smoke, C2 / C4 / C5 benches, rocprofv3 kernel stats
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r6d; mkdir -p $O
-for rep in 1 2; do
-  for v in fa fd fa2 fe; do
-    L=$PWD/tmrnet_amd/libtmr_${v%2}.so; W=7
-    [ $v = fa2 ] && W=2
-    TMR_DGRAD32_WIDE_CFG=$W TMR_LIB_PATH=$L timeout -k 10 300 python -u bench.py --precision bf16 --seq 30 --lfb 300 --steps 6 --no-cpu-baseline > $O/c5_${v}_$rep.json 2> $O/c5_${v}_$rep.err || exit 2
-    TMR_DGRAD32_WIDE_CFG=$W TMR_LIB_PATH=$L timeout -k 10 300 python -u bench.py --steps 10 --no-cpu-baseline --conv-table > $O/c2_${v}_$rep.json 2> $O/c2_${v}_$rep.err || exit 3
-  done
-done
+O=gpurun_out/r6h; mkdir -p $O
+timeout -k 10 1000 python -u -m pytest -v --timeout 400 --timeout-method thread -m gpu tests/ > $O/pytest.txt 2>&1
+echo "pytest rc=$?" >> $O/pytest.txt
+tail -3 $O/pytest.txt
+grep -E "FAILED|ERROR" $O/pytest.txt | head -20
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py > $O/c2.json 2> $O/c2.err || exit 2
+timeout -k 10 300 python -u bench.py --model resnest50 --precision bf16 --steps 10 --no-cpu-baseline > $O/c4.json 2> $O/c4.err || exit 3
+timeout -k 10 300 python -u bench.py --precision bf16 --seq 30 --lfb 300 --steps 6 --no-cpu-baseline > $O/c5.json 2> $O/c5.err || exit 4
 python - <<'PY'
 import json
-for w in ('c5','c2'):
-    for v in ('fa','fd','fa2','fe'):
-        for rep in (1,2):
-            d=json.load(open('gpurun_out/r6d/%s_%s_%d.json'%(w,v,rep)))
-            dg=[x for k,x in d['roofline']['per_kind'].items() if 'dgrad' in k][0]
-            print(w,v,rep,d['value'],d['ms_per_step'],'dgrad',dg['ms'],dg['tflops'],'loss',d['loss_last'])
+for w in ('c2','c4','c5'):
+    d=json.load(open('gpurun_out/r6h/%s.json'%w)); r=d['roofline']
+    print(w, d['value'], d['ms_per_step'], r['frac'], r['build_sha'], {k: v['ms'] for k, v in r['per_kind'].items()}, (d.get('cpu_baseline') or {}).get('value'))
 PY
+PROF_NAME=r6h/prof_c2 STEPS=3 BENCH_ARGS="" bash scripts/profile.sh > $O/prof_c2.txt 2>&1 || exit 5
+PROF_NAME=r6h/prof_c4 STEPS=3 BENCH_ARGS="--precision bf16 --model resnest50 --seq 10 --lfb 40" bash scripts/profile.sh > $O/prof_c4.txt 2>&1 || exit 6
+PROF_NAME=r6h/prof_c5 STEPS=3 BENCH_ARGS="--precision bf16 --seq 30 --lfb 300" bash scripts/profile.sh > $O/prof_c5.txt 2>&1 || exit 7
+echo profiles done
