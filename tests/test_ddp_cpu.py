@@ -26,25 +26,27 @@ def _worker(rank, world, port, q, early=False):
     torch.manual_seed(100 + rank)           # different init per rank -> broadcast must fix it
     m = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.Linear(200, 7))
     red = GradAllReduce(m, dist, bucket_bytes=4 * 1024)
-    for i, p in enumerate(m.parameters()):
-        p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
-    if early:   # the trunk's per-block launch during the backward (TrunkFn.backward)
-        ps = list(m.parameters())
-        red.grads_ready([(p, p.grad.clone()) for p in ps[2:]])
+    ps = list(m.parameters())
+    grads = [torch.full_like(p, float(rank + 1) * (i + 1)) for i, p in enumerate(ps)]
+    if early:   # the trunk's per-block launch during the backward (TrunkFn.backward), made
+        # before autograd stores the gradients into p.grad (else the launch is skipped)
+        red.grads_ready([(p, g.clone()) for p, g in zip(ps[2:], grads[2:])])
+    for p, g in zip(ps, grads):
+        p.grad = g
     red.all_reduce_sum()
     # numpy copies: torch tensors would travel as shared-memory fds that vanish with the child
     out = [p.grad.numpy().copy() for p in m.parameters()]
     w = [p.detach().numpy().copy() for p in m.parameters()]
-    q.put((rank, out, w, len(red.buckets)))
+    q.put((rank, out, w, len(red.buckets), dict(red.counts)))
     dist.destroy_process_group()
 
 
 import pytest
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("early", [False, True])
-def test_grad_all_reduce_sum_world2(early):
-    world = 2
+def test_grad_all_reduce_sum_world2(early, world):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -53,18 +55,30 @@ def test_grad_all_reduce_sum_world2(early):
         p.start()
     res = {}
     for _ in range(world):
-        rank, grads, weights, nb = q.get(timeout=120)
-        res[rank] = (grads, weights, nb)
+        rank, grads, weights, nb, counts = q.get(timeout=120)
+        res[rank] = (grads, weights, nb, counts)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0][2] > 1                       # several buckets exercised
+    ranks_sum = sum(r + 1 for r in range(world))
     for i, g in enumerate(res[0][0]):
-        expect = (1 + 2) * (i + 1)             # sum over ranks, not mean
+        expect = ranks_sum * (i + 1)           # sum over ranks, not mean
         assert (g == expect).all()
-        assert (g == res[1][0][i]).all()
-    for w0, w1 in zip(res[0][1], res[1][1]):
-        assert (w0 == w1).all()
+        for r in range(1, world):
+            assert (g == res[r][0][i]).all()
+    for r in range(1, world):
+        for w0, w1 in zip(res[0][1], res[r][1]):
+            assert (w0 == w1).all()
+    # the exchange's diagnostics (bench.rank_diagnostics): one exchange, the early launch counted,
+    # every gradient element (+ one presence flag per bucketed parameter) sent exactly once
+    n_el = sum(g.size for g in res[0][0])
+    for r in range(world):
+        c = res[r][3]
+        assert c["reduces"] == 1 and c["early_launches"] == (1 if early else 0), c
+        assert c["bucket_launches"] >= 1
+        n_flags = 2 if early else 4            # presence flags of the bucketed parameters
+        assert c["bytes"] == 4 * (n_el + n_flags), (c, n_el)
 
 
 def _accum_worker(rank, world, port, q):
