@@ -368,8 +368,9 @@ def rank_diagnostics(dist, world, dev, elapsed, marks, reducer, c0, steps):
             "early_launches_per_step": rows[0][6], "bucket_launches_per_step": rows[0][7],
             "allreduce_mb_per_step": round(rows[0][8] / 2 ** 20, 2),
             "exchange": ("none (one rank)" if reducer is None else
-                         "RCCL all-reduce SUM, %d trunk blocks launched during the backward"
-                         % rows[0][6])}
+                         "%s all-reduce SUM, %d trunk blocks launched during the backward"
+                         % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend(),
+                            rows[0][6]))}
 
 
 def workload_name(args):
