@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 7
+#define TMR_ABI_VERSION 8
 
 int tmr_abi_version(void);
 const char* tmr_last_error(void);
@@ -95,6 +95,10 @@ typedef struct tmr_conv_desc {
 #define TMR_IO_CLASSES 512 /* dgrad, any math: a strided dgrad as one launch per stride-parity
                               class, as before round 5 -- the form the one-launch path
                               (every class's tiles in one grid) is compared with; same values */
+#define TMR_IO_TILES 1024 /* fused BN-backward dgrad, any math: one output tile per workgroup (the
+                              LDS-DMA engine's launch) also where the wave-specialised persistent
+                              dgrad serves the shape (1x1 stride-1, round 6) -- the form that one is
+                              compared with; same dx bits, partials bit-identical on 4-wave tiles */
 #define TMR_IO_WT_F32 64   /* dgrad only, TMR_MATH_F32 (the io bits fp32 math takes: this one and
                               TMR_IO_ENGINE): w is the
                               transposed fp32 copy Wt[Cin][R][S][Cout] (tmr_weight_oihw_to_crsk_x,
@@ -695,6 +699,11 @@ int tmr_lstm_status_or(const void* ws, int32_t* status, hipStream_t stream);
  * stream launches work -- the persistent LSTM next to a resident kernel (no reference
  * counterpart). */
 int tmr_test_hold_cus(int wgs, float ms, hipStream_t stream);
+/* Test instrumentation: the wave-specialised fused BN-backward dgrads this process has launched
+ * (gemm16_ws.h: the 1x1 stride-1 dgrads of the train step, round 6), so a test can tell which
+ * kernel served a call (its results equal the one-tile-per-workgroup launch's; no reference
+ * counterpart). */
+long tmr_dgrad_ws_launches(void);
 
 /* TimeConv (NLBlock_MutiConv6_3.py:43-79, generalised in L): the three Conv1d branches run
  * on tmr_conv2d_* (L as H, W=1); these kernels take the elementwise max of

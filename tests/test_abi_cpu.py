@@ -50,7 +50,7 @@ def test_retired_prologues_absent_from_default_library(built):
 def test_library_loads_and_reports_version(built):
     from tmrnet_amd import _lib
     h = _lib.lib()
-    assert h.tmr_abi_version() == 7
+    assert h.tmr_abi_version() == 8
     assert isinstance(h.tmr_last_error(), bytes)
 
 

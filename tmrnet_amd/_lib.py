@@ -169,6 +169,7 @@ SIGNATURES = {
     "tmr_lstm_sync_status": [P, ctypes.POINTER(ctypes.c_uint), P],
     "tmr_lstm_status_or": [P, P, P],
     "tmr_test_hold_cus": [I, F, P],
+    "tmr_dgrad_ws_launches": [],
     "tmr_timeconv_max5_fwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_timeconv_max5_bwd": [P, P, P, P, P, P, I, I, I, P],
     "tmr_lstm_cell_fwd": [P, I, P, P, P, I, P, P, I, I, P],
@@ -190,6 +191,7 @@ _RESTYPES = {
     "tmr_last_error": ctypes.c_char_p,
     "tmr_clear_error": None,
     "tmr_conv2d_wgrad_ws_bytes": SZ,
+    "tmr_dgrad_ws_launches": L,
     "tmr_resize_tmp_bytes": SZ,
     "tmr_bn_ws_bytes": SZ,
     "tmr_bn_parts_ws_bytes": SZ,

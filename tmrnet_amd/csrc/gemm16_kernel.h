@@ -1180,6 +1180,10 @@ void gemm16_par_kernel(const GemmPar p) {
   gemm16_body<MODE_DGRAD, BM, BN, WM, WN, 0, 1, F32, 0, 2, EPF>(a, t, 0);
 }
 
+}  // namespace tmrg
+#include "gemm16_ws.h"
+namespace tmrg {
+
 template <int MODE, int BM, int BN, int WM, int WN, int F32, int PRO = 0>
 int launch16_cfg(const GemmArgs& a, bool tapv, dim3 grid, hipStream_t st) {
   const dim3 blk(64 * WM * WN);
@@ -1307,6 +1311,10 @@ int launch_gemm16_t(const GemmArgs& a, int splits, hipStream_t st) {
   const int bk = f32 ? 32 : 64;
   const bool tapv = MODE != MODE_WGRAD && a.ntaps > 1 && ((1 << a.log2C) % bk) != 0;
   if (MODE == MODE_WGRAD && (c.bm < 64 || c.bn < 64)) return -1;
+  if constexpr (MODE == MODE_DGRAD) {   // the wave-specialised persistent form (gemm16_ws.h)
+    const int rc = launch_dgrad_ws<F32>(a, cfg, st);
+    if (rc >= 0) return rc;
+  }
 #if TMR_PROLOGUES
   // prologue variants (A/B build; fp32 and bf16): FWD X, DGRAD dY, WGRAD dY / dY + X / X
   if (a.pro) {

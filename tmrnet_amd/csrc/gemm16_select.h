@@ -176,6 +176,9 @@ struct GemmPar {
 // tiles of one class in a row (par_tile): a round of one XCD's workgroup slots (32 CUs x 2)
 constexpr int PAR_G = 64;
 
+// wave-specialised dgrad launches so far (gemm16_ws.h; tmr_dgrad_ws_launches)
+extern long g_dgrad_ws_launches;
+
 // one view x precision per translation unit (gemm16_<view>_<prec>.hip, explicit instantiations:
 // they compile in parallel)
 template <int F32>

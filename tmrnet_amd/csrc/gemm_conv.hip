@@ -179,7 +179,7 @@ static int conv_fwd_args(const tmr_conv_desc* d, const float* x, const float* w_
                          const float* bias, float* y, float beta, GemmArgs& a, bool& al) {
   TMR_CHECK_ARG(d, "tmr_conv2d_fwd: null descriptor");
   TMR_CHECK_ARG(d->math == TMR_MATH_F32 || d->math == TMR_MATH_BF16, "tmr_conv2d: bad math mode %d", d->math);
-  TMR_CHECK_ARG((d->io & ~(TMR_IO_ENGINE | TMR_IO_CLASSES)) == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
+  TMR_CHECK_ARG((d->io & ~(TMR_IO_ENGINE | TMR_IO_CLASSES | TMR_IO_TILES)) == 0 || d->math == TMR_MATH_BF16, "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int lc = ilog2_exact(d->c);
   TMR_CHECK_ARG(lc >= 2, "tmr_conv2d_fwd: stored input channels %d must be a power of two >= 4", d->c);
   a = GemmArgs{};
@@ -521,10 +521,10 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
   TMR_CHECK_ARG(!(d->io & TMR_IO_WT_BF16) || !(d->io & TMR_IO_W_BF16),
                 "tmr_conv2d_dgrad: TMR_IO_WT_BF16 and TMR_IO_W_BF16 are exclusive weight layouts");
   TMR_CHECK_ARG(!(d->io & TMR_IO_WT_F32) ||
-                    (d->math == TMR_MATH_F32 && (d->io & ~(TMR_IO_ENGINE | TMR_IO_CLASSES)) == TMR_IO_WT_F32),
+                    (d->math == TMR_MATH_F32 && (d->io & ~(TMR_IO_ENGINE | TMR_IO_CLASSES | TMR_IO_TILES)) == TMR_IO_WT_F32),
                 "tmr_conv2d_dgrad: TMR_IO_WT_F32 (fp32 transposed weights) needs TMR_MATH_F32 and "
                 "no bf16-stored operand");
-  TMR_CHECK_ARG((d->io & ~(TMR_IO_WT_F32 | TMR_IO_ENGINE | TMR_IO_CLASSES)) == 0 ||
+  TMR_CHECK_ARG((d->io & ~(TMR_IO_WT_F32 | TMR_IO_ENGINE | TMR_IO_CLASSES | TMR_IO_TILES)) == 0 ||
                     d->math == TMR_MATH_BF16,
                 "tmr_conv2d: bf16-stored operands (io %d) need TMR_MATH_BF16", d->io);
   const int st = d->stride;
@@ -584,6 +584,7 @@ static int conv_dgrad_impl(const tmr_conv_desc* d, const float* dy, const float*
         a.part_ld = fz->part_ld;
         a.Cold = fz->old;
         a.cold16 = fz->old16;
+        a.io_tiles = (d->io & TMR_IO_TILES) ? 1 : 0;
         fz->part += nmt * fz->part_ld;
         fz->nparts += nmt;
       }
@@ -644,6 +645,9 @@ static int dgrad_bnbwd_run(const tmr_conv_desc* d, const float* dy, const float*
   fz->part = part0;
   return 0;
 }
+
+long tmrg::g_dgrad_ws_launches = 0;
+TMR_API long tmr_dgrad_ws_launches(void) { return __atomic_load_n(&g_dgrad_ws_launches, __ATOMIC_RELAXED); }
 
 TMR_API int tmr_conv2d_dgrad_bnbwd_parts(const tmr_conv_desc* d) {
   if (!d || d->n <= 0) {

@@ -128,6 +128,9 @@ struct GemmArgs {
   // cold16: the old dx is bf16 (element offsets as C's).  Cold == nullptr: C.
   const void* Cold;
   int cold16;
+  // DGRAD: keep the one-tile-per-workgroup launch where the wave-specialised persistent dgrad
+  // (gemm16_ws.h) would serve the shape (TMR_IO_TILES; tests)
+  int io_tiles;
 };
 
 __device__ __forceinline__ float bf16_rne(float v) { return (float)(__bf16)v; }

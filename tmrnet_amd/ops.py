@@ -82,6 +82,7 @@ IO_WT32 = 64            # dgrad, fp32 math: w is the transposed fp32 copy (fp32 
 IO_G16 = 128            # fused BN-backward dgrad: g (dx) written bf16 (non-residual bf16 units)
 IO_ENGINE = 256         # the implicit-GEMM engine even where a direct kernel serves the geometry
 IO_CLASSES = 512        # strided dgrad: one launch per stride-parity class (tests' comparison form)
+IO_TILES = 1024         # fused dgrad: one tile per workgroup, not the wave-specialised kernel (tests)
 
 # test instrumentation (process-wide: autograd runs the backward of a CUDA graph on its own
 # device thread, which must see the same routing as the forward)
@@ -118,6 +119,22 @@ def dgrad_class_launches():
         yield
     finally:
         _CLASSES[0] = prev
+
+_TILES = [False]
+
+
+@contextlib.contextmanager
+def dgrad_tile_launches():
+    """Within the block a fused BN-backward dgrad runs one output tile per workgroup
+    (TMR_IO_TILES) also where the wave-specialised persistent kernel serves its shape (the 1x1
+    stride-1 dgrads, round 6).  Tests only."""
+    prev = _TILES[0]
+    _TILES[0] = True
+    try:
+        yield
+    finally:
+        _TILES[0] = prev
+
 
 BF16 = torch.bfloat16
 
@@ -170,6 +187,8 @@ def conv_desc(n, h, w, c, k, r, s, stride, pad, pad_w=None, x_ld=0, y_ld=0, math
         io |= IO_ENGINE
     if _CLASSES[0] and stride == 2:
         io |= IO_CLASSES
+    if _TILES[0] and r == 1 and s == 1 and stride == 1:
+        io |= IO_TILES
     return ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, pad_w, x_ld, y_ld, MATH[math],
                     MAX_FRAMES, io, groups if groups > 1 else 0)
 
