@@ -3,13 +3,13 @@ one-tile-per-workgroup engine launch it replaces (TMR_IO_TILES, ops.dgrad_tile_l
 
 The 1x1 stride-1 dgrads of the train step in their own forms: the Bottleneck conv1 dgrads adding
 into the residual-stream gradient (bf16: y, z, the old gradient in place and g bf16; fp32: ReLU
-bits, the fp32 old gradient) and the fp32 conv3 dgrads (mask from y, no beta).  Both launches
+bits, the fp32 old gradient), K <= 256 (bf16) / 128 (fp32).  Both launches
 run the same MFMA sequence per output element, so dx must match bit for bit; the partials too where
 the engine would use the 4-wave 128x128 tile (the same thread -> row map and summation order), and
 to summation-order tolerance where it would use the 8-wave one (fp32, N >= 512), both against
 float64 sums of the returned gradient.  Each case is sized past the kernel's 512-tile threshold
 with a partial last m-tile, and checks (tmr_dgrad_ws_launches) that the new kernel really ran.
-Reference: the backward of torchvision Bottleneck.conv1 / conv3 + bn + relu that
+Reference: the backward of torchvision Bottleneck.conv1 + the previous block's bn3 + relu that
 code/Training TMRNet/train_only_non-local_pretrained.py:724-725 (loss.backward) runs.
 """
 import numpy as np
@@ -40,9 +40,6 @@ CASES = [
     ("bf16", "res", 43, 14, 1024, 256),   # layer3: four k-tiles
     ("fp32", "res", 11, 56, 256, 64),     # fp32 (32-float k-tiles): two
     ("fp32", "res", 21, 28, 512, 128),    # four; the engine's 8-wave tile (partials reordered)
-    ("fp32", "res", 43, 14, 1024, 256),   # eight
-    ("fp32", "res", 85, 7, 2048, 512),    # sixteen, 16 n-tiles
-    ("fp32", "c3", 85, 28, 128, 512),     # conv3 dgrad: mask from y, no beta, sixteen k-tiles
 ]
 
 
@@ -58,24 +55,18 @@ def test_dgrad_ws_vs_tiles(dev, case):
     y = torch.randn(F, h, h, n, generator=g).to(dev).to(dt)
     ye = y.float()
     mean = ye.view(-1, n).mean(0)
-    kw = dict(math=prec, wt=True)
-    if kind == "res":
-        z = torch.relu(ye + torch.randn(F, h, h, n, generator=g).to(dev) * 0.5)
-        old = torch.randn(F, h, h, n, generator=g).to(dev).to(dt)
-        if bf:
-            zm, mask = z.to(dt), 1
-            kw.update(g16=True)
-        else:
-            zm, mask = _pack_bits(z > 0), 3
-        kw.update(z=zm, beta=1.0)
+    kw = dict(math=prec, wt=True, beta=1.0)
+    z = torch.relu(ye + torch.randn(F, h, h, n, generator=g).to(dev) * 0.5)
+    old = torch.randn(F, h, h, n, generator=g).to(dev).to(dt)
+    if bf:
+        zm, mask = z.to(dt), 1
+        kw.update(g16=True)
     else:
-        old = None
-        mask = 2
-        kw.update(scale=(torch.rand(n, generator=g) + 0.5).to(dev),
-                  shift=(torch.randn(n, generator=g) * 0.1).to(dev))
+        zm, mask = _pack_bits(z > 0), 3
+    kw.update(z=zm)
 
     def run(tiles):
-        o = old.clone() if old is not None else None
+        o = old.clone()
         if tiles:
             with ops.dgrad_tile_launches():
                 return ops.conv_dgrad_bnbwd(dy, wct, (h, h), 1, 0, y, mean, mask, out=o, **kw)
@@ -104,8 +95,8 @@ def test_dgrad_ws_vs_tiles(dev, case):
 
 
 def test_dgrad_ws_small_launch_stays_tiled(dev):
-    """Below the 512-tile threshold (or at a shape the kernel does not take: a 3x3, a stride)
-    the engine's own launch runs."""
+    """Below the 512-tile threshold the engine's own launch runs (as for the shapes the kernel
+    does not take: 3x3, strided, the MFMA-bound fp32 K >= 256 -- below)."""
     g = torch.Generator().manual_seed(5)
     F, h, n, k = 2, 14, 256, 64
     dy = torch.randn(F, h, h, k, generator=g).to(dev).to(torch.bfloat16)
@@ -116,5 +107,21 @@ def test_dgrad_ws_small_launch_stays_tiled(dev):
     n0 = _launches()
     ops.conv_dgrad_bnbwd(dy, wct, (h, h), 1, 0, y, y.float().view(-1, n).mean(0), 1, z=z,
                          out=old, beta=1.0, math="bf16", wt=True, g16=True)
+    torch.cuda.synchronize()
+    assert _launches() == n0
+
+
+def test_dgrad_ws_mfma_bound_stays_tiled(dev):
+    """fp32 K = 256 (14x14 1024<-256, 8 k-tiles): MFMA-bound, left to the engine's tiles."""
+    g = torch.Generator().manual_seed(6)
+    F, h, n, k = 43, 14, 1024, 256
+    dy = torch.randn(F, h, h, k, generator=g).to(dev)
+    wct = ops.weight_to_crsk((torch.randn(k, n, 1, 1, generator=g) / 16).to(dev), bf16=False)
+    y = torch.randn(F, h, h, n, generator=g).to(dev)
+    bits = _pack_bits(y > 0)
+    old = torch.randn(F, h, h, n, generator=g).to(dev)
+    n0 = _launches()
+    ops.conv_dgrad_bnbwd(dy, wct, (h, h), 1, 0, y, y.view(-1, n).mean(0), 3, z=bits, out=old,
+                         beta=1.0, math="fp32", wt=True)
     torch.cuda.synchronize()
     assert _launches() == n0

@@ -1,31 +1,36 @@
-// Wave-specialised fused BN-backward dgrad (round 6): the 1x1 stride-1 dgrads of the train step --
-// the Bottleneck conv1 dgrads that add into the residual-stream gradient and, in fp32, the conv3
-// dgrads -- as a persistent kernel whose workgroup runs the GEMM of output tile i+1 on four
-// "producer" waves while four "consumer" waves drain tile i's fused BatchNorm-backward epilogue.
+// Wave-specialised fused BN-backward dgrad (round 6): the 1x1 stride-1 dgrads of the train step
+// whose fused epilogue outweighs their GEMM -- the Bottleneck conv1 dgrads that add into the
+// residual-stream gradient, K <= 256 (bf16) / 128 (fp32) -- as a persistent kernel whose
+// workgroups run the GEMM of output tile i+1 on four "producer" waves while four "consumer" waves
+// drain tile i's fused BatchNorm-backward epilogue.
 //
 // Why: in gemm16_kernel a workgroup runs its tile's MFMA phase and then its epilogue, one after
 // the other.  The stall counters of the bf16 dgrad (profiles/r6/r6b/pmc_stall_c5/) put 56% of its
 // wave cycles on s_waitcnt / barriers with MFMA busy 12%: the epilogue's global loads are the
-// critical path and the MFMA phase does not overlap them; for the fp32 dgrads whose MFMA phase is
-// as long as the epilogue (14x14 1024<-256: 0.42 + 0.25 ms) the two add up.
+// critical path and the MFMA phase does not overlap them.
 //
-// Layout of one workgroup (512 threads, one per CU: 146 KB of LDS):
-//   * waves 0-3, the producers: the 128x128 tile as 2x2 waves of 64x64 (gemm16_kernel's 4-wave
-//     128x128 tile: the same LDS-DMA k-tile images, swizzle, fragment reads and MFMA order, so dx is
-//     bit-identical to it), two k-tile stages; after the last k-tile of tile i they issue the first
-//     k-tile of tile i+1, then write the accumulators to the staging buffer;
+// Layout of one workgroup (512 threads, one per CU, all 160 KB of LDS):
+//   * waves 0-3, the producers (one per SIMD: waves w and w + 4 share one, scripts/probe/
+//     simd_map.hip): the 128x128 tile as 2x2 waves of 64x64 -- gemm16_kernel's 4-wave 128x128
+//     tile: the same LDS-DMA k-tile images, swizzle, fragment reads and MFMA order, so dx is
+//     bit-identical to it -- over a ring of three k-tile stages that runs on across tiles; after
+//     the tile's last k-tile they write the accumulators to the staging tile;
 //   * waves 4-7, the consumers: the epilogue of LdsBnbwd with the same thread -> (row, 8 columns)
 //     map (rows rsub + 16 j, j = 0..7) and the same summation order of the partials, so bn_part is
 //     bit-identical to the 4-wave tile's too; each thread holds all 8 of its rows' operands in
-//     flight and re-issues every slot for tile i+1 as soon as it has consumed tile i's row.
+//     flight and re-issues every slot for tile i+1 as soon as it has consumed tile i's row;
 //   * every wave runs the same barrier sequence (each role its own loop, wave-uniform): per tile
 //     nk k-tile barriers (the producers' stage hand-off; the consumers process 8 / NKC rows after
-//     each group of nk / NKC of them), B1 (staging free: the consumers are done with tile i-1 and
-//     its partials are in `red`), B2 (staging holds tile i); a last B1 for the final tile.
+//     each group of nk / NKC of them), B1 (the producers are done with the tile's k-tiles, the
+//     consumers with the staging tile), B2 (the staging tile holds the next tile, the consumers'
+//     column sums are in the stage just freed); B1, B2 once more for the last tile.
 //   * the work: XCD x (blockIdx & 7) owns a contiguous range of m-tiles; its 32 workgroups split
 //     into N/128 n-lanes x 32/(N/128) m-lanes, so each workgroup keeps one n-tile (coefficients
 //     loaded once) and the n-tiles of one m-tile -- which gather the same dy rows -- run side by
 //     side on one L2.
+// Measured (profiles/r6/dgrad_ws/): bf16 28x28 512<-128 0.523 -> 0.469 ms, 14x14 1024<-256 0.297
+// -> 0.239 ms (4.6-4.9 TB/s of the step's own bytes); the MFMA-bound dgrads (fp32 K >= 256, the
+// conv3 dgrads) stay on the engine's tiles: there the producers alone reach the same ~100 TF.
 #pragma once
 
 namespace tmrg {
@@ -34,6 +39,11 @@ namespace tmrg {
 #define TMR_DGRAD_WS 1
 #endif
 constexpr int WS_NWG = 256;   // workgroups: one per CU (8 XCDs x 32)
+// timing experiments only (wrong results): 1 -- the consumers keep the barrier sequence but do no
+// epilogue work; 2 -- the producers keep their loads and barriers but issue no MFMA
+#ifndef TMR_WS_EXP
+#define TMR_WS_EXP 0
+#endif
 
 // The epilogue variant is fixed at compile time -- ReLU mask MSK (1: z > 0, 2: y*scale+shift >
 // 0, 3: bits), the beta operand BETA -- so every row issues the same loads and the compiler can
@@ -48,15 +58,22 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
   constexpr int TM = 2, TN = 2;
   constexpr int ABYTES = BM * 128, STAGE = 2 * ABYTES;   // A and B images of one k-tile
   constexpr int NIA = ABYTES / (1024 * NW);                // LDS-DMA pieces per wave per image
-  constexpr int LDC = BN + 4;                              // padded fp32 row of the staged tile
+  constexpr int NST = 3;                                   // k-tile stages
+  constexpr int LDC = BN;                                  // fp32 row of the staged tile
   constexpr int STG = BM * LDC * 4;
   constexpr int CG = BN / 8, RPP = 256 / CG, NR = BM / RPP;   // 16 column groups, 16 rows / pass
   constexpr int R = NR / NKC;                               // consumer rows per group
   static_assert(NR == 8 && R * NKC == NR, "consumer row groups");
+  static_assert(RPP * BN * 8 <= STAGE, "the partial sums fit a stage");
   using Frag = typename std::conditional<F32 != 0, f32x4_t, bf16x8>::type;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE + STG + RPP * BN * 8];
-  float* const stg = reinterpret_cast<float*>(smem + 2 * STAGE);
-  float* const red = reinterpret_cast<float*>(smem + 2 * STAGE + STG);   // [RPP][BN][2]
+  // 3 x 32 KB stages + the 64 KB staging tile: the whole 160 KB.  The staged tile is unpadded, its
+  // 32-column halves swapped on rows with bit 2 set (the two row sets of one accumulator store hit
+  // disjoint banks); the consumers' column sums go to the stage whose k-tile was the tile's last
+  // (free from the producers' last MFMAs until they issue into it again after the next k-tile
+  // barrier).
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NST * STAGE + STG];
+  float* const stg = reinterpret_cast<float*>(smem + NST * STAGE);
+  auto scol = [](int row, int c) { return c ^ (((row >> 2) & 1) << 5); };
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -128,6 +145,10 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     auto mfmas = [&](const Frag (&av)[TM], const Frag (&bv)[TN]) {
+      if constexpr (TMR_WS_EXP == 2) {
+        asm volatile("" ::"v"(av[0]), "v"(bv[0]), "v"(av[TM - 1]), "v"(bv[TN - 1]));
+        return;
+      }
       __builtin_amdgcn_s_setprio(1);
       if constexpr (F32) {
 #pragma unroll
@@ -146,19 +167,28 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
       }
       __builtin_amdgcn_s_setprio(0);
     };
+    // global k-tile G of this workgroup = k-tile G % nk of its tile G / nk, in stage G % NST
+    const int ng = ntl * nk;
+    auto stage_g = [&](int G) {
+      const int ti = G / nk;
+      stage((mlo + ms + ti * mstr) * BM, G - ti * nk, G % NST);
+    };
     if (ntl > 0) {
-      stage((mlo + ms) * BM, 0, 0);
-      int g = 0;   // k-tiles consumed so far (stage g & 1)
+      stage_g(0);
+      if (ng > 1) stage_g(1);
+      int g = 0;   // k-tiles consumed so far
       for (int i = 0; i < ntl; ++i) {
-        const int m0 = (mlo + ms + i * mstr) * BM;
         for (int kt = 0; kt < nk; ++kt) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();   // every producer's pieces of this k-tile landed; the other stage free
-          const int buf = g & 1;
+          // this wave's pieces of k-tile g landed (those of g + 1, issued after them, may not)
+          if (g + 1 < ng)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIA) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();   // every producer's pieces of k-tile g landed; stage (g + 2) % 3 free
+          const int buf = g % NST;
           Frag a0[TM], b0[TN], a1[TM], b1[TN];
           frags(buf, 0, a0, b0);
-          if (kt + 1 < nk) stage(m0, kt + 1, buf ^ 1);
-          else if (i + 1 < ntl) stage(m0 + mstr * BM, 0, buf ^ 1);
+          if (g + 2 < ng) stage_g(g + 2);
           frags(buf, 1, a1, b1);
           mfmas(a0, b0);
           frags(buf, 2, a0, b0);
@@ -176,13 +206,14 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = wm * (BM / 2) + 32 * i2 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              stg[row * LDC + wn * (BN / WN) + 32 * j + l31] = acc[i2][j][r];
+              stg[row * LDC + scol(row, wn * (BN / WN) + 32 * j + l31)] = acc[i2][j][r];
               acc[i2][j][r] = 0.f;
             }
         __syncthreads();   // B2: the staging buffer holds tile i
       }
     }
-    __syncthreads();   // B1 of the last tile's epilogue
+    __syncthreads();   // B1 and
+    __syncthreads();   // B2 of the last tile's epilogue
     return;
   }
 
@@ -287,8 +318,9 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
       for (int e = 0; e < 8; ++e) old[e] = 0.f;
     }
     const int rr = rsub + j * RPP;
-    const float4 a0 = *reinterpret_cast<const float4*>(stg + rr * LDC + 8 * cg);
-    const float4 a1 = *reinterpret_cast<const float4*>(stg + rr * LDC + 8 * cg + 4);
+    const float* srow = stg + rr * LDC + scol(rr, 8 * cg);
+    const float4 a0 = *reinterpret_cast<const float4*>(srow);
+    const float4 a1 = *reinterpret_cast<const float4*>(srow + 4);
     const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     float v[8];
 #pragma unroll
@@ -319,9 +351,12 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
       __builtin_amdgcn_raw_buffer_store_b128(q1, rC, x.ok ? so + 16u : OOB, 0, 0);
     }
   };
-  // the tile's column sums: this thread's 8 columns -> red (before B1); the sums over the RPP
-  // row slots -> bn_part row of m-tile mi (after B1)
-  auto put_red = [&]() {
+  // the tile's column sums: this thread's 8 columns -> red (between B1 and B2), in the stage of
+  // k-tile `gl` (the tile's last); the sums over the RPP row slots -> bn_part row of m-tile mi
+  // (after B2)
+  float* red = nullptr;
+  auto put_red = [&](int gl) {
+    red = reinterpret_cast<float*>(smem + (gl % NST) * STAGE);   // [RPP][BN][2]
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       red[(rsub * BN + 8 * cg + e) * 2] = cs[e];
@@ -360,6 +395,7 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int j = jj * R + r;
+          if constexpr (TMR_WS_EXP == 1) continue;
           consume(pf[j], j);
           // (the scheduler would hoist the next row's loads over this row's use: both sets live)
           __builtin_amdgcn_sched_barrier(0);
@@ -367,13 +403,14 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      put_red();
       __syncthreads();   // B1
+      put_red(more ? (i + 1) * nk - 1 : i * nk - 1);   // (the k-tile the producers just finished)
+      __syncthreads();   // B2: tile i staged (the last tile: the partials written)
       finalize(mlo + ms + (i - 1) * mstr);
-      if (more) __syncthreads();   // B2: tile i staged
     }
   } else {
     __syncthreads();   // the producers' last B1
+    __syncthreads();   // and B2
   }
 
 }
@@ -381,12 +418,10 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
 // The launch for a fused BN-backward dgrad, when its shape qualifies (else -1, nothing launched):
 // 1x1, stride 1, no padding, one tap (dx row = dy row); the tile rules' 128-row tiles (so the
 // partial rows are the ones the host counted); N a multiple of 128 with N / 128 dividing the 32
-// workgroups of an XCD; whole k-tiles, a power-of-two count up to 4 (bf16: one k-tile's MFMAs are
-// short against the LDS-DMA latency, so a longer reduction would leave the producers latency-bound)
-// or any multiple of 8 (fp32: MFMA-bound per k-tile); enough tiles for 256 persistent workgroups;
-// the train step's epilogue variants: bf16 -- the residual conv1 dgrad (mask from z, beta 1 on a
-// bf16 old gradient, g stored bf16); fp32 -- the residual conv1 dgrad (mask bits, beta 1) and the
-// conv3 dgrad (mask from y, no beta).
+// workgroups of an XCD; whole k-tiles, 1, 2 or 4 of them (bf16 K <= 256, fp32 K <= 128: the
+// epilogue-bound dgrads -- where the MFMA phase dominates, the engine's tiles do as well); enough
+// tiles for 256 persistent workgroups; the train step's residual conv1 dgrad: bf16 -- mask from z,
+// beta 1 on a bf16 old gradient, g stored bf16; fp32 -- mask bits, beta 1 on the fp32 old gradient.
 // `a.io_tiles` (TMR_IO_TILES) keeps the one-tile-per-workgroup launch (the tests' comparison).
 template <int F32>
 int launch_dgrad_ws(const GemmArgs& a, int cfg, hipStream_t st) {
@@ -411,14 +446,12 @@ int launch_dgrad_ws(const GemmArgs& a, int cfg, hipStream_t st) {
     return 0;
   };
   if constexpr (F32) {
-    if (a.bn16 || a.g16 || a.cold16) return -1;
-    if (a.bn_mask == 3 && beta1) {
-      if (nk == 2) return go(dgrad_ws_kernel<1, 2, 3, 1>);
-      if (nk == 4) return go(dgrad_ws_kernel<1, 4, 3, 1>);
-      if (nk % 8 == 0) return go(dgrad_ws_kernel<1, 8, 3, 1>);
-    } else if (a.bn_mask == 2 && a.beta == 0.f && nk % 8 == 0) {
-      return go(dgrad_ws_kernel<1, 8, 2, 0>);
-    }
+    // (K >= 256 and the conv3 dgrads are MFMA-bound: the four producer waves alone reach the
+    // engine's ~100 TF and the epilogue traffic beside them costs 20-35%, so they stay on the
+    // engine's tiles; profiles/r6/dgrad_ws/README.md)
+    if (a.bn16 || a.g16 || a.cold16 || a.bn_mask != 3 || !beta1) return -1;
+    if (nk == 2) return go(dgrad_ws_kernel<1, 2, 3, 1>);
+    if (nk == 4) return go(dgrad_ws_kernel<1, 4, 3, 1>);
   } else {
     if (!a.bn16 || !a.g16 || a.bn_mask != 1 || !beta1 || !(a.Cold == nullptr || a.cold16))
       return -1;
