@@ -246,7 +246,9 @@ def main():
             a[0] += 1; a[1] += f; a[2] += e0.elapsed_time(e1)
         peak = MFMA_F32_PEAK_TF if args.precision == "fp32" else MFMA_BF16_PEAK_TF
         roof = {"bound": "mfma",
-                "kernel": ("gemm16_kernel (LDS-DMA implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA)%s"
+                "kernel": ("gemm16_kernel (LDS-DMA implicit-GEMM conv fwd/dgrad/wgrad, %s MFMA; "
+                           "gemm16_par_kernel: strided dgrads; dgrad_ws_kernel: the 1x1 residual "
+                           "dgrads)%s"
                            % ("f32" if args.precision == "fp32" else "bf16 operands, f32 acc",
                               " + stem_fwd_k / stem_wgrad_k (direct fp32 7x7 stem)"
                               if args.precision == "fp32" else "")),
@@ -428,11 +430,13 @@ def load_traffic(model, precision, seq, lfb):
         d = json.load(f)
     fams = d.get("families", {})
     # the conv family: gemm_kernel / tmrg::gemm_kernel (register-staged), tmrg::gemm16_kernel
-    # (LDS-DMA engine), the direct stems (stem_fwd_k / stem_wgrad_k, round 3; stem16_*, round 4),
+    # (LDS-DMA engine) with its one-launch strided dgrads (gemm16_par_kernel, round 5) and the
+    # wave-specialised 1x1 dgrads (dgrad_ws_kernel, round 6), the direct stems (stem_fwd_k / stem_wgrad_k, round 3; stem16_*, round 4),
     # the direct 3x3 kernels (d3_k, d3w_k, d3s_k, d3sw_k, round 4) and the split-K weight-gradient
     # reductions
     conv = [k for k in fams
-            if any(t in k for t in ("gemm_kernel", "gemm16_kernel", "wgrad_reduce", "stem_fwd_k",
+            if any(t in k for t in ("gemm_kernel", "gemm16_kernel", "gemm16_par_kernel",
+                                    "dgrad_ws_kernel", "wgrad_reduce", "stem_fwd_k",
                                     "stem_wgrad_k", "stem16_fwd_k", "stem16_wgrad_k", "d3_k",
                                     "d3w_k", "d3s_k", "d3sw_k"))]
     if not conv:
