@@ -12,6 +12,8 @@ with a partial last m-tile, and checks (tmr_dgrad_ws_launches) that the new kern
 Reference: the backward of torchvision Bottleneck.conv1 + the previous block's bn3 + relu that
 code/Training TMRNet/train_only_non-local_pretrained.py:724-725 (loss.backward) runs.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -111,6 +113,8 @@ def test_dgrad_ws_small_launch_stays_tiled(dev):
     assert _launches() == n0
 
 
+@pytest.mark.skipif(os.environ.get("TMR_DGRAD_WS_MFMA", "0") != "0",
+                    reason="TMR_DGRAD_WS_MFMA widens the kernel's scope to these shapes")
 def test_dgrad_ws_mfma_bound_stays_tiled(dev):
     """fp32 K = 256 (14x14 1024<-256, 8 k-tiles): MFMA-bound, left to the engine's tiles."""
     g = torch.Generator().manual_seed(6)
@@ -125,3 +129,18 @@ def test_dgrad_ws_mfma_bound_stays_tiled(dev):
                          beta=1.0, math="fp32", wt=True)
     torch.cuda.synchronize()
     assert _launches() == n0
+
+
+WIDE = [
+    ("fp32", "res", 43, 14, 1024, 256),   # eight k-tiles
+    ("fp32", "res", 85, 7, 2048, 512),    # sixteen, 16 n-tiles
+]
+
+
+@pytest.mark.skipif(os.environ.get("TMR_DGRAD_WS_MFMA", "0") == "0",
+                    reason="the MFMA-bound fp32 shapes run on the engine's tiles by default")
+@pytest.mark.parametrize("case", WIDE, ids=lambda c: "%s-%dx%d-%d<-%d" % (c[0], c[3], c[3], c[4], c[5]))
+def test_dgrad_ws_wide_scope(dev, case):
+    """TMR_DGRAD_WS_MFMA=1 (A/B of the wider scope): the fp32 K >= 256 residual dgrads on the
+    wave-specialised kernel, against the one-tile launch."""
+    test_dgrad_ws_vs_tiles(dev, case)

@@ -853,7 +853,7 @@ def _pack_bits(m):
     return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
 
 
-@pytest.mark.parametrize("rows,c", [(1000, 256), (77, 64), (3, 8)])
+@pytest.mark.parametrize("rows,c", [(1000, 256), (77, 64), (3, 8), (101, 12), (5001, 512)])
 def test_bn_apply_relu_bits(dev, rows, c):
     """bn_apply_bits / bn_apply2_bits: z bit-identical to bn_apply / bn_apply2 (ReLU) and the
     bits are exactly (z > 0) packed 32 per word (ragged tails included)."""
@@ -873,6 +873,18 @@ def test_bn_apply_relu_bits(dev, rows, c):
     z2r = ops.bn_apply2(y, sc, sh, yr, rs, rf, True)
     torch.cuda.synchronize()
     assert torch.equal(z2, z2r) and torch.equal(bits2.cpu(), _pack_bits((z2r > 0).cpu()))
+    # the 8-wide forms (round 6; c % 8 == 0, 16-B aligned) against the 4-wide ones, which the
+    # library takes for operands 8 bytes off a 16-B boundary: identical z and bits
+    from tests.test_stem_pool8_gpu import _off8
+    for resid in (res, None):
+        z8, b8 = ops.bn_apply_bits(y, sc, sh, resid)
+        z4, b4 = ops.bn_apply_bits(_off8(y), sc, sh, _off8(resid) if resid is not None else None)
+        torch.cuda.synchronize()
+        assert torch.equal(z8, z4) and torch.equal(b8, b4)
+    z8, b8 = ops.bn_apply2_bits(y, sc, sh, yr, rs, rf)
+    z4, b4 = ops.bn_apply2_bits(_off8(y), sc, sh, _off8(yr), rs, rf)
+    torch.cuda.synchronize()
+    assert torch.equal(z8, z4) and torch.equal(b8, b4)
     with pytest.raises(RuntimeError):
         ops.conv_dgrad_bnbwd(torch.randn(1, 4, 4, 64, device=dev),
                              ops.weight_to_krsc(torch.randn(64, 64, 1, 1, device=dev)), (4, 4), 1, 0,

@@ -1044,6 +1044,87 @@ __global__ __launch_bounds__(NT) void stem_bwd_apply8q(const PoolGeo pg, int h, 
   }
 }
 
+// The forward BN + ReLU with the ReLU mask as bits (bn_apply_bits_k's fp32 forms: RES the residual
+// add, yr the downsample branch's BN on the fly), 8 elements per thread and two groups in flight
+// per thread, each group's 8 mask bits one byte of its word (round 6: the 4-wide form moved its
+// 12 B per element at 4.8 TB/s, the 8-wide BN passes at 5.6-5.9).  Same arithmetic per element:
+// z and the bits identical to bn_apply_bits_k's.  The loop runs whole waves (the bit words are
+// gathered across 4 lanes).
+#ifndef TMR_BN_BITS8
+#define TMR_BN_BITS8 1   // 0: the 4-wide form only (A/B build)
+#endif
+template <bool RES>
+__global__ __launch_bounds__(NT) void bn_apply_bits8_k(const float* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ res,
+                                                       const float* __restrict__ yr,
+                                                       const float* __restrict__ rscale,
+                                                       const float* __restrict__ rshift,
+                                                       float* __restrict__ z,
+                                                       uint32_t* __restrict__ bits, long n8, int c8) {
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * NT;
+  // one group: z of elements 8i .. 8i + 7 and their mask byte
+  auto apply = [&](long i, const float (&yv)[8], const float (&rv)[8]) -> uint32_t {
+    const int cc = chan_of(i, c8) * 8;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 sc = *reinterpret_cast<const float4*>(scale + cc + 4 * h);
+      const float4 sf = *reinterpret_cast<const float4*>(shift + cc + 4 * h);
+      const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, f4[4] = {sf.x, sf.y, sf.z, sf.w};
+      if (yr) {
+        const float4 rs = *reinterpret_cast<const float4*>(rscale + cc + 4 * h);
+        const float4 rf = *reinterpret_cast<const float4*>(rshift + cc + 4 * h);
+        const float r4[4] = {rs.x, rs.y, rs.z, rs.w}, q4[4] = {rf.x, rf.y, rf.z, rf.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[4 * h + e] = fmaf(yv[4 * h + e], s4[e], f4[e]) + fmaf(rv[4 * h + e], r4[e], q4[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[4 * h + e] = fmaf(yv[4 * h + e], s4[e], f4[e]);
+          if (RES) v[4 * h + e] += rv[4 * h + e];
+        }
+      }
+    }
+    uint32_t b = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = fmaxf(v[e], 0.f);
+      b |= (uint32_t)(v[e] > 0.f) << e;
+    }
+    st8(z, i, v);
+    return b;
+  };
+  // the word of 4 lanes' bytes (group indices 4k .. 4k + 3: base is a multiple of 64)
+  auto put = [&](uint32_t byte, long i, bool ok) {
+    uint32_t w = byte << (8 * (lane & 3));
+    w |= (uint32_t)__shfl_xor((int)w, 1, 64);
+    w |= (uint32_t)__shfl_xor((int)w, 2, 64);
+    if ((lane & 3) == 0 && ok) bits[i >> 2] = w;
+  };
+  const float* rsrc = RES ? res : yr;
+  for (long base = blockIdx.x * (long)NT + (threadIdx.x & ~63); base < n8; base += 2 * stride) {
+    const long i = base + lane, j = i + stride;
+    const bool oi = i < n8, oj = j < n8;
+    float ya[8], ra[8], yb[8], rb[8];
+    if (oi) {
+      ld8(y, i, ya);
+      if (rsrc) ld8(rsrc, i, ra);
+    }
+    if (oj) {
+      ld8(y, j, yb);
+      if (rsrc) ld8(rsrc, j, rb);
+    }
+    const uint32_t bi = oi ? apply(i, ya, ra) : 0u;
+    const uint32_t bj = oj ? apply(j, yb, rb) : 0u;
+    put(bi, i, oi);
+    put(bj, j, oj);
+  }
+}
+
 int ew_blocks(long n4) {
   long b = (n4 + NT - 1) / NT;
   if (b > 2048 * 4) b = 2048 * 4;
@@ -1195,7 +1276,14 @@ TMR_API int tmr_bn_apply_bits(const float* y, const float* scale, const float* s
                 "tmr_bn_apply_bits: null operand or channels %d not a multiple of 4", c);
   const long n4 = (long)rows * c / 4;
   if (n4 == 0) return 0;
-  if (residual)
+  if (TMR_BN_BITS8 && c % 8 == 0 && (((uintptr_t)y | (uintptr_t)residual | (uintptr_t)z) & 15) == 0) {
+    if (residual)
+      hipLaunchKernelGGL((bn_apply_bits8_k<true>), dim3(ew_blocks(n4 / 2)), dim3(NT), 0, stream, y,
+                         scale, shift, residual, nullptr, nullptr, nullptr, z, bits, n4 / 2, c / 8);
+    else
+      hipLaunchKernelGGL((bn_apply_bits8_k<false>), dim3(ew_blocks(n4 / 2)), dim3(NT), 0, stream, y,
+                         scale, shift, nullptr, nullptr, nullptr, nullptr, z, bits, n4 / 2, c / 8);
+  } else if (residual)
     hipLaunchKernelGGL((bn_apply_bits_k<true, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
                        shift, residual, nullptr, nullptr, nullptr, z, bits, n4, c / 4);
   else
@@ -1213,8 +1301,12 @@ TMR_API int tmr_bn_apply2_bits(const float* y, const float* scale, const float* 
   TMR_CHECK_ARG(yr != z, "tmr_bn_apply2_bits: the branch input must not alias z");
   const long n4 = (long)rows * c / 4;
   if (n4 == 0) return 0;
-  hipLaunchKernelGGL((bn_apply_bits_k<false, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
-                     shift, nullptr, yr, rscale, rshift, z, bits, n4, c / 4);
+  if (TMR_BN_BITS8 && c % 8 == 0 && (((uintptr_t)y | (uintptr_t)yr | (uintptr_t)z) & 15) == 0)
+    hipLaunchKernelGGL((bn_apply_bits8_k<false>), dim3(ew_blocks(n4 / 2)), dim3(NT), 0, stream, y,
+                       scale, shift, nullptr, yr, rscale, rshift, z, bits, n4 / 2, c / 8);
+  else
+    hipLaunchKernelGGL((bn_apply_bits_k<false, float>), dim3(ew_blocks(n4)), dim3(NT), 0, stream, y, scale,
+                       shift, nullptr, yr, rscale, rshift, z, bits, n4, c / 4);
   TMR_CHECK_LAUNCH("bn_apply2_bits");
   return 0;
 }

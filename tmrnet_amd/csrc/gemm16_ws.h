@@ -45,6 +45,19 @@ constexpr int WS_NWG = 256;   // workgroups: one per CU (8 XCDs x 32)
 #define TMR_WS_EXP 0
 #endif
 
+// The workgroup barrier of this kernel: LDS writes retired, then a raw s_barrier -- never
+// __syncthreads(), whose fence emits vmcnt(0) while an LDS-DMA is in flight (an LDS-DMA is a
+// pending LDS write on the VM counter: cdna_hip_programming.md, "Pipelining across barriers") and
+// would drain the producers' next k-tile at every k-tile barrier.  The empty asm statements keep
+// the compiler from moving memory accesses across it (the intrinsic itself is not a memory
+// barrier to LLVM).  LDS-DMA data is ordered for another wave's ds_read by the issuing wave's
+// counted vmcnt before this barrier.
+__device__ __forceinline__ void ws_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // The epilogue variant is fixed at compile time -- ReLU mask MSK (1: z > 0, 2: y*scale+shift >
 // 0, 3: bits), the beta operand BETA -- so every row issues the same loads and the compiler can
 // count vmcnt exactly (with loads behind run-time flags it waits for all of them).  bf16 (EpiForm
@@ -106,22 +119,21 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
       boff[q] = (uint32_t)(n0 + prow[q]) * (uint32_t)a.ldbt * ES + (uint32_t)pch[q] * ES;
     }
     // k-tile kt of the tile at row m0 -> LDS stage buf (A: dy rows, B: Wt rows of the n-tile)
-    auto stage = [&](int m0, int kt, int buf) {
+    // piece q of the A and of the B image
+    auto stage_q = [&](int m0, int kt, int buf, int q) {
       const int kb = kt * BK;
       unsigned char* As = smem + buf * STAGE;
       unsigned char* Bs = As + ABYTES;
+      const int m = m0 + prow[q];
+      const bool ok = m < a.M && kb + pch[q] < a.K;
+      const uint32_t off = (uint32_t)m * (uint32_t)a.lds * ES + (uint32_t)(kb + pch[q]) * ES;
+      glds16(rA, As + 1024 * (wave + NW * q), ok ? off : OOB);
+      const bool okb = kb + pch[q] < a.K;
+      glds16(rB, Bs + 1024 * (wave + NW * q), okb ? boff[q] + (uint32_t)kb * ES : OOB);
+    };
+    auto stage = [&](int m0, int kt, int buf) {
 #pragma unroll
-      for (int q = 0; q < NIA; ++q) {
-        const int m = m0 + prow[q];
-        const bool ok = m < a.M && kb + pch[q] < a.K;
-        const uint32_t off = (uint32_t)m * (uint32_t)a.lds * ES + (uint32_t)(kb + pch[q]) * ES;
-        glds16(rA, As + 1024 * (wave + NW * q), ok ? off : OOB);
-      }
-#pragma unroll
-      for (int q = 0; q < NIA; ++q) {
-        const bool ok = kb + pch[q] < a.K;
-        glds16(rB, Bs + 1024 * (wave + NW * q), ok ? boff[q] + (uint32_t)kb * ES : OOB);
-      }
+      for (int q = 0; q < NIA; ++q) stage_q(m0, kt, buf, q);
     };
     const int kx = (l31 >> 1) & 7;
     const int arow0 = wm * (BM / 2) + l31;
@@ -173,6 +185,7 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
       const int ti = G / nk;
       stage((mlo + ms + ti * mstr) * BM, G - ti * nk, G % NST);
     };
+
     if (ntl > 0) {
       stage_g(0);
       if (ng > 1) stage_g(1);
@@ -184,10 +197,11 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIA) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();   // every producer's pieces of k-tile g landed; stage (g + 2) % 3 free
+          ws_barrier();   // every producer's pieces of k-tile g landed; stage (g + 2) % 3 free
           const int buf = g % NST;
           Frag a0[TM], b0[TN], a1[TM], b1[TN];
           frags(buf, 0, a0, b0);
+          // (spreading these pieces over the four k-steps measured no faster, round 6)
           if (g + 2 < ng) stage_g(g + 2);
           frags(buf, 1, a1, b1);
           mfmas(a0, b0);
@@ -198,7 +212,7 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
           mfmas(a1, b1);
           ++g;
         }
-        __syncthreads();   // B1: the consumers are done with the staging buffer
+        ws_barrier();   // B1: the consumers are done with the staging buffer
 #pragma unroll
         for (int i2 = 0; i2 < TM; ++i2)
 #pragma unroll
@@ -209,11 +223,11 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
               stg[row * LDC + scol(row, wn * (BN / WN) + 32 * j + l31)] = acc[i2][j][r];
               acc[i2][j][r] = 0.f;
             }
-        __syncthreads();   // B2: the staging buffer holds tile i
+        ws_barrier();   // B2: the staging buffer holds tile i
       }
     }
-    __syncthreads();   // B1 and
-    __syncthreads();   // B2 of the last tile's epilogue
+    ws_barrier();   // B1 and
+    ws_barrier();   // B2 of the last tile's epilogue
     return;
   }
 
@@ -379,9 +393,9 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
     // tile 0: its rows' operands go in flight while the producers run its GEMM
 #pragma unroll
     for (int j = 0; j < NR; ++j) issue((mlo + ms) * BM, j, pf[j], true);
-    for (int kt = 0; kt < nk; ++kt) __syncthreads();
-    __syncthreads();   // B1
-    __syncthreads();   // B2: tile 0 staged
+    for (int kt = 0; kt < nk; ++kt) ws_barrier();
+    ws_barrier();   // B1
+    ws_barrier();   // B2: tile 0 staged
     // iteration i: tile i - 1 is staged; the loads of tile i go out as its rows are consumed
     // (i == ntl: the last tile, its GEMM barriers absent and its loads out of range -- the same
     // instructions, so the loop body and its vmcnt counts stay uniform)
@@ -391,7 +405,7 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
       const int kg = more ? kpg : 0;
 #pragma unroll
       for (int jj = 0; jj < NKC; ++jj) {
-        for (int u = 0; u < kg; ++u) __syncthreads();
+        for (int u = 0; u < kg; ++u) ws_barrier();
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int j = jj * R + r;
@@ -403,14 +417,14 @@ __global__ __launch_bounds__(512) void dgrad_ws_kernel(const GemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      __syncthreads();   // B1
+      ws_barrier();   // B1
       put_red(more ? (i + 1) * nk - 1 : i * nk - 1);   // (the k-tile the producers just finished)
-      __syncthreads();   // B2: tile i staged (the last tile: the partials written)
+      ws_barrier();   // B2: tile i staged (the last tile: the partials written)
       finalize(mlo + ms + (i - 1) * mstr);
     }
   } else {
-    __syncthreads();   // the producers' last B1
-    __syncthreads();   // and B2
+    ws_barrier();   // the producers' last B1
+    ws_barrier();   // and B2
   }
 
 }
@@ -449,9 +463,15 @@ int launch_dgrad_ws(const GemmArgs& a, int cfg, hipStream_t st) {
     // (K >= 256 and the conv3 dgrads are MFMA-bound: the four producer waves alone reach the
     // engine's ~100 TF and the epilogue traffic beside them costs 20-35%, so they stay on the
     // engine's tiles; profiles/r6/dgrad_ws/README.md)
-    if (a.bn16 || a.g16 || a.cold16 || a.bn_mask != 3 || !beta1) return -1;
-    if (nk == 2) return go(dgrad_ws_kernel<1, 2, 3, 1>);
-    if (nk == 4) return go(dgrad_ws_kernel<1, 4, 3, 1>);
+    if (a.bn16 || a.g16 || a.cold16) return -1;
+    static const int mfma_bound = env_int("TMR_DGRAD_WS_MFMA", 0);   // A/B of the wider scope
+    if (a.bn_mask == 3 && beta1) {
+      if (nk == 2) return go(dgrad_ws_kernel<1, 2, 3, 1>);
+      if (nk == 4) return go(dgrad_ws_kernel<1, 4, 3, 1>);
+      if (mfma_bound && nk % 8 == 0) return go(dgrad_ws_kernel<1, 8, 3, 1>);
+    } else if (mfma_bound && a.bn_mask == 2 && a.beta == 0.f && nk % 8 == 0) {
+      return go(dgrad_ws_kernel<1, 8, 2, 0>);
+    }
   } else {
     if (!a.bn16 || !a.g16 || a.bn_mask != 1 || !beta1 || !(a.Cold == nullptr || a.cold16))
       return -1;
