@@ -1856,12 +1856,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ds8(const T* __restrict__ g, 
                                                        T* __restrict__ dy, T* __restrict__ dyd, long n8,
                                                        int c8) {
   const int c = c8 * 8;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+  auto apply = [&](long i, const float (&gv)[8], const float (&yv)[8], const float (&dv)[8]) {
     const int cc = chan_of(i, c8) * 8;
-    float gv[8], yv[8], dv[8], o[8], od[8];
-    ld8(g, i, gv);
-    ld8(y, i, yv);
-    ld8(yd, i, dv);
+    float o[8], od[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       o[e] = fmaf(coef[cc + e], gv[e], fmaf(coef[c + cc + e], yv[e], coef[2 * c + cc + e]));
@@ -1869,6 +1866,23 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_ds8(const T* __restrict__ g, 
     }
     st8(dy, i, o);
     st8(dyd, i, od);
+  };
+  // two groups in flight per thread (round 6: one group moved its 5 tensors at 4.8 TB/s)
+  const long stride = (long)gridDim.x * NT;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += 2 * stride) {
+    const long j = i + stride;
+    const bool hj = j < n8;
+    float ga[8], ya[8], da[8], gb[8], yb[8], db[8];
+    ld8(g, i, ga);
+    ld8(y, i, ya);
+    ld8(yd, i, da);
+    if (hj) {
+      ld8(g, j, gb);
+      ld8(y, j, yb);
+      ld8(yd, j, db);
+    }
+    apply(i, ga, ya, da);
+    if (hj) apply(j, gb, yb, db);
   }
 }
 
@@ -1927,11 +1941,11 @@ TMR_API int tmr_bn_bwd_parts_ds(const void* g, const void* y, const void* parts,
   TMR_CHECK_LAUNCH("bn_bwd_final");
   const long n8 = (long)rows * c / 8;
   if (bf16)
-    hipLaunchKernelGGL(bn_bwd_apply_ds8<__bf16>, dim3(ew_blocks(n8)), dim3(NT), 0, stream,
+    hipLaunchKernelGGL(bn_bwd_apply_ds8<__bf16>, dim3(ew_blocks(n8 / 2)), dim3(NT), 0, stream,
                        (const __bf16*)g, (const __bf16*)y, (const __bf16*)yd, coef, coefd,
                        (__bf16*)dy, (__bf16*)dyd, n8, c / 8);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_ds8<float>, dim3(ew_blocks(n8)), dim3(NT), 0, stream,
+    hipLaunchKernelGGL(bn_bwd_apply_ds8<float>, dim3(ew_blocks(n8 / 2)), dim3(NT), 0, stream,
                        (const float*)g, (const float*)y, (const float*)yd, coef, coefd, (float*)dy,
                        (float*)dyd, n8, c / 8);
   TMR_CHECK_LAUNCH("bn_bwd_apply_ds");
