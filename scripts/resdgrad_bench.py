@@ -21,6 +21,8 @@ from tmrnet_amd import ops  # noqa: E402
 # conv3 dgrads (N = planes, K = 4 planes) of ResNet-50's stride-1 blocks
 RES = [(56, 256, 64), (28, 512, 128), (14, 1024, 256), (7, 2048, 512)]
 C3 = [(56, 64, 256), (28, 128, 512), (14, 256, 1024), (7, 512, 2048)]
+# the 1x1 stride-1 forwards with the fused BN statistics: (h, output channels N, input channels K)
+FWD = [(56, 256, 64), (28, 512, 128), (14, 1024, 256), (56, 128, 256), (7, 2048, 512)]
 
 
 def pack_bits(keep):
@@ -41,7 +43,13 @@ def run(kind, prec, F, h, n, k, reps, dev):
     y = torch.randn(F, h, h, n, generator=g).to(dev).to(dt)
     mean = torch.zeros(n, device=dev)
     zf = torch.relu(y.float() + 0.3)
-    if kind == "res":
+    if kind == "fwd":
+        x = torch.randn(F, h, h, k, generator=g).to(dev).to(dt)
+        wk = ops.weight_to_krsc((torch.randn(n, k, 1, 1, generator=g) / k ** 0.5).to(dev), bf16=bf)
+        fn = lambda: ops.conv_fwd_bnstats(x, wk, 1, 0, math=prec, y16=bf)
+        per = 2 if bf else 4   # y
+        dy = x                 # (the operand read: x)
+    elif kind == "res":
         old = torch.randn(F, h, h, n, generator=g).to(dev).to(dt)
         if bf:
             z = zf.to(dt)
@@ -79,7 +87,7 @@ def main():
     ap.add_argument("--frames", type=int, default=640)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--prec", default="bf16,fp32")
-    ap.add_argument("--kinds", default="res,c3")
+    ap.add_argument("--kinds", default="res,c3,fwd")
     ap.add_argument("--json", default=None)
     ap.add_argument("--tiles", action="store_true",
                     help="one tile per workgroup (TMR_IO_TILES): the launch the wave-specialised "
@@ -91,7 +99,7 @@ def main():
     rows = []
     for prec in args.prec.split(","):
         for kind in args.kinds.split(","):
-            for h, n, k in (RES if kind == "res" else C3):
+            for h, n, k in {"res": RES, "c3": C3, "fwd": FWD}[kind]:
                 r = run(kind, prec, args.frames, h, n, k, args.reps, dev)
                 rows.append(r)
                 print(json.dumps(r), flush=True)
